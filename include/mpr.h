@@ -1,0 +1,143 @@
+/*
+ * mpr.h — C ABI of libmpr.so, the MI355X (gfx950) hot path of multimodal prompt-retrieval VQA.
+ *
+ * The reference (tossowski/MultimodalPromptRetrieval) is pure Python with no native layer; every
+ * entry point below replaces a Python call site on its encode -> retrieve -> prompt -> T5-generate
+ * path.  The reference call each function stands in for is cited next to it (paths relative to
+ * the reference repository root).  The Python host (multimodalpromptretrieval_amd/_lib.py) binds
+ * these symbols with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Every function returns 0 on success, a negative MPR_E* code on failure; the message is in
+ *     mpr_last_error() (thread-local).  No C++ exception crosses the boundary.
+ *   - Pointers named *_dev are device pointers (e.g. torch tensor .data_ptr() on cuda).  Weight
+ *     tensors passed to *_create may be host or device pointers (copied with hipMemcpyDefault);
+ *     the library owns its copies until *_destroy.  The caller owns every I/O buffer.
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream).  Work is enqueued on it; the
+ *     functions do not synchronise the host unless stated.
+ *   - All floating-point arithmetic is IEEE fp32 (f32-input MFMA / VALU), like the reference's
+ *     CPU path.
+ */
+#ifndef MPR_H_
+#define MPR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPR_OK 0
+#define MPR_EINVAL (-1)   /* bad argument / shape */
+#define MPR_EHIP (-2)     /* HIP runtime error */
+#define MPR_ENOMEM (-3)   /* device allocation failed */
+#define MPR_EUNSUP (-4)   /* unsupported configuration */
+
+typedef struct mpr_index mpr_index;
+typedef struct mpr_model mpr_model;
+
+/* ---- runtime ----------------------------------------------------------------------------- */
+int mpr_init(int32_t device);
+const char* mpr_last_error(void);
+int32_t mpr_abi_version(void);
+/* Waits for all work on `stream` (host sync).  Used by the Python host only where the
+ * reference itself syncs (D2H of retrieved ids, generated tokens). */
+int mpr_stream_sync(void* stream);
+
+/* ---- retrieval index: dataset/VQAFeatureDataset.py:192-197 (torch.cdist + torch.argsort) ----
+ * rows: [n, d] fp32 row-major (host or device).  metric 0 = L2 (cdist, ascending distance),
+ * 1 = cosine (utils.py:57-62 cosine_similarity, descending similarity).  row_offset is added to
+ * every returned id (global id of row 0 of this shard, §8(e) index sharding). */
+int mpr_index_create(const float* rows, int64_t n, int32_t d, int32_t metric, int64_t row_offset,
+                     mpr_index** out);
+int mpr_index_destroy(mpr_index* index);
+int64_t mpr_index_rows(const mpr_index* index);
+/* Top-k nearest rows for each of b queries q_dev [b, d] (fp32, device).  ids_dev [b, k] int64,
+ * dist_dev [b, k] fp32: L2 distance (sqrt(max(|q|^2+|x|^2-2q.x, 0)), cdist mm-path) or cosine
+ * similarity.  Order: best first; exact ties broken by lowest id.  1 <= k <= 64, k <= n. */
+int mpr_index_search(mpr_index* index, const float* q_dev, int32_t b, int32_t k, int64_t* ids_dev,
+                     float* dist_dev, void* stream);
+/* Full score matrix out_dev [b, n] (L2 distance or cosine similarity), the torch.cdist output
+ * (dataset/VQAFeatureDataset.py:192) / pairwise cosine_similarity (utils.py:57-62). */
+int mpr_index_scores(mpr_index* index, const float* q_dev, int32_t b, float* out_dev, void* stream);
+/* Merge per-shard candidates: cand_* [b, n_cand] (e.g. the RCCL all-gather of W shards' local
+ * top-k) -> best k per query with the same order/tie rule.  metric as above. */
+int mpr_topk_merge(const float* cand_dist_dev, const int64_t* cand_ids_dev, int32_t b,
+                   int32_t n_cand, int32_t k, int32_t metric, float* out_dist_dev,
+                   int64_t* out_ids_dev, void* stream);
+/* Row-wise cosine similarity (utils.py:57-62 with aligned rows): out[i] =
+ * sum(x1[i]*x2[i]) / max(|x1[i]|*|x2[i]|, eps), x1/x2 [m, d]. */
+int mpr_cosine_rows(const float* x1_dev, const float* x2_dev, int64_t m, int32_t d, float eps,
+                    float* out_dev, void* stream);
+
+/* ---- CLIP ViT-B/32 image encoder ------------------------------------------------------------
+ * openai CLIP VisionTransformer; called at dataset/VQAFeatureDataset.py:189 (encode_image, CLS)
+ * and architectures/T5VisionModel.py:112-139 (get_image_token_features, all tokens).
+ * cfg = {width, layers, heads, patch, image_size, out_dim}.  tensors (fp32), in order:
+ *   conv1.weight [w,3,p,p], class_embedding [w], positional_embedding [g*g+1, w],
+ *   ln_pre.weight [w], ln_pre.bias [w],
+ *   per layer: ln_1.weight, ln_1.bias, attn.in_proj_weight [3w,w], attn.in_proj_bias [3w],
+ *              attn.out_proj.weight [w,w], attn.out_proj.bias [w], ln_2.weight, ln_2.bias,
+ *              mlp.c_fc.weight [4w,w], mlp.c_fc.bias [4w], mlp.c_proj.weight [w,4w], mlp.c_proj.bias [w]
+ *   ln_post.weight, ln_post.bias, proj [w, out_dim]                      (5 + 12*layers + 3) */
+int mpr_vit_create(const int32_t* cfg, int32_t n_cfg, const float* const* tensors,
+                   int32_t n_tensors, mpr_model** out);
+/* img_dev [b,3,S,S] fp32 NCHW.  mode 0: CLS path (encode_image) -> out[b*out_bstride + c],
+ * mode 1: token path (ln_post on all tokens, @proj) -> out[b*out_bstride + t*out_dim + c]. */
+int mpr_vit_forward(mpr_model* m, const float* img_dev, int32_t b, int32_t mode, float* out_dev,
+                    int64_t out_bstride, void* stream);
+
+/* ---- CLIP text encoder: dataset/VQAFeatureDataset.py:190 (clip_model.encode_text) -----------
+ * cfg = {width, layers, heads, context_length, vocab, out_dim}.  tensors: token_embedding
+ * [vocab,w], positional_embedding [ctx,w], 12 per layer (as ViT), ln_final.weight,
+ * ln_final.bias, text_projection [w,out_dim]                                (2 + 12*layers + 3) */
+int mpr_clip_text_create(const int32_t* cfg, int32_t n_cfg, const float* const* tensors,
+                         int32_t n_tensors, mpr_model** out);
+/* tok_dev [b, ctx] int32 (clip.tokenize ids).  Pools at argmax(token id) (the EOT token).
+ * seq_len (<= ctx) = number of leading positions to run; the attention is causal, so any
+ * seq_len > max_b argmax_t tok[b, t] gives bit-identical pooled outputs (pass ctx if unknown). */
+int mpr_clip_text_forward(mpr_model* m, const int32_t* tok_dev, int32_t b, int32_t seq_len,
+                          float* out_dev, int64_t out_bstride, void* stream);
+
+/* ---- T5 encoder/decoder: architectures/T5VisionModel.py:169,200-205,233 -----------------------
+ * (transformers T5ForConditionalGeneration: encoder, greedy generate, teacher-forced logits)
+ * cfg = {d_model, d_kv, n_heads, d_ff, n_enc_layers, n_dec_layers, vocab, num_buckets,
+ *        scale_decoder_outputs}.
+ * tensors: shared [vocab,d], enc relative_attention_bias [nb,H],
+ *   per enc layer: ln0 [d], q [H*dkv,d], k, v, o [d,H*dkv], ln1 [d], wi [dff,d], wo [d,dff]
+ *   enc final_layer_norm [d], dec relative_attention_bias [nb,H],
+ *   per dec layer: ln0, q, k, v, o, ln1, cq, ck, cv, co, ln2, wi, wo
+ *   dec final_layer_norm [d], lm_head [vocab,d]            (2 + 8*Le + 1 + 1 + 13*Ld + 2)
+ * bucket luts: relative-position bucket of (key_pos - query_pos) for rel in [-radius, radius],
+ * index rel + radius (encoder: bidirectional, decoder: causal), as computed by
+ * T5Attention._relative_position_bucket. */
+int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* tensors, int32_t n_tensors,
+                  const int32_t* enc_lut, const int32_t* dec_lut, int32_t lut_radius,
+                  mpr_model** out);
+/* Gather shared[ids] into out[b*out_bstride + (row0+t)*d + c] (T5VisionModel.py:169). */
+int mpr_t5_embed(mpr_model* m, const int32_t* ids_dev, int32_t b, int32_t len, float* out_dev,
+                 int64_t out_bstride, int32_t row0, void* stream);
+/* Encoder stack over inputs_embeds [b,L,d] with attention mask [b,L] (1/0 fp32) -> out [b,L,d]. */
+int mpr_t5_encode(mpr_model* m, const float* embeds_dev, const float* mask_dev, int32_t b,
+                  int32_t L, float* out_dev, void* stream);
+/* Greedy generation (GenerationMixin greedy search, do_sample=False): encoder once, then
+ * max_new decoder steps with KV cache; rows that emitted eos keep emitting pad.
+ * out_tokens_dev [b, max_new+1] int32 (column 0 = decoder_start).  No host sync. */
+int mpr_t5_generate(mpr_model* m, const float* embeds_dev, const float* mask_dev, int32_t b,
+                    int32_t L, int32_t max_new, int32_t decoder_start, int32_t eos, int32_t pad,
+                    int32_t* out_tokens_dev, void* stream);
+/* Teacher-forced decoder logits: dec_in_dev [b,T] int32 decoder input ids -> logits [b,T,vocab]. */
+int mpr_t5_logits(mpr_model* m, const float* embeds_dev, const float* mask_dev, int32_t b,
+                  int32_t L, const int32_t* dec_in_dev, int32_t T, float* logits_dev,
+                  void* stream);
+/* Mean token cross-entropy of logits [n, vocab] against labels [n] (label -100 ignored),
+ * torch.nn.CrossEntropyLoss semantics (T5ForConditionalGeneration loss). out_dev: 1 float. */
+int mpr_cross_entropy(const float* logits_dev, const int32_t* labels_dev, int64_t n, int32_t vocab,
+                      float* out_dev, void* stream);
+
+int mpr_model_destroy(mpr_model* m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPR_H_ */

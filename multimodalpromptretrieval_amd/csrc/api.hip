@@ -1,0 +1,353 @@
+// api.hip — the extern "C" boundary of libmpr.so (declared in include/mpr.h).
+#include <cstring>
+
+#include "models.h"
+
+namespace mpr {
+
+namespace {
+thread_local char g_err[1024] = "";
+}
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int upload(DevBuf& dst, const float* src, size_t count) {
+  MPR_REQUIRE(src != nullptr, "upload: null tensor pointer");
+  MPR_TRY(dst.ensure(count * sizeof(float)));
+  MPR_HIP(hipMemcpy(dst.ptr, src, count * sizeof(float), hipMemcpyDefault));
+  return MPR_OK;
+}
+
+namespace {
+
+// Copy `count` floats into dst at float offset `off` (dst already sized).
+int upload_at(DevBuf& dst, size_t off, const float* src, size_t count) {
+  MPR_REQUIRE(src != nullptr, "upload: null tensor pointer");
+  MPR_REQUIRE((off + count) * sizeof(float) <= dst.bytes, "upload: overflow");
+  MPR_HIP(hipMemcpy(dst.as<float>() + off, src, count * sizeof(float), hipMemcpyDefault));
+  return MPR_OK;
+}
+
+// dst = src^T for src [rows, cols] given on host or device.
+int upload_t(DevBuf& dst, const float* src, int64_t rows, int64_t cols) {
+  std::vector<float> h((size_t)rows * cols), t((size_t)rows * cols);
+  MPR_HIP(hipMemcpy(h.data(), src, h.size() * sizeof(float), hipMemcpyDefault));
+  for (int64_t r = 0; r < rows; ++r)
+    for (int64_t c = 0; c < cols; ++c) t[(size_t)c * rows + r] = h[(size_t)r * cols + c];
+  MPR_TRY(dst.ensure(t.size() * sizeof(float)));
+  MPR_HIP(hipMemcpy(dst.ptr, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+  return MPR_OK;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::exception& e) {
+    set_error("exception: %s", e.what());
+    return MPR_ENOMEM;
+  } catch (...) {
+    set_error("unknown exception");
+    return MPR_EINVAL;
+  }
+}
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+}  // namespace mpr
+
+using namespace mpr;
+
+extern "C" {
+
+int32_t mpr_abi_version(void) { return 1; }
+
+const char* mpr_last_error(void) { return mpr::g_err; }
+
+int mpr_init(int32_t device) {
+  int n = 0;
+  MPR_HIP(hipGetDeviceCount(&n));
+  MPR_REQUIRE(device >= 0 && device < n, "mpr_init: device %d of %d", device, n);
+  MPR_HIP(hipSetDevice(device));
+  return MPR_OK;
+}
+
+int mpr_stream_sync(void* stream) {
+  MPR_HIP(hipStreamSynchronize(S(stream)));
+  return MPR_OK;
+}
+
+// ---- index -------------------------------------------------------------------------------------
+int mpr_index_create(const float* rows, int64_t n, int32_t d, int32_t metric, int64_t row_offset,
+                     mpr_index** out) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(out != nullptr, "index_create: out is null");
+    MPR_REQUIRE(n >= 1 && rows != nullptr, "index_create: empty index");
+    MPR_REQUIRE(d >= 16 && d % 16 == 0, "index_create: d=%d must be a positive multiple of 16", d);
+    MPR_REQUIRE(metric == 0 || metric == 1, "index_create: metric %d (0=L2, 1=cosine)", metric);
+    MPR_REQUIRE(n < (int64_t)0x7fffffff, "index_create: n=%lld rows exceeds int32 row ids per shard",
+                (long long)n);
+    auto ix = std::make_unique<mpr_index>();
+    ix->n = n;
+    ix->d = d;
+    ix->metric = metric;
+    ix->row_offset = row_offset;
+    MPR_TRY(upload(ix->rows, rows, (size_t)n * d));
+    MPR_TRY(ix->norms.ensure((size_t)n * sizeof(float)));
+    MPR_TRY(row_sqnorms(ix->rows.as<float>(), n, d, ix->norms.as<float>(), nullptr));
+    MPR_HIP(hipStreamSynchronize(nullptr));
+    *out = ix.release();
+    return MPR_OK;
+  });
+}
+
+int mpr_index_destroy(mpr_index* index) {
+  delete index;
+  return MPR_OK;
+}
+
+int64_t mpr_index_rows(const mpr_index* index) { return index ? index->n : -1; }
+
+int mpr_index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_t* ids,
+                     float* dist, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(ix != nullptr, "search: null index");
+    MPR_REQUIRE(b == 0 || (q && ids && dist), "search: null buffer");
+    if (b == 0) return MPR_OK;
+    MPR_REQUIRE(k >= 1 && k <= 64 && k <= ix->n, "search: k=%d (1..64, <= %lld rows)", k,
+                (long long)ix->n);
+    const size_t ws = scan_topk_workspace(ix->n, b, k);
+    MPR_TRY(ix->ws.ensure(ws));
+    return scan_topk(ix->rows.as<float>(), ix->norms.as<float>(), ix->n, ix->d, ix->row_offset,
+                     ix->metric, q, b, k, ix->ws.as<float>(), ix->ws.bytes, dist, ids, S(stream));
+  });
+}
+
+int mpr_index_scores(mpr_index* ix, const float* q, int32_t b, float* out, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(ix != nullptr, "scores: null index");
+    return scan_scores(ix->rows.as<float>(), ix->norms.as<float>(), ix->n, ix->d, ix->metric, q,
+                       b, out, S(stream));
+  });
+}
+
+int mpr_topk_merge(const float* cand_dist, const int64_t* cand_ids, int32_t b, int32_t n_cand,
+                   int32_t k, int32_t metric, float* out_dist, int64_t* out_ids, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(metric == 0 || metric == 1, "merge: metric %d", metric);
+    return topk_merge(cand_dist, cand_ids, b, n_cand, k, metric, out_dist, out_ids, S(stream));
+  });
+}
+
+int mpr_cosine_rows(const float* x1, const float* x2, int64_t m, int32_t d, float eps, float* out,
+                    void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(d >= 1, "cosine_rows: d=%d", d);
+    return cosine_rows(x1, x2, m, d, eps, out, S(stream));
+  });
+}
+
+// ---- CLIP ViT -------------------------------------------------------------------------------------
+int mpr_vit_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int32_t nt,
+                   mpr_model** out) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(cfg && n_cfg >= 6 && t && out, "vit_create: bad arguments");
+    const int W = cfg[0], layers = cfg[1], heads = cfg[2], patch = cfg[3], image = cfg[4],
+              out_dim = cfg[5];
+    MPR_REQUIRE(W % 64 == 0 && heads * 64 == W, "vit_create: width %d / heads %d (head dim 64)", W,
+                heads);
+    MPR_REQUIRE(image % patch == 0 && patch % 4 == 0 && W <= 1024, "vit_create: geometry");
+    MPR_REQUIRE(nt == 5 + 12 * layers + 3, "vit_create: expected %d tensors, got %d",
+                5 + 12 * layers + 3, nt);
+    auto m = std::make_unique<VitModel>();
+    m->width = W;
+    m->patch = patch;
+    m->image = image;
+    m->out_dim = out_dim;
+    m->grid = image / patch;
+    const int g2 = m->grid * m->grid;
+    MPR_TRY(upload(m->conv_w, t[0], (size_t)W * 3 * patch * patch));
+    MPR_TRY(upload(m->cls, t[1], W));
+    MPR_TRY(upload(m->pos, t[2], (size_t)(g2 + 1) * W));
+    MPR_TRY(upload(m->lnpre_w, t[3], W));
+    MPR_TRY(upload(m->lnpre_b, t[4], W));
+    MPR_TRY(m->tower.load_blocks(t + 5, W, layers));
+    const float* const* tail = t + 5 + 12 * layers;
+    MPR_TRY(upload(m->lnpost_w, tail[0], W));
+    MPR_TRY(upload(m->lnpost_b, tail[1], W));
+    MPR_TRY(upload_t(m->projT, tail[2], W, out_dim));
+    *out = m.release();
+    return MPR_OK;
+  });
+}
+
+int mpr_vit_forward(mpr_model* m, const float* img, int32_t b, int32_t mode, float* out,
+                    int64_t out_bs, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(m && m->kind == mpr_model::VIT, "vit_forward: not a ViT handle");
+    return static_cast<VitModel*>(m)->forward(img, b, mode, out, out_bs, S(stream));
+  });
+}
+
+// ---- CLIP text ------------------------------------------------------------------------------------
+int mpr_clip_text_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int32_t nt,
+                         mpr_model** out) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(cfg && n_cfg >= 6 && t && out, "text_create: bad arguments");
+    const int W = cfg[0], layers = cfg[1], heads = cfg[2], ctx = cfg[3], vocab = cfg[4],
+              out_dim = cfg[5];
+    MPR_REQUIRE(heads * 64 == W && W <= 1024, "text_create: width %d / heads %d", W, heads);
+    MPR_REQUIRE(nt == 2 + 12 * layers + 3, "text_create: expected %d tensors, got %d",
+                2 + 12 * layers + 3, nt);
+    auto m = std::make_unique<TextModel>();
+    m->width = W;
+    m->ctx = ctx;
+    m->vocab = vocab;
+    m->out_dim = out_dim;
+    MPR_TRY(upload(m->tok_emb, t[0], (size_t)vocab * W));
+    MPR_TRY(upload(m->pos, t[1], (size_t)ctx * W));
+    MPR_TRY(m->tower.load_blocks(t + 2, W, layers));
+    const float* const* tail = t + 2 + 12 * layers;
+    MPR_TRY(upload(m->lnf_w, tail[0], W));
+    MPR_TRY(upload(m->lnf_b, tail[1], W));
+    MPR_TRY(upload_t(m->projT, tail[2], W, out_dim));
+    *out = m.release();
+    return MPR_OK;
+  });
+}
+
+int mpr_clip_text_forward(mpr_model* m, const int32_t* tok, int32_t b, int32_t seq_len, float* out,
+                          int64_t out_bs, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(m && m->kind == mpr_model::CLIP_TEXT, "text_forward: not a CLIP text handle");
+    return static_cast<TextModel*>(m)->forward(tok, b, seq_len, out, out_bs, S(stream));
+  });
+}
+
+// ---- T5 -------------------------------------------------------------------------------------------
+int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int32_t nt,
+                  const int32_t* enc_lut, const int32_t* dec_lut, int32_t radius,
+                  mpr_model** out) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(cfg && n_cfg >= 9 && t && out && enc_lut && dec_lut, "t5_create: bad arguments");
+    auto m = std::make_unique<T5Model>();
+    m->d = cfg[0];
+    m->dkv = cfg[1];
+    m->H = cfg[2];
+    m->dff = cfg[3];
+    m->Le = cfg[4];
+    m->Ld = cfg[5];
+    m->V = cfg[6];
+    m->nb = cfg[7];
+    m->scale_out = cfg[8];
+    m->inner = m->H * m->dkv;
+    m->lut_radius = radius;
+    const int d = m->d, inner = m->inner, dff = m->dff, Le = m->Le, Ld = m->Ld;
+    MPR_REQUIRE(m->dkv == 64, "t5_create: d_kv=%d (head dim 64 supported)", m->dkv);
+    MPR_REQUIRE(d % 16 == 0 && d <= 1024 && dff % 16 == 0, "t5_create: d_model=%d d_ff=%d", d, dff);
+    MPR_REQUIRE(radius >= 64, "t5_create: lut radius %d too small", radius);
+    const int expect = 2 + 8 * Le + 1 + 1 + 13 * Ld + 2;
+    MPR_REQUIRE(nt == expect, "t5_create: expected %d tensors, got %d", expect, nt);
+    int p = 0;
+    MPR_TRY(upload(m->shared, t[p++], (size_t)m->V * d));
+    MPR_TRY(upload(m->enc_rel, t[p++], (size_t)m->nb * m->H));
+    for (int l = 0; l < Le; ++l) {
+      auto ly = std::make_unique<T5Layer>();
+      MPR_TRY(upload(ly->ln0, t[p++], d));
+      MPR_TRY(ly->qkv.ensure((size_t)3 * inner * d * 4));
+      for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly->qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
+      MPR_TRY(upload(ly->o, t[p++], (size_t)d * inner));
+      MPR_TRY(upload(ly->ln1, t[p++], d));
+      MPR_TRY(upload(ly->wi, t[p++], (size_t)dff * d));
+      MPR_TRY(upload(ly->wo, t[p++], (size_t)d * dff));
+      m->enc.push_back(std::move(ly));
+    }
+    MPR_TRY(upload(m->enc_final, t[p++], d));
+    MPR_TRY(upload(m->dec_rel, t[p++], (size_t)m->nb * m->H));
+    MPR_TRY(m->cross_kv_w.ensure((size_t)Ld * 2 * inner * d * 4));
+    for (int l = 0; l < Ld; ++l) {
+      auto ly = std::make_unique<T5Layer>();
+      MPR_TRY(upload(ly->ln0, t[p++], d));
+      MPR_TRY(ly->qkv.ensure((size_t)3 * inner * d * 4));
+      for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly->qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
+      MPR_TRY(upload(ly->o, t[p++], (size_t)d * inner));
+      MPR_TRY(upload(ly->ln1, t[p++], d));
+      MPR_TRY(upload(ly->cq, t[p++], (size_t)inner * d));
+      MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l) * inner * d, t[p++], (size_t)inner * d));
+      MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l + 1) * inner * d, t[p++], (size_t)inner * d));
+      MPR_TRY(upload(ly->co, t[p++], (size_t)d * inner));
+      MPR_TRY(upload(ly->ln2, t[p++], d));
+      MPR_TRY(upload(ly->wi, t[p++], (size_t)dff * d));
+      MPR_TRY(upload(ly->wo, t[p++], (size_t)d * dff));
+      m->dec.push_back(std::move(ly));
+    }
+    MPR_TRY(upload(m->dec_final, t[p++], d));
+    MPR_TRY(upload(m->lm_head, t[p++], (size_t)m->V * d));
+    const size_t nl = (size_t)2 * radius + 1;
+    MPR_TRY(m->enc_lut.ensure(nl * 4));
+    MPR_TRY(m->dec_lut.ensure(nl * 4));
+    MPR_HIP(hipMemcpy(m->enc_lut.ptr, enc_lut, nl * 4, hipMemcpyDefault));
+    MPR_HIP(hipMemcpy(m->dec_lut.ptr, dec_lut, nl * 4, hipMemcpyDefault));
+    *out = m.release();
+    return MPR_OK;
+  });
+}
+
+#define T5_HANDLE(m)                                                            \
+  MPR_REQUIRE((m) && (m)->kind == mpr_model::T5, "t5: not a T5 handle");        \
+  T5Model* t5 = static_cast<T5Model*>(m)
+
+int mpr_t5_embed(mpr_model* m, const int32_t* ids, int32_t b, int32_t len, float* out,
+                 int64_t out_bs, int32_t row0, void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    return t5->embed(ids, b, len, out, out_bs, row0, S(stream));
+  });
+}
+
+int mpr_t5_encode(mpr_model* m, const float* embeds, const float* mask, int32_t b, int32_t L,
+                  float* out, void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    return t5->encode(embeds, mask, b, L, out, S(stream));
+  });
+}
+
+int mpr_t5_generate(mpr_model* m, const float* embeds, const float* mask, int32_t b, int32_t L,
+                    int32_t max_new, int32_t start, int32_t eos, int32_t pad, int32_t* out_tokens,
+                    void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    return t5->generate(embeds, mask, b, L, max_new, start, eos, pad, out_tokens, S(stream));
+  });
+}
+
+int mpr_t5_logits(mpr_model* m, const float* embeds, const float* mask, int32_t b, int32_t L,
+                  const int32_t* dec_in, int32_t T, float* logits, void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    return t5->logits_tf(embeds, mask, b, L, dec_in, T, logits, S(stream));
+  });
+}
+
+int mpr_cross_entropy(const float* logits, const int32_t* labels, int64_t n, int32_t vocab,
+                      float* out, void* stream) {
+  return guarded([&]() -> int {
+    static DevBuf ws;  // 2n floats of per-row partials
+    MPR_TRY(ws.ensure((size_t)n * 2 * sizeof(float)));
+    return cross_entropy(logits, labels, n, vocab, ws.as<float>(), out, S(stream));
+  });
+}
+
+int mpr_model_destroy(mpr_model* m) {
+  delete m;
+  return MPR_OK;
+}
+
+}  // extern "C"

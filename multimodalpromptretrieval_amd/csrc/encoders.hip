@@ -1,0 +1,146 @@
+// encoders.hip — CLIP ViT-B/32 image tower and CLIP text tower on the gfx950 kernels.
+//
+// Reference semantics (openai CLIP model.py, called from the reference at
+// dataset/VQAFeatureDataset.py:189-190 and architectures/T5VisionModel.py:112-139):
+//   image: conv1 (patch 32, stride 32, no bias) -> [CLS; patches] + positional -> ln_pre ->
+//          12 x ResidualAttentionBlock -> ln_post -> @ proj      (CLS row only for encode_image,
+//          every token for get_image_token_features)
+//   text:  token_embedding + positional -> 12 x causal ResidualAttentionBlock -> ln_final ->
+//          row at argmax(token id) (EOT) -> @ text_projection
+//   ResidualAttentionBlock: x = x + out_proj(MHA(ln_1(x)));  x = x + c_proj(QuickGELU(c_fc(ln_2(x))))
+// Data layout in HBM: activations [B*L, width] fp32 row-major; QKV [B*L, 3*width] with head h
+// of q/k/v at columns h*64, width + h*64, 2*width + h*64 (nn.MultiheadAttention in_proj order).
+#include "models.h"
+
+namespace mpr {
+
+namespace {
+constexpr float CLIP_LN_EPS = 1e-5f;
+}
+
+int ClipTower::load_blocks(const float* const* t, int w, int nl) {
+  width = w;
+  layers = nl;
+  heads = w / 64;
+  blocks.clear();
+  for (int l = 0; l < nl; ++l) {
+    auto b = std::make_unique<ClipBlock>();
+    const float* const* p = t + 12 * l;
+    MPR_TRY(upload(b->ln1_w, p[0], w));
+    MPR_TRY(upload(b->ln1_b, p[1], w));
+    MPR_TRY(upload(b->in_w, p[2], (size_t)3 * w * w));
+    MPR_TRY(upload(b->in_b, p[3], (size_t)3 * w));
+    MPR_TRY(upload(b->out_w, p[4], (size_t)w * w));
+    MPR_TRY(upload(b->out_b, p[5], w));
+    MPR_TRY(upload(b->ln2_w, p[6], w));
+    MPR_TRY(upload(b->ln2_b, p[7], w));
+    MPR_TRY(upload(b->fc_w, p[8], (size_t)4 * w * w));
+    MPR_TRY(upload(b->fc_b, p[9], (size_t)4 * w));
+    MPR_TRY(upload(b->pj_w, p[10], (size_t)4 * w * w));
+    MPR_TRY(upload(b->pj_b, p[11], w));
+    blocks.push_back(std::move(b));
+  }
+  return MPR_OK;
+}
+
+int ClipTower::run(float* x, int B, int L, bool causal, hipStream_t s) {
+  const int W = width, M = B * L;
+  MPR_TRY(h.ensure((size_t)M * W * 4));
+  MPR_TRY(qkv.ensure((size_t)M * 3 * W * 4));
+  MPR_TRY(ao.ensure((size_t)M * W * 4));
+  MPR_TRY(mlp.ensure((size_t)M * 4 * W * 4));
+  float* hp = h.as<float>();
+  float* qp = qkv.as<float>();
+  float* ap = ao.as<float>();
+  float* mp = mlp.as<float>();
+  for (auto& bp : blocks) {
+    const ClipBlock& b = *bp;
+    MPR_TRY(layernorm(x, W, M, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(), CLIP_LN_EPS, hp, W, s));
+    GemmArgs g;
+    g.A = hp; g.lda = W; g.W = b.in_w.as<float>(); g.ldw = W; g.bias = b.in_b.as<float>();
+    g.C = qp; g.ldc = 3 * W; g.M = M; g.N = 3 * W; g.K = W;
+    MPR_TRY(gemm(g, s));
+    AttnArgs at;
+    at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
+    at.k = qp + W; at.k_bs = at.q_bs; at.k_rs = 3 * W;
+    at.v = qp + 2 * W; at.v_bs = at.q_bs; at.v_rs = 3 * W;
+    at.o = ap; at.o_bs = (int64_t)L * W; at.o_rs = W;
+    at.B = B; at.H = heads; at.Lq = L; at.Lk = L;
+    at.scale = 0.125f;  // 64 ** -0.5, exact power of two
+    at.causal = causal ? 1 : 0;
+    MPR_TRY(attention(at, s));
+    GemmArgs o;
+    o.A = ap; o.lda = W; o.W = b.out_w.as<float>(); o.ldw = W; o.bias = b.out_b.as<float>();
+    o.R = x; o.ldr = W; o.C = x; o.ldc = W; o.M = M; o.N = W; o.K = W;
+    MPR_TRY(gemm(o, s));
+    MPR_TRY(layernorm(x, W, M, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(), CLIP_LN_EPS, hp, W, s));
+    GemmArgs f;
+    f.A = hp; f.lda = W; f.W = b.fc_w.as<float>(); f.ldw = W; f.bias = b.fc_b.as<float>();
+    f.C = mp; f.ldc = 4 * W; f.M = M; f.N = 4 * W; f.K = W; f.act = ACT_QUICKGELU;
+    MPR_TRY(gemm(f, s));
+    GemmArgs pj;
+    pj.A = mp; pj.lda = 4 * W; pj.W = b.pj_w.as<float>(); pj.ldw = 4 * W; pj.bias = b.pj_b.as<float>();
+    pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M; pj.N = W; pj.K = 4 * W;
+    MPR_TRY(gemm(pj, s));
+  }
+  return MPR_OK;
+}
+
+int VitModel::forward(const float* img, int B, int mode, float* out, int64_t out_bs,
+                      hipStream_t s) {
+  MPR_REQUIRE(mode == 0 || mode == 1, "vit: mode must be 0 (CLS) or 1 (tokens)");
+  if (B == 0) return MPR_OK;
+  const int W = width, g2 = grid * grid, T = g2 + 1, P = 3 * patch * patch;
+  MPR_TRY(cols.ensure((size_t)B * g2 * P * 4));
+  MPR_TRY(patches.ensure((size_t)B * g2 * W * 4));
+  MPR_TRY(x.ensure((size_t)B * T * W * 4));
+  MPR_TRY(tmp.ensure((size_t)B * T * W * 4));
+  float* xp = x.as<float>();
+  MPR_TRY(im2col_patches(img, B, image, patch, cols.as<float>(), s));
+  GemmArgs pe;
+  pe.A = cols.as<float>(); pe.lda = P; pe.W = conv_w.as<float>(); pe.ldw = P;
+  pe.C = patches.as<float>(); pe.ldc = W; pe.M = B * g2; pe.N = W; pe.K = P;
+  MPR_TRY(gemm(pe, s));
+  MPR_TRY(vit_assemble(patches.as<float>(), cls.as<float>(), pos.as<float>(), B, g2, W, xp, s));
+  MPR_TRY(layernorm(xp, W, B * T, W, lnpre_w.as<float>(), lnpre_b.as<float>(), CLIP_LN_EPS, xp, W,
+                    s));
+  MPR_TRY(tower.run(xp, B, T, /*causal=*/false, s));
+  float* tp = tmp.as<float>();
+  GemmArgs pj;
+  pj.W = projT.as<float>(); pj.ldw = W; pj.N = out_dim; pj.K = W; pj.A = tp; pj.lda = W;
+  if (mode == 0) {
+    // ln_post on the CLS rows only (x[b*T]), then @ proj
+    MPR_TRY(layernorm(xp, (int64_t)T * W, B, W, lnpost_w.as<float>(), lnpost_b.as<float>(),
+                      CLIP_LN_EPS, tp, W, s));
+    pj.M = B; pj.C = out; pj.ldc = out_bs;
+  } else {
+    MPR_TRY(layernorm(xp, W, B * T, W, lnpost_w.as<float>(), lnpost_b.as<float>(), CLIP_LN_EPS,
+                      tp, W, s));
+    pj.M = B * T; pj.C = out; pj.ldc = out_dim; pj.c_rpb = T; pj.c_bs = out_bs;
+  }
+  MPR_TRY(gemm(pj, s));
+  return MPR_OK;
+}
+
+int TextModel::forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs,
+                       hipStream_t s) {
+  MPR_REQUIRE(L >= 1 && L <= ctx, "clip text: seq_len %d outside [1, %d]", L, ctx);
+  if (B == 0) return MPR_OK;
+  const int W = width;
+  MPR_TRY(x.ensure((size_t)B * L * W * 4));
+  MPR_TRY(pooled.ensure((size_t)B * W * 4));
+  float* xp = x.as<float>();
+  MPR_TRY(embed_gather(tok_emb.as<float>(), tok, ctx, B, L, W, pos.as<float>(), xp, (int64_t)L * W,
+                       0, s));
+  MPR_TRY(tower.run(xp, B, L, /*causal=*/true, s));
+  float* pp = pooled.as<float>();
+  MPR_TRY(eot_gather(xp, tok, B, L, ctx, W, pp, s));
+  MPR_TRY(layernorm(pp, W, B, W, lnf_w.as<float>(), lnf_b.as<float>(), CLIP_LN_EPS, pp, W, s));
+  GemmArgs pj;
+  pj.A = pp; pj.lda = W; pj.W = projT.as<float>(); pj.ldw = W; pj.M = B; pj.N = out_dim; pj.K = W;
+  pj.C = out; pj.ldc = out_bs;
+  MPR_TRY(gemm(pj, s));
+  return MPR_OK;
+}
+
+}  // namespace mpr

@@ -1,0 +1,110 @@
+// kernels.h — launchers for the gfx950 kernels used by the model runners (csrc/*.hip).
+#pragma once
+
+#include "common.h"
+
+namespace mpr {
+
+enum Act : int { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_RELU = 2 };
+
+// C[m, n] = R[m, n] + act(sum_k A[m, k] * W[n, k] + bias[n])      (R, bias optional)
+// fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32 (exact f32 FMA chains).
+struct GemmArgs {
+  const float* A = nullptr;
+  int64_t lda = 0;
+  const float* W = nullptr;  // [N, K] row-major (torch nn.Linear layout)
+  int64_t ldw = 0;
+  const float* bias = nullptr;
+  const float* R = nullptr;  // residual, may alias C
+  int64_t ldr = 0;
+  float* C = nullptr;
+  int64_t ldc = 0;
+  int M = 0, N = 0, K = 0;
+  int act = ACT_NONE;
+  // Optional batched C rows: row r is stored at C + (r / c_rpb) * c_bs + (r % c_rpb) * ldc.
+  int c_rpb = 0;
+  int64_t c_bs = 0;
+};
+int gemm(const GemmArgs& a, hipStream_t s);
+
+// Skinny GEMM for M <= 16 rows (decode steps): same contract as gemm() plus an optional fused
+// T5 RMSNorm of the A rows: A'[m,k] = ln_w[k] * (A[m,k] * rsqrt(mean_k A[m,:]^2 + eps)).
+struct SkinnyArgs {
+  GemmArgs g;
+  const float* rms_w = nullptr;  // fuse RMSNorm prologue when non-null
+  float rms_eps = 1e-6f;
+  float a_scale = 1.f;           // A' = (ln_w * (A * rstd)) * a_scale (T5 tied-head d^-0.5)
+};
+int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
+
+// LayerNorm over rows of width D (eps, affine), out may alias x.  ld in floats.
+int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, const float* beta,
+              float eps, float* out, int64_t ldo, hipStream_t s);
+// T5LayerNorm (RMSNorm, weight only).
+int rmsnorm(const float* x, int64_t ldx, int M, int D, const float* w, float eps, float* out,
+            int64_t ldo, hipStream_t s);
+
+// Multi-head attention with head_dim 64 for short sequences.
+// q(b,i,h,:) at q + b*q_bs + i*q_rs + h*64  (same for k, v, o).
+struct AttnArgs {
+  const float* q = nullptr;
+  int64_t q_bs = 0, q_rs = 0;
+  const float* k = nullptr;
+  int64_t k_bs = 0, k_rs = 0;
+  const float* v = nullptr;
+  int64_t v_bs = 0, v_rs = 0;
+  float* o = nullptr;
+  int64_t o_bs = 0, o_rs = 0;
+  int B = 0, H = 0, Lq = 0, Lk = 0;
+  float scale = 1.f;
+  int causal = 0;   // key j visible iff j <= i + q_pos0
+  int q_pos0 = 0;   // absolute position of query row 0
+  const float* key_mask = nullptr;  // [B, mask_bs] 1/0 (0 = padded key), optional
+  int64_t mask_bs = 0;
+  const float* rel_bias = nullptr;  // [num_buckets, H] T5 relative attention bias, optional
+  const int* bucket_lut = nullptr;  // bucket of (j - (i + q_pos0)) at index rel + lut_radius
+  int lut_radius = 0;
+};
+int attention(const AttnArgs& a, hipStream_t s);
+
+// ViT patch extraction: img [B,3,S,S] -> cols [B*g*g, 3*p*p] in (c, kh, kw) order (conv1 weight
+// flattening).
+int im2col_patches(const float* img, int B, int S, int p, float* cols, hipStream_t s);
+// x[b,0,:] = cls + pos[0]; x[b,1+t,:] = patch[b*g2+t,:] + pos[1+t]   (x: [B, g2+1, W])
+int vit_assemble(const float* patches, const float* cls, const float* pos, int B, int g2, int W,
+                 float* x, hipStream_t s);
+// Embedding gather: out[b*obs + (row0+t)*D + c] = table[ids[b*len+t]*D + c] (+ pos[t*D + c])
+int embed_gather(const float* table, const int32_t* ids, int64_t ids_bs, int B, int len, int D,
+                 const float* pos, float* out, int64_t obs, int row0, hipStream_t s);
+// CLIP text pooling: for each b, row e = argmax_t tok[b,t] (first max); out_rows[b,:] = x[b*L+e,:]
+int eot_gather(const float* x, const int32_t* tok, int B, int L, int ctx, int D, float* out,
+               hipStream_t s);
+// Row argmax (first maximal index, torch.argmax semantics).
+int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hipStream_t s);
+// Greedy-search step (GenerationMixin._sample, do_sample=False): next = argmax(logits[b]);
+// finished rows emit pad; tokens[b*tok_ld + col] = next; unfinished[b] &= next != eos;
+// x[b, :] = table[next, :] (decoder input embedding of the next step, may be null).
+int greedy_step(const float* logits, int M, int V, int32_t* unfinished, int32_t* tokens,
+                int64_t tok_ld, int col, int eos, int pad, const float* table, int D, float* x,
+                hipStream_t s);
+
+// Generic device helpers.
+int fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s);
+int scale_inplace(float* p, int64_t n, float scale, hipStream_t s);
+
+// Retrieval scan (scan.hip).
+int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
+              int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
+              float* out_dist, int64_t* out_ids, hipStream_t s);
+size_t scan_topk_workspace(int64_t n, int b, int k);
+int scan_scores(const float* X, const float* xnorm, int64_t n, int d, int metric, const float* Q,
+                int b, float* out, hipStream_t s);
+int row_sqnorms(const float* X, int64_t n, int d, float* out, hipStream_t s);
+int topk_merge(const float* cand_d, const int64_t* cand_i, int b, int64_t n_cand, int k,
+               int metric, float* out_d, int64_t* out_i, hipStream_t s);
+int cosine_rows(const float* x1, const float* x2, int64_t m, int d, float eps, float* out,
+                hipStream_t s);
+int cross_entropy(const float* logits, const int32_t* labels, int64_t n, int V, float* ws,
+                  float* out, hipStream_t s);
+
+}  // namespace mpr

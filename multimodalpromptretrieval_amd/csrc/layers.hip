@@ -1,0 +1,519 @@
+// layers.hip — normalisation, attention and data-movement kernels of the encoders.
+//
+// Row reductions (LayerNorm / T5 RMSNorm) run one 64-lane wave per row with __shfl_xor
+// butterflies; attention for the short sequences of this path (ViT 50 tokens, CLIP text <= 77,
+// T5 <= 562, decoder steps of 1 query) keeps a 64-key chunk of K and V of one (batch, head) in
+// LDS and runs an online softmax per query row, one key per lane.
+#include <cfloat>
+
+#include "kernels.h"
+
+namespace mpr {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// ---- LayerNorm / RMSNorm: one wave per row, row cached in registers (D <= 64*MAXV) ---------
+template <int MAXV>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t ldx, int M, int D,
+                                                        const float* g, const float* b, float eps,
+                                                        float* out, int64_t ldo) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + j * 64;
+    v[j] = c < D ? xr[c] : 0.f;
+    s += v[j];
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + j * 64;
+    const float d = c < D ? v[j] - mean : 0.f;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+  float* orow = out + (int64_t)row * ldo;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + j * 64;
+    if (c < D) orow[c] = (v[j] - mean) * rstd * g[c] + b[c];
+  }
+}
+
+template <int MAXV>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, int64_t ldx, int M, int D,
+                                                      const float* w, float eps, float* out,
+                                                      int64_t ldo) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + j * 64;
+    v[j] = c < D ? xr[c] : 0.f;
+    s += v[j] * v[j];
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(s) / (float)D + eps);
+  float* orow = out + (int64_t)row * ldo;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + j * 64;
+    if (c < D) orow[c] = w[c] * (v[j] * rstd);
+  }
+}
+
+// ---- attention -------------------------------------------------------------------------------
+constexpr int ATT_QR = 16;      // query rows per block (4 per wave)
+constexpr int ATT_KC = 64;      // keys per LDS chunk (one per lane)
+constexpr int ATT_D = 64;       // head dim
+
+__global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) float Ks[ATT_KC][ATT_D + 4];
+  __shared__ __attribute__((aligned(16))) float Vs[ATT_KC][ATT_D];
+  __shared__ __attribute__((aligned(16))) float Qs[ATT_QR][ATT_D];
+  __shared__ __attribute__((aligned(16))) float Ps[4][4][ATT_KC];
+
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * ATT_QR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {
+    const int r = tid >> 4, c4 = (tid & 15) * 4, i = q0 + r;
+    f32x4 qv = {0.f, 0.f, 0.f, 0.f};
+    if (i < a.Lq)
+      qv = *reinterpret_cast<const f32x4*>(a.q + (int64_t)b * a.q_bs + (int64_t)i * a.q_rs +
+                                            h * ATT_D + c4);
+    *reinterpret_cast<f32x4*>(&Qs[r][c4]) = qv;
+  }
+  float m[4], l[4], o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+    o[r] = 0.f;
+  }
+  const int row0 = q0 + wave * 4;
+  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
+  int lk_end = a.Lk;
+  if (a.causal) lk_end = min(lk_end, q0 + ATT_QR - 1 + a.q_pos0 + 1);
+
+  for (int kc = 0; kc < lk_end; kc += ATT_KC) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = tid + u * 256, r = idx >> 4, c4 = (idx & 15) * 4, j = kc + r;
+      f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+      if (j < a.Lk) {
+        kv = *reinterpret_cast<const f32x4*>(a.k + (int64_t)b * a.k_bs + (int64_t)j * a.k_rs +
+                                              h * ATT_D + c4);
+        vv = *reinterpret_cast<const f32x4*>(a.v + (int64_t)b * a.v_bs + (int64_t)j * a.v_rs +
+                                              h * ATT_D + c4);
+      }
+      *reinterpret_cast<f32x4*>(&Ks[r][c4]) = kv;
+      *reinterpret_cast<f32x4*>(&Vs[r][c4]) = vv;
+    }
+    __syncthreads();
+    if (row0 >= a.Lq) continue;  // wave-uniform; keeps participating in the barriers
+
+    const int j = kc + lane;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < ATT_D; d += 4) {
+      const f32x4 kv = *reinterpret_cast<const f32x4*>(&Ks[lane][d]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f32x4 qv = *reinterpret_cast<const f32x4*>(&Qs[wave * 4 + r][d]);
+        s[r] += qv[0] * kv[0] + qv[1] * kv[1] + qv[2] * kv[2] + qv[3] * kv[3];
+      }
+    }
+    bool kvalid = j < a.Lk;
+    if (maskb && kvalid) kvalid = maskb[j] != 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = row0 + r;
+      if (i >= a.Lq) break;  // wave-uniform
+      const int qpos = i + a.q_pos0;
+      bool valid = kvalid && (!a.causal || j <= qpos);
+      float sc = s[r] * a.scale;
+      if (a.rel_bias && valid) {
+        const int bucket = a.bucket_lut[j - qpos + a.lut_radius];
+        sc += a.rel_bias[bucket * a.H + h];
+      }
+      sc = valid ? sc : -INFINITY;
+      const float mnew = fmaxf(m[r], wave_max(sc));
+      float p = 0.f, alpha = 1.f;
+      if (mnew != -INFINITY) {
+        p = valid ? expf(sc - mnew) : 0.f;
+        alpha = m[r] == -INFINITY ? 0.f : expf(m[r] - mnew);
+        m[r] = mnew;
+      }
+      l[r] = l[r] * alpha + wave_sum(p);
+      o[r] *= alpha;
+      Ps[wave][r][lane] = p;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int kn = min(ATT_KC, a.Lk - kc);
+    for (int jj = 0; jj < kn; jj += 4) {
+      const float v0 = Vs[jj][lane], v1 = Vs[jj + 1][lane], v2 = Vs[jj + 2][lane],
+                  v3 = Vs[jj + 3][lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f32x4 p = *reinterpret_cast<const f32x4*>(&Ps[wave][r][jj]);
+        o[r] += p[0] * v0 + p[1] * v1 + p[2] * v2 + p[3] * v3;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = row0 + r;
+    if (i < a.Lq)
+      a.o[(int64_t)b * a.o_bs + (int64_t)i * a.o_rs + h * ATT_D + lane] = o[r] / l[r];
+  }
+}
+
+// ---- data movement ----------------------------------------------------------------------------
+__global__ void im2col_kernel(const float* img, int B, int S, int p, float* cols) {
+  // one thread per float4 of a patch row (kx contiguous)
+  const int g = S / p, g2 = g * g, P4 = 3 * p * p / 4;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * g2 * P4) return;
+  const int e4 = (int)(idx % P4);
+  const int64_t pr = idx / P4;
+  const int b = (int)(pr / g2), t = (int)(pr % g2), py = t / g, px = t % g;
+  const int e = e4 * 4, c = e / (p * p), rem = e % (p * p), ky = rem / p, kx = rem % p;
+  const float* src = img + (((int64_t)b * 3 + c) * S + (py * p + ky)) * S + px * p + kx;
+  *reinterpret_cast<f32x4*>(cols + pr * (3 * p * p) + e) = *reinterpret_cast<const f32x4*>(src);
+}
+
+__global__ void vit_assemble_kernel(const float* patches, const float* cls, const float* pos,
+                                    int B, int g2, int W, float* x) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int T = g2 + 1;
+  if (idx >= (int64_t)B * T * W) return;
+  const int c = (int)(idx % W);
+  const int64_t bt = idx / W;
+  const int t = (int)(bt % T), b = (int)(bt / T);
+  const float base = t == 0 ? cls[c] : patches[((int64_t)b * g2 + t - 1) * W + c];
+  x[idx] = base + pos[(int64_t)t * W + c];
+}
+
+__global__ void embed_gather_kernel(const float* table, const int32_t* ids, int64_t ids_bs, int B,
+                                    int len, int D, const float* pos, float* out, int64_t obs,
+                                    int row0) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * len * D) return;
+  const int c = (int)(idx % D);
+  const int64_t bt = idx / D;
+  const int t = (int)(bt % len), b = (int)(bt / len);
+  float v = table[(int64_t)ids[(int64_t)b * ids_bs + t] * D + c];
+  if (pos) v = v + pos[(int64_t)t * D + c];
+  out[(int64_t)b * obs + (int64_t)(row0 + t) * D + c] = v;
+}
+
+__global__ void eot_gather_kernel(const float* x, const int32_t* tok, int L, int ctx, int D,
+                                  float* out) {
+  const int b = blockIdx.x;
+  __shared__ int e_s;
+  if (threadIdx.x == 0) {
+    int best = tok[(int64_t)b * ctx], e = 0;
+    for (int t = 1; t < ctx; ++t) {
+      const int v = tok[(int64_t)b * ctx + t];
+      if (v > best) {
+        best = v;
+        e = t;
+      }
+    }
+    e_s = e < L ? e : L - 1;
+  }
+  __syncthreads();
+  const float* src = x + ((int64_t)b * L + e_s) * D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) out[(int64_t)b * D + c] = src[c];
+}
+
+__global__ __launch_bounds__(256) void argmax_rows_kernel(const float* logits, int V, int64_t ld,
+                                                          int32_t* out) {
+  const int row = blockIdx.x;
+  const float* x = logits + (int64_t)row * ld;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    const float v = x[c];
+    if (v > best || (v == best && c < bi)) {
+      best = v;
+      bi = c;
+    }
+  }
+  __shared__ float bv[256];
+  __shared__ int bix[256];
+  bv[threadIdx.x] = best;
+  bix[threadIdx.x] = bi;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const float ov = bv[threadIdx.x + s];
+      const int oi = bix[threadIdx.x + s];
+      if (ov > bv[threadIdx.x] || (ov == bv[threadIdx.x] && oi < bix[threadIdx.x])) {
+        bv[threadIdx.x] = ov;
+        bix[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[row] = bix[0] == 0x7fffffff ? 0 : bix[0];
+}
+
+// One block per row: argmax over the vocabulary, then the greedy-search bookkeeping and the
+// embedding gather of the chosen token for the next decoder step.
+__global__ __launch_bounds__(256) void greedy_step_kernel(const float* logits, int V,
+                                                          int32_t* unfinished, int32_t* tokens,
+                                                          int64_t tok_ld, int col, int eos,
+                                                          int pad, const float* table, int D,
+                                                          float* x) {
+  const int row = blockIdx.x;
+  const float* lg = logits + (int64_t)row * V;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    const float v = lg[c];
+    if (v > best || (v == best && c < bi)) {
+      best = v;
+      bi = c;
+    }
+  }
+  __shared__ float bv[256];
+  __shared__ int bix[256];
+  __shared__ int next_s;
+  bv[threadIdx.x] = best;
+  bix[threadIdx.x] = bi;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const float ov = bv[threadIdx.x + s];
+      const int oi = bix[threadIdx.x + s];
+      if (ov > bv[threadIdx.x] || (ov == bv[threadIdx.x] && oi < bix[threadIdx.x])) {
+        bv[threadIdx.x] = ov;
+        bix[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int next = bix[0] == 0x7fffffff ? 0 : bix[0];
+    const int unf = unfinished[row];
+    next = unf ? next : pad;
+    tokens[(int64_t)row * tok_ld + col] = next;
+    unfinished[row] = (unf && next != eos) ? 1 : 0;
+    next_s = next;
+  }
+  __syncthreads();
+  if (x) {
+    const float* src = table + (int64_t)next_s * D;
+    for (int c = threadIdx.x; c < D; c += 256) x[(int64_t)row * D + c] = src[c];
+  }
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int32_t v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void scale_kernel(float* p, int64_t n, float sc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = p[i] * sc;
+}
+
+// Cross entropy, stage 1: per-row loss (logsumexp - logit[label]) and validity.
+__global__ __launch_bounds__(256) void ce_rows_kernel(const float* logits, const int32_t* labels,
+                                                      int V, float* loss, float* valid) {
+  const int row = blockIdx.x;
+  const int lab = labels[row];
+  const float* x = logits + (int64_t)row * V;
+  float mx = -INFINITY;
+  for (int c = threadIdx.x; c < V; c += 256) mx = fmaxf(mx, x[c]);
+  __shared__ float red[4];
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int c = threadIdx.x; c < V; c += 256) s += expf(x[c] - mx);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tot = red[0] + red[1] + red[2] + red[3];
+    const bool ok = lab >= 0 && lab < V;
+    loss[row] = ok ? (logf(tot) + mx - x[lab]) : 0.f;
+    valid[row] = ok ? 1.f : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_reduce_kernel(const float* loss, const float* valid,
+                                                        int64_t n, float* out) {
+  float s = 0.f, c = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    s += loss[i];
+    c += valid[i];
+  }
+  __shared__ float rs[4], rc[4];
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) {
+    rs[threadIdx.x >> 6] = s;
+    rc[threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float ts = rs[0] + rs[1] + rs[2] + rs[3], tc = rc[0] + rc[1] + rc[2] + rc[3];
+    out[0] = ts / tc;  // NaN when every label is ignored, as torch
+  }
+}
+
+}  // namespace
+
+int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, const float* beta,
+              float eps, float* out, int64_t ldo, hipStream_t s) {
+  MPR_REQUIRE(D > 0 && D <= 1024, "layernorm: D=%d unsupported", D);
+  if (M <= 0) return MPR_OK;
+  dim3 grid((unsigned)cdiv(M, 4));
+  if (D <= 512)
+    hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, M, D, gamma, beta, eps,
+                       out, ldo);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<16>, grid, dim3(256), 0, s, x, ldx, M, D, gamma, beta,
+                       eps, out, ldo);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int rmsnorm(const float* x, int64_t ldx, int M, int D, const float* w, float eps, float* out,
+            int64_t ldo, hipStream_t s) {
+  MPR_REQUIRE(D > 0 && D <= 1024, "rmsnorm: D=%d unsupported", D);
+  if (M <= 0) return MPR_OK;
+  dim3 grid((unsigned)cdiv(M, 4));
+  if (D <= 512)
+    hipLaunchKernelGGL(rmsnorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, M, D, w, eps, out, ldo);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel<16>, grid, dim3(256), 0, s, x, ldx, M, D, w, eps, out, ldo);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int attention(const AttnArgs& a, hipStream_t s) {
+  MPR_REQUIRE(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attention: bad shape");
+  if (a.B == 0 || a.Lq == 0) return MPR_OK;
+  MPR_REQUIRE(!a.rel_bias || a.bucket_lut, "attention: rel_bias needs a bucket lut");
+  if (a.rel_bias)
+    MPR_REQUIRE(a.lut_radius >= a.Lk + a.Lq + a.q_pos0, "attention: bucket lut radius %d too small",
+                a.lut_radius);
+  dim3 grid((unsigned)cdiv(a.Lq, ATT_QR), (unsigned)a.H, (unsigned)a.B);
+  hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, a);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int im2col_patches(const float* img, int B, int S, int p, float* cols, hipStream_t s) {
+  MPR_REQUIRE(S % p == 0 && p % 4 == 0, "im2col: S=%d p=%d", S, p);
+  const int g = S / p;
+  const int64_t n = (int64_t)B * g * g * (3 * p * p / 4);
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, img, B, S, p,
+                     cols);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int vit_assemble(const float* patches, const float* cls, const float* pos, int B, int g2, int W,
+                 float* x, hipStream_t s) {
+  const int64_t n = (int64_t)B * (g2 + 1) * W;
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(vit_assemble_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, patches,
+                     cls, pos, B, g2, W, x);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int embed_gather(const float* table, const int32_t* ids, int64_t ids_bs, int B, int len, int D,
+                 const float* pos, float* out, int64_t obs, int row0, hipStream_t s) {
+  const int64_t n = (int64_t)B * len * D;
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(embed_gather_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, table,
+                     ids, ids_bs, B, len, D, pos, out, obs, row0);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int eot_gather(const float* x, const int32_t* tok, int B, int L, int ctx, int D, float* out,
+               hipStream_t s) {
+  if (B == 0) return MPR_OK;
+  hipLaunchKernelGGL(eot_gather_kernel, dim3(B), dim3(256), 0, s, x, tok, L, ctx, D, out);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hipStream_t s) {
+  if (M == 0) return MPR_OK;
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(M), dim3(256), 0, s, logits, V, ld, out);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int greedy_step(const float* logits, int M, int V, int32_t* unfinished, int32_t* tokens,
+                int64_t tok_ld, int col, int eos, int pad, const float* table, int D, float* x,
+                hipStream_t s) {
+  if (M == 0) return MPR_OK;
+  hipLaunchKernelGGL(greedy_step_kernel, dim3(M), dim3(256), 0, s, logits, V, unfinished, tokens,
+                     tok_ld, col, eos, pad, table, D, x);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int scale_inplace(float* p, int64_t n, float sc, hipStream_t s) {
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(scale_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, p, n, sc);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s) {
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, p, v, n);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int cross_entropy(const float* logits, const int32_t* labels, int64_t n, int V, float* ws,
+                  float* out, hipStream_t s) {
+  MPR_REQUIRE(n > 0 && V > 0, "cross_entropy: bad shape");
+  hipLaunchKernelGGL(ce_rows_kernel, dim3((unsigned)n), dim3(256), 0, s, logits, labels, V, ws,
+                     ws + n);
+  MPR_LAUNCHED();
+  hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, s, ws, ws + n, n, out);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+}  // namespace mpr

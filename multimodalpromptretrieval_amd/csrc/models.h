@@ -1,0 +1,88 @@
+// models.h — device-resident model handles behind the opaque mpr_model of the C ABI.
+#pragma once
+
+#include <map>
+#include <memory>
+#include <tuple>
+
+#include "kernels.h"
+
+struct mpr_model {
+  enum Kind { VIT = 1, CLIP_TEXT = 2, T5 = 3 };
+  explicit mpr_model(int k) : kind(k) {}
+  virtual ~mpr_model() = default;
+  int kind;
+};
+
+struct mpr_index {
+  mpr::DevBuf rows;   // [n, d] fp32
+  mpr::DevBuf norms;  // [n] squared L2 norms
+  mpr::DevBuf ws;     // search workspace
+  int64_t n = 0;
+  int d = 0;
+  int metric = 0;
+  int64_t row_offset = 0;
+};
+
+namespace mpr {
+
+// One pre-LN residual attention block of the CLIP transformers (openai CLIP ResidualAttentionBlock).
+struct ClipBlock {
+  DevBuf ln1_w, ln1_b, in_w, in_b, out_w, out_b, ln2_w, ln2_b, fc_w, fc_b, pj_w, pj_b;
+};
+
+struct ClipTower {
+  int width = 0, layers = 0, heads = 0;
+  std::vector<std::unique_ptr<ClipBlock>> blocks;
+  // workspace
+  DevBuf h, qkv, ao, mlp;
+  int load_blocks(const float* const* t, int width, int layers);
+  // x [B*L, width] in place; causal for the text tower.
+  int run(float* x, int B, int L, bool causal, hipStream_t s);
+};
+
+struct VitModel : mpr_model {
+  VitModel() : mpr_model(VIT) {}
+  int width = 0, patch = 0, image = 0, out_dim = 0, grid = 0;
+  DevBuf conv_w, cls, pos, lnpre_w, lnpre_b, lnpost_w, lnpost_b, projT;
+  ClipTower tower;
+  DevBuf cols, patches, x, tmp;
+  int forward(const float* img, int B, int mode, float* out, int64_t out_bs, hipStream_t s);
+};
+
+struct TextModel : mpr_model {
+  TextModel() : mpr_model(CLIP_TEXT) {}
+  int width = 0, ctx = 0, vocab = 0, out_dim = 0;
+  DevBuf tok_emb, pos, lnf_w, lnf_b, projT;
+  ClipTower tower;
+  DevBuf x, pooled;
+  int forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs, hipStream_t s);
+};
+
+struct T5Layer {
+  DevBuf ln0, qkv, o, ln1, wi, wo;         // encoder layer / decoder self-attn + ffn
+  DevBuf cq, co, ln2;                      // decoder only: cross-attn q/o, ffn norm
+};
+
+struct T5Model : mpr_model {
+  T5Model() : mpr_model(T5) {}
+  int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
+  int inner = 0, lut_radius = 0;
+  DevBuf shared, enc_rel, dec_rel, enc_final, dec_final, lm_head, cross_kv_w, enc_lut, dec_lut;
+  std::vector<std::unique_ptr<T5Layer>> enc, dec;
+  // workspace
+  DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, logits, unfinished, cur_tok, cew;
+
+  int encode(const float* embeds, const float* mask, int B, int L, float* out, hipStream_t s);
+  int generate(const float* embeds, const float* mask, int B, int L, int max_new, int start,
+               int eos, int pad, int32_t* out_tokens, hipStream_t s);
+  int logits_tf(const float* embeds, const float* mask, int B, int L, const int32_t* dec_in,
+                int T, float* logits_out, hipStream_t s);
+  int embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
+            hipStream_t s);
+
+ private:
+  int cross_kv_project(int B, int L, hipStream_t s);
+};
+
+}  // namespace mpr

@@ -1,0 +1,269 @@
+// t5.hip — T5 encoder, greedy decoder and teacher-forced logits on the gfx950 kernels.
+//
+// Reference semantics: transformers T5ForConditionalGeneration as driven by
+// architectures/T5VisionModel.py:200-205 (generate(inputs_embeds, attention_mask, do_sample=False,
+// max_new_tokens=20)) and :233 (teacher-forced loss):
+//   T5LayerNorm = RMSNorm (no mean, no bias, eps 1e-6);  attention without 1/sqrt(d) scaling,
+//   relative position bias from layer 0 (bidirectional buckets in the encoder, causal in the
+//   decoder) shared by every layer, padding mask on encoder keys; ReLU FFN; final RMSNorm, then
+//   * d_model^-0.5 before the tied lm_head (scale_decoder_outputs).
+// Decoder steps run M = batch rows: every projection is a skinny GEMM with the preceding RMSNorm
+// fused into its operand load; K/V of the self-attention live in a per-layer cache laid out
+// [B][max_new][3*inner] (the fused q|k|v row of each generated position), and the cross-attention
+// K/V of every decoder layer are projected once from the encoder output by one GEMM.
+#include "models.h"
+
+namespace mpr {
+
+namespace {
+constexpr float T5_EPS = 1e-6f;
+}
+
+int T5Model::embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
+                   hipStream_t s) {
+  return embed_gather(shared.as<float>(), ids, len, B, len, d, nullptr, out, out_bs, row0, s);
+}
+
+int T5Model::encode(const float* embeds, const float* mask, int B, int L, float* out,
+                    hipStream_t s) {
+  MPR_REQUIRE(L >= 1, "t5 encode: L=%d", L);
+  MPR_REQUIRE(2 * L <= lut_radius, "t5 encode: L=%d exceeds the bucket lut radius %d", L,
+              lut_radius);
+  if (B == 0) return MPR_OK;
+  const int M = B * L;
+  MPR_TRY(x.ensure((size_t)M * d * 4));
+  MPR_TRY(h.ensure((size_t)M * d * 4));
+  MPR_TRY(qkv.ensure((size_t)M * 3 * inner * 4));
+  MPR_TRY(ao.ensure((size_t)M * inner * 4));
+  MPR_TRY(ff.ensure((size_t)M * dff * 4));
+  float* xp = x.as<float>();
+  float* hp = h.as<float>();
+  float* qp = qkv.as<float>();
+  float* ap = ao.as<float>();
+  float* fp = ff.as<float>();
+  MPR_HIP(hipMemcpyAsync(xp, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
+  for (auto& lp : enc) {
+    const T5Layer& ly = *lp;
+    MPR_TRY(rmsnorm(xp, d, M, d, ly.ln0.as<float>(), T5_EPS, hp, d, s));
+    GemmArgs g;
+    g.A = hp; g.lda = d; g.W = ly.qkv.as<float>(); g.ldw = d; g.C = qp; g.ldc = 3 * inner;
+    g.M = M; g.N = 3 * inner; g.K = d;
+    MPR_TRY(gemm(g, s));
+    AttnArgs at;
+    at.q = qp; at.q_bs = (int64_t)L * 3 * inner; at.q_rs = 3 * inner;
+    at.k = qp + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
+    at.v = qp + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
+    at.o = ap; at.o_bs = (int64_t)L * inner; at.o_rs = inner;
+    at.B = B; at.H = H; at.Lq = L; at.Lk = L; at.scale = 1.f;
+    at.key_mask = mask; at.mask_bs = L;
+    at.rel_bias = enc_rel.as<float>(); at.bucket_lut = enc_lut.as<int>();
+    at.lut_radius = lut_radius;
+    MPR_TRY(attention(at, s));
+    GemmArgs o;
+    o.A = ap; o.lda = inner; o.W = ly.o.as<float>(); o.ldw = inner; o.R = xp; o.ldr = d;
+    o.C = xp; o.ldc = d; o.M = M; o.N = d; o.K = inner;
+    MPR_TRY(gemm(o, s));
+    MPR_TRY(rmsnorm(xp, d, M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
+    GemmArgs f;
+    f.A = hp; f.lda = d; f.W = ly.wi.as<float>(); f.ldw = d; f.C = fp; f.ldc = dff;
+    f.M = M; f.N = dff; f.K = d; f.act = ACT_RELU;
+    MPR_TRY(gemm(f, s));
+    GemmArgs w;
+    w.A = fp; w.lda = dff; w.W = ly.wo.as<float>(); w.ldw = dff; w.R = xp; w.ldr = d;
+    w.C = xp; w.ldc = d; w.M = M; w.N = d; w.K = dff;
+    MPR_TRY(gemm(w, s));
+  }
+  MPR_TRY(rmsnorm(xp, d, M, d, enc_final.as<float>(), T5_EPS, out, d, s));
+  return MPR_OK;
+}
+
+int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
+  const int M = B * L, N = Ld * 2 * inner;
+  MPR_TRY(cross_kv.ensure((size_t)M * N * 4));
+  GemmArgs g;
+  g.A = enc_out.as<float>(); g.lda = d; g.W = cross_kv_w.as<float>(); g.ldw = d;
+  g.C = cross_kv.as<float>(); g.ldc = N; g.M = M; g.N = N; g.K = d;
+  return gemm(g, s);
+}
+
+int T5Model::generate(const float* embeds, const float* mask, int B, int L, int max_new,
+                      int start, int eos, int pad, int32_t* out_tokens, hipStream_t s) {
+  MPR_REQUIRE(B >= 0 && B <= 16, "t5 generate: batch %d > 16 unsupported by the decode path", B);
+  MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
+  MPR_REQUIRE(max_new + 1 <= lut_radius, "t5 generate: max_new exceeds lut radius");
+  if (B == 0) return MPR_OK;
+  const int T1 = max_new + 1;
+  MPR_TRY(enc_out.ensure((size_t)B * L * d * 4));
+  MPR_TRY(encode(embeds, mask, B, L, enc_out.as<float>(), s));
+  MPR_TRY(cross_kv_project(B, L, s));
+  const int Tc = max_new > 0 ? max_new : 1;
+  const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
+  MPR_TRY(cache.ensure((size_t)Ld * cache_layer * 4));
+  MPR_TRY(dx.ensure((size_t)B * d * 4));
+  MPR_TRY(dq.ensure((size_t)B * inner * 4));
+  MPR_TRY(ao.ensure((size_t)B * inner * 4));
+  MPR_TRY(ff.ensure((size_t)B * dff * 4));
+  MPR_TRY(logits.ensure((size_t)B * V * 4));
+  MPR_TRY(unfinished.ensure((size_t)B * 4));
+  MPR_TRY(cur_tok.ensure((size_t)B * 4));
+  float* xp = dx.as<float>();
+  float* qp = dq.as<float>();
+  float* ap = ao.as<float>();
+  float* fp = ff.as<float>();
+  float* lg = logits.as<float>();
+  int32_t* unf = unfinished.as<int32_t>();
+  int32_t* ct = cur_tok.as<int32_t>();
+  const float* ckv = cross_kv.as<float>();
+  const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
+
+  MPR_TRY(fill_i32(unf, 1, B, s));
+  MPR_TRY(fill_i32(ct, start, B, s));
+  // tokens[:, 0] = decoder_start
+  MPR_TRY(embed_gather(shared.as<float>(), ct, 1, B, 1, d, nullptr, xp, d, 0, s));
+  {
+    // column 0 of the output
+    MPR_HIP(hipMemcpy2DAsync(out_tokens, (size_t)T1 * 4, ct, 4, 4, B, hipMemcpyDeviceToDevice, s));
+  }
+  const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
+  for (int t = 0; t < max_new; ++t) {
+    for (int l = 0; l < Ld; ++l) {
+      const T5Layer& ly = *dec[l];
+      float* cl = cache.as<float>() + l * cache_layer;
+      SkinnyArgs sq;
+      sq.g.A = xp; sq.g.lda = d; sq.g.W = ly.qkv.as<float>(); sq.g.ldw = d;
+      sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
+      sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
+      MPR_TRY(gemm_skinny(sq, s));
+      AttnArgs at;
+      at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
+      at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
+      at.v = cl + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
+      at.o = ap; at.o_bs = inner; at.o_rs = inner;
+      at.B = B; at.H = H; at.Lq = 1; at.Lk = t + 1; at.scale = 1.f; at.causal = 1; at.q_pos0 = t;
+      at.rel_bias = dec_rel.as<float>(); at.bucket_lut = dec_lut.as<int>();
+      at.lut_radius = lut_radius;
+      MPR_TRY(attention(at, s));
+      SkinnyArgs so;
+      so.g.A = ap; so.g.lda = inner; so.g.W = ly.o.as<float>(); so.g.ldw = inner; so.g.R = xp;
+      so.g.ldr = d; so.g.C = xp; so.g.ldc = d; so.g.M = B; so.g.N = d; so.g.K = inner;
+      MPR_TRY(gemm_skinny(so, s));
+      SkinnyArgs cq;
+      cq.g.A = xp; cq.g.lda = d; cq.g.W = ly.cq.as<float>(); cq.g.ldw = d; cq.g.C = qp;
+      cq.g.ldc = inner; cq.g.M = B; cq.g.N = inner; cq.g.K = d; cq.rms_w = ly.ln1.as<float>();
+      cq.rms_eps = T5_EPS;
+      MPR_TRY(gemm_skinny(cq, s));
+      AttnArgs ca;
+      ca.q = qp; ca.q_bs = inner; ca.q_rs = inner;
+      ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
+      ca.v = ckv + (int64_t)l * 2 * inner + inner; ca.v_bs = ca.k_bs; ca.v_rs = ckv_ld;
+      ca.o = ap; ca.o_bs = inner; ca.o_rs = inner;
+      ca.B = B; ca.H = H; ca.Lq = 1; ca.Lk = L; ca.scale = 1.f;
+      ca.key_mask = mask; ca.mask_bs = L;
+      MPR_TRY(attention(ca, s));
+      SkinnyArgs co;
+      co.g.A = ap; co.g.lda = inner; co.g.W = ly.co.as<float>(); co.g.ldw = inner; co.g.R = xp;
+      co.g.ldr = d; co.g.C = xp; co.g.ldc = d; co.g.M = B; co.g.N = d; co.g.K = inner;
+      MPR_TRY(gemm_skinny(co, s));
+      SkinnyArgs fi;
+      fi.g.A = xp; fi.g.lda = d; fi.g.W = ly.wi.as<float>(); fi.g.ldw = d; fi.g.C = fp;
+      fi.g.ldc = dff; fi.g.M = B; fi.g.N = dff; fi.g.K = d; fi.g.act = ACT_RELU;
+      fi.rms_w = ly.ln2.as<float>(); fi.rms_eps = T5_EPS;
+      MPR_TRY(gemm_skinny(fi, s));
+      SkinnyArgs fo;
+      fo.g.A = fp; fo.g.lda = dff; fo.g.W = ly.wo.as<float>(); fo.g.ldw = dff; fo.g.R = xp;
+      fo.g.ldr = d; fo.g.C = xp; fo.g.ldc = d; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
+      MPR_TRY(gemm_skinny(fo, s));
+    }
+    SkinnyArgs hd;
+    hd.g.A = xp; hd.g.lda = d; hd.g.W = lm_head.as<float>(); hd.g.ldw = d; hd.g.C = lg;
+    hd.g.ldc = V; hd.g.M = B; hd.g.N = V; hd.g.K = d; hd.rms_w = dec_final.as<float>();
+    hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
+    MPR_TRY(gemm_skinny(hd, s));
+    MPR_TRY(greedy_step(lg, B, V, unf, out_tokens, T1, t + 1, eos, pad, shared.as<float>(), d,
+                        t + 1 < max_new ? xp : nullptr, s));
+  }
+  return MPR_OK;
+}
+
+int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
+                       const int32_t* dec_in, int T, float* logits_out, hipStream_t s) {
+  MPR_REQUIRE(T >= 1 && T <= lut_radius, "t5 logits: T=%d", T);
+  if (B == 0) return MPR_OK;
+  MPR_TRY(enc_out.ensure((size_t)B * L * d * 4));
+  MPR_TRY(encode(embeds, mask, B, L, enc_out.as<float>(), s));
+  MPR_TRY(cross_kv_project(B, L, s));
+  const int M = B * T;
+  MPR_TRY(x.ensure((size_t)M * d * 4));
+  MPR_TRY(h.ensure((size_t)M * d * 4));
+  MPR_TRY(qkv.ensure((size_t)M * 3 * inner * 4));
+  MPR_TRY(ao.ensure((size_t)M * inner * 4));
+  MPR_TRY(dq.ensure((size_t)M * inner * 4));
+  MPR_TRY(ff.ensure((size_t)M * dff * 4));
+  float* xp = x.as<float>();
+  float* hp = h.as<float>();
+  float* qp = qkv.as<float>();
+  float* ap = ao.as<float>();
+  float* cqp = dq.as<float>();
+  float* fp = ff.as<float>();
+  const float* ckv = cross_kv.as<float>();
+  const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
+  MPR_TRY(embed_gather(shared.as<float>(), dec_in, T, B, T, d, nullptr, xp, (int64_t)T * d, 0, s));
+  for (int l = 0; l < Ld; ++l) {
+    const T5Layer& ly = *dec[l];
+    MPR_TRY(rmsnorm(xp, d, M, d, ly.ln0.as<float>(), T5_EPS, hp, d, s));
+    GemmArgs g;
+    g.A = hp; g.lda = d; g.W = ly.qkv.as<float>(); g.ldw = d; g.C = qp; g.ldc = 3 * inner;
+    g.M = M; g.N = 3 * inner; g.K = d;
+    MPR_TRY(gemm(g, s));
+    AttnArgs at;
+    at.q = qp; at.q_bs = (int64_t)T * 3 * inner; at.q_rs = 3 * inner;
+    at.k = qp + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
+    at.v = qp + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
+    at.o = ap; at.o_bs = (int64_t)T * inner; at.o_rs = inner;
+    at.B = B; at.H = H; at.Lq = T; at.Lk = T; at.scale = 1.f; at.causal = 1;
+    at.rel_bias = dec_rel.as<float>(); at.bucket_lut = dec_lut.as<int>();
+    at.lut_radius = lut_radius;
+    MPR_TRY(attention(at, s));
+    GemmArgs o;
+    o.A = ap; o.lda = inner; o.W = ly.o.as<float>(); o.ldw = inner; o.R = xp; o.ldr = d;
+    o.C = xp; o.ldc = d; o.M = M; o.N = d; o.K = inner;
+    MPR_TRY(gemm(o, s));
+    MPR_TRY(rmsnorm(xp, d, M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
+    GemmArgs cq;
+    cq.A = hp; cq.lda = d; cq.W = ly.cq.as<float>(); cq.ldw = d; cq.C = cqp; cq.ldc = inner;
+    cq.M = M; cq.N = inner; cq.K = d;
+    MPR_TRY(gemm(cq, s));
+    AttnArgs ca;
+    ca.q = cqp; ca.q_bs = (int64_t)T * inner; ca.q_rs = inner;
+    ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
+    ca.v = ckv + (int64_t)l * 2 * inner + inner; ca.v_bs = ca.k_bs; ca.v_rs = ckv_ld;
+    ca.o = ap; ca.o_bs = (int64_t)T * inner; ca.o_rs = inner;
+    ca.B = B; ca.H = H; ca.Lq = T; ca.Lk = L; ca.scale = 1.f;
+    ca.key_mask = mask; ca.mask_bs = L;
+    MPR_TRY(attention(ca, s));
+    GemmArgs co;
+    co.A = ap; co.lda = inner; co.W = ly.co.as<float>(); co.ldw = inner; co.R = xp; co.ldr = d;
+    co.C = xp; co.ldc = d; co.M = M; co.N = d; co.K = inner;
+    MPR_TRY(gemm(co, s));
+    MPR_TRY(rmsnorm(xp, d, M, d, ly.ln2.as<float>(), T5_EPS, hp, d, s));
+    GemmArgs f;
+    f.A = hp; f.lda = d; f.W = ly.wi.as<float>(); f.ldw = d; f.C = fp; f.ldc = dff;
+    f.M = M; f.N = dff; f.K = d; f.act = ACT_RELU;
+    MPR_TRY(gemm(f, s));
+    GemmArgs w;
+    w.A = fp; w.lda = dff; w.W = ly.wo.as<float>(); w.ldw = dff; w.R = xp; w.ldr = d;
+    w.C = xp; w.ldc = d; w.M = M; w.N = d; w.K = dff;
+    MPR_TRY(gemm(w, s));
+  }
+  // final norm * d^-0.5 -> tied head
+  MPR_TRY(rmsnorm(xp, d, M, d, dec_final.as<float>(), T5_EPS, hp, d, s));
+  // h *= d^-0.5 after the norm, the reference's op order (modeling_t5.py scale_decoder_outputs)
+  if (scale_out) MPR_TRY(scale_inplace(hp, (int64_t)M * d, 1.0f / sqrtf((float)d), s));
+  GemmArgs hd;
+  hd.A = hp; hd.lda = d; hd.W = lm_head.as<float>(); hd.ldw = d; hd.C = logits_out; hd.ldc = V;
+  hd.M = M; hd.N = V; hd.K = d;
+  MPR_TRY(gemm(hd, s));
+  return MPR_OK;
+}
+
+}  // namespace mpr

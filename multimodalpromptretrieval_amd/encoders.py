@@ -1,0 +1,149 @@
+"""Device CLIP encoders (ViT-B/32 image tower, text tower) backed by libmpr.so.
+
+Replace the openai CLIP calls of the reference:
+* ``clip_model.encode_image`` — dataset/VQAFeatureDataset.py:146,189 (mode "cls")
+* ``vision_model.visual`` monkey-patched to ``get_image_token_features`` —
+  architectures/T5VisionModel.py:46-48,112-139 (mode "tokens")
+* ``clip_model.encode_text(clip.tokenize(q))`` — dataset/VQAFeatureDataset.py:147,190
+Weights are openai-CLIP-named state-dict tensors; the library copies them into its own HBM
+layout at construction (re-create the encoder to pick up new weights).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+CLS, TOKENS = 0, 1
+
+
+def _block_tensors(sd: dict, prefix: str, layers: int) -> list:
+    out = []
+    for i in range(layers):
+        p = f"{prefix}.resblocks.{i}"
+        out += [sd[p + ".ln_1.weight"], sd[p + ".ln_1.bias"], sd[p + ".attn.in_proj_weight"],
+                sd[p + ".attn.in_proj_bias"], sd[p + ".attn.out_proj.weight"],
+                sd[p + ".attn.out_proj.bias"], sd[p + ".ln_2.weight"], sd[p + ".ln_2.bias"],
+                sd[p + ".mlp.c_fc.weight"], sd[p + ".mlp.c_fc.bias"],
+                sd[p + ".mlp.c_proj.weight"], sd[p + ".mlp.c_proj.bias"]]
+    return out
+
+
+def _count_layers(sd: dict, prefix: str) -> int:
+    n = 0
+    while f"{prefix}.resblocks.{n}.ln_1.weight" in sd:
+        n += 1
+    return n
+
+
+def _host_f32(ts: list) -> list:
+    return [t.detach().to("cpu", torch.float32).contiguous() for t in ts]
+
+
+class _Handle:
+    def __init__(self):
+        self._h = None
+
+    def close(self):
+        if self._h is not None and _lib._lib is not None:
+            _lib.load().mpr_model_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceViT(_Handle):
+    """CLIP VisionTransformer (openai naming, prefix ``visual.``) on one GPU."""
+
+    def __init__(self, sd: dict, device, prefix: str = "visual."):
+        super().__init__()
+        _lib.ensure_device(device)
+        self.device = torch.device(device)
+        g = lambda k: sd[prefix + k]  # noqa: E731
+        conv = g("conv1.weight")
+        self.width, self.patch = conv.shape[0], conv.shape[-1]
+        pos = g("positional_embedding")
+        self.grid = int(round((pos.shape[0] - 1) ** 0.5))
+        self.image_size = self.grid * self.patch
+        self.layers = _count_layers(sd, prefix + "transformer")
+        self.out_dim = g("proj").shape[1]
+        self.tokens = self.grid * self.grid + 1
+        tensors = ([conv, g("class_embedding"), pos, g("ln_pre.weight"), g("ln_pre.bias")]
+                   + _block_tensors(sd, prefix + "transformer", self.layers)
+                   + [g("ln_post.weight"), g("ln_post.bias"), g("proj")])
+        host = _host_f32(tensors)
+        cfg = [self.width, self.layers, self.width // 64, self.patch, self.image_size,
+               self.out_dim]
+        h = _lib.ctypes.c_void_p()
+        _lib.call("mpr_vit_create", _lib.int_array(cfg), len(cfg), _lib.tensor_array(host),
+                  len(host), _lib.ctypes.byref(h))
+        self._h = h
+
+    def forward(self, img: torch.Tensor, mode: int = CLS, out: torch.Tensor = None,
+                out_bstride: int = None) -> torch.Tensor:
+        img = img.to(self.device, torch.float32, non_blocking=True).contiguous()
+        B = img.shape[0]
+        if tuple(img.shape[1:]) != (3, self.image_size, self.image_size):
+            raise ValueError(f"expected images [B,3,{self.image_size},{self.image_size}], "
+                             f"got {tuple(img.shape)}")
+        if out is None:
+            shape = (B, self.out_dim) if mode == CLS else (B, self.tokens, self.out_dim)
+            out = torch.empty(shape, device=self.device, dtype=torch.float32)
+            out_bstride = self.out_dim if mode == CLS else self.tokens * self.out_dim
+        _lib.call("mpr_vit_forward", self._h, _lib.ptr(img), B, mode, _lib.ptr(out),
+                  int(out_bstride), _lib.stream_ptr(self.device))
+        return out
+
+    __call__ = forward
+
+
+class DeviceCLIPText(_Handle):
+    """CLIP text transformer (openai naming, no prefix) on one GPU."""
+
+    def __init__(self, sd: dict, device, prefix: str = ""):
+        super().__init__()
+        _lib.ensure_device(device)
+        self.device = torch.device(device)
+        g = lambda k: sd[prefix + k]  # noqa: E731
+        emb = g("token_embedding.weight")
+        self.vocab, self.width = emb.shape
+        self.context_length = g("positional_embedding").shape[0]
+        self.layers = _count_layers(sd, prefix + "transformer")
+        self.out_dim = g("text_projection").shape[1]
+        tensors = ([emb, g("positional_embedding")]
+                   + _block_tensors(sd, prefix + "transformer", self.layers)
+                   + [g("ln_final.weight"), g("ln_final.bias"), g("text_projection")])
+        host = _host_f32(tensors)
+        cfg = [self.width, self.layers, self.width // 64, self.context_length, self.vocab,
+               self.out_dim]
+        h = _lib.ctypes.c_void_p()
+        _lib.call("mpr_clip_text_create", _lib.int_array(cfg), len(cfg),
+                  _lib.tensor_array(host), len(host), _lib.ctypes.byref(h))
+        self._h = h
+
+    def forward(self, tokens: torch.Tensor, out: torch.Tensor = None,
+                out_bstride: int = None) -> torch.Tensor:
+        """tokens int [B, ctx] (host or device).  Runs only the leading positions up to the
+        last EOT of the batch (causal attention makes the pooled output independent of the
+        positions after each row's EOT)."""
+        if tokens.shape[1] != self.context_length:
+            raise ValueError(f"expected tokens [B,{self.context_length}], got "
+                             f"{tuple(tokens.shape)}")
+        B = tokens.shape[0]
+        if tokens.device.type == "cpu":
+            seq_len = int(tokens.argmax(dim=1).max()) + 1 if B else 1
+        else:
+            seq_len = self.context_length
+        tok = tokens.to(self.device, torch.int32, non_blocking=True).contiguous()
+        if out is None:
+            out = torch.empty((B, self.out_dim), device=self.device, dtype=torch.float32)
+            out_bstride = self.out_dim
+        _lib.call("mpr_clip_text_forward", self._h, _lib.ptr(tok), B, seq_len, _lib.ptr(out),
+                  int(out_bstride), _lib.stream_ptr(self.device))
+        return out
+
+    __call__ = forward

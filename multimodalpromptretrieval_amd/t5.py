@@ -1,0 +1,181 @@
+"""Device T5 (encoder, greedy generate, teacher-forced logits/loss) backed by libmpr.so.
+
+Replaces the transformers T5ForConditionalGeneration calls of the reference:
+``T5_model.shared(ids)`` (architectures/T5VisionModel.py:169), ``T5_model.generate(...)``
+(:200-205) and ``T5_model(inputs_embeds, attention_mask, labels).loss`` (:233).
+Weights are transformers-named state-dict tensors; relative-position bucket tables are computed
+here on the host with the exact float32 expression of T5Attention._relative_position_bucket and
+handed to the library once.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+LUT_RADIUS = 1024  # covers encoder lengths up to 512 and any decode length here
+
+
+def relative_position_bucket(rel: torch.Tensor, bidirectional: bool, num_buckets: int = 32,
+                             max_distance: int = 128) -> torch.Tensor:
+    """T5Attention._relative_position_bucket (host-side integer metadata)."""
+    buckets = torch.zeros_like(rel)
+    if bidirectional:
+        num_buckets //= 2
+        buckets += (rel > 0).to(torch.long) * num_buckets
+        rel = torch.abs(rel)
+    else:
+        rel = -torch.min(rel, torch.zeros_like(rel))
+    max_exact = num_buckets // 2
+    is_small = rel < max_exact
+    large = max_exact + (torch.log(rel.float() / max_exact) / math.log(max_distance / max_exact)
+                         * (num_buckets - max_exact)).to(torch.long)
+    large = torch.min(large, torch.full_like(large, num_buckets - 1))
+    return buckets + torch.where(is_small, rel, large)
+
+
+def _layers(sd: dict, stack: str) -> int:
+    n = 0
+    while f"{stack}.block.{n}.layer.0.layer_norm.weight" in sd:
+        n += 1
+    return n
+
+
+class DeviceT5:
+    """T5ForConditionalGeneration arithmetic on one GPU (handle into libmpr)."""
+
+    def __init__(self, sd: dict, device, scale_decoder_outputs: bool = True,
+                 max_distance: int = 128):
+        _lib.ensure_device(device)
+        self.device = torch.device(device)
+        self._h = None
+        shared = sd["shared.weight"]
+        self.vocab, self.d_model = shared.shape
+        q0 = sd["encoder.block.0.layer.0.SelfAttention.q.weight"]
+        rel = sd["encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"]
+        self.num_buckets, self.num_heads = rel.shape
+        self.inner = q0.shape[0]
+        self.d_kv = self.inner // self.num_heads
+        self.d_ff = sd["encoder.block.0.layer.1.DenseReluDense.wi.weight"].shape[0]
+        self.n_enc = _layers(sd, "encoder")
+        self.n_dec = _layers(sd, "decoder")
+        lm_head = sd.get("lm_head.weight", shared)
+        t = [shared, rel]
+        for i in range(self.n_enc):
+            p = f"encoder.block.{i}.layer"
+            t += [sd[p + ".0.layer_norm.weight"], sd[p + ".0.SelfAttention.q.weight"],
+                  sd[p + ".0.SelfAttention.k.weight"], sd[p + ".0.SelfAttention.v.weight"],
+                  sd[p + ".0.SelfAttention.o.weight"], sd[p + ".1.layer_norm.weight"],
+                  sd[p + ".1.DenseReluDense.wi.weight"], sd[p + ".1.DenseReluDense.wo.weight"]]
+        t += [sd["encoder.final_layer_norm.weight"],
+              sd["decoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"]]
+        for i in range(self.n_dec):
+            p = f"decoder.block.{i}.layer"
+            t += [sd[p + ".0.layer_norm.weight"], sd[p + ".0.SelfAttention.q.weight"],
+                  sd[p + ".0.SelfAttention.k.weight"], sd[p + ".0.SelfAttention.v.weight"],
+                  sd[p + ".0.SelfAttention.o.weight"], sd[p + ".1.layer_norm.weight"],
+                  sd[p + ".1.EncDecAttention.q.weight"], sd[p + ".1.EncDecAttention.k.weight"],
+                  sd[p + ".1.EncDecAttention.v.weight"], sd[p + ".1.EncDecAttention.o.weight"],
+                  sd[p + ".2.layer_norm.weight"], sd[p + ".2.DenseReluDense.wi.weight"],
+                  sd[p + ".2.DenseReluDense.wo.weight"]]
+        t += [sd["decoder.final_layer_norm.weight"], lm_head]
+        host = [x.detach().to("cpu", torch.float32).contiguous() for x in t]
+        rel_pos = torch.arange(-LUT_RADIUS, LUT_RADIUS + 1, dtype=torch.long)
+        enc_lut = relative_position_bucket(rel_pos, True, self.num_buckets, max_distance)
+        dec_lut = relative_position_bucket(rel_pos, False, self.num_buckets, max_distance)
+        cfg = [self.d_model, self.d_kv, self.num_heads, self.d_ff, self.n_enc, self.n_dec,
+               self.vocab, self.num_buckets, 1 if scale_decoder_outputs else 0]
+        h = _lib.ctypes.c_void_p()
+        _lib.call("mpr_t5_create", _lib.int_array(cfg), len(cfg), _lib.tensor_array(host),
+                  len(host), _lib.int_array(enc_lut.tolist()), _lib.int_array(dec_lut.tolist()),
+                  LUT_RADIUS, _lib.ctypes.byref(h))
+        self._h = h
+
+    def close(self):
+        if self._h is not None and _lib._lib is not None:
+            _lib.load().mpr_model_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return _lib.stream_ptr(self.device)
+
+    def embed(self, ids: torch.Tensor, out: torch.Tensor, row0: int = 0) -> torch.Tensor:
+        """out[b, row0 + t, :] = shared[ids[b, t]] (out: [B, L, d] fp32 on device)."""
+        ids32 = ids.to(self.device, torch.int32, non_blocking=True).contiguous()
+        B, n = ids32.shape
+        _lib.call("mpr_t5_embed", self._h, _lib.ptr(ids32), B, n, _lib.ptr(out),
+                  out.shape[1] * out.shape[2], row0, self._stream())
+        return out
+
+    def _inputs(self, embeds, mask):
+        embeds = embeds.to(self.device, torch.float32).contiguous()
+        mask = mask.to(self.device, torch.float32).contiguous()
+        if embeds.shape[-1] != self.d_model:
+            raise RuntimeError(f"inputs_embeds width {embeds.shape[-1]} != d_model "
+                               f"{self.d_model}")
+        if mask.shape != embeds.shape[:2]:
+            raise RuntimeError(f"attention_mask {tuple(mask.shape)} != {tuple(embeds.shape[:2])}")
+        return embeds, mask
+
+    def encode(self, embeds: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        embeds, mask = self._inputs(embeds, mask)
+        B, L, _ = embeds.shape
+        out = torch.empty_like(embeds)
+        _lib.call("mpr_t5_encode", self._h, _lib.ptr(embeds), _lib.ptr(mask), B, L,
+                  _lib.ptr(out), self._stream())
+        return out
+
+    def generate_padded(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
+                        eos_token_id=1, pad_token_id=0) -> torch.Tensor:
+        """All max_new_tokens greedy steps on device: int32 [B, 1+max_new] (no host sync)."""
+        embeds, mask = self._inputs(embeds, mask)
+        B, L, _ = embeds.shape
+        out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
+        _lib.call("mpr_t5_generate", self._h, _lib.ptr(embeds), _lib.ptr(mask), B, L,
+                  int(max_new_tokens), int(decoder_start_token_id), int(eos_token_id),
+                  int(pad_token_id), _lib.ptr(out), self._stream())
+        return out
+
+    @staticmethod
+    def trim(tokens: torch.Tensor, eos_token_id: int = 1) -> torch.Tensor:
+        """Cut the padded token matrix where GenerationMixin stops (all rows finished)."""
+        tok = tokens.cpu().long()
+        T = tok.shape[1] - 1
+        hit = (tok[:, 1:] == eos_token_id)
+        if T == 0 or not bool(hit.any(dim=1).all()):
+            return tok
+        first = hit.float().argmax(dim=1) + 1        # column of each row's first eos
+        return tok[:, :int(first.max()) + 1]
+
+    def generate(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
+                 eos_token_id=1, pad_token_id=0) -> torch.Tensor:
+        """GenerationMixin.generate(do_sample=False) result (int64, host, trimmed)."""
+        toks = self.generate_padded(embeds, mask, max_new_tokens, decoder_start_token_id,
+                                    eos_token_id, pad_token_id)
+        return self.trim(toks, eos_token_id)
+
+    def logits(self, embeds, mask, decoder_input_ids) -> torch.Tensor:
+        embeds, mask = self._inputs(embeds, mask)
+        B, L, _ = embeds.shape
+        dec = decoder_input_ids.to(self.device, torch.int32).contiguous()
+        T = dec.shape[1]
+        out = torch.empty((B, T, self.vocab), device=self.device, dtype=torch.float32)
+        _lib.call("mpr_t5_logits", self._h, _lib.ptr(embeds), _lib.ptr(mask), B, L,
+                  _lib.ptr(dec), T, _lib.ptr(out), self._stream())
+        return out
+
+    def loss(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        lab = labels.to(self.device, torch.int32).contiguous()
+        lg = logits.contiguous()
+        out = torch.empty((), device=self.device, dtype=torch.float32)
+        _lib.call("mpr_cross_entropy", _lib.ptr(lg), _lib.ptr(lab), lab.numel(),
+                  lg.shape[-1], _lib.ptr(out), self._stream())
+        return out

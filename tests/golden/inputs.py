@@ -1,0 +1,101 @@
+"""Seed-derived inputs of the golden fixtures (shared by make_goldens.py and the tests).
+
+Nothing here imports the reference; the GPU box regenerates every input from these seeds.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from multimodalpromptretrieval_amd import synthetic as syn
+
+# ---- G1: retrieval scan -------------------------------------------------------------------
+G1_CASES = [(512, 512), (6500, 1024)]
+G1_K = [1, 3, 5, 15]
+G1_B = 16
+G1_ANS_VOCAB = 7
+TIE_DUPES = [17, 101, 250]
+TIE_SOURCE = 200
+TIE_QUERIES = [200, 5, 17, 101]
+
+
+def g1_seed(N, D):
+    return 100 + N + D
+
+
+def g1_queries(N, D, seed):
+    """Index [N, D] and 16 queries near index rows (self-matches for the training phase) at
+    increasing noise, so both exact self-hits and genuinely nearest-neighbour cases occur."""
+    X = syn.index_rows(seed, N, D)
+    rng = np.random.Generator(np.random.PCG64(seed + 1000))
+    rows = rng.choice(N, size=G1_B, replace=False)
+    noise = syn.index_rows(seed + 2000, G1_B, D)
+    scale = torch.tensor([0.0, 0.0, 0.0, 0.0, 0.01, 0.01, 0.05, 0.05, 0.1, 0.1, 0.3, 0.3,
+                          1.0, 1.0, 3.0, 3.0])[:, None]
+    q = X[rows] + noise * scale
+    return X, q, rows
+
+
+def question_info(N):
+    return {"question_id": [str(j) for j in range(N)],
+            "question_type": ["open" if j % 3 else "closed" for j in range(N)],
+            "question": [f"q{j}" for j in range(N)]}
+
+
+def tie_index():
+    g = np.random.Generator(np.random.PCG64(5))
+    X = torch.from_numpy(g.integers(-3, 4, size=(300, 64)).astype(np.float32))
+    X[TIE_DUPES] = X[TIE_SOURCE].clone()
+    return X, X[TIE_QUERIES].clone()
+
+
+# ---- G2: tiny end-to-end pipeline (reference T5VisionModel + retrieval) ------------------------
+G2 = {"clip_cfg": dict(width=128, layers=2, heads=2, patch=32, image_size=64, embed_dim=64,
+                       text_width=128, text_layers=2, text_heads=2),
+      "tok_cfg": dict(width=128, layers=2, heads=2, patch=32, image_size=64, embed_dim=128,
+                      text_width=128, text_layers=1, text_heads=2),
+      "t5_cfg": dict(d_model=128, d_kv=64, num_heads=2, d_ff=256, num_layers=2,
+                     num_decoder_layers=2),
+      "seeds": {"clip": 301, "tok": 302, "t5": 303, "index": 304, "images": 305},
+      "N": 300, "B": 6, "k": 3, "index_sigma": 0.15, "ans_vocab": 5}
+
+
+def g2_models():
+    ccfg = syn.ClipConfig(**G2["clip_cfg"])
+    tcfg = syn.ClipConfig(**G2["tok_cfg"])
+    t5cfg = syn.T5Config(**G2["t5_cfg"])
+    return (ccfg, syn.clip_state_dict(G2["seeds"]["clip"], ccfg),
+            tcfg, syn.clip_state_dict(G2["seeds"]["tok"], tcfg),
+            t5cfg, syn.t5_state_dict(G2["seeds"]["t5"], t5cfg))
+
+
+def g2_index(ccfg):
+    N = G2["N"]
+    X = syn.index_rows(G2["seeds"]["index"], N, 2 * ccfg.embed_dim, sigma=G2["index_sigma"])
+    return X, syn.answers(N, G2["ans_vocab"]), question_info(N)
+
+
+def g2_batch():
+    B = G2["B"]
+    rng = np.random.Generator(np.random.PCG64(306))
+    words = ["what", "is", "the", "organ", "shown", "in", "this", "image", "does", "picture",
+             "contain", "lung", "liver", "brain", "which", "modality", "used", "where", "mass"]
+    qs = [" ".join(rng.choice(words, size=int(rng.integers(4, 10)))) for _ in range(B)]
+    tasks = [["organ", "modality", "position", "abnormality"][i % 4] for i in range(B)]
+    answers = [["yes", "no", "lung", "liver cancer", "ct", "left lung"][i % 6] for i in range(B)]
+    return {"image": syn.images(G2["seeds"]["images"], B, G2["clip_cfg"]["image_size"]),
+            "question": qs, "task": tasks, "answer": answers,
+            "question_id": [str(i) for i in range(B)], "question_type": ["open"] * B}
+
+
+# ---- G3 / G4: full-size third-party arithmetic (transformers T5 / CLIP second source) ---------
+G3 = {"t5_seed": 401, "ids_seed": 402, "img_seed": 403, "B": 4, "vocab_sel_seed": 404}
+G4 = {"clip_seed": 501, "img_seed": 502, "tok_seed": 503, "B_img": 2, "B_txt": 3}
+
+
+def g3_inputs(d_model=512):
+    B = G3["B"]
+    ids, tmask = syn.t5_prompt_ids(G3["ids_seed"], B)
+    img_tok = syn._normal(syn._rng(G3["img_seed"]), (B, 50, d_model), 0.5)
+    mask = torch.cat([torch.ones(B, 50, dtype=torch.long), tmask], 1)
+    return ids, img_tok, mask

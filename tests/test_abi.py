@@ -1,0 +1,56 @@
+"""C-ABI checks that need no GPU: libmpr.so loads, exports every symbol include/mpr.h declares,
+the ctypes table mirrors the header, and argument validation fails loudly without compute."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from multimodalpromptretrieval_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mpr.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mpr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exists_and_loads():
+    assert os.path.exists(_lib.LIB_PATH), "build libmpr.so first (__graft_entry__.build())"
+    lib = _lib.load()
+    assert lib.mpr_abi_version() == 1
+
+
+def test_every_header_symbol_exported():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    declared = header_functions()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in include/mpr.h but not exported"
+
+
+def test_ctypes_table_matches_header():
+    assert sorted(_lib.exported_symbols()) == header_functions()
+
+
+def test_invalid_arguments_fail_loudly():
+    lib = _lib.load()
+    out = ctypes.c_void_p()
+    rc = lib.mpr_index_create(None, 0, 1024, 0, 0, ctypes.byref(out))
+    assert rc != 0
+    assert b"empty index" in lib.mpr_last_error()
+    rc = lib.mpr_index_create(ctypes.c_void_p(1), 10, 1000, 0, 0, ctypes.byref(out))
+    assert rc != 0 and b"multiple of 16" in lib.mpr_last_error()
+    rc = lib.mpr_vit_create((ctypes.c_int32 * 6)(768, 12, 12, 32, 224, 512), 6, None, 0,
+                            ctypes.byref(out))
+    assert rc != 0
+    with pytest.raises(RuntimeError):
+        _lib.check(rc, "mpr_vit_create")
+
+
+def test_device_required_for_product_path():
+    with pytest.raises(RuntimeError):
+        _lib.ensure_device("cpu")

@@ -1,0 +1,168 @@
+"""GPU parity: libmpr kernels (through the C ABI) vs the CPU oracle on seeded inputs.
+
+Tolerances (fp32 everywhere; only the summation order differs from the CPU reference):
+* retrieval ids: bit-exact; distances rel 2e-5.
+* encoder / T5 float outputs: max|gpu - cpu| <= FP_TOL * max|cpu|.
+"""
+import numpy as np
+import pytest
+import torch
+
+from multimodalpromptretrieval_amd import synthetic as syn
+from oracle import clip as oclip
+from oracle import retrieval as oret
+from oracle import t5 as ot5
+
+pytestmark = pytest.mark.gpu
+FP_TOL = 2e-4
+DIST_RTOL = 2e-5
+
+
+def _rel_err(a: torch.Tensor, b: torch.Tensor) -> float:
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+@pytest.fixture(scope="module")
+def index_mod():
+    from multimodalpromptretrieval_amd import index
+    return index
+
+
+@pytest.mark.parametrize("n,d,b,k", [(6500, 1024, 16, 1), (6500, 1024, 16, 3),
+                                     (6500, 1024, 16, 5), (10000, 1024, 16, 15),
+                                     (512, 512, 33, 64), (7, 16, 3, 7), (65536, 1024, 16, 5)])
+def test_scan_topk_l2(device, index_mod, n, d, b, k):
+    X = syn.index_rows(1, n, d)
+    q = syn.index_rows(2, b, d)
+    ix = index_mod.DeviceIndex(X, device)
+    dist, ids = ix.search(q.to(device), k)
+    torch.cuda.synchronize()
+    ref = oret.cdist(q, X)
+    ref_ids = oret.topk_ids(ref, k, skip_first=False)
+    assert torch.equal(ids.cpu(), ref_ids), "retrieved ids differ from the CPU reference"
+    ref_d = torch.gather(ref, 1, ref_ids)
+    assert torch.allclose(dist.cpu(), ref_d, rtol=DIST_RTOL, atol=1e-5)
+
+
+def test_scan_ties_lowest_id(device, index_mod):
+    # Integer-valued rows: every dot product is exact in any order, so duplicates tie exactly.
+    g = np.random.Generator(np.random.PCG64(5))
+    X = torch.from_numpy(g.integers(-3, 4, size=(300, 64)).astype(np.float32))
+    X[[17, 101, 250]] = X[200].clone()  # exact duplicates of row 200
+    q = X[[200, 5, 17]].clone()
+    ix = index_mod.DeviceIndex(X, device)
+    dist, ids = ix.search(q.to(device), 6)
+    ref_ids = oret.topk_ids(oret.cdist(q, X), 6, skip_first=False)
+    assert torch.equal(ids.cpu(), ref_ids)
+    assert ids[0, :4].tolist() == [17, 101, 200, 250]
+
+
+def test_scan_cosine(device, index_mod):
+    X = syn.index_rows(3, 5000, 512)
+    q = syn.index_rows(4, 16, 512)
+    ix = index_mod.DeviceIndex(X, device, metric=index_mod.COSINE)
+    sim, ids = ix.search(q.to(device), 5)
+    ref_ids, ref_sim = oret.cosine_topk(q, X, 5)
+    assert torch.equal(ids.cpu(), ref_ids)
+    assert torch.allclose(sim.cpu(), ref_sim, rtol=1e-5, atol=1e-6)
+
+
+def test_scan_scores_matrix(device, index_mod):
+    X = syn.index_rows(6, 1000, 1024)
+    q = syn.index_rows(7, 20, 1024)
+    ix = index_mod.DeviceIndex(X, device)
+    s = ix.scores(q.to(device))
+    assert _rel_err(s, oret.cdist(q, X)) < 1e-5
+
+
+def test_topk_merge_shards(device, index_mod):
+    X = syn.index_rows(8, 4000, 1024)
+    q = syn.index_rows(9, 16, 1024)
+    shards = [index_mod.DeviceIndex(X[i * 1000:(i + 1) * 1000], device, row_offset=i * 1000)
+              for i in range(4)]
+    parts = [s.search(q.to(device), 5) for s in shards]
+    cd = torch.cat([p[0] for p in parts], 1)
+    ci = torch.cat([p[1] for p in parts], 1)
+    d, ids = index_mod.topk_merge(cd, ci, 5)
+    ref_ids = oret.topk_ids(oret.cdist(q, X), 5, False)
+    assert torch.equal(ids.cpu(), ref_ids)
+
+
+@pytest.fixture(scope="module")
+def clip_sd():
+    return syn.clip_state_dict(11)
+
+
+def test_vit_cls_and_tokens(device, clip_sd):
+    from multimodalpromptretrieval_amd.encoders import CLS, TOKENS, DeviceViT
+    vit = DeviceViT(clip_sd, device)
+    img = syn.images(12, 4)
+    cls = vit(img.to(device), CLS)
+    tok = vit(img.to(device), TOKENS)
+    assert _rel_err(cls, oclip.encode_image(clip_sd, img)) < FP_TOL
+    assert _rel_err(tok, oclip.image_token_features(clip_sd, img)) < FP_TOL
+
+
+def test_clip_text(device, clip_sd):
+    from multimodalpromptretrieval_amd.encoders import DeviceCLIPText
+    txt = DeviceCLIPText(clip_sd, device)
+    toks = syn.clip_tokens(13, 5)
+    out = txt(toks)
+    assert _rel_err(out, oclip.encode_text(clip_sd, toks)) < FP_TOL
+    full = txt(toks.to(device))  # device tokens: all 77 positions, same pooled result
+    assert _rel_err(full, out) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def t5_sd():
+    return syn.t5_state_dict(21)
+
+
+def _t5_inputs(b=4, seed=22):
+    ids, mask = syn.t5_prompt_ids(seed, b)
+    sd_img = syn.images(seed, b)  # noqa: F841  (image tokens come from a random tensor here)
+    g = torch.Generator().manual_seed(seed)
+    img_tok = torch.randn(b, 50, 512, generator=g) * 0.5
+    return ids, mask, img_tok
+
+
+def test_t5_encode_logits_generate(device, t5_sd):
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    m = DeviceT5(t5_sd, device)
+    ids, mask, img_tok = _t5_inputs()
+    B = ids.shape[0]
+    emb = torch.cat([img_tok, t5_sd["shared.weight"][ids]], 1)
+    full_mask = torch.cat([torch.ones(B, 50, dtype=torch.long), mask], 1)
+    enc = m.encode(emb, full_mask)
+    ref_enc = ot5.encode(t5_sd, emb, full_mask, 8)
+    assert _rel_err(enc, ref_enc) < FP_TOL
+    dec_in = torch.randint(0, 32100, (B, 7), generator=torch.Generator().manual_seed(3))
+    lg = m.logits(emb, full_mask, dec_in)
+    ref_lg = ot5.decoder_logits(t5_sd, ref_enc, full_mask, dec_in, 8)
+    assert _rel_err(lg, ref_lg) < FP_TOL
+    toks = m.generate(emb, full_mask, max_new_tokens=20)
+    ref_toks, step_logits = ot5.generate(t5_sd, emb, full_mask, 8, 20)
+    # greedy ids are compared where the reference's top-2 margin exceeds the fp tolerance
+    margins = [float((s.topk(2).values[:, 0] - s.topk(2).values[:, 1]).min()) for s in step_logits]
+    if min(margins) > 1e-3:
+        assert torch.equal(toks, ref_toks)
+    else:
+        n = next(i for i, mg in enumerate(margins) if mg <= 1e-3)
+        assert torch.equal(toks[:, :n + 1], ref_toks[:, :n + 1])
+
+
+def test_t5_embed_and_loss(device, t5_sd):
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    m = DeviceT5(t5_sd, device)
+    ids, mask, img_tok = _t5_inputs(3, 31)
+    out = torch.zeros(3, 50 + ids.shape[1], 512, device=device)
+    m.embed(ids, out, row0=50)
+    assert torch.equal(out[:, 50:].cpu(), t5_sd["shared.weight"][ids])
+    logits = torch.randn(3, 5, 32101)
+    labels = torch.randint(0, 32101, (3, 5))
+    labels[0, 3:] = -100
+    loss = m.loss(logits.to(device), labels)
+    ref = ot5.lm_loss(logits, labels)
+    assert abs(float(loss) - float(ref)) < 1e-5 * max(1.0, abs(float(ref)))
