@@ -1,0 +1,217 @@
+"""bench.py — QA pairs/s of the encode -> retrieve -> prompt -> T5-generate hot path on MI355X.
+
+Metric (BASELINE.json): "QA pairs/sec (encode+retrieve+T5 gen), SLAKE k=1; 1/2/4/8 GPU scaling".
+Workload (config C2): per GPU a batch of B=16 QA pairs (synthetic 224x224
+images resident in HBM + random-word questions), retrieval over a 6,500 x 1,024 fp32 index
+(k=1, test phase), prompt build + T5 tokenisation on the host, ViT-B/32 token features,
+t5-small encoder and 20 forced greedy decode steps, answers decoded on the host.  One step =
+``T5VisionModel.predict(batch)`` with ``VQARetrieval.retrieve_closest_qa_pairs`` as the
+retrieval function (the reference's main.py --test inner loop, main.py:262-263), i.e. every
+stage of the path, host included.  Weights are seeded random (no checkpoints offline).
+
+N > 1: one process per GPU (torch.distributed.run), each with its own batch of 16 (weak
+scaling); the retrieval index is row-sharded over the ranks and every batch exchanges queries
+(all_gather) and per-shard top-k candidates (all_to_all) over RCCL.
+
+Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel (the tiled f32-MFMA
+GEMM), timed with hipEvents around each of its launches on its own stream during a probed pass
+over the same steps; ``cpu_baseline`` is the CPU oracle pipeline (torch-CPU fp32, KV-cached
+greedy decode) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from multimodalpromptretrieval_amd import _lib  # noqa: E402
+from multimodalpromptretrieval_amd import synthetic as syn  # noqa: E402
+
+CONFIGS = {
+    # name: (batch per GPU, index rows, index dim, k, t5 config)
+    "c2": dict(B=16, N=6500, D=1024, k=1, t5="t5-small",
+               desc="SLAKE k=1: ~6.5k x 1024 index, t5-small + ViT-B/32, batch 16"),
+    "c3": dict(B=16, N=10000, D=1024, k=3, t5="t5-small",
+               desc="VQA_RAD->SLAKE k=3: 10k x 1024 combined index, batch 16"),
+    "c4": dict(B=16, N=65536, D=1024, k=5, t5="t5-small",
+               desc="ROCO synthetic corpus k=5: 65,536 x 1024 index, batch 16"),
+}
+WORDS = ("what is the organ shown in this image does picture contain lung liver brain which "
+         "modality used where mass abnormal left right heart kidney chest abdomen ct mri "
+         "x-ray largest normal").split()
+TASKS = ["organ", "modality", "position", "abnormality", "plane", "quantity", "color", "size"]
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def make_batches(n_batches: int, B: int, device, seed: int):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    for i in range(n_batches):
+        qs = [" ".join(rng.choice(WORDS, size=int(rng.integers(6, 20)))) for _ in range(B)]
+        out.append({
+            "image": syn.images(seed * 1000 + i, B).to(device),
+            "question": qs,
+            "task": [TASKS[int(t)] for t in rng.integers(0, len(TASKS), size=B)],
+            "answer": ["yes"] * B,
+            "question_id": [str(i * B + j) for j in range(B)],
+            "question_type": ["open"] * B,
+        })
+    return out
+
+
+def build(cfg, device, group):
+    from multimodalpromptretrieval_amd.dataset import VQARetrieval
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    retr_sd = syn.clip_state_dict(1)                 # vanilla CLIP (retrieval, encode_image/text)
+    tok_sd = syn.clip_state_dict(2)                  # PubMedCLIP stand-in (token features)
+    t5_sd = syn.t5_state_dict(3, syn.T5Config() if cfg["t5"] == "t5-small" else syn.T5_BASE)
+    retr = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=syn.hash_clip_tokenize,
+                        group=group)
+    X = syn.index_rows(4, cfg["N"], cfg["D"])
+    info = {"question_id": [str(j) for j in range(cfg["N"])],
+            "question_type": ["open"] * cfg["N"], "question": [""] * cfg["N"]}
+    retr.set_index(X, syn.answers(cfg["N"], 50), info, cfg["k"], is_training_phase=False)
+    retr.cache_enabled = False                        # every step re-encodes and re-scans
+    model = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=t5_sd,
+                          tokenizer=syn.HashT5Tokenizer(),
+                          retrieval_function=retr.retrieve_closest_qa_pairs)
+    model.eval()
+    return model, retr, (retr_sd, tok_sd, t5_sd, X, info)
+
+
+def cpu_baseline(cfg, weights, batches, seconds: float):
+    """The CPU oracle pipeline (restated reference path, torch-CPU fp32) on a bounded sample."""
+    from oracle import pipeline
+    retr_sd, tok_sd, t5_sd, X, info = weights
+    answers = syn.answers(cfg["N"], 50)
+    tok = syn.HashT5Tokenizer()
+    tok.add_tokens(["[itk]"])
+    heads = 8 if cfg["t5"] == "t5-small" else 12
+    cpu_batches = [{**b, "image": b["image"].cpu()} for b in batches]
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            b = cpu_batches[n % len(cpu_batches)]
+            pipeline.predict(b, retr_sd, tok_sd, t5_sd, heads, X, answers, info, cfg["k"], False,
+                             syn.hash_clip_tokenize, tok, 20, forced_steps=True)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or n >= 32:
+                break
+    pairs = n * cfg["B"]
+    return {"value": pairs / el, "unit": "QA pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{n} batches x {cfg['B']} QA pairs of the same workload ({el:.1f} s), "
+                      f"oracle/pipeline.py (torch-CPU fp32, KV-cached greedy, 20 forced steps)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
+                         f"torch.distributed.run --nproc-per-node {args.gpus}")
+    device = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(device)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+        group = dist.group.WORLD
+
+    model, retr, weights = build(cfg, device, group)
+    batches = make_batches(4, cfg["B"], device, seed=100 + rank)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def run(steps):
+        with torch.no_grad():
+            for s in range(steps):
+                model.predict(batches[s % len(batches)])
+
+    run(args.warmup)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    roofline = None
+    if not args.no_probe:
+        # Probed pass over the same steps: hipEvents around every tiled-GEMM launch.
+        _lib.probe_enable(1)
+        torch.cuda.synchronize()
+        run(args.steps)
+        torch.cuda.synchronize()
+        ms, launches, flops, _ = _lib.probe_read()
+        _lib.probe_enable(0)
+        if launches:
+            ach = flops / (ms * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "achieved": round(ach, 2),
+                        "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                        "kernel": "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)",
+                        "launches_per_step": launches // args.steps,
+                        "kernel_ms_per_step": round(ms / args.steps, 3),
+                        "algorithmic_gflop_per_launch": round(flops / launches / 1e9, 4)}
+        barrier()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, weights, batches, args.cpu_seconds)
+
+    if rank == 0:
+        pairs = world * cfg["B"] * args.steps
+        value = pairs / elapsed
+        line = {
+            "metric": "QA pairs/sec (encode+retrieve+T5 gen), SLAKE k=1; 1/2/4/8 GPU scaling",
+            "value": round(value, 2), "unit": "QA pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded random weights of ViT-B/32 x2, CLIP text, t5-small; "
+                    "random 224x224 images + random-word questions)",
+            "config": {"workload": cfg["desc"], "global_batch": world * cfg["B"],
+                       "index_rows": cfg["N"], "index_dim": cfg["D"], "k": cfg["k"],
+                       "decode_steps": 20, "index_sharding": f"rows/{world}" if world > 1
+                       else "single", "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

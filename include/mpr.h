@@ -137,6 +137,14 @@ int mpr_cross_entropy(const float* logits_dev, const int32_t* labels_dev, int64_
 
 int mpr_model_destroy(mpr_model* m);
 
+/* ---- measurement (bench.py roofline; no reference counterpart) --------------------------------
+ * kind 1 = tiled f32-MFMA GEMM, 2 = skinny (decode) GEMM, 0 = off.  While enabled, every launch
+ * of that kernel (outside graph capture) is bracketed by hipEvents on its own stream.
+ * mpr_probe_read waits for the recorded events and returns the summed kernel time (ms), the
+ * launch count and the summed algorithmic FLOPs and bytes of those launches, then resets. */
+int mpr_probe_enable(int32_t kind);
+int mpr_probe_read(double* total_ms, int64_t* launches, double* flops, double* bytes);
+
 #ifdef __cplusplus
 }
 #endif

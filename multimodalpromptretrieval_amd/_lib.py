@@ -53,7 +53,21 @@ SIGNATURES = [
                                 c_int32, c_void_p, c_void_p]),
     ("mpr_cross_entropy", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     ("mpr_model_destroy", c_int32, [c_void_p]),
+    ("mpr_probe_enable", c_int32, [c_int32]),
+    ("mpr_probe_read", c_int32, [POINTER(ctypes.c_double), I64P, POINTER(ctypes.c_double),
+                                 POINTER(ctypes.c_double)]),
 ]
+
+
+def probe_enable(kind: int) -> None:
+    call("mpr_probe_enable", kind)
+
+
+def probe_read():
+    """(kernel ms, launches, algorithmic flops, algorithmic bytes) since the last read."""
+    ms, n, fl, by = ctypes.c_double(), c_int64(), ctypes.c_double(), ctypes.c_double()
+    call("mpr_probe_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl), ctypes.byref(by))
+    return ms.value, n.value, fl.value, by.value
 
 _lib = None
 

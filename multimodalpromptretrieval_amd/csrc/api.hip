@@ -350,4 +350,13 @@ int mpr_model_destroy(mpr_model* m) {
   return MPR_OK;
 }
 
+int mpr_probe_enable(int32_t kind) {
+  MPR_REQUIRE(kind >= 0 && kind <= 2, "probe: kind %d", kind);
+  return probe_enable(kind);
+}
+
+int mpr_probe_read(double* ms, int64_t* launches, double* flops, double* bytes) {
+  return guarded([&]() -> int { return probe_read(ms, launches, flops, bytes); });
+}
+
 }  // extern "C"

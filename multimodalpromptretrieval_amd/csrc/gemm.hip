@@ -255,7 +255,76 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs sa) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// ---- kernel probe: hipEvent pairs around every GEMM launch of the probed kind ----------------
+struct ProbeRec {
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+int g_probe_kind = 0;
+std::vector<ProbeRec> g_recs;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t pool_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+bool probing(int kind, hipStream_t s) {
+  if (g_probe_kind != kind) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
+  return true;
+}
+
+double gemm_bytes(const GemmArgs& a) {
+  return 4.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N * (a.R ? 2 : 1) +
+                (a.bias ? a.N : 0));
+}
+
+template <class F>
+int probed(int kind, const GemmArgs& a, hipStream_t s, F&& launch) {
+  if (!probing(kind, s)) return launch();
+  ProbeRec r{pool_event(), pool_event(), 2.0 * a.M * a.N * a.K, gemm_bytes(a)};
+  if (!r.a || !r.b) return launch();
+  (void)hipEventRecord(r.a, s);
+  const int rc = launch();
+  (void)hipEventRecord(r.b, s);
+  g_recs.push_back(r);
+  return rc;
+}
+
 }  // namespace
+
+int probe_enable(int kind) {
+  g_probe_kind = kind;
+  return MPR_OK;
+}
+
+int probe_read(double* ms, int64_t* launches, double* flops, double* bytes) {
+  double t = 0, f = 0, by = 0;
+  for (auto& r : g_recs) {
+    float e = 0.f;
+    MPR_HIP(hipEventSynchronize(r.b));
+    MPR_HIP(hipEventElapsedTime(&e, r.a, r.b));
+    t += e;
+    f += r.flops;
+    by += r.bytes;
+    g_pool.push_back(r.a);
+    g_pool.push_back(r.b);
+  }
+  if (ms) *ms = t;
+  if (launches) *launches = (int64_t)g_recs.size();
+  if (flops) *flops = f;
+  if (bytes) *bytes = by;
+  g_recs.clear();
+  return MPR_OK;
+}
 
 int gemm(const GemmArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
@@ -263,12 +332,12 @@ int gemm(const GemmArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                   aligned16(a.W),
               "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-  const int64_t blocks64 = cdiv(a.M, 64) * cdiv(a.N, 64);
   const int64_t blocks128 = cdiv(a.M, 128) * cdiv(a.N, 64);
   // Larger tiles halve LDS traffic per FLOP but only pay while the grid still fills the chip.
-  if (blocks128 >= 512) return launch_gemm<128, 64, 2, 1>(a, s);
-  (void)blocks64;
-  return launch_gemm<64, 64, 1, 1>(a, s);
+  return probed(PROBE_GEMM, a, s, [&]() {
+    if (blocks128 >= 512) return launch_gemm<128, 64, 2, 1>(a, s);
+    return launch_gemm<64, 64, 1, 1>(a, s);
+  });
 }
 
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
@@ -278,10 +347,12 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                   aligned16(a.W) && (!sa.rms_w || aligned16(sa.rms_w)),
               "gemm_skinny: K/lda/ldw must be multiples of 4, operands 16-byte aligned");
-  dim3 grid((unsigned)cdiv(a.N, 16));
-  hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), 0, s, sa);
-  MPR_LAUNCHED();
-  return MPR_OK;
+  return probed(PROBE_SKINNY, a, s, [&]() {
+    dim3 grid((unsigned)cdiv(a.N, 16));
+    hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), 0, s, sa);
+    MPR_LAUNCHED();
+    return MPR_OK;
+  });
 }
 
 }  // namespace mpr

@@ -37,6 +37,11 @@ struct SkinnyArgs {
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
+// Kernel probe (bench roofline): hipEvent pairs around every launch of one GEMM kind.
+enum ProbeKind : int { PROBE_OFF = 0, PROBE_GEMM = 1, PROBE_SKINNY = 2 };
+int probe_enable(int kind);
+int probe_read(double* ms, int64_t* launches, double* flops, double* bytes);
+
 // LayerNorm over rows of width D (eps, affine), out may alias x.  ld in floats.
 int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, const float* beta,
               float eps, float* out, int64_t ldo, hipStream_t s);

@@ -1,0 +1,195 @@
+"""Retrieval surface of the reference's VQADataset, on the MI355X.
+
+``VQARetrieval`` carries the two methods the reference's ``main.py`` wires into the model
+(dataset/VQAFeatureDataset.py:118-246):
+
+* ``create_retrieval_dataset(data_loader, prefix, is_training_phase=True, retrieval_k=15,
+  use_additional_data=False)`` — encodes every retrieval example as [CLS image ‖ EOT text]
+  (fp32, D = 1024 for ViT-B/32) and keeps the index resident in HBM (sharded over the process
+  group when one is given);
+* ``retrieve_closest_qa_pairs(batch, return_ans=False, return_info=None, return_dists=False,
+  use_quantifier=True)`` — same four return types, same vote/bucket prompt.
+
+Differences, all deliberate: exact distance ties resolve to the lowest row id (the reference's
+unstable argsort is order-undefined there); the index cache is written in safe
+formats (tensor + JSON, no pickles) under a key that includes the dataset size (the reference's
+class-name key collides, F9); ``use_additional_data`` merges question-info dicts instead of
+calling ``.extend`` on a dict (F9).  One search serves the analytics calls that ``main.py --test``
+makes on the same batch (F10): the last batch's top-k is reused while the batch is unchanged.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from .encoders import CLS, DeviceCLIPText, DeviceViT
+from .index import L2, DeviceIndex
+
+BUCKETS = ["very unlikely", "unlikely", "maybe", "likely", "very likely", "certainly"]
+
+
+def _default_clip():
+    try:
+        import clip  # noqa: F401
+    except ImportError as e:
+        raise RuntimeError("openai `clip` is not installed: pass clip_state_dict= and "
+                           "clip_tokenizer= (e.g. multimodalpromptretrieval_amd.synthetic)") from e
+    import clip
+    model, _ = clip.load("ViT-B/32", device="cpu")
+    return model.float().state_dict(), clip.tokenize
+
+
+def vote_prompt(row: list, use_quantifier: bool = True) -> str:
+    """dataset/VQAFeatureDataset.py:216-230."""
+    counts: dict = {}
+    for a in row:
+        counts[a] = counts.get(a, 0) + 1
+    pred = max(counts, key=counts.get)
+    certainty = max(counts.values()) / sum(counts.values())
+    if use_quantifier:
+        return f"I believe the answer is {BUCKETS[int(certainty * (len(BUCKETS) - 1))]} {pred}"
+    return f"The most frequent answer is {pred}"
+
+
+class VQARetrieval:
+    """Retrieval index + CLIP query encoders on one GPU (or sharded over a process group)."""
+
+    def __init__(self, device="cuda", clip_state_dict: dict = None, clip_tokenizer=None,
+                 metric: int = L2, group=None):
+        self.device = torch.device(device)
+        _lib.ensure_device(self.device)
+        if clip_state_dict is None:
+            clip_state_dict, default_tok = _default_clip()
+            clip_tokenizer = clip_tokenizer or default_tok
+        if clip_tokenizer is None:
+            raise RuntimeError("VQARetrieval needs a clip tokenizer (clip.tokenize)")
+        self.clip_tokenize = clip_tokenizer
+        self.image_encoder = DeviceViT(clip_state_dict, self.device)
+        self.text_encoder = DeviceCLIPText(clip_state_dict, self.device)
+        self.embed_dim = self.image_encoder.out_dim + self.text_encoder.out_dim
+        self.metric = metric
+        self.group = group
+        self.retrieval_k = 15
+        self.is_training_phase = False
+        self.index = None
+        self.cache_enabled = True
+        self._cache_key = None
+        self._cache_val = None
+        self._cache_ref = None
+
+    # ---- encoding ------------------------------------------------------------------------------
+    def encode_queries(self, batch) -> torch.Tensor:
+        """[CLS image embedding ‖ EOT text embedding] fp32 [B, 1024] on the device
+        (dataset/VQAFeatureDataset.py:189-191, 146-148)."""
+        img = batch["image"]
+        B = img.shape[0]
+        q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
+        di = self.image_encoder.out_dim
+        self.image_encoder(img, CLS, out=q, out_bstride=self.embed_dim)
+        toks = self.clip_tokenize(batch["question"])
+        self.text_encoder(toks, out=q[:, di:], out_bstride=self.embed_dim)
+        return q
+
+    # ---- index -------------------------------------------------------------------------------
+    def set_index(self, embeddings: torch.Tensor, answers: list, question_info: dict,
+                  retrieval_k: int = 15, is_training_phase: bool = False):
+        self.retrieval_k = retrieval_k
+        self.is_training_phase = is_training_phase
+        self.retrieval_answers = list(answers)
+        self.retrieval_question_info = {k: list(v) for k, v in question_info.items()}
+        emb = embeddings.detach().to(torch.float32)
+        if self.group is not None:
+            from .distributed import ShardedIndex
+            self.index = ShardedIndex(emb, self.device, self.metric, group=self.group)
+        else:
+            self.index = DeviceIndex(emb, self.device, self.metric)
+        self.retrieval_embeddings = emb
+        self._cache_key = None
+
+    def _cache_paths(self, root, data_loader):
+        n = len(getattr(data_loader, "dataset", []))
+        name = getattr(getattr(data_loader, "dataset", None), "name", "dataset")
+        d = os.path.join(root, type(self).__name__, f"{name}_{n}")
+        return d, os.path.join(d, "embedding.pt"), os.path.join(d, "answers.json"), \
+            os.path.join(d, "question_info.json")
+
+    def create_retrieval_dataset(self, data_loader, prefix=None, is_training_phase=True,
+                                 retrieval_k=15, use_additional_data=False, cache_dir="cache"):
+        """dataset/VQAFeatureDataset.py:118-185."""
+        d, emb_p, ans_p, info_p = self._cache_paths(cache_dir, data_loader)
+        if os.path.exists(emb_p) and os.path.exists(ans_p) and os.path.exists(info_p):
+            emb = torch.load(emb_p, map_location="cpu", weights_only=True).float()
+            with open(ans_p) as f:
+                answers = json.load(f)
+            with open(info_p) as f:
+                info = json.load(f)
+        else:
+            embs, answers = [], []
+            info = {"question_type": [], "question_id": [], "question": []}
+            for batch in data_loader:
+                embs.append(self.encode_queries(batch).cpu())
+                answers.extend(batch["answer"])
+                info["question_type"].extend(batch["question_type"])
+                info["question_id"].extend(batch["question_id"])
+                info["question"].extend(batch["question"])
+            emb = torch.cat(embs, 0)
+            os.makedirs(d, exist_ok=True)
+            torch.save(emb, emb_p)
+            with open(ans_p, "w") as f:
+                json.dump(answers, f)
+            with open(info_p, "w") as f:
+                json.dump(info, f)
+        if use_additional_data:
+            extra = os.path.join("synthetic_data", "cache", "ROCOFeatureDataset")
+            emb = torch.cat([emb, torch.load(os.path.join(extra, "embedding.pt"),
+                                             map_location="cpu", weights_only=True).float()], 0)
+            with open(os.path.join(extra, "answers.json")) as f:
+                answers = answers + json.load(f)
+            with open(os.path.join(extra, "question_info.json")) as f:
+                more = json.load(f)
+            info = {k: list(info.get(k, [])) + list(more.get(k, [])) for k in set(info) | set(more)}
+        self.set_index(emb, answers, info, retrieval_k, is_training_phase)
+
+    # ---- search --------------------------------------------------------------------------------
+    def _topk(self, batch):
+        """(dists [B, s+k], ids [B, s+k]) as host numpy, s = 1 in the training phase.  Cached
+        while the same batch object (same images, same questions) is queried again."""
+        # the cached image tensor is kept alive, so an equal id() means the same object
+        key = (id(batch["image"]), tuple(batch["question"]), self.retrieval_k,
+               self.is_training_phase)
+        if self.cache_enabled and key == self._cache_key:
+            return self._cache_val
+        if self.index is None:
+            raise RuntimeError("create_retrieval_dataset() / set_index() first")
+        q = self.encode_queries(batch)
+        kk = self.retrieval_k + (1 if self.is_training_phase else 0)
+        dist, ids = self.index.search(q, kk)
+        both = torch.cat([ids.to(torch.float64), dist.to(torch.float64)], 1).cpu().numpy()
+        val = (both[:, kk:].astype(np.float32), both[:, :kk].astype(np.int64))
+        self._cache_key, self._cache_val, self._cache_ref = key, val, batch["image"]
+        return val
+
+    def retrieve_closest_qa_pairs(self, batch, return_ans=False, return_info=None,
+                                  return_dists=False, use_quantifier=True):
+        """dataset/VQAFeatureDataset.py:187-246."""
+        dists, ids = self._topk(batch)
+        s = 1 if self.is_training_phase else 0
+        sel = ids[:, s:s + self.retrieval_k]
+        answers = [[self.retrieval_answers[j] for j in row] for row in sel]
+        if return_ans:
+            return answers
+        if return_info:
+            out = []
+            for row in sel:
+                info = []
+                for j in row:
+                    info.extend(self.retrieval_question_info[e][j] for e in return_info)
+                out.append(info)
+            return out
+        if return_dists:
+            return list(zip(answers, dists[:, 0:self.retrieval_k]))
+        return [vote_prompt(r, use_quantifier) for r in answers]

@@ -1,0 +1,77 @@
+"""Index sharding across the GPUs of one node.
+
+Rank r of W holds index rows [lo_r, hi_r) (global ids preserved through ``row_offset``).  One
+retrieval step per batch:
+  1. all_gather of the per-rank query blocks  -> every rank scans its shard for the whole batch;
+  2. local fused scan + top-k (libmpr)         -> [W*b, k] (dist, global id) candidates;
+  3. all_to_all of the candidates              -> each rank receives the W shard-candidates of
+                                                  its own b queries: [W, b, k];
+  4. merge (libmpr topk_merge)                 -> [b, k], ties by lowest global id, so the result
+                                                  is identical to the single-GPU scan.
+Messages are KB-scale (latency-bound over xGMI).  The collectives go through
+torch.distributed (backend "nccl" = RCCL on ROCm; "gloo" in the CPU tests, which inject a CPU
+searcher/merger so the sharding logic is exercised without a GPU).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .index import L2, DeviceIndex, topk_merge
+
+
+def shard_bounds(n: int, world: int, rank: int):
+    per = (n + world - 1) // world
+    lo = min(n, rank * per)
+    return lo, min(n, lo + per)
+
+
+class ShardedIndex:
+    def __init__(self, rows: torch.Tensor, device, metric: int = L2, group=None,
+                 rows_are_local: bool = False, row_offset: int = None, searcher=None,
+                 merger=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.metric = metric
+        self.device = torch.device(device)
+        if rows_are_local:
+            local, lo = rows, int(row_offset or 0)
+        else:
+            lo, hi = shard_bounds(rows.shape[0], self.world, self.rank)
+            local = rows[lo:hi]
+        if local.shape[0] < 1:
+            raise ValueError(f"rank {self.rank}: empty index shard (n < world size)")
+        self.n_local = local.shape[0]
+        self.row_offset = lo
+        self.d = rows.shape[1]
+        if searcher is None:
+            self._local = DeviceIndex(local, self.device, metric, row_offset=lo)
+            self._search = self._local.search
+        else:
+            self._search = lambda q, k: searcher(local, lo, q, k)
+        self._merge = merger or (lambda d, i, k: topk_merge(d, i, k, metric))
+
+    def search(self, q: torch.Tensor, k: int):
+        """q: this rank's [b, d] queries (same b on every rank).  Returns (dist, ids) [b, k]."""
+        b = q.shape[0]
+        kk = min(k, self.n_local)
+        q = q.to(self.device, torch.float32).contiguous()
+        q_all = torch.empty((self.world * b, self.d), device=q.device, dtype=q.dtype)
+        dist.all_gather_into_tensor(q_all, q, group=self.group)
+        d_loc, i_loc = self._search(q_all, kk)                  # [W*b, kk]
+        if kk < k:                                              # tiny shard: pad with sentinels
+            pad = k - kk
+            fill = float("inf") if self.metric == L2 else float("-inf")
+            d_loc = torch.cat([d_loc, torch.full((d_loc.shape[0], pad), fill,
+                                                 device=d_loc.device)], 1)
+            i_loc = torch.cat([i_loc, torch.full((i_loc.shape[0], pad), -1, dtype=torch.int64,
+                                                 device=i_loc.device)], 1)
+        d_recv = torch.empty_like(d_loc)
+        i_recv = torch.empty_like(i_loc)
+        dist.all_to_all_single(d_recv, d_loc.contiguous(), group=self.group)
+        dist.all_to_all_single(i_recv, i_loc.contiguous(), group=self.group)
+        # [W(src shard), b, k] -> [b, W*k]
+        cd = d_recv.view(self.world, b, k).permute(1, 0, 2).reshape(b, self.world * k)
+        ci = i_recv.view(self.world, b, k).permute(1, 0, 2).reshape(b, self.world * k)
+        return self._merge(cd.contiguous(), ci.contiguous(), k)

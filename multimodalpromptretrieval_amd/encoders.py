@@ -37,7 +37,8 @@ def _count_layers(sd: dict, prefix: str) -> int:
 
 
 def _host_f32(ts: list) -> list:
-    return [t.detach().to("cpu", torch.float32).contiguous() for t in ts]
+    """fp32 contiguous tensors (host or device: the library copies with hipMemcpyDefault)."""
+    return [t.detach().to(torch.float32).contiguous() for t in ts]
 
 
 class _Handle:

@@ -1,0 +1,248 @@
+"""``T5VisionModel`` — drop-in for architectures/T5VisionModel.py on the MI355X.
+
+Same constructor, same ``prepare_input`` / ``predict`` / ``forward`` contracts, same attributes
+(``device``, ``tokenizer``, ``T5_model`` with ``shared`` / ``generate`` / ``__call__``,
+``vision_model.visual`` callable) and the same ``state_dict`` keys (``vision_model.*`` in openai
+CLIP naming, ``T5_model.*`` in transformers naming), so ``main.py`` and its checkpoints work
+unchanged.  The arithmetic runs in libmpr: the token-feature ViT (get_image_token_features,
+:112-139), the T5 embedding gather (:169), the encoder + greedy decoder (:200-205) and the
+teacher-forced loss (:233).  Parameters stay the PyTorch source of truth; the device handles are
+rebuilt from them whenever they change (load_state_dict, optimizer steps, .to()).
+
+Scope notes: inference path.  ``forward`` returns the loss value without autograd (training /
+backward is SURVEY.md §8(f) "next"); RN vision encoders, the mapping checkpoint and t5-large's
+untrained 512->1024 projection raise NotImplementedError; ``predict(output_attentions=True)``
+(attention plots) is out of scope.  As in the reference, image tokens (512-d) only fit a
+512-d T5 (t5-small); other widths raise like the reference's torch.cat.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import _lib
+from .encoders import TOKENS, DeviceViT
+from .t5 import DeviceT5
+
+
+class ParamTree(nn.Module):
+    """nn.Module tree whose parameter names reproduce a flat state_dict's dotted keys."""
+
+    def __init__(self, flat: dict = None):
+        super().__init__()
+        for k, v in (flat or {}).items():
+            self.put(k, v)
+
+    def put(self, key: str, value):
+        parts = key.split(".")
+        mod = self
+        for p in parts[:-1]:
+            if not hasattr(mod, p) or getattr(mod, p) is None:
+                mod.add_module(p, ParamTree())
+            mod = getattr(mod, p)
+        if isinstance(value, nn.Parameter):
+            mod.register_parameter(parts[-1], value)
+        else:
+            mod.register_parameter(parts[-1], nn.Parameter(value.detach().clone(),
+                                                           requires_grad=False))
+
+
+class _VisualTower(ParamTree):
+    """``vision_model.visual``: calling it returns the [B, 50, 512] token features."""
+
+    def forward(self, x):
+        return self._owner_fn(x)
+
+
+class _CLIPParams(ParamTree):
+    def __init__(self, sd: dict):
+        super().__init__()
+        self.add_module("visual", _VisualTower())
+        for k, v in sd.items():
+            self.put(k, v)
+
+
+class _GenerationOutput:
+    def __init__(self, loss, logits):
+        self.loss = loss
+        self.logits = logits
+
+
+class T5Shell(ParamTree):
+    """``T5_model``: parameters under transformers names + generate / __call__ on the device."""
+
+    def __init__(self, sd: dict, owner):
+        super().__init__()
+        shared = nn.Parameter(sd["shared.weight"].detach().clone(), requires_grad=False)
+        self.shared = nn.Embedding(shared.shape[0], shared.shape[1])
+        self.shared.weight = shared
+        for k, v in sd.items():
+            if k in ("shared.weight", "lm_head.weight", "encoder.embed_tokens.weight",
+                     "decoder.embed_tokens.weight"):
+                continue
+            self.put(k, v)
+        # tied weights share one Parameter (T5ForConditionalGeneration tie_word_embeddings)
+        self.put("encoder.embed_tokens.weight", shared)
+        self.put("decoder.embed_tokens.weight", shared)
+        self.put("lm_head.weight", shared)
+        object.__setattr__(self, "_owner", owner)
+
+    def generate(self, inputs_embeds=None, attention_mask=None, do_sample=False,
+                 max_new_tokens=20, **kw):
+        if do_sample:
+            raise NotImplementedError("sampling is not on the reference's path (do_sample=False)")
+        dev = self._owner._device_t5()
+        return dev.generate(inputs_embeds, attention_mask, max_new_tokens).to(
+            self._owner.device)
+
+    def forward(self, inputs_embeds=None, attention_mask=None, labels=None,
+                decoder_input_ids=None, **kw):
+        dev = self._owner._device_t5()
+        if attention_mask is None:
+            attention_mask = torch.ones(inputs_embeds.shape[:2], device=inputs_embeds.device)
+        if decoder_input_ids is None:
+            if labels is None:
+                raise ValueError("need labels or decoder_input_ids")
+            decoder_input_ids = labels.new_zeros(labels.shape)
+            decoder_input_ids[:, 1:] = labels[:, :-1]
+            decoder_input_ids.masked_fill_(decoder_input_ids == -100, 0)
+        logits = dev.logits(inputs_embeds, attention_mask, decoder_input_ids)
+        loss = dev.loss(logits, labels) if labels is not None else None
+        return _GenerationOutput(loss, logits)
+
+
+def _load_t5(version: str, tokenizer):
+    try:
+        from transformers import T5ForConditionalGeneration
+        m = T5ForConditionalGeneration.from_pretrained(version)
+        m.resize_token_embeddings(len(tokenizer))
+        return {k: v.float() for k, v in m.state_dict().items()}
+    except Exception as e:  # offline image: no hub access
+        raise RuntimeError(f"cannot load {version} weights ({e}); pass t5_state_dict=") from e
+
+
+class T5VisionModel(nn.Module):
+    def __init__(self, device, vision_encoder="ViT-B/32", T5_version="t5-small",
+                 max_source_length=512, max_target_length=128, use_image_info=True,
+                 vision_checkpoint=None, mapping_checkpoint=None, retrieval_function=None,
+                 use_quantifier=True, *, clip_state_dict=None, t5_state_dict=None,
+                 tokenizer=None, max_new_tokens=20):
+        super().__init__()
+        self.device = torch.device(device)
+        _lib.ensure_device(self.device)
+        self.vision_encoder = vision_encoder
+        self.T5_version = T5_version
+        self.max_source_length = max_source_length
+        self.max_target_length = max_target_length
+        self.use_image_info = use_image_info
+        self.retrieval_function = retrieval_function
+        self.use_quantifier = use_quantifier
+        self.max_new_tokens = max_new_tokens
+        self.use_mapping = bool(mapping_checkpoint)
+        if self.use_mapping:
+            raise NotImplementedError("mapping_checkpoint (CrossModalMapping) is not on the "
+                                      "reference's main path (main.py passes None)")
+        if "ViT" not in vision_encoder:
+            raise NotImplementedError(f"{vision_encoder}: only the ViT-B/32 path is built")
+        if "large" in T5_version:
+            raise NotImplementedError("t5-large's untrained 512->1024 projection is not built")
+        if clip_state_dict is None:
+            from .dataset import _default_clip
+            clip_state_dict, _ = _default_clip()
+        if vision_checkpoint:
+            ck = torch.load(vision_checkpoint, map_location="cpu", weights_only=True)
+            clip_state_dict = {k: v.float() for k, v in ck["state_dict"].items()}
+        if tokenizer is None:
+            from transformers import T5Tokenizer
+            tokenizer = T5Tokenizer.from_pretrained(T5_version)
+        self.tokenizer = tokenizer
+        self.tokenizer.add_tokens(["[itk]"])
+        if t5_state_dict is None:
+            t5_state_dict = _load_t5(T5_version, self.tokenizer)
+        self.vision_model = _CLIPParams({k: v.float() for k, v in clip_state_dict.items()})
+        object.__setattr__(self.vision_model.visual, "_owner_fn", self.get_image_token_features)
+        self.T5_model = T5Shell(t5_state_dict, self)
+        self.image_token_id = self.tokenizer.convert_tokens_to_ids("[itk]")
+        self._dev = {}
+        self.to(self.device)
+
+    # ---- device handles, rebuilt when parameters change ------------------------------------------
+    def _params_key(self, prefix):
+        return tuple((n, p.data_ptr(), p._version) for n, p in self.named_parameters()
+                     if n.startswith(prefix))
+
+    def _handle(self, name, prefix, build):
+        key = self._params_key(prefix)
+        ent = self._dev.get(name)
+        if ent is None or ent[0] != key:
+            sd = {n[len(prefix):]: p.detach() for n, p in self.named_parameters()
+                  if n.startswith(prefix)}
+            ent = (key, build(sd))
+            self._dev[name] = ent
+        return ent[1]
+
+    def _device_vit(self):
+        return self._handle("vit", "vision_model.", lambda sd: DeviceViT(sd, self.device))
+
+    def _device_t5(self):
+        # named_parameters() lists the tied embedding once, as shared.weight; DeviceT5 reuses it
+        # for the lm_head when lm_head.weight is absent.
+        return self._handle("t5", "T5_model.", lambda sd: DeviceT5(sd, self.device))
+
+    # ---- reference surface -----------------------------------------------------------------------
+    def get_image_token_features(self, x):
+        """architectures/T5VisionModel.py:112-139 -> [B, 50, 512] fp32 on the device."""
+        return self._device_vit()(x, TOKENS)
+
+    def prepare_input(self, batch):
+        """architectures/T5VisionModel.py:141-184."""
+        if self.retrieval_function:
+            if self.use_quantifier:
+                retrieved_info = self.retrieval_function(batch)
+            else:
+                retrieved_info = self.retrieval_function(batch, use_quantifier=False)
+        else:
+            retrieved_info = ["" for _ in batch["task"]]
+        task_prefixes = [f"Answer the {x} question: " for x in batch["task"]]
+        vit = self._device_vit()
+        t5 = self._device_t5()
+        img = batch["image"]
+        B = img.shape[0]
+        sentences = [task_prefixes[i] + batch["question"][i] + retrieved_info[i]
+                     for i in range(len(batch["question"]))]
+        encoding = self.tokenizer(sentences, padding="longest",
+                                  max_length=self.max_source_length, truncation=True,
+                                  return_tensors="pt")
+        ids = encoding["input_ids"]
+        L = ids.shape[1]
+        T = vit.tokens if self.use_image_info else 0
+        if self.use_image_info and vit.out_dim != t5.d_model:
+            raise RuntimeError(f"Sizes of tensors must match: image tokens are {vit.out_dim}-d, "
+                               f"{self.T5_version} d_model is {t5.d_model} (torch.cat at "
+                               f"architectures/T5VisionModel.py:176)")
+        combined = torch.empty((B, T + L, t5.d_model), device=self.device, dtype=torch.float32)
+        if self.use_image_info:
+            vit(img, TOKENS, out=combined, out_bstride=(T + L) * t5.d_model)
+        t5.embed(ids, combined, row0=T)
+        mask = torch.ones((B, T + L), dtype=torch.float32)
+        mask[:, T:] = encoding["attention_mask"].float()
+        return combined, mask.to(self.device), encoding
+
+    def predict(self, batch, output_attentions=False):
+        """architectures/T5VisionModel.py:196-216 (greedy, max_new_tokens=20)."""
+        if output_attentions:
+            raise NotImplementedError("output_attentions is the eval-only plotting path")
+        combined, mask, _ = self.prepare_input(batch)
+        seqs = self.T5_model.generate(inputs_embeds=combined, attention_mask=mask,
+                                      do_sample=False, max_new_tokens=self.max_new_tokens)
+        return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
+
+    def forward(self, batch):
+        """architectures/T5VisionModel.py:219-234 (loss value; no autograd)."""
+        combined, mask, _ = self.prepare_input(batch)
+        target = self.tokenizer(batch["answer"], padding="longest",
+                                max_length=self.max_target_length, truncation=True)
+        labels = torch.tensor(target["input_ids"])
+        labels[labels == self.tokenizer.pad_token_id] = -100
+        labels = labels.to(self.device)
+        return self.T5_model(inputs_embeds=combined, attention_mask=mask, labels=labels).loss

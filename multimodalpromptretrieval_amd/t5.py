@@ -81,7 +81,7 @@ class DeviceT5:
                   sd[p + ".2.layer_norm.weight"], sd[p + ".2.DenseReluDense.wi.weight"],
                   sd[p + ".2.DenseReluDense.wo.weight"]]
         t += [sd["decoder.final_layer_norm.weight"], lm_head]
-        host = [x.detach().to("cpu", torch.float32).contiguous() for x in t]
+        host = [x.detach().to(torch.float32).contiguous() for x in t]  # host or device
         rel_pos = torch.arange(-LUT_RADIUS, LUT_RADIUS + 1, dtype=torch.long)
         enc_lut = relative_position_bucket(rel_pos, True, self.num_buckets, max_distance)
         dec_lut = relative_position_bucket(rel_pos, False, self.num_buckets, max_distance)

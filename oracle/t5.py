@@ -142,6 +142,68 @@ def generate(sd: dict, embeds: torch.Tensor, mask: torch.Tensor, heads: int,
     return toks, step_logits
 
 
+def generate_cached(sd: dict, embeds: torch.Tensor, mask: torch.Tensor, heads: int,
+                    max_new_tokens: int = 20, start: int = 0, eos: int = 1, pad: int = 0,
+                    forced_steps: bool = False) -> torch.Tensor:
+    """Greedy search with a KV cache (the path transformers' generate takes: one decoder
+    position per step, cross-attention K/V projected once).  Same tokens as ``generate``; this
+    is the timed CPU baseline of bench.py."""
+    enc = encode(sd, embeds, mask, heads)
+    B = enc.shape[0]
+    n_dec = _n_layers(sd, "decoder")
+    cross_bias = _mask_bias(mask)
+    table = sd["decoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"]
+
+    def split(x):
+        return x.reshape(B, x.shape[1], heads, -1).transpose(1, 2)
+
+    ck, cv = [], []
+    for i in range(n_dec):
+        p = f"decoder.block.{i}.layer.1.EncDecAttention"
+        ck.append(split(enc @ sd[p + ".k.weight"].T))
+        cv.append(split(enc @ sd[p + ".v.weight"].T))
+    sk = [None] * n_dec
+    sv = [None] * n_dec
+    toks = torch.full((B, 1), start, dtype=torch.long)
+    cur = toks[:, 0]
+    unfinished = torch.ones(B, dtype=torch.long)
+    for t in range(max_new_tokens):
+        x = sd["shared.weight"][cur][:, None, :]
+        rel = torch.arange(t + 1, dtype=torch.long) - t
+        bias = table[relative_position_bucket(rel, False, table.shape[0])].T[None, :, None, :]
+        for i in range(n_dec):
+            p = f"decoder.block.{i}.layer"
+            h = _rms(x, sd[p + ".0.layer_norm.weight"])
+            a = p + ".0.SelfAttention"
+            q = split(h @ sd[a + ".q.weight"].T)
+            k = split(h @ sd[a + ".k.weight"].T)
+            v = split(h @ sd[a + ".v.weight"].T)
+            sk[i] = k if sk[i] is None else torch.cat([sk[i], k], 2)
+            sv[i] = v if sv[i] is None else torch.cat([sv[i], v], 2)
+            w = torch.softmax(q @ sk[i].transpose(-1, -2) + bias, dim=-1)
+            o = (w @ sv[i]).transpose(1, 2).reshape(B, 1, -1)
+            x = x + o @ sd[a + ".o.weight"].T
+            h = _rms(x, sd[p + ".1.layer_norm.weight"])
+            c = p + ".1.EncDecAttention"
+            q = split(h @ sd[c + ".q.weight"].T)
+            w = torch.softmax(q @ ck[i].transpose(-1, -2) + cross_bias, dim=-1)
+            o = (w @ cv[i]).transpose(1, 2).reshape(B, 1, -1)
+            x = x + o @ sd[c + ".o.weight"].T
+            h = _rms(x, sd[p + ".2.layer_norm.weight"])
+            f = torch.relu(h @ sd[p + ".2.DenseReluDense.wi.weight"].T)
+            x = x + f @ sd[p + ".2.DenseReluDense.wo.weight"].T
+        x = _rms(x, sd["decoder.final_layer_norm.weight"]) * (x.shape[-1] ** -0.5)
+        lg = (x @ sd["lm_head.weight"].T)[:, 0, :]
+        nxt = torch.argmax(lg, dim=-1)
+        nxt = nxt * unfinished + pad * (1 - unfinished)
+        toks = torch.cat([toks, nxt[:, None]], dim=1)
+        unfinished = unfinished & (nxt != eos).long()
+        cur = nxt
+        if not forced_steps and int(unfinished.max()) == 0:
+            break
+    return toks
+
+
 def lm_loss(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     """CrossEntropyLoss(ignore_index=-100) over [B, T, V] logits (T5ForConditionalGeneration)."""
     return torch.nn.functional.cross_entropy(logits.reshape(-1, logits.shape[-1]),

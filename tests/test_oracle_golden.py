@@ -122,6 +122,11 @@ def test_g2_pipeline_oracle(g2):
     seqs, _ = ot5.generate(t5_sd, emb, mask, t5cfg.num_heads, 20)
     assert seqs.tolist() == z["sequences"].tolist()
     assert tok.batch_decode(seqs, skip_special_tokens=True) == j["predictions"]
+    from oracle import pipeline
+    preds, prompts2, _ = pipeline.predict(
+        batch, clip_sd, tok_sd, t5_sd, t5cfg.num_heads, X, answers, info, gi.G2["k"], False,
+        syn.hash_clip_tokenize, tok)
+    assert prompts2 == j["prompts"] and preds == j["predictions"]
     labels = torch.tensor(tok(batch["answer"], padding="longest", max_length=128,
                               truncation=True)["input_ids"])
     labels[labels == 0] = -100
@@ -141,6 +146,7 @@ def test_g3_t5_small_oracle():
     assert _rel(enc[:, :8], z["enc_head"]) < FP_TOL
     seqs, _ = ot5.generate(sd, emb, mask, cfg.num_heads, 20)
     assert seqs.tolist() == z["sequences"].tolist()
+    assert ot5.generate_cached(sd, emb, mask, cfg.num_heads, 20).tolist() == seqs.tolist()
     labels = torch.from_numpy(z["labels"])
     lg = ot5.decoder_logits(sd, enc, mask, ot5.shift_right(labels), cfg.num_heads)
     assert _rel(lg[:, :, torch.from_numpy(z["vocab_sel"])], z["logits_sel"]) < FP_TOL
