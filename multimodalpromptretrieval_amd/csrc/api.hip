@@ -254,9 +254,24 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
     MPR_REQUIRE(radius >= 64, "t5_create: lut radius %d too small", radius);
     const int expect = 2 + 8 * Le + 1 + 1 + 13 * Ld + 2;
     MPR_REQUIRE(nt == expect, "t5_create: expected %d tensors, got %d", expect, nt);
+    // Relative position bias by offset r = key - query: tab[(r + radius) * H + h] =
+    // rel_bias[lut[r + radius], h] (the bucket gather done once here, not per score).
+    auto bias_table = [&](DevBuf& dst, const float* rel, const int32_t* lut) -> int {
+      std::vector<float> hrel((size_t)m->nb * m->H);
+      MPR_HIP(hipMemcpy(hrel.data(), rel, hrel.size() * 4, hipMemcpyDefault));
+      const size_t nr = (size_t)2 * radius + 1;
+      std::vector<int32_t> hl(nr);
+      MPR_HIP(hipMemcpy(hl.data(), lut, nr * 4, hipMemcpyDefault));
+      std::vector<float> tab(nr * m->H);
+      for (size_t r = 0; r < nr; ++r) {
+        MPR_REQUIRE(hl[r] >= 0 && hl[r] < m->nb, "t5_create: lut bucket %d out of range", hl[r]);
+        for (int hh = 0; hh < m->H; ++hh) tab[r * m->H + hh] = hrel[(size_t)hl[r] * m->H + hh];
+      }
+      return upload(dst, tab.data(), tab.size());
+    };
     int p = 0;
     MPR_TRY(upload(m->shared, t[p++], (size_t)m->V * d));
-    MPR_TRY(upload(m->enc_rel, t[p++], (size_t)m->nb * m->H));
+    MPR_TRY(bias_table(m->enc_tab, t[p++], enc_lut));
     for (int l = 0; l < Le; ++l) {
       auto ly = std::make_unique<T5Layer>();
       MPR_TRY(upload(ly->ln0, t[p++], d));
@@ -269,7 +284,7 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
       m->enc.push_back(std::move(ly));
     }
     MPR_TRY(upload(m->enc_final, t[p++], d));
-    MPR_TRY(upload(m->dec_rel, t[p++], (size_t)m->nb * m->H));
+    MPR_TRY(bias_table(m->dec_tab, t[p++], dec_lut));
     MPR_TRY(m->cross_kv_w.ensure((size_t)Ld * 2 * inner * d * 4));
     for (int l = 0; l < Ld; ++l) {
       auto ly = std::make_unique<T5Layer>();
@@ -289,11 +304,6 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
     }
     MPR_TRY(upload(m->dec_final, t[p++], d));
     MPR_TRY(upload(m->lm_head, t[p++], (size_t)m->V * d));
-    const size_t nl = (size_t)2 * radius + 1;
-    MPR_TRY(m->enc_lut.ensure(nl * 4));
-    MPR_TRY(m->dec_lut.ensure(nl * 4));
-    MPR_HIP(hipMemcpy(m->enc_lut.ptr, enc_lut, nl * 4, hipMemcpyDefault));
-    MPR_HIP(hipMemcpy(m->dec_lut.ptr, dec_lut, nl * 4, hipMemcpyDefault));
     *out = m.release();
     return MPR_OK;
   });

@@ -10,9 +10,9 @@
 // are padded to 36 floats, which makes those 128-bit reads bank-conflict free.
 //
 // gemm_skinny() serves decoder steps (M = batch <= 16): W streams straight from HBM/L2 into
-// registers as the A operand of v_mfma_f32_16x16x4_f32 (16 output columns per wave), the 16
-// activation rows are the B operand, K is split across the 4 waves of a block and reduced through
-// LDS, and T5's RMSNorm of the activation rows can be fused into the operand load.
+// registers as the A operand of v_mfma_f32_16x16x4_f32 (16 output columns per block), the 16
+// activation rows are the B operand, K is split across the 8 waves of a block and reduced through
+// LDS, and T5's RMSNorm of the activation rows is folded into the operand and the epilogue.
 #include "kernels.h"
 
 namespace mpr {
@@ -154,101 +154,150 @@ int launch_gemm(const GemmArgs& a, hipStream_t s) {
 
 // ---------------------------------------------------------------------------------------------
 // Skinny GEMM (M <= 16), optional fused RMSNorm of the A rows.
-constexpr int SK_WAVES = 4;
+// A block = 8 waves = 16 output columns (W rows n0..n0+15); wave w owns the K slice w of the
+// row, issues ALL of its loads (MAXC chunks of 16 columns, sized to the slice) before the first
+// MFMA, and the 8 partial 16x16 tiles are summed through LDS.  With RMSNorm fused, the operand
+// is ln_w[k] * A[m,k] and the per-row 1/rms (from the squares of the same loaded A values, summed
+// across the block) scales the accumulator in the epilogue, so A is read exactly once.
+constexpr int SK_WAVES = 8;
 
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs sa) {
+// NT 16-column tiles per block share the activation loads (NT > 1 for the 32k-column lm_head,
+// which needs more bytes in flight per wave); two accumulator chains per tile halve the
+// dependent-MFMA latency of the K loop.
+template <int SK_MAXC, int NT>
+__global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   const GemmArgs& a = sa.g;
-  __shared__ float rstd_s[16];
-  __shared__ __attribute__((aligned(16))) float red[SK_WAVES][64][4];
+  __shared__ __attribute__((aligned(16))) f32x4 red[NT][SK_WAVES][64];
+  __shared__ float ssq_s[SK_WAVES][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = a.M, N = a.N, K = a.K;
-  const int n0 = blockIdx.x * 16;
   const int i = lane & 15, h = lane >> 4;
+  const bool rms = sa.rms_w != nullptr;
 
-  if (sa.rms_w) {
-    // 16 threads per row: sum of squares of A[row, :].
-    const int row = tid >> 4, sub = tid & 15;
-    float ss = 0.f;
-    if (row < M) {
-      const float* x = a.A + (int64_t)row * a.lda;
-      for (int k = sub * 4; k < K; k += 64) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(x + k);
-        ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
-      }
-    }
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) ss += __shfl_xor(ss, off, 64);
-    if (sub == 0) rstd_s[row] = 1.0f / sqrtf(ss / (float)K + sa.rms_eps);
-    __syncthreads();
-  }
-
-  // Each wave owns the K range [k_lo, k_hi) in 16-wide chunks.
   const int nchunk = (K + 15) / 16;
   const int per = (nchunk + SK_WAVES - 1) / SK_WAVES;
   const int c_lo = wave * per, c_hi = min(nchunk, c_lo + per);
-  const int wrow = n0 + i;
-  const bool wok = wrow < N, xok = i < M;
-  const float* wp = a.W + (int64_t)(wok ? wrow : 0) * a.ldw + h * 4;
-  const float* xp = a.A + (int64_t)(xok ? i : 0) * a.lda + h * 4;
-  const float xr = sa.rms_w && xok ? rstd_s[i] : 1.f;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  constexpr int U = 4;
-  const int c_full = min(c_hi, K / 16);
-  int c = c_lo;
-  for (; c + U <= c_full; c += U) {
-    f32x4 wv[U], xv[U];
+  const bool xok = i < M;
+  // Out-of-range lanes read a valid address and are zeroed after the load (no predicated
+  // loads: those serialize the load stream).
+  const float* wp[NT];
+  float wmask[NT];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = (c + u) * 16;
-      wv[u] = wok ? *reinterpret_cast<const f32x4*>(wp + k) : f32x4{0.f, 0.f, 0.f, 0.f};
-      xv[u] = xok ? *reinterpret_cast<const f32x4*>(xp + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NT; ++t) {
+    const int wrow = (blockIdx.x * NT + t) * 16 + i;
+    wp[t] = a.W + (int64_t)(wrow < N ? wrow : 0) * a.ldw + h * 4;
+    wmask[t] = wrow < N ? 1.f : 0.f;
+  }
+  const float* xp = a.A + (int64_t)(xok ? i : 0) * a.lda + h * 4;
+  const float xmask = xok ? 1.f : 0.f;
+  // Epilogue operands (residual, bias) are fetched up front by the epilogue waves.
+  const int m_ep = lane & 15;
+  float rres[4] = {0.f, 0.f, 0.f, 0.f}, rbias[4] = {0.f, 0.f, 0.f, 0.f};
+  if (wave < NT) {
+    const int n0e = (blockIdx.x * NT + wave) * 16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = min(n0e + (lane >> 4) * 4 + r, N - 1);
+      if (a.R) rres[r] = a.R[(int64_t)min(m_ep, M - 1) * a.ldr + n];
+      if (a.bias) rbias[r] = a.bias[n];
+    }
+  }
+  f32x4 acc[NT][2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
+  for (int c0 = c_lo; c0 < c_hi; c0 += SK_MAXC) {
+    f32x4 wv[NT][SK_MAXC], xv[SK_MAXC], gv[SK_MAXC];
+#pragma unroll
+    for (int u = 0; u < SK_MAXC; ++u) {
+      const int c = c0 + u;
+      const bool ok = c < c_hi && c * 16 + h * 4 < K;
+      const int cc = ok ? c : c_lo;
+      const float km = ok ? 1.f : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        wv[t][u] = *reinterpret_cast<const f32x4*>(wp[t] + cc * 16);
+        wv[t][u] *= km * wmask[t];
+      }
+      xv[u] = *reinterpret_cast<const f32x4*>(xp + cc * 16);
+      if (rms) gv[u] = *reinterpret_cast<const f32x4*>(sa.rms_w + cc * 16 + h * 4);
+      xv[u] *= km * xmask;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (sa.rms_w) {
-        const f32x4 g = *reinterpret_cast<const f32x4*>(sa.rms_w + (c + u) * 16 + h * 4);
+    for (int u = 0; u < SK_MAXC; ++u) {
+      if (rms) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xv[u][e] = (g[e] * (xv[u][e] * xr)) * sa.a_scale;
+        for (int e = 0; e < 4; ++e) {
+          ss += xv[u][e] * xv[u][e];
+          xv[u][e] = gv[u][e] * xv[u][e];
+        }
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u][e], xv[u][e], acc, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t][u & 1] =
+              __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][u][e], xv[u][e], acc[t][u & 1], 0, 0, 0);
     }
   }
-  for (; c < c_hi; ++c) {
-    const int k = c * 16 + h * 4;
-    f32x4 wv = {0.f, 0.f, 0.f, 0.f}, xv = {0.f, 0.f, 0.f, 0.f};
-    if (k < K) {
-      if (wok) wv = *reinterpret_cast<const f32x4*>(wp + c * 16);
-      if (xok) xv = *reinterpret_cast<const f32x4*>(xp + c * 16);
-      if (sa.rms_w) {
-        const f32x4 g = *reinterpret_cast<const f32x4*>(sa.rms_w + k);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] = (g[e] * (xv[e] * xr)) * sa.a_scale;
+  for (int t = 0; t < NT; ++t) red[t][wave][lane] = acc[t][0] + acc[t][1];
+  if (rms) {
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (lane < 16) ssq_s[wave][lane] = ss;
+  }
+  __syncthreads();
+  if (wave >= NT) return;
+  const int tile = blockIdx.x * NT + wave;
+  const int n0 = tile * 16;
+  f32x4 sum = red[wave][0][lane];
+#pragma unroll
+  for (int w = 1; w < SK_WAVES; ++w) sum += red[wave][w][lane];
+  // D[row = W row (n), col = A row (m)]: col = lane&15, row = (lane>>4)*4 + r.
+  const int m = lane & 15;
+  float scale = sa.a_scale;
+  if (rms) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][m];
+    scale = (1.0f / sqrtf(t / (float)K + sa.rms_eps)) * sa.a_scale;
+  }
+  if (sa.amax_val) {
+    // greedy head: per (row m, block) best column, lowest index on ties (torch.argmax)
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + (lane >> 4) * 4 + r;
+      const float v = sum[r] * scale;
+      if (n < N && (v > bv || (v == bv && n < bi))) {
+        bv = v;
+        bi = n;
       }
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[e], xv[e], acc, 0, 0, 0);
+    for (int off = 16; off <= 32; off <<= 1) {
+      const float ov = __shfl_xor(bv, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane < 16 && n0 < N) {
+      sa.amax_val[(int64_t)tile * 16 + m] = bv;
+      sa.amax_idx[(int64_t)tile * 16 + m] = bi;
+    }
+    if (!a.C) return;
   }
-  *reinterpret_cast<f32x4*>(&red[wave][lane][0]) = acc;
-  __syncthreads();
-  if (wave != 0) return;
-  f32x4 sum = *reinterpret_cast<const f32x4*>(&red[0][lane][0]);
-#pragma unroll
-  for (int w = 1; w < SK_WAVES; ++w) {
-    const f32x4 p = *reinterpret_cast<const f32x4*>(&red[w][lane][0]);
-    sum += p;
-  }
-  // D[row = W row (n), col = A row (m)]: col = lane&15, row = (lane>>4)*4 + r.
-  const int m = lane & 15;
   if (m >= M) return;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int n = n0 + (lane >> 4) * 4 + r;
     if (n >= N) continue;
-    float v = act_exact(sum[r] + (a.bias ? a.bias[n] : 0.f), a.act);
-    if (a.R) v = a.R[(int64_t)m * a.ldr + n] + v;
+    float v = act_exact(sum[r] * scale + rbias[r], a.act);
+    if (a.R) v = rres[r] + v;
     a.C[(int64_t)m * a.ldc + n] = v;
   }
 }
@@ -332,11 +381,17 @@ int gemm(const GemmArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                   aligned16(a.W),
               "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-  const int64_t blocks128 = cdiv(a.M, 128) * cdiv(a.N, 64);
-  // Larger tiles halve LDS traffic per FLOP but only pay while the grid still fills the chip.
+  // Larger tiles cut LDS/L2 traffic per FLOP but only pay while the grid still covers the 256
+  // CUs; at batch 16 many projections have N = 512..768 over M = 300..1200 rows, where a 64x64
+  // grid leaves most CUs idle, so the tile shrinks until the grid fills the chip.
+  const int64_t b128 = cdiv(a.M, 128) * cdiv(a.N, 64);
+  const int64_t b64 = cdiv(a.M, 64) * cdiv(a.N, 64);
+  const int64_t b3264 = cdiv(a.M, 32) * cdiv(a.N, 64);
   return probed(PROBE_GEMM, a, s, [&]() {
-    if (blocks128 >= 512) return launch_gemm<128, 64, 2, 1>(a, s);
-    return launch_gemm<64, 64, 1, 1>(a, s);
+    if (b128 >= 512) return launch_gemm<128, 64, 2, 1>(a, s);
+    if (b64 >= 384) return launch_gemm<64, 64, 1, 1>(a, s);
+    if (b3264 >= 256) return launch_gemm<32, 64, 1, 1>(a, s);
+    return launch_gemm<32, 32, 1, 1>(a, s);
   });
 }
 
@@ -347,9 +402,20 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                   aligned16(a.W) && (!sa.rms_w || aligned16(sa.rms_w)),
               "gemm_skinny: K/lda/ldw must be multiples of 4, operands 16-byte aligned");
+  MPR_REQUIRE(!sa.amax_val || (sa.amax_idx && !a.R && !a.bias && a.act == ACT_NONE),
+              "gemm_skinny: argmax mode takes plain logits");
+  const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
+  const int64_t tiles = cdiv(a.N, 16);
   return probed(PROBE_SKINNY, a, s, [&]() {
-    dim3 grid((unsigned)cdiv(a.N, 16));
-    hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), 0, s, sa);
+    if (tiles >= 1024 && per <= 4)   // lm_head: 4 tiles per block, more loads in flight
+      hipLaunchKernelGGL((gemm_skinny_kernel<4, 4>), dim3((unsigned)cdiv(tiles, 4)), dim3(512),
+                         0, s, sa);
+    else if (per <= 4)
+      hipLaunchKernelGGL((gemm_skinny_kernel<4, 1>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
+    else if (per <= 8)
+      hipLaunchKernelGGL((gemm_skinny_kernel<8, 1>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
+    else
+      hipLaunchKernelGGL((gemm_skinny_kernel<16, 1>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
     MPR_LAUNCHED();
     return MPR_OK;
   });

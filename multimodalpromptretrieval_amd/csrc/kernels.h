@@ -34,6 +34,9 @@ struct SkinnyArgs {
   const float* rms_w = nullptr;  // fuse RMSNorm prologue when non-null
   float rms_eps = 1e-6f;
   float a_scale = 1.f;           // A' = (ln_w * (A * rstd)) * a_scale (T5 tied-head d^-0.5)
+  // Greedy head: per (block, row) best column -> amax_val/idx[block*16 + row] (C may be null).
+  float* amax_val = nullptr;
+  int32_t* amax_idx = nullptr;
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
@@ -66,8 +69,9 @@ struct AttnArgs {
   int q_pos0 = 0;   // absolute position of query row 0
   const float* key_mask = nullptr;  // [B, mask_bs] 1/0 (0 = padded key), optional
   int64_t mask_bs = 0;
-  const float* rel_bias = nullptr;  // [num_buckets, H] T5 relative attention bias, optional
-  const int* bucket_lut = nullptr;  // bucket of (j - (i + q_pos0)) at index rel + lut_radius
+  // T5 relative position bias by offset: rel_tab[(j - (i + q_pos0) + lut_radius) * H + h]
+  // (the layer-0 bias table gathered through the bucket LUT once at model load), optional.
+  const float* rel_tab = nullptr;
   int lut_radius = 0;
 };
 int attention(const AttnArgs& a, hipStream_t s);
@@ -86,12 +90,13 @@ int eot_gather(const float* x, const int32_t* tok, int B, int L, int ctx, int D,
                hipStream_t s);
 // Row argmax (first maximal index, torch.argmax semantics).
 int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hipStream_t s);
-// Greedy-search step (GenerationMixin._sample, do_sample=False): next = argmax(logits[b]);
-// finished rows emit pad; tokens[b*tok_ld + col] = next; unfinished[b] &= next != eos;
+// Greedy-search step (GenerationMixin._sample, do_sample=False): next = argmax over the
+// lm_head's per-block partials part_*[p*16 + b] (first maximal index); finished rows emit pad;
+// tokens[b*tok_ld + col] = next; unfinished[b] &= next != eos;
 // x[b, :] = table[next, :] (decoder input embedding of the next step, may be null).
-int greedy_step(const float* logits, int M, int V, int32_t* unfinished, int32_t* tokens,
-                int64_t tok_ld, int col, int eos, int pad, const float* table, int D, float* x,
-                hipStream_t s);
+int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int M,
+                int32_t* unfinished, int32_t* tokens, int64_t tok_ld, int col, int eos, int pad,
+                const float* table, int D, float* x, hipStream_t s);
 
 // Generic device helpers.
 int fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s);

@@ -152,10 +152,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
       const int qpos = i + a.q_pos0;
       bool valid = kvalid && (!a.causal || j <= qpos);
       float sc = s[r] * a.scale;
-      if (a.rel_bias && valid) {
-        const int bucket = a.bucket_lut[j - qpos + a.lut_radius];
-        sc += a.rel_bias[bucket * a.H + h];
-      }
+      if (a.rel_tab && valid) sc += a.rel_tab[(int64_t)(j - qpos + a.lut_radius) * a.H + h];
       sc = valid ? sc : -INFINITY;
       const float mnew = fmaxf(m[r], wave_max(sc));
       float p = 0.f, alpha = 1.f;
@@ -190,6 +187,82 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
     const int i = row0 + r;
     if (i < a.Lq)
       a.o[(int64_t)b * a.o_bs + (int64_t)i * a.o_rs + h * ATT_D + lane] = o[r] / l[r];
+  }
+}
+
+// Single query row (decoder step): one 256-thread block per (batch, head), up to 256 keys per
+// pass.  Every global load of a pass — q (broadcast), the thread's key row (16 x 16 B), the
+// thread's value slice (4 dims x 16 keys as 16 x 16 B; a wave-instruction covers 4 whole 256 B
+// value rows), the mask word and the bias-by-offset word — is independent of the others and
+// issued up front, so a pass costs one memory round trip; max / sum / P go through LDS.
+constexpr int DEC_KC = 256;
+
+__global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
+  __shared__ float red[2][4];
+  __shared__ float Ps[DEC_KC];
+  __shared__ __attribute__((aligned(16))) float Os[16][ATT_D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const float* qp = a.q + (int64_t)b * a.q_bs + h * ATT_D;
+  const int qpos = a.q_pos0;
+  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
+  const float* kb = a.k + (int64_t)b * a.k_bs + h * ATT_D;
+  const float* vb = a.v + (int64_t)b * a.v_bs + h * ATT_D;
+  int lk_end = a.Lk;
+  if (a.causal) lk_end = min(lk_end, qpos + 1);
+  const int dg = tid & 15, kg = tid >> 4;  // PV: dims 4*dg..4*dg+3, keys kg*16..kg*16+15
+  float m = -INFINITY, l = 0.f;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < lk_end; kc += DEC_KC) {
+    const int j = kc + tid;
+    const bool in = j < lk_end;
+    const float* kp = kb + (int64_t)(in ? j : kc) * a.k_rs;
+    f32x4 kr[ATT_D / 4], qv[ATT_D / 4], vr[16];
+#pragma unroll
+    for (int d = 0; d < ATT_D / 4; ++d) {
+      kr[d] = *reinterpret_cast<const f32x4*>(kp + 4 * d);
+      qv[d] = *reinterpret_cast<const f32x4*>(qp + 4 * d);
+    }
+    const int jv0 = kc + kg * 16;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int jv = jv0 + u < lk_end ? jv0 + u : kc;
+      vr[u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)jv * a.v_rs + 4 * dg);
+    }
+    const float mk = (maskb && in) ? maskb[j] : 1.f;
+    const float rb = (a.rel_tab && in) ? a.rel_tab[(int64_t)(j - qpos + a.lut_radius) * a.H + h]
+                                       : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < ATT_D / 4; ++d)
+      s += qv[d][0] * kr[d][0] + qv[d][1] * kr[d][1] + qv[d][2] * kr[d][2] + qv[d][3] * kr[d][3];
+    const bool valid = in && mk != 0.f;
+    const float sc = valid ? s * a.scale + rb : -INFINITY;
+    float wm = wave_max(sc);
+    if (lane == 0) red[0][wave] = wm;
+    __syncthreads();
+    const float cmax = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    const float mnew = fmaxf(m, cmax);
+    const float p = valid ? expf(sc - mnew) : 0.f;
+    const float alpha = (m == -INFINITY) ? (mnew == -INFINITY ? 1.f : 0.f) : expf(m - mnew);
+    Ps[tid] = p;
+    const float ws = wave_sum(p);
+    if (lane == 0) red[1][wave] = ws;
+    __syncthreads();
+    l = l * alpha + ((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+    m = mnew;
+    o *= alpha;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) o += Ps[kg * 16 + u] * vr[u];
+    __syncthreads();  // Ps / red reused by the next pass
+  }
+  *reinterpret_cast<f32x4*>(&Os[kg][4 * dg]) = o;
+  __syncthreads();
+  if (wave == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += Os[g][lane];
+    a.o[(int64_t)b * a.o_bs + h * ATT_D + lane] = s / l;
   }
 }
 
@@ -286,20 +359,32 @@ __global__ __launch_bounds__(256) void argmax_rows_kernel(const float* logits, i
 
 // One block per row: argmax over the vocabulary, then the greedy-search bookkeeping and the
 // embedding gather of the chosen token for the next decoder step.
-__global__ __launch_bounds__(256) void greedy_step_kernel(const float* logits, int V,
+__global__ __launch_bounds__(256) void greedy_step_kernel(const float* part_val,
+                                                          const int32_t* part_idx, int nparts,
                                                           int32_t* unfinished, int32_t* tokens,
                                                           int64_t tok_ld, int col, int eos,
                                                           int pad, const float* table, int D,
                                                           float* x) {
   const int row = blockIdx.x;
-  const float* lg = logits + (int64_t)row * V;
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int c = threadIdx.x; c < V; c += 256) {
-    const float v = lg[c];
-    if (v > best || (v == best && c < bi)) {
-      best = v;
-      bi = c;
+  for (int p0 = 0; p0 < nparts; p0 += 256 * 8) {
+    float v[8];
+    int c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // all loads first: one round trip per 2048 partials
+      const int p = p0 + u * 256 + threadIdx.x;
+      const int pc = p < nparts ? p : 0;
+      v[u] = part_val[(int64_t)pc * 16 + row];
+      c[u] = part_idx[(int64_t)pc * 16 + row];
+      if (p >= nparts) v[u] = -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (v[u] > best || (v[u] == best && c[u] < bi)) {
+        best = v[u];
+        bi = c[u];
+      }
     }
   }
   __shared__ float bv[256];
@@ -425,10 +510,15 @@ int rmsnorm(const float* x, int64_t ldx, int M, int D, const float* w, float eps
 int attention(const AttnArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attention: bad shape");
   if (a.B == 0 || a.Lq == 0) return MPR_OK;
-  MPR_REQUIRE(!a.rel_bias || a.bucket_lut, "attention: rel_bias needs a bucket lut");
-  if (a.rel_bias)
-    MPR_REQUIRE(a.lut_radius >= a.Lk + a.Lq + a.q_pos0, "attention: bucket lut radius %d too small",
+  if (a.rel_tab)
+    MPR_REQUIRE(a.lut_radius >= a.Lk + a.Lq + a.q_pos0, "attention: bias table radius %d too small",
                 a.lut_radius);
+  if (a.Lq == 1) {
+    hipLaunchKernelGGL(attention_decode_kernel, dim3((unsigned)((int64_t)a.B * a.H)), dim3(256),
+                       0, s, a);
+    MPR_LAUNCHED();
+    return MPR_OK;
+  }
   dim3 grid((unsigned)cdiv(a.Lq, ATT_QR), (unsigned)a.H, (unsigned)a.B);
   hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, a);
   MPR_LAUNCHED();
@@ -481,12 +571,13 @@ int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hip
   return MPR_OK;
 }
 
-int greedy_step(const float* logits, int M, int V, int32_t* unfinished, int32_t* tokens,
-                int64_t tok_ld, int col, int eos, int pad, const float* table, int D, float* x,
-                hipStream_t s) {
+int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int M,
+                int32_t* unfinished, int32_t* tokens, int64_t tok_ld, int col, int eos, int pad,
+                const float* table, int D, float* x, hipStream_t s) {
   if (M == 0) return MPR_OK;
-  hipLaunchKernelGGL(greedy_step_kernel, dim3(M), dim3(256), 0, s, logits, V, unfinished, tokens,
-                     tok_ld, col, eos, pad, table, D, x);
+  MPR_REQUIRE(M <= 16, "greedy_step: %d rows > 16", M);
+  hipLaunchKernelGGL(greedy_step_kernel, dim3(M), dim3(256), 0, s, part_val, part_idx, nparts,
+                     unfinished, tokens, tok_ld, col, eos, pad, table, D, x);
   MPR_LAUNCHED();
   return MPR_OK;
 }

@@ -66,12 +66,23 @@ struct T5Layer {
 
 struct T5Model : mpr_model {
   T5Model() : mpr_model(T5) {}
+  ~T5Model() override;
   int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
   int inner = 0, lut_radius = 0;
-  DevBuf shared, enc_rel, dec_rel, enc_final, dec_final, lm_head, cross_kv_w, enc_lut, dec_lut;
+  DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
+  // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
+  DevBuf enc_tab, dec_tab;
   std::vector<std::unique_ptr<T5Layer>> enc, dec;
-  // workspace
-  DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, logits, unfinished, cur_tok, cew;
+  // workspace (every growth bumps `gen`, which invalidates captured decode graphs)
+  DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, unfinished, cur_tok;
+  DevBuf enc_in, mask_in, part_val, part_idx, tok_buf;
+  uint64_t gen = 0;
+  hipStream_t cap_stream = nullptr;
+  struct GraphEnt {
+    hipGraphExec_t exec;
+    uint64_t gen;
+  };
+  std::map<std::tuple<int, int, int, int, int, int>, GraphEnt> graphs;
 
   int encode(const float* embeds, const float* mask, int B, int L, float* out, hipStream_t s);
   int generate(const float* embeds, const float* mask, int B, int L, int max_new, int start,
@@ -82,7 +93,9 @@ struct T5Model : mpr_model {
             hipStream_t s);
 
  private:
+  int grow(DevBuf& b, size_t bytes);
   int cross_kv_project(int B, int L, hipStream_t s);
+  int generate_body(int B, int L, int max_new, int start, int eos, int pad, hipStream_t s);
 };
 
 }  // namespace mpr

@@ -8,15 +8,39 @@
 //   decoder) shared by every layer, padding mask on encoder keys; ReLU FFN; final RMSNorm, then
 //   * d_model^-0.5 before the tied lm_head (scale_decoder_outputs).
 // Decoder steps run M = batch rows: every projection is a skinny GEMM with the preceding RMSNorm
-// fused into its operand load; K/V of the self-attention live in a per-layer cache laid out
-// [B][max_new][3*inner] (the fused q|k|v row of each generated position), and the cross-attention
-// K/V of every decoder layer are projected once from the encoder output by one GEMM.
+// fused (operand ln_w*x, 1/rms applied in the epilogue); K/V of the self-attention live in a
+// per-layer cache laid out [B][max_new][3*inner] (the fused q|k|v row of each generated position);
+// the cross-attention K/V of every decoder layer come from one GEMM over the encoder output; the
+// lm_head never materialises logits: each block emits its per-row best column and greedy_step
+// reduces those and gathers the next input embedding.  The whole generate() — encoder, cross K/V
+// projection and all decode steps, ~50 launches per step — is captured once per shape into a
+// hipGraph (private capture stream) and replayed on the caller's stream.
+#include <cstdlib>
+
 #include "models.h"
 
 namespace mpr {
 
 namespace {
 constexpr float T5_EPS = 1e-6f;
+constexpr size_t MAX_GRAPHS = 64;
+
+bool graphs_enabled() {
+  const char* e = getenv("MPR_GRAPHS");
+  return !(e && e[0] == '0');
+}
+}  // namespace
+
+T5Model::~T5Model() {
+  for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
+  if (cap_stream) (void)hipStreamDestroy(cap_stream);
+}
+
+int T5Model::grow(DevBuf& b, size_t bytes) {
+  void* before = b.ptr;
+  MPR_TRY(b.ensure(bytes));
+  if (b.ptr != before) ++gen;
+  return MPR_OK;
 }
 
 int T5Model::embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
@@ -31,11 +55,11 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
               lut_radius);
   if (B == 0) return MPR_OK;
   const int M = B * L;
-  MPR_TRY(x.ensure((size_t)M * d * 4));
-  MPR_TRY(h.ensure((size_t)M * d * 4));
-  MPR_TRY(qkv.ensure((size_t)M * 3 * inner * 4));
-  MPR_TRY(ao.ensure((size_t)M * inner * 4));
-  MPR_TRY(ff.ensure((size_t)M * dff * 4));
+  MPR_TRY(grow(x, (size_t)M * d * 4));
+  MPR_TRY(grow(h, (size_t)M * d * 4));
+  MPR_TRY(grow(qkv, (size_t)M * 3 * inner * 4));
+  MPR_TRY(grow(ao, (size_t)M * inner * 4));
+  MPR_TRY(grow(ff, (size_t)M * dff * 4));
   float* xp = x.as<float>();
   float* hp = h.as<float>();
   float* qp = qkv.as<float>();
@@ -56,7 +80,7 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
     at.o = ap; at.o_bs = (int64_t)L * inner; at.o_rs = inner;
     at.B = B; at.H = H; at.Lq = L; at.Lk = L; at.scale = 1.f;
     at.key_mask = mask; at.mask_bs = L;
-    at.rel_bias = enc_rel.as<float>(); at.bucket_lut = enc_lut.as<int>();
+    at.rel_tab = enc_tab.as<float>();
     at.lut_radius = lut_radius;
     MPR_TRY(attention(at, s));
     GemmArgs o;
@@ -79,51 +103,36 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
 
 int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
   const int M = B * L, N = Ld * 2 * inner;
-  MPR_TRY(cross_kv.ensure((size_t)M * N * 4));
   GemmArgs g;
   g.A = enc_out.as<float>(); g.lda = d; g.W = cross_kv_w.as<float>(); g.ldw = d;
   g.C = cross_kv.as<float>(); g.ldc = N; g.M = M; g.N = N; g.K = d;
   return gemm(g, s);
 }
 
-int T5Model::generate(const float* embeds, const float* mask, int B, int L, int max_new,
-                      int start, int eos, int pad, int32_t* out_tokens, hipStream_t s) {
-  MPR_REQUIRE(B >= 0 && B <= 16, "t5 generate: batch %d > 16 unsupported by the decode path", B);
-  MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
-  MPR_REQUIRE(max_new + 1 <= lut_radius, "t5 generate: max_new exceeds lut radius");
-  if (B == 0) return MPR_OK;
-  const int T1 = max_new + 1;
-  MPR_TRY(enc_out.ensure((size_t)B * L * d * 4));
-  MPR_TRY(encode(embeds, mask, B, L, enc_out.as<float>(), s));
-  MPR_TRY(cross_kv_project(B, L, s));
-  const int Tc = max_new > 0 ? max_new : 1;
+// Everything generate() enqueues after its inputs sit in enc_in / mask_in.  Only model-owned
+// buffers are touched, so the sequence can be captured into a graph and replayed.
+int T5Model::generate_body(int B, int L, int max_new, int start, int eos, int pad,
+                           hipStream_t s) {
+  const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
-  MPR_TRY(cache.ensure((size_t)Ld * cache_layer * 4));
-  MPR_TRY(dx.ensure((size_t)B * d * 4));
-  MPR_TRY(dq.ensure((size_t)B * inner * 4));
-  MPR_TRY(ao.ensure((size_t)B * inner * 4));
-  MPR_TRY(ff.ensure((size_t)B * dff * 4));
-  MPR_TRY(logits.ensure((size_t)B * V * 4));
-  MPR_TRY(unfinished.ensure((size_t)B * 4));
-  MPR_TRY(cur_tok.ensure((size_t)B * 4));
+  const int nparts = (int)cdiv(V, 16);
+  const float* maskp = mask_in.as<float>();
+  MPR_TRY(encode(enc_in.as<float>(), maskp, B, L, enc_out.as<float>(), s));
+  MPR_TRY(cross_kv_project(B, L, s));
   float* xp = dx.as<float>();
   float* qp = dq.as<float>();
   float* ap = ao.as<float>();
   float* fp = ff.as<float>();
-  float* lg = logits.as<float>();
   int32_t* unf = unfinished.as<int32_t>();
   int32_t* ct = cur_tok.as<int32_t>();
+  int32_t* toks = tok_buf.as<int32_t>();
   const float* ckv = cross_kv.as<float>();
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
 
   MPR_TRY(fill_i32(unf, 1, B, s));
   MPR_TRY(fill_i32(ct, start, B, s));
-  // tokens[:, 0] = decoder_start
+  MPR_TRY(fill_i32(toks, start, (int64_t)B * T1, s));  // column 0 = decoder_start
   MPR_TRY(embed_gather(shared.as<float>(), ct, 1, B, 1, d, nullptr, xp, d, 0, s));
-  {
-    // column 0 of the output
-    MPR_HIP(hipMemcpy2DAsync(out_tokens, (size_t)T1 * 4, ct, 4, 4, B, hipMemcpyDeviceToDevice, s));
-  }
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
   for (int t = 0; t < max_new; ++t) {
     for (int l = 0; l < Ld; ++l) {
@@ -140,7 +149,7 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
       at.v = cl + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
       at.o = ap; at.o_bs = inner; at.o_rs = inner;
       at.B = B; at.H = H; at.Lq = 1; at.Lk = t + 1; at.scale = 1.f; at.causal = 1; at.q_pos0 = t;
-      at.rel_bias = dec_rel.as<float>(); at.bucket_lut = dec_lut.as<int>();
+      at.rel_tab = dec_tab.as<float>();
       at.lut_radius = lut_radius;
       MPR_TRY(attention(at, s));
       SkinnyArgs so;
@@ -158,7 +167,7 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
       ca.v = ckv + (int64_t)l * 2 * inner + inner; ca.v_bs = ca.k_bs; ca.v_rs = ckv_ld;
       ca.o = ap; ca.o_bs = inner; ca.o_rs = inner;
       ca.B = B; ca.H = H; ca.Lq = 1; ca.Lk = L; ca.scale = 1.f;
-      ca.key_mask = mask; ca.mask_bs = L;
+      ca.key_mask = maskp; ca.mask_bs = L;
       MPR_TRY(attention(ca, s));
       SkinnyArgs co;
       co.g.A = ap; co.g.lda = inner; co.g.W = ly.co.as<float>(); co.g.ldw = inner; co.g.R = xp;
@@ -175,13 +184,82 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
       MPR_TRY(gemm_skinny(fo, s));
     }
     SkinnyArgs hd;
-    hd.g.A = xp; hd.g.lda = d; hd.g.W = lm_head.as<float>(); hd.g.ldw = d; hd.g.C = lg;
-    hd.g.ldc = V; hd.g.M = B; hd.g.N = V; hd.g.K = d; hd.rms_w = dec_final.as<float>();
+    hd.g.A = xp; hd.g.lda = d; hd.g.W = lm_head.as<float>(); hd.g.ldw = d; hd.g.C = nullptr;
+    hd.g.M = B; hd.g.N = V; hd.g.K = d; hd.rms_w = dec_final.as<float>();
     hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
+    hd.amax_val = part_val.as<float>(); hd.amax_idx = part_idx.as<int32_t>();
     MPR_TRY(gemm_skinny(hd, s));
-    MPR_TRY(greedy_step(lg, B, V, unf, out_tokens, T1, t + 1, eos, pad, shared.as<float>(), d,
-                        t + 1 < max_new ? xp : nullptr, s));
+    MPR_TRY(greedy_step(part_val.as<float>(), part_idx.as<int32_t>(), nparts, B, unf, toks, T1,
+                        t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,
+                        s));
   }
+  return MPR_OK;
+}
+
+int T5Model::generate(const float* embeds, const float* mask, int B, int L, int max_new,
+                      int start, int eos, int pad, int32_t* out_tokens, hipStream_t s) {
+  MPR_REQUIRE(B >= 0 && B <= 16, "t5 generate: batch %d > 16 unsupported by the decode path", B);
+  MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
+  MPR_REQUIRE(max_new + 1 <= lut_radius, "t5 generate: max_new exceeds lut radius");
+  MPR_REQUIRE(2 * L <= lut_radius && L >= 1, "t5 generate: L=%d", L);
+  if (B == 0) return MPR_OK;
+  const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
+  const int M = B * L, nparts = (int)cdiv(V, 16);
+  // Every buffer the body touches is sized before capture (no allocation inside a graph).
+  MPR_TRY(grow(enc_in, (size_t)M * d * 4));
+  MPR_TRY(grow(mask_in, (size_t)M * 4));
+  MPR_TRY(grow(enc_out, (size_t)M * d * 4));
+  MPR_TRY(grow(cross_kv, (size_t)M * Ld * 2 * inner * 4));
+  MPR_TRY(grow(x, (size_t)M * d * 4));
+  MPR_TRY(grow(h, (size_t)M * d * 4));
+  MPR_TRY(grow(qkv, (size_t)M * 3 * inner * 4));
+  MPR_TRY(grow(ao, (size_t)M * (inner > dff ? inner : dff) * 4));
+  MPR_TRY(grow(ff, (size_t)M * dff * 4));
+  MPR_TRY(grow(cache, (size_t)Ld * B * Tc * 3 * inner * 4));
+  MPR_TRY(grow(dx, (size_t)B * d * 4));
+  MPR_TRY(grow(dq, (size_t)B * inner * 4));
+  MPR_TRY(grow(part_val, (size_t)nparts * 16 * 4));
+  MPR_TRY(grow(part_idx, (size_t)nparts * 16 * 4));
+  MPR_TRY(grow(unfinished, (size_t)16 * 4));
+  MPR_TRY(grow(cur_tok, (size_t)16 * 4));
+  MPR_TRY(grow(tok_buf, (size_t)B * T1 * 4));
+  MPR_HIP(hipMemcpyAsync(enc_in.ptr, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
+  MPR_HIP(hipMemcpyAsync(mask_in.ptr, mask, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
+  if (!graphs_enabled()) {
+    MPR_TRY(generate_body(B, L, max_new, start, eos, pad, s));
+  } else {
+    auto key = std::make_tuple(B, L, max_new, start, eos, pad);
+    auto it = graphs.find(key);
+    if (it != graphs.end() && it->second.gen != gen) {
+      for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
+      graphs.clear();
+      it = graphs.end();
+    }
+    if (it == graphs.end()) {
+      if (graphs.size() >= MAX_GRAPHS) {
+        for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
+        graphs.clear();
+      }
+      if (!cap_stream) MPR_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+      hipGraph_t graph = nullptr;
+      MPR_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
+      const int rc = generate_body(B, L, max_new, start, eos, pad, cap_stream);
+      const hipError_t ec = hipStreamEndCapture(cap_stream, &graph);
+      if (rc != MPR_OK) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+      }
+      MPR_HIP(ec);
+      hipGraphExec_t exec = nullptr;
+      const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      MPR_HIP(ei);
+      it = graphs.emplace(key, GraphEnt{exec, gen}).first;
+    }
+    MPR_HIP(hipGraphLaunch(it->second.exec, s));
+  }
+  MPR_HIP(hipMemcpyAsync(out_tokens, tok_buf.ptr, (size_t)B * T1 * 4, hipMemcpyDeviceToDevice,
+                         s));
   return MPR_OK;
 }
 
@@ -189,16 +267,17 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
                        const int32_t* dec_in, int T, float* logits_out, hipStream_t s) {
   MPR_REQUIRE(T >= 1 && T <= lut_radius, "t5 logits: T=%d", T);
   if (B == 0) return MPR_OK;
-  MPR_TRY(enc_out.ensure((size_t)B * L * d * 4));
+  MPR_TRY(grow(enc_out, (size_t)B * L * d * 4));
+  MPR_TRY(grow(cross_kv, (size_t)B * L * Ld * 2 * inner * 4));
   MPR_TRY(encode(embeds, mask, B, L, enc_out.as<float>(), s));
   MPR_TRY(cross_kv_project(B, L, s));
   const int M = B * T;
-  MPR_TRY(x.ensure((size_t)M * d * 4));
-  MPR_TRY(h.ensure((size_t)M * d * 4));
-  MPR_TRY(qkv.ensure((size_t)M * 3 * inner * 4));
-  MPR_TRY(ao.ensure((size_t)M * inner * 4));
-  MPR_TRY(dq.ensure((size_t)M * inner * 4));
-  MPR_TRY(ff.ensure((size_t)M * dff * 4));
+  MPR_TRY(grow(x, (size_t)M * d * 4));
+  MPR_TRY(grow(h, (size_t)M * d * 4));
+  MPR_TRY(grow(qkv, (size_t)M * 3 * inner * 4));
+  MPR_TRY(grow(ao, (size_t)M * inner * 4));
+  MPR_TRY(grow(dq, (size_t)M * inner * 4));
+  MPR_TRY(grow(ff, (size_t)M * dff * 4));
   float* xp = x.as<float>();
   float* hp = h.as<float>();
   float* qp = qkv.as<float>();
@@ -221,7 +300,7 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
     at.v = qp + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
     at.o = ap; at.o_bs = (int64_t)T * inner; at.o_rs = inner;
     at.B = B; at.H = H; at.Lq = T; at.Lk = T; at.scale = 1.f; at.causal = 1;
-    at.rel_bias = dec_rel.as<float>(); at.bucket_lut = dec_lut.as<int>();
+    at.rel_tab = dec_tab.as<float>();
     at.lut_radius = lut_radius;
     MPR_TRY(attention(at, s));
     GemmArgs o;
@@ -255,9 +334,8 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
     w.C = xp; w.ldc = d; w.M = M; w.N = d; w.K = dff;
     MPR_TRY(gemm(w, s));
   }
-  // final norm * d^-0.5 -> tied head
+  // final norm, then * d^-0.5 (the reference's op order, modeling_t5.py scale_decoder_outputs)
   MPR_TRY(rmsnorm(xp, d, M, d, dec_final.as<float>(), T5_EPS, hp, d, s));
-  // h *= d^-0.5 after the norm, the reference's op order (modeling_t5.py scale_decoder_outputs)
   if (scale_out) MPR_TRY(scale_inplace(hp, (int64_t)M * d, 1.0f / sqrtf((float)d), s));
   GemmArgs hd;
   hd.A = hp; hd.lda = d; hd.W = lm_head.as<float>(); hd.ldw = d; hd.C = logits_out; hd.ldc = V;

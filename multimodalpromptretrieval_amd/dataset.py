@@ -84,14 +84,30 @@ class VQARetrieval:
     # ---- encoding ------------------------------------------------------------------------------
     def encode_queries(self, batch) -> torch.Tensor:
         """[CLS image embedding ‖ EOT text embedding] fp32 [B, 1024] on the device
-        (dataset/VQAFeatureDataset.py:189-191, 146-148)."""
-        img = batch["image"]
+        (dataset/VQAFeatureDataset.py:189-191, 146-148).  The two towers run concurrently on
+        two side streams (each fills only part of the chip at batch 16) and write their halves
+        of the query rows in place; the caller's stream waits for both."""
+        cur = torch.cuda.current_stream(self.device)
+        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+        toks = self.clip_tokenize(batch["question"])
         B = img.shape[0]
         q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
         di = self.image_encoder.out_dim
-        self.image_encoder(img, CLS, out=q, out_bstride=self.embed_dim)
-        toks = self.clip_tokenize(batch["question"])
-        self.text_encoder(toks, out=q[:, di:], out_bstride=self.embed_dim)
+        if not hasattr(self, "_s_img"):
+            self._s_img = torch.cuda.Stream(self.device)
+            self._s_txt = torch.cuda.Stream(self.device)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        for s in (self._s_img, self._s_txt):
+            s.wait_event(ev)
+            q.record_stream(s)
+        img.record_stream(self._s_img)
+        with torch.cuda.stream(self._s_img):
+            self.image_encoder(img, CLS, out=q, out_bstride=self.embed_dim)
+        with torch.cuda.stream(self._s_txt):
+            self.text_encoder(toks, out=q[:, di:], out_bstride=self.embed_dim)
+        cur.wait_stream(self._s_img)
+        cur.wait_stream(self._s_txt)
         return q
 
     # ---- index -------------------------------------------------------------------------------

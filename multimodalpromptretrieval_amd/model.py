@@ -195,7 +195,27 @@ class T5VisionModel(nn.Module):
         return self._device_vit()(x, TOKENS)
 
     def prepare_input(self, batch):
-        """architectures/T5VisionModel.py:141-184."""
+        """architectures/T5VisionModel.py:141-184.
+
+        The token-feature ViT does not depend on retrieval, so it is enqueued first on a side
+        stream and runs on the GPU while the retrieval function encodes/scans and the host
+        builds and tokenises the prompts."""
+        vit = self._device_vit()
+        t5 = self._device_t5()
+        if self.use_image_info and vit.out_dim != t5.d_model:
+            raise RuntimeError(f"Sizes of tensors must match: image tokens are {vit.out_dim}-d, "
+                               f"{self.T5_version} d_model is {t5.d_model} (torch.cat at "
+                               f"architectures/T5VisionModel.py:176)")
+        cur = torch.cuda.current_stream(self.device)
+        img_tok = None
+        if self.use_image_info:
+            img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+            if not hasattr(self, "_s_tok"):
+                self._s_tok = torch.cuda.Stream(self.device)
+            self._s_tok.wait_stream(cur)
+            img.record_stream(self._s_tok)
+            with torch.cuda.stream(self._s_tok):
+                img_tok = vit(img, TOKENS)
         if self.retrieval_function:
             if self.use_quantifier:
                 retrieved_info = self.retrieval_function(batch)
@@ -204,10 +224,7 @@ class T5VisionModel(nn.Module):
         else:
             retrieved_info = ["" for _ in batch["task"]]
         task_prefixes = [f"Answer the {x} question: " for x in batch["task"]]
-        vit = self._device_vit()
-        t5 = self._device_t5()
-        img = batch["image"]
-        B = img.shape[0]
+        B = batch["image"].shape[0]
         sentences = [task_prefixes[i] + batch["question"][i] + retrieved_info[i]
                      for i in range(len(batch["question"]))]
         encoding = self.tokenizer(sentences, padding="longest",
@@ -216,25 +233,32 @@ class T5VisionModel(nn.Module):
         ids = encoding["input_ids"]
         L = ids.shape[1]
         T = vit.tokens if self.use_image_info else 0
-        if self.use_image_info and vit.out_dim != t5.d_model:
-            raise RuntimeError(f"Sizes of tensors must match: image tokens are {vit.out_dim}-d, "
-                               f"{self.T5_version} d_model is {t5.d_model} (torch.cat at "
-                               f"architectures/T5VisionModel.py:176)")
         combined = torch.empty((B, T + L, t5.d_model), device=self.device, dtype=torch.float32)
         if self.use_image_info:
-            vit(img, TOKENS, out=combined, out_bstride=(T + L) * t5.d_model)
+            cur.wait_stream(self._s_tok)
+            img_tok.record_stream(cur)
+            combined[:, :T].copy_(img_tok)
         t5.embed(ids, combined, row0=T)
-        mask = torch.ones((B, T + L), dtype=torch.float32)
-        mask[:, T:] = encoding["attention_mask"].float()
+        if self.use_image_info:
+            mask = torch.ones((B, T + L), dtype=torch.float32)
+            mask[:, T:] = encoding["attention_mask"].float()
+        else:
+            mask = encoding["attention_mask"]
         return combined, mask.to(self.device), encoding
 
     def predict(self, batch, output_attentions=False):
         """architectures/T5VisionModel.py:196-216 (greedy, max_new_tokens=20)."""
         if output_attentions:
             raise NotImplementedError("output_attentions is the eval-only plotting path")
-        combined, mask, _ = self.prepare_input(batch)
-        seqs = self.T5_model.generate(inputs_embeds=combined, attention_mask=mask,
-                                      do_sample=False, max_new_tokens=self.max_new_tokens)
+        # Whole predict() on a private (non-default) stream: eager launches on the legacy
+        # default stream cost more per kernel; the result is host strings, so no stream handoff.
+        if not hasattr(self, "_s_main"):
+            self._s_main = torch.cuda.Stream(self.device)
+        self._s_main.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._s_main):
+            combined, mask, _ = self.prepare_input(batch)
+            seqs = self.T5_model.generate(inputs_embeds=combined, attention_mask=mask,
+                                          do_sample=False, max_new_tokens=self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     def forward(self, batch):

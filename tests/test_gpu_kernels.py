@@ -153,6 +153,21 @@ def test_t5_encode_logits_generate(device, t5_sd):
         assert torch.equal(toks[:, :n + 1], ref_toks[:, :n + 1])
 
 
+def test_t5_generate_graph_replay_matches_eager(device, t5_sd, monkeypatch):
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    m = DeviceT5(t5_sd, device)
+    ids, mask, img_tok = _t5_inputs(5, 41)
+    emb = torch.cat([img_tok, t5_sd["shared.weight"][ids]], 1).to(device)
+    fm = torch.cat([torch.ones(5, 50, dtype=torch.long), mask], 1).to(device)
+    a = m.generate_padded(emb, fm, 20).cpu()        # captured + replayed
+    b = m.generate_padded(emb, fm, 20).cpu()        # graph cache hit
+    monkeypatch.setenv("MPR_GRAPHS", "0")
+    c = m.generate_padded(emb, fm, 20).cpu()        # eager launches
+    assert torch.equal(a, b) and torch.equal(a, c)
+    d = m.generate_padded(emb[:3], fm[:3], 7).cpu() # another shape
+    assert torch.equal(d, c[:3, :8])
+
+
 def test_t5_embed_and_loss(device, t5_sd):
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     m = DeviceT5(t5_sd, device)
