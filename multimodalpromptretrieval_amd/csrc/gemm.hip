@@ -38,8 +38,12 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
   constexpr int LA = BM * (BK / 4) / NT, LB = BN * (BK / 4) / NT;
   static_assert(LA * NT == BM * (BK / 4) && LB * NT == BN * (BK / 4), "loader split");
 
-  __shared__ __attribute__((aligned(16))) float As[2][BM][LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LDK];
+  // ONE __shared__ object for the A/B double buffers and the split-K flag: a second LDS object
+  // (e.g. a 4-byte flag) makes hipcc drain vmcnt before every k-step's first ds_read.
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK + 4];
+  float(*As)[BM][LDK] = reinterpret_cast<float(*)[BM][LDK]>(smem);
+  float(*Bs)[BN][LDK] = reinterpret_cast<float(*)[BN][LDK]>(smem + 2 * BM * LDK);
+  int* last_flag = reinterpret_cast<int*>(smem + 2 * (BM + BN) * LDK);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -47,34 +51,37 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
   const int M = a.M, N = a.N, K = a.K;
 
   f32x4 ra[LA], rb[LB];
+  bool oka[LA], okb[LB];
+  // Unconditional loads from clamped addresses, zeroed by a select only when written to LDS
+  // (after the MFMAs of the current tile): an exec-masked load makes hipcc branch around every
+  // load, and an early select makes it wait for the data right after issuing the load.
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT, r = idx >> 3, c = k0 + (idx & 7) * 4, row = m0 + r;
-      if (row < M && c < K)
-        ra[i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)row * a.lda + c);
-      else
-        ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      oka[i] = row < M && c < K;
+      ra[i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
+                                              min(c, K - 4));
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT, r = idx >> 3, c = k0 + (idx & 7) * 4, row = n0 + r;
-      if (row < N && c < K)
-        rb[i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)row * a.ldw + c);
-      else
-        rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      okb[i] = row < N && c < K;
+      rb[i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
+                                              min(c, K - 4));
     }
   };
   auto swrite = [&](int buf) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&As[buf][idx >> 3][(idx & 7) * 4]) = ra[i];
+      *reinterpret_cast<f32x4*>(&As[buf][idx >> 3][(idx & 7) * 4]) = oka[i] ? ra[i] : z;
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&Bs[buf][idx >> 3][(idx & 7) * 4]) = rb[i];
+      *reinterpret_cast<f32x4*>(&Bs[buf][idx >> 3][(idx & 7) * 4]) = okb[i] ? rb[i] : z;
     }
   };
 
@@ -86,15 +93,18 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
-  const int nk = (K + BK - 1) / BK;
-  gload(0);
+  // Split-K: blockIdx.z owns k-tiles [kt_lo, kt_hi); S == 1 is the plain GEMM.
+  const int S = gridDim.z;
+  const int nk_all = (K + BK - 1) / BK;
+  const int kper = (nk_all + S - 1) / S;
+  const int kt_lo = blockIdx.z * kper;
+  const int nk = min(nk_all, kt_lo + kper);
+  gload(kt_lo * BK);
   swrite(0);
   __syncthreads();
 
   const int li = lane & 31, lh = lane >> 5;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       f32x4 af[WM], bf[WN];
@@ -115,10 +125,68 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
             acc[mi][ni] =
                 __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][c], bf[ni][c], acc[mi][ni], 0, 0, 0);
     }
-    if (kt + 1 < nk) {
-      swrite(buf ^ 1);
-      __syncthreads();
+  };
+  // Branch-free steady state (the last tile is peeled), so the accumulators stay in AGPRs.
+  int buf = 0;
+  for (int kt = kt_lo; kt + 1 < nk; ++kt) {
+    gload((kt + 1) * BK);
+    // keep the next tile's loads ahead of this tile's MFMAs (hipcc otherwise sinks them to
+    // just before their first use, exposing the whole load latency every k-step)
+    __builtin_amdgcn_sched_barrier(0);
+    compute(buf);
+    __builtin_amdgcn_sched_barrier(0);  // and the selects/LDS stores that consume them behind
+    swrite(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (nk > kt_lo) compute(buf);
+
+  if (S > 1) {
+    // Deterministic split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction"):
+    // every slice stores its fp32 partial tile, releases it (agent scope) and draws a ticket;
+    // the slice that draws S-1 acquires and sums the S slabs in slice order 0..S-1, so the
+    // result does not depend on which slice finishes last.
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    float* slab = a.sk_ws + (int64_t)tile * S * (BM * BN);
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = wm * 32 * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int lc = wn * 32 * WN + ni * 32 + li;
+          slab[(int64_t)blockIdx.z * (BM * BN) + lr * BN + lc] = acc[mi][ni][r];
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(&a.sk_cnt[tile], 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      *last_flag = (t == S - 1);
     }
+    __syncthreads();
+    if (!*last_flag) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = wm * 32 * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int lc = wn * 32 * WN + ni * 32 + li;
+          float sum = slab[lr * BN + lc];
+          for (int z = 1; z < S; ++z) sum += slab[(int64_t)z * (BM * BN) + lr * BN + lc];
+          acc[mi][ni][r] = sum;
+        }
+    if (tid == 0) a.sk_cnt[tile] = 0;  // ready for the next launch (stream-ordered)
   }
 
   // Epilogue: 32x32 accumulator, col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
@@ -144,9 +212,9 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
 }
 
 template <int BM, int BN, int WM, int WN>
-int launch_gemm(const GemmArgs& a, hipStream_t s) {
+int launch_gemm(const GemmArgs& a, hipStream_t s, int splits = 1) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN));
-  dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM));
+  dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)splits);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN>), grid, dim3(NT), 0, s, a);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -350,6 +418,13 @@ int probed(int kind, const GemmArgs& a, hipStream_t s, F&& launch) {
 
 }  // namespace
 
+int SplitKWs::init() {
+  MPR_TRY(slab.ensure((size_t)kElems * sizeof(float)));
+  MPR_TRY(cnt.ensure((size_t)kTiles * sizeof(int)));
+  MPR_HIP(hipMemset(cnt.ptr, 0, (size_t)kTiles * sizeof(int)));
+  return MPR_OK;
+}
+
 int probe_enable(int kind) {
   g_probe_kind = kind;
   return MPR_OK;
@@ -384,14 +459,23 @@ int gemm(const GemmArgs& a, hipStream_t s) {
   // Larger tiles cut LDS/L2 traffic per FLOP but only pay while the grid still covers the 256
   // CUs; at batch 16 many projections have N = 512..768 over M = 300..1200 rows, where a 64x64
   // grid leaves most CUs idle, so the tile shrinks until the grid fills the chip.
+  // Measured on MI355X: below 64x64 the per-block efficiency loss outweighs the better fill
+  // (a 32x64 tile made the N=768 ViT projections slower), so 64x64 is the floor.
   const int64_t b128 = cdiv(a.M, 128) * cdiv(a.N, 64);
   const int64_t b64 = cdiv(a.M, 64) * cdiv(a.N, 64);
-  const int64_t b3264 = cdiv(a.M, 32) * cdiv(a.N, 64);
+  // Grids below ~0.75 of the CU count with a long K (the N=512/768 projections at batch 16)
+  // split K over blockIdx.z with the deterministic in-launch combine.
+  int splits = 1;
+  const int nk = (int)cdiv(a.K, 32);
+  if (a.sk_ws && a.sk_cnt && b64 < 192 && nk >= 16) {
+    splits = (int)std::min<int64_t>(4, cdiv(384, b64));
+    while (splits > 1 && nk / splits < 8) --splits;
+    if (b64 > a.sk_tiles || (int64_t)b64 * splits * 64 * 64 > a.sk_ws_elems) splits = 1;
+  }
   return probed(PROBE_GEMM, a, s, [&]() {
+    if (splits > 1) return launch_gemm<64, 64, 1, 1>(a, s, splits);
     if (b128 >= 512) return launch_gemm<128, 64, 2, 1>(a, s);
-    if (b64 >= 384) return launch_gemm<64, 64, 1, 1>(a, s);
-    if (b3264 >= 256) return launch_gemm<32, 64, 1, 1>(a, s);
-    return launch_gemm<32, 32, 1, 1>(a, s);
+    return launch_gemm<64, 64, 1, 1>(a, s);
   });
 }
 
