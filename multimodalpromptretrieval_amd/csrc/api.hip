@@ -305,6 +305,21 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
     }
     MPR_TRY(upload(m->dec_final, t[p++], d));
     MPR_TRY(upload(m->lm_head, t[p++], (size_t)m->V * d));
+    // lane-order images of the decoder projections for the decode-step GEMMs
+    auto pack = [](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
+      MPR_TRY(dst.ensure((size_t)packed_rows16_elems(n, k) * 4));
+      return pack_rows16(src.as<float>(), n, k, k, dst.as<float>(), nullptr);
+    };
+    for (auto& ly : m->dec) {
+      MPR_TRY(pack(ly->pk_qkv, ly->qkv, 3 * inner, d));
+      MPR_TRY(pack(ly->pk_o, ly->o, d, inner));
+      MPR_TRY(pack(ly->pk_cq, ly->cq, inner, d));
+      MPR_TRY(pack(ly->pk_co, ly->co, d, inner));
+      MPR_TRY(pack(ly->pk_wi, ly->wi, dff, d));
+      MPR_TRY(pack(ly->pk_wo, ly->wo, d, dff));
+    }
+    MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
+    MPR_HIP(hipDeviceSynchronize());
     *out = m.release();
     return MPR_OK;
   });

@@ -80,7 +80,7 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(ptr); }
 };
 
-inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Copies `count` floats from a host-or-device pointer into a fresh device buffer.
 int upload(DevBuf& dst, const float* src, size_t count);

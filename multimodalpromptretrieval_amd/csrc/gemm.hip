@@ -34,16 +34,17 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
     GemmArgs a) {
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int NT = 64 * (BM / (32 * WM)) * WAVES_N;
-  constexpr int BK = 32, LDK = BK + 4;
-  constexpr int LA = BM * (BK / 4) / NT, LB = BN * (BK / 4) / NT;
-  static_assert(LA * NT == BM * (BK / 4) && LB * NT == BN * (BK / 4), "loader split");
+  constexpr int BK = 32, LDK = BK + 4, KQ = BK / 4;  // KQ float4 per row of a K tile
+  constexpr int LA = BM * KQ / NT, LB = BN * KQ / NT;
+  constexpr int STAGE = (BM + BN) * LDK;  // floats per LDS stage (A rows then W rows)
+  static_assert(LA * NT == BM * KQ && LB * NT == BN * KQ, "loader split");
 
-  // ONE __shared__ object for the A/B double buffers and the split-K flag: a second LDS object
-  // (e.g. a 4-byte flag) makes hipcc drain vmcnt before every k-step's first ds_read.
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK + 4];
-  float(*As)[BM][LDK] = reinterpret_cast<float(*)[BM][LDK]>(smem);
-  float(*Bs)[BN][LDK] = reinterpret_cast<float(*)[BN][LDK]>(smem + 2 * BM * LDK);
-  int* last_flag = reinterpret_cast<int*>(smem + 2 * (BM + BN) * LDK);
+  // Three LDS stages: tile kt+1 is already visible while tile kt is multiplied, so its fragments
+  // are read into registers under tile kt's MFMAs and the next k-step starts on the barrier
+  // without waiting for LDS.  ONE __shared__ object holds the stages and the split-K flag: a
+  // second LDS object makes hipcc drain vmcnt before every k-step's first ds_read.
+  __shared__ __attribute__((aligned(16))) float smem[3 * STAGE + 4];
+  int* last_flag = reinterpret_cast<int*>(smem + 3 * STAGE);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -58,30 +59,32 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      const int idx = tid + i * NT, r = idx >> 3, c = k0 + (idx & 7) * 4, row = m0 + r;
+      const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = m0 + r;
       oka[i] = row < M && c < K;
       ra[i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
                                               min(c, K - 4));
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int idx = tid + i * NT, r = idx >> 3, c = k0 + (idx & 7) * 4, row = n0 + r;
+      const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = n0 + r;
       okb[i] = row < N && c < K;
       rb[i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
                                               min(c, K - 4));
     }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](int st) {
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    float* base = smem + st * STAGE;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&As[buf][idx >> 3][(idx & 7) * 4]) = oka[i] ? ra[i] : z;
+      *reinterpret_cast<f32x4*>(base + (idx / KQ) * LDK + (idx % KQ) * 4) = oka[i] ? ra[i] : z;
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT;
-      *reinterpret_cast<f32x4*>(&Bs[buf][idx >> 3][(idx & 7) * 4]) = okb[i] ? rb[i] : z;
+      *reinterpret_cast<f32x4*>(base + (BM + idx / KQ) * LDK + (idx % KQ) * 4) =
+          okb[i] ? rb[i] : z;
     }
   };
 
@@ -93,53 +96,85 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
-  // Split-K: blockIdx.z owns k-tiles [kt_lo, kt_hi); S == 1 is the plain GEMM.
-  const int S = gridDim.z;
-  const int nk_all = (K + BK - 1) / BK;
-  const int kper = (nk_all + S - 1) / S;
-  const int kt_lo = blockIdx.z * kper;
-  const int nk = min(nk_all, kt_lo + kper);
-  gload(kt_lo * BK);
-  swrite(0);
-  __syncthreads();
-
+  // Operand fragments of one K tile: lane (li, lh) holds row li's k = 16*lh .. 16*lh+15 as four
+  // float4 (the contraction order inside the tile is permuted identically for A and W).
   const int li = lane & 31, lh = lane >> 5;
-  auto compute = [&](int buf) {
+  f32x4 fa[WM][4], fb[WN][4], na[WM][4], nb[WN][4];
+  auto sread = [&](int st, f32x4(&xa)[WM][4], f32x4(&xb)[WN][4]) {
+    const float* base = smem + st * STAGE;
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      f32x4 af[WM], bf[WN];
 #pragma unroll
       for (int mi = 0; mi < WM; ++mi)
-        af[mi] = *reinterpret_cast<const f32x4*>(
-            &As[buf][wm * 32 * WM + mi * 32 + li][lh * 16 + s4 * 4]);
+        xa[mi][s4] = *reinterpret_cast<const f32x4*>(
+            base + (wm * 32 * WM + mi * 32 + li) * LDK + lh * 16 + s4 * 4);
 #pragma unroll
       for (int ni = 0; ni < WN; ++ni)
-        bf[ni] = *reinterpret_cast<const f32x4*>(
-            &Bs[buf][wn * 32 * WN + ni * 32 + li][lh * 16 + s4 * 4]);
+        xb[ni][s4] = *reinterpret_cast<const f32x4*>(
+            base + (BM + wn * 32 * WN + ni * 32 + li) * LDK + lh * 16 + s4 * 4);
+    }
+  };
+  auto mfmas = [&](int s_lo, int s_hi) {
+#pragma unroll
+    for (int s4 = s_lo; s4 < s_hi; ++s4)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
           for (int ni = 0; ni < WN; ++ni)
-            acc[mi][ni] =
-                __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][c], bf[ni][c], acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[mi][s4][c], fb[ni][s4][c],
+                                                               acc[mi][ni], 0, 0, 0);
+  };
+  auto advance = [&]() {
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+#pragma unroll
+      for (int mi = 0; mi < WM; ++mi) fa[mi][s4] = na[mi][s4];
+#pragma unroll
+      for (int ni = 0; ni < WN; ++ni) fb[ni][s4] = nb[ni][s4];
     }
   };
-  // Branch-free steady state (the last tile is peeled), so the accumulators stay in AGPRs.
-  int buf = 0;
-  for (int kt = kt_lo; kt + 1 < nk; ++kt) {
-    gload((kt + 1) * BK);
-    // keep the next tile's loads ahead of this tile's MFMAs (hipcc otherwise sinks them to
-    // just before their first use, exposing the whole load latency every k-step)
+
+  // Split-K: blockIdx.z owns k-tiles [kt_lo, nk); S == 1 is the plain GEMM.
+  const int S = gridDim.z;
+  const int nk_all = (K + BK - 1) / BK;
+  const int kper = (nk_all + S - 1) / S;
+  const int kt_lo = blockIdx.z * kper;
+  const int nk = min(nk_all, kt_lo + kper);
+
+  gload(kt_lo * BK);
+  swrite(0);
+  gload((kt_lo + 1) * BK);  // clamped/zeroed when past K
+  swrite(1);
+  __syncthreads();
+  sread(0, fa, fb);
+  int kt = kt_lo, st = 0;
+  // Steady state, branch-free (the accumulators stay in AGPRs): global loads of tile kt+2 in
+  // flight across tile kt's MFMAs, LDS reads of tile kt+1 issued after its first quarter.
+  for (; kt + 2 < nk; ++kt) {
+    const int st1 = st == 2 ? 0 : st + 1, st2 = st1 == 2 ? 0 : st1 + 1;
+    gload((kt + 2) * BK);
     __builtin_amdgcn_sched_barrier(0);
-    compute(buf);
-    __builtin_amdgcn_sched_barrier(0);  // and the selects/LDS stores that consume them behind
-    swrite(buf ^ 1);
+    mfmas(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    sread(st1, na, nb);
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(1, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    swrite(st2);
     __syncthreads();
-    buf ^= 1;
+    advance();
+    st = st1;
   }
-  if (nk > kt_lo) compute(buf);
+  if (kt + 1 < nk) {  // second-to-last tile: its successor is already in LDS
+    mfmas(0, 1);
+    sread(st == 2 ? 0 : st + 1, na, nb);
+    mfmas(1, 4);
+    advance();
+    ++kt;
+  }
+  if (kt < nk) mfmas(0, 4);
 
   if (S > 1) {
     // Deterministic split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction"):
@@ -222,19 +257,43 @@ int launch_gemm(const GemmArgs& a, hipStream_t s, int splits = 1) {
 
 // ---------------------------------------------------------------------------------------------
 // Skinny GEMM (M <= 16), optional fused RMSNorm of the A rows.
-// A block = 8 waves = 16 output columns (W rows n0..n0+15); wave w owns the K slice w of the
-// row, issues ALL of its loads (MAXC chunks of 16 columns, sized to the slice) before the first
-// MFMA, and the 8 partial 16x16 tiles are summed through LDS.  With RMSNorm fused, the operand
-// is ln_w[k] * A[m,k] and the per-row 1/rms (from the squares of the same loaded A values, summed
-// across the block) scales the accumulator in the epilogue, so A is read exactly once.
+// A block = 8 waves = NT tiles of 16 output columns; wave w owns the K slice w of the rows.
+// v_mfma_f32_16x16x4_f32 wants lane (i, h) to hold row i, k = 4h..4h+3 of a 16-column chunk, so
+// adjacent lanes sit on different rows; loading that straight from row-major memory scatters
+// every wave load over 16 rows (measured: ~0.85 us of a 3.5 us kernel).  Both operands therefore
+// arrive lane-contiguous: W from its pack_rows16 image (1 KiB per wave load), A rows through a
+// wave-private LDS slab filled with 256-byte row segments and read back as MFMA fragments
+// (wave-private: no block barrier, the wave's own LDS ops stay in order).
+// With RMSNorm fused, the operand is ln_w[k] * A[m,k] and the per-row 1/rms (from the squares of
+// the same loaded A values, summed across the block) scales the accumulator in the epilogue.
 constexpr int SK_WAVES = 8;
 
-// NT 16-column tiles per block share the activation loads (NT > 1 for the 32k-column lm_head,
+__global__ __launch_bounds__(256) void pack_rows16_kernel(const float* __restrict__ W, int64_t N,
+                                                          int64_t K, int64_t ldw, int64_t nch,
+                                                          float* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of the image
+  const int64_t total = cdiv(N, 16) * nch * 64;
+  if (q >= total) return;
+  const int l = (int)(q & 63);
+  const int64_t tc = q >> 6, t = tc / nch, c = tc % nch;
+  const int64_t row = t * 16 + (l & 15), k0 = c * 16 + (l >> 4) * 4;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (row < N) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (k0 + e < K) v[e] = W[row * ldw + k0 + e];
+  }
+  reinterpret_cast<f32x4*>(out)[q] = v;
+}
+
+// NT 16-column tiles per block share the activation slab (NT > 1 for the 32k-column lm_head,
 // which needs more bytes in flight per wave); two accumulator chains per tile halve the
-// dependent-MFMA latency of the K loop.
-template <int SK_MAXC, int NT>
+// dependent-MFMA latency of the K loop.  MAXC = chunks of 16 columns staged per pass.
+template <int MAXC, int NT>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   const GemmArgs& a = sa.g;
+  constexpr int XLD = MAXC * 16 + 4;  // slab row stride (floats): conflict-free fragment reads
+  __shared__ __attribute__((aligned(16))) float xs[SK_WAVES][16][XLD];
   __shared__ __attribute__((aligned(16))) f32x4 red[NT][SK_WAVES][64];
   __shared__ float ssq_s[SK_WAVES][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -243,21 +302,18 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   const bool rms = sa.rms_w != nullptr;
 
   const int nchunk = (K + 15) / 16;
+  const int ntiles = (N + 15) / 16;
   const int per = (nchunk + SK_WAVES - 1) / SK_WAVES;
   const int c_lo = wave * per, c_hi = min(nchunk, c_lo + per);
-  const bool xok = i < M;
-  // Out-of-range lanes read a valid address and are zeroed after the load (no predicated
-  // loads: those serialize the load stream).
-  const float* wp[NT];
+  const f32x4* wp[NT];
   float wmask[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int wrow = (blockIdx.x * NT + t) * 16 + i;
-    wp[t] = a.W + (int64_t)(wrow < N ? wrow : 0) * a.ldw + h * 4;
-    wmask[t] = wrow < N ? 1.f : 0.f;
+    const int tile = blockIdx.x * NT + t;
+    wp[t] = reinterpret_cast<const f32x4*>(sa.wpk) +
+            ((int64_t)min(tile, ntiles - 1) * nchunk) * 64 + lane;
+    wmask[t] = tile < ntiles ? 1.f : 0.f;
   }
-  const float* xp = a.A + (int64_t)(xok ? i : 0) * a.lda + h * 4;
-  const float xmask = xok ? 1.f : 0.f;
   // Epilogue operands (residual, bias) are fetched up front by the epilogue waves.
   const int m_ep = lane & 15;
   float rres[4] = {0.f, 0.f, 0.f, 0.f}, rbias[4] = {0.f, 0.f, 0.f, 0.f};
@@ -274,30 +330,44 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
-  for (int c0 = c_lo; c0 < c_hi; c0 += SK_MAXC) {
-    f32x4 wv[NT][SK_MAXC], xv[SK_MAXC], gv[SK_MAXC];
+  for (int c0 = c_lo; c0 < c_hi; c0 += MAXC) {
+    // weights first (the long pole), then this pass's activation rows as 256-byte segments:
+    // float4 q of the pass = row q / (4*MAXC), column (q % (4*MAXC)) * 4 of the pass
+    f32x4 wv[NT][MAXC], xr[MAXC];
 #pragma unroll
-    for (int u = 0; u < SK_MAXC; ++u) {
+    for (int u = 0; u < MAXC; ++u) {
       const int c = c0 + u;
-      const bool ok = c < c_hi && c * 16 + h * 4 < K;
-      const int cc = ok ? c : c_lo;
-      const float km = ok ? 1.f : 0.f;
+      const float km = c < c_hi ? 1.f : 0.f;
+      const int cc = c < c_hi ? c : c_lo;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        wv[t][u] = *reinterpret_cast<const f32x4*>(wp[t] + cc * 16);
+        wv[t][u] = wp[t][(int64_t)cc * 64];
         wv[t][u] *= km * wmask[t];
       }
-      xv[u] = *reinterpret_cast<const f32x4*>(xp + cc * 16);
-      if (rms) gv[u] = *reinterpret_cast<const f32x4*>(sa.rms_w + cc * 16 + h * 4);
-      xv[u] *= km * xmask;
     }
 #pragma unroll
-    for (int u = 0; u < SK_MAXC; ++u) {
+    for (int u = 0; u < MAXC; ++u) {
+      const int q = u * 64 + lane, row = q / (4 * MAXC), col = c0 * 16 + (q % (4 * MAXC)) * 4;
+      const bool ok = row < M && col < c_hi * 16 && col < K;
+      xr[u] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
+                                              min(col, K - 4));
+      if (!ok) xr[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+      const int q = u * 64 + lane;
+      *reinterpret_cast<f32x4*>(&xs[wave][q / (4 * MAXC)][(q % (4 * MAXC)) * 4]) = xr[u];
+    }
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+      f32x4 xv = *reinterpret_cast<const f32x4*>(&xs[wave][i][u * 16 + h * 4]);
       if (rms) {
+        const int cc = min(c0 + u, nchunk - 1);
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(sa.rms_w + cc * 16 + h * 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          ss += xv[u][e] * xv[u][e];
-          xv[u][e] = gv[u][e] * xv[u][e];
+          ss += xv[e] * xv[e];
+          xv[e] = gv[e] * xv[e];
         }
       }
 #pragma unroll
@@ -305,7 +375,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
           acc[t][u & 1] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][u][e], xv[u][e], acc[t][u & 1], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][u][e], xv[e], acc[t][u & 1], 0, 0, 0);
     }
   }
 #pragma unroll
@@ -479,13 +549,26 @@ int gemm(const GemmArgs& a, hipStream_t s) {
   });
 }
 
+int64_t packed_rows16_elems(int64_t N, int64_t K) { return cdiv(N, 16) * cdiv(K, 16) * 256; }
+
+int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, hipStream_t s) {
+  MPR_REQUIRE(N > 0 && K > 0 && ldw >= K, "pack_rows16: bad shape N=%lld K=%lld",
+              (long long)N, (long long)K);
+  const int64_t q = packed_rows16_elems(N, K) / 4;
+  hipLaunchKernelGGL(pack_rows16_kernel, dim3((unsigned)cdiv(q, 256)), dim3(256), 0, s, W, N, K,
+                     ldw, cdiv(K, 16), out);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const GemmArgs& a = sa.g;
   MPR_REQUIRE(a.M >= 0 && a.M <= 16 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
   if (a.M == 0 || a.N == 0) return MPR_OK;
-  MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
-                  aligned16(a.W) && (!sa.rms_w || aligned16(sa.rms_w)),
-              "gemm_skinny: K/lda/ldw must be multiples of 4, operands 16-byte aligned");
+  MPR_REQUIRE(sa.wpk && aligned16(sa.wpk), "gemm_skinny: needs the 16-byte aligned packed weight");
+  MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && aligned16(a.A) &&
+                  (!sa.rms_w || aligned16(sa.rms_w)),
+              "gemm_skinny: K/lda must be multiples of 4, operands 16-byte aligned");
   MPR_REQUIRE(!sa.amax_val || (sa.amax_idx && !a.R && !a.bias && a.act == ACT_NONE),
               "gemm_skinny: argmax mode takes plain logits");
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave

@@ -49,8 +49,16 @@ int gemm(const GemmArgs& a, hipStream_t s);
 
 // Skinny GEMM for M <= 16 rows (decode steps): same contract as gemm() plus an optional fused
 // T5 RMSNorm of the A rows: A'[m,k] = ln_w[k] * (A[m,k] * rsqrt(mean_k A[m,:]^2 + eps)).
+// Skinny GEMM weights live in a lane-order image of W (pack_rows16): for 16-row tile t and
+// 16-column chunk c, the 256 floats sit in the order the MFMA lanes consume them, so a wave's
+// weight load is one contiguous 1 KiB (W row-major would put adjacent lanes 2 KiB apart).
+//   Wp[(t * cdiv(K,16) + c) * 256 + l * 4 + e] = W[16t + (l & 15)][16c + 4(l >> 4) + e]  (0 outside)
+int64_t packed_rows16_elems(int64_t N, int64_t K);
+int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, hipStream_t s);
+
 struct SkinnyArgs {
-  GemmArgs g;
+  GemmArgs g;                    // g.W / g.ldw unused: the weights come from wpk
+  const float* wpk = nullptr;    // pack_rows16 image of the [N, K] weight
   const float* rms_w = nullptr;  // fuse RMSNorm prologue when non-null
   float rms_eps = 1e-6f;
   float a_scale = 1.f;           // A' = (ln_w * (A * rstd)) * a_scale (T5 tied-head d^-0.5)

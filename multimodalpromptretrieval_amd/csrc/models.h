@@ -69,6 +69,8 @@ struct TextModel : mpr_model {
 struct T5Layer {
   DevBuf ln0, qkv, o, ln1, wi, wo;         // encoder layer / decoder self-attn + ffn
   DevBuf cq, co, ln2;                      // decoder only: cross-attn q/o, ffn norm
+  // decoder only: pack_rows16 images of qkv, o, cq, co, wi, wo for the decode-step GEMMs
+  DevBuf pk_qkv, pk_o, pk_cq, pk_co, pk_wi, pk_wo;
 };
 
 struct T5Model : mpr_model {
@@ -77,6 +79,7 @@ struct T5Model : mpr_model {
   int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
   int inner = 0, lut_radius = 0;
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
+  DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
   // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
   DevBuf enc_tab, dec_tab;
   std::vector<std::unique_ptr<T5Layer>> enc, dec;

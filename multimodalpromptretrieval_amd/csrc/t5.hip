@@ -139,9 +139,10 @@ int T5Model::generate_body(int B, int L, int max_new, int start, int eos, int pa
       const T5Layer& ly = *dec[l];
       float* cl = cache.as<float>() + l * cache_layer;
       SkinnyArgs sq;
-      sq.g.A = xp; sq.g.lda = d; sq.g.W = ly.qkv.as<float>(); sq.g.ldw = d;
+      sq.g.A = xp; sq.g.lda = d;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
+      sq.wpk = ly.pk_qkv.as<float>();
       MPR_TRY(gemm_skinny(sq, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
@@ -153,13 +154,15 @@ int T5Model::generate_body(int B, int L, int max_new, int start, int eos, int pa
       at.lut_radius = lut_radius;
       MPR_TRY(attention(at, s));
       SkinnyArgs so;
-      so.g.A = ap; so.g.lda = inner; so.g.W = ly.o.as<float>(); so.g.ldw = inner; so.g.R = xp;
+      so.g.A = ap; so.g.lda = inner; so.g.R = xp;
       so.g.ldr = d; so.g.C = xp; so.g.ldc = d; so.g.M = B; so.g.N = d; so.g.K = inner;
+      so.wpk = ly.pk_o.as<float>();
       MPR_TRY(gemm_skinny(so, s));
       SkinnyArgs cq;
-      cq.g.A = xp; cq.g.lda = d; cq.g.W = ly.cq.as<float>(); cq.g.ldw = d; cq.g.C = qp;
+      cq.g.A = xp; cq.g.lda = d; cq.g.C = qp;
       cq.g.ldc = inner; cq.g.M = B; cq.g.N = inner; cq.g.K = d; cq.rms_w = ly.ln1.as<float>();
       cq.rms_eps = T5_EPS;
+      cq.wpk = ly.pk_cq.as<float>();
       MPR_TRY(gemm_skinny(cq, s));
       AttnArgs ca;
       ca.q = qp; ca.q_bs = inner; ca.q_rs = inner;
@@ -170,24 +173,28 @@ int T5Model::generate_body(int B, int L, int max_new, int start, int eos, int pa
       ca.key_mask = maskp; ca.mask_bs = L;
       MPR_TRY(attention(ca, s));
       SkinnyArgs co;
-      co.g.A = ap; co.g.lda = inner; co.g.W = ly.co.as<float>(); co.g.ldw = inner; co.g.R = xp;
+      co.g.A = ap; co.g.lda = inner; co.g.R = xp;
       co.g.ldr = d; co.g.C = xp; co.g.ldc = d; co.g.M = B; co.g.N = d; co.g.K = inner;
+      co.wpk = ly.pk_co.as<float>();
       MPR_TRY(gemm_skinny(co, s));
       SkinnyArgs fi;
-      fi.g.A = xp; fi.g.lda = d; fi.g.W = ly.wi.as<float>(); fi.g.ldw = d; fi.g.C = fp;
+      fi.g.A = xp; fi.g.lda = d; fi.g.C = fp;
       fi.g.ldc = dff; fi.g.M = B; fi.g.N = dff; fi.g.K = d; fi.g.act = ACT_RELU;
       fi.rms_w = ly.ln2.as<float>(); fi.rms_eps = T5_EPS;
+      fi.wpk = ly.pk_wi.as<float>();
       MPR_TRY(gemm_skinny(fi, s));
       SkinnyArgs fo;
-      fo.g.A = fp; fo.g.lda = dff; fo.g.W = ly.wo.as<float>(); fo.g.ldw = dff; fo.g.R = xp;
+      fo.g.A = fp; fo.g.lda = dff; fo.g.R = xp;
       fo.g.ldr = d; fo.g.C = xp; fo.g.ldc = d; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
+      fo.wpk = ly.pk_wo.as<float>();
       MPR_TRY(gemm_skinny(fo, s));
     }
     SkinnyArgs hd;
-    hd.g.A = xp; hd.g.lda = d; hd.g.W = lm_head.as<float>(); hd.g.ldw = d; hd.g.C = nullptr;
+    hd.g.A = xp; hd.g.lda = d; hd.g.C = nullptr;
     hd.g.M = B; hd.g.N = V; hd.g.K = d; hd.rms_w = dec_final.as<float>();
     hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
     hd.amax_val = part_val.as<float>(); hd.amax_idx = part_idx.as<int32_t>();
+    hd.wpk = pk_lm_head.as<float>();
     MPR_TRY(gemm_skinny(hd, s));
     MPR_TRY(greedy_step(part_val.as<float>(), part_idx.as<int32_t>(), nparts, B, unf, toks, T1,
                         t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,

@@ -94,8 +94,10 @@ class VQARetrieval:
         q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
         di = self.image_encoder.out_dim
         if not hasattr(self, "_s_img"):
-            self._s_img = torch.cuda.Stream(self.device)
-            self._s_txt = torch.cuda.Stream(self.device)
+            # High priority: the host blocks on these results (prompt building), while other
+            # device work queued meanwhile (the token-feature ViT) is not needed until later.
+            self._s_img = torch.cuda.Stream(self.device, priority=-1)
+            self._s_txt = torch.cuda.Stream(self.device, priority=-1)
         ev = torch.cuda.Event()
         ev.record(cur)
         for s in (self._s_img, self._s_txt):

@@ -75,8 +75,7 @@ int main() {
     SkinnyArgs a;
     a.g.A = (i & 1) ? y : x;
     a.g.lda = K;
-    a.g.W = W + (size_t)(i % 6) * (4 << 20);
-    a.g.ldw = K;
+    a.wpk = W + (size_t)(i % 6) * (4 << 20);
     a.g.C = (i & 1) ? x : y;
     a.g.ldc = N;
     a.g.M = 16;
@@ -89,6 +88,7 @@ int main() {
     if (rms) a.rms_w = g;
     gemm_skinny(a, s);
   };
+  time_chain("skinny N512 K512 plain", s, [&](int i) { skinny(512, 512, false, false, i); });
   time_chain("skinny N512 K512 rms", s, [&](int i) { skinny(512, 512, true, false, i); });
   time_chain("skinny N512 K512 +res", s, [&](int i) { skinny(512, 512, false, true, i); });
   time_chain("skinny N1536 K512 rms", s, [&](int i) { skinny(1536, 512, true, false, i); });
@@ -96,7 +96,7 @@ int main() {
   time_chain("skinny N512 K2048 +res", s, [&](int i) { skinny(512, 2048, false, true, i); });
   time_chain("lm_head N32101 K512 argmax", s, [&](int i) {
     SkinnyArgs a;
-    a.g.A = x; a.g.lda = 512; a.g.W = W; a.g.ldw = 512; a.g.C = nullptr; a.g.M = 16;
+    a.g.A = x; a.g.lda = 512; a.wpk = W; a.g.C = nullptr; a.g.M = 16;
     a.g.N = 32101; a.g.K = 512; a.rms_w = g; a.amax_val = pv; a.amax_idx = pi;
     gemm_skinny(a, s);
   }, 200);

@@ -14,7 +14,7 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = collections.defaultdict(lambda: [0, 0])
     for r in rows:
-        n = r["Kernel_Name"].split("(")[0].replace("mpr::(anonymous namespace)::", "")
+        n = r["Kernel_Name"].replace("mpr::(anonymous namespace)::", "").split("(")[0]
         n = n.replace("void ", "")[:50]
         key = (n, r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"], r["Workgroup_Size_X"])
         d[key][0] += 1

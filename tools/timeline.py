@@ -1,0 +1,81 @@
+"""Unprofiled per-phase timeline of one bench step (development aid; not the bench contract).
+
+Wraps the device entry points (ViT, CLIP text, index search, T5 generate) so that each call
+records a hipEvent on the stream it runs on before and after, plus host enqueue timestamps;
+prints device start/end of every phase relative to the step's first event.
+
+usage: python tools/timeline.py [--steps 3]
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from multimodalpromptretrieval_amd import encoders, index, t5  # noqa: E402
+
+RECS = []
+
+
+def wrap(cls, name, label):
+    orig = getattr(cls, name)
+
+    def f(self, *a, **kw):
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        h0 = time.perf_counter()
+        e0.record(s)
+        out = orig(self, *a, **kw)
+        e1.record(s)
+        h1 = time.perf_counter()
+        mode = a[0] if label == "vit" and len(a) > 1 else None
+        tag = label if mode is None else f"{label}[{'tok' if a[1] else 'cls'}]"
+        RECS.append((tag, s.stream_id, e0, e1, h0, h1))
+        return out
+
+    setattr(cls, name, f)
+    if name == "forward":
+        cls.__call__ = f
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=3)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    cfg = bench.CONFIGS["c2"]
+    model, _, _ = bench.build(cfg, dev, None)
+    batches = bench.make_batches(4, cfg["B"], dev, seed=100)
+    wrap(encoders.DeviceViT, "forward", "vit")
+    wrap(encoders.DeviceCLIPText, "forward", "text")
+    wrap(index.DeviceIndex, "search", "scan")
+    wrap(t5.DeviceT5, "generate_padded", "t5.generate")
+    with torch.no_grad():
+        for i in range(3):
+            model.predict(batches[i % 4])
+        torch.cuda.synchronize()
+        for i in range(args.steps):
+            RECS.clear()
+            cur = torch.cuda.current_stream()
+            ref = torch.cuda.Event(enable_timing=True)
+            ref.record(cur)
+            h_ref = time.perf_counter()
+            model.predict(batches[i % 4])
+            end = torch.cuda.Event(enable_timing=True)
+            end.record(torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            h_end = time.perf_counter()
+            print(f"step {i}: host {1e3 * (h_end - h_ref):.3f} ms")
+            for tag, sid, e0, e1, h0, h1 in RECS:
+                print(f"  {tag:14s} stream {sid:>4}  host {1e3 * (h0 - h_ref):8.3f}->"
+                      f"{1e3 * (h1 - h_ref):8.3f}  dev {ref.elapsed_time(e0):8.3f}->"
+                      f"{ref.elapsed_time(e1):8.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
