@@ -254,7 +254,6 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
     MPR_REQUIRE(radius >= 64, "t5_create: lut radius %d too small", radius);
     const int expect = 2 + 8 * Le + 1 + 1 + 13 * Ld + 2;
     MPR_REQUIRE(nt == expect, "t5_create: expected %d tensors, got %d", expect, nt);
-    MPR_TRY(m->sk.init());
     // Relative position bias by offset r = key - query: tab[(r + radius) * H + h] =
     // rel_bias[lut[r + radius], h] (the bucket gather done once here, not per score).
     auto bias_table = [&](DevBuf& dst, const float* rel, const int32_t* lut) -> int {

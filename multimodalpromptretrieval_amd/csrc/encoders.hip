@@ -23,7 +23,6 @@ int ClipTower::load_blocks(const float* const* t, int w, int nl) {
   layers = nl;
   heads = w / 64;
   blocks.clear();
-  MPR_TRY(sk.init());
   for (int l = 0; l < nl; ++l) {
     auto b = std::make_unique<ClipBlock>();
     const float* const* p = t + 12 * l;
@@ -60,7 +59,7 @@ int ClipTower::run(float* x, int B, int L, bool causal, hipStream_t s) {
     GemmArgs g;
     g.A = hp; g.lda = W; g.W = b.in_w.as<float>(); g.ldw = W; g.bias = b.in_b.as<float>();
     g.C = qp; g.ldc = 3 * W; g.M = M; g.N = 3 * W; g.K = W;
-    MPR_TRY(gemm_sk(g, s));
+    MPR_TRY(gemm(g, s));
     AttnArgs at;
     at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
     at.k = qp + W; at.k_bs = at.q_bs; at.k_rs = 3 * W;
@@ -73,16 +72,16 @@ int ClipTower::run(float* x, int B, int L, bool causal, hipStream_t s) {
     GemmArgs o;
     o.A = ap; o.lda = W; o.W = b.out_w.as<float>(); o.ldw = W; o.bias = b.out_b.as<float>();
     o.R = x; o.ldr = W; o.C = x; o.ldc = W; o.M = M; o.N = W; o.K = W;
-    MPR_TRY(gemm_sk(o, s));
+    MPR_TRY(gemm(o, s));
     MPR_TRY(layernorm(x, W, M, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(), CLIP_LN_EPS, hp, W, s));
     GemmArgs f;
     f.A = hp; f.lda = W; f.W = b.fc_w.as<float>(); f.ldw = W; f.bias = b.fc_b.as<float>();
     f.C = mp; f.ldc = 4 * W; f.M = M; f.N = 4 * W; f.K = W; f.act = ACT_QUICKGELU;
-    MPR_TRY(gemm_sk(f, s));
+    MPR_TRY(gemm(f, s));
     GemmArgs pj;
     pj.A = mp; pj.lda = 4 * W; pj.W = b.pj_w.as<float>(); pj.ldw = 4 * W; pj.bias = b.pj_b.as<float>();
     pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M; pj.N = W; pj.K = 4 * W;
-    MPR_TRY(gemm_sk(pj, s));
+    MPR_TRY(gemm(pj, s));
   }
   return MPR_OK;
 }
@@ -101,7 +100,7 @@ int VitModel::forward(const float* img, int B, int mode, float* out, int64_t out
   GemmArgs pe;
   pe.A = cols.as<float>(); pe.lda = P; pe.W = conv_w.as<float>(); pe.ldw = P;
   pe.C = patches.as<float>(); pe.ldc = W; pe.M = B * g2; pe.N = W; pe.K = P;
-  MPR_TRY(gemm_sk(pe, s));
+  MPR_TRY(gemm(pe, s));
   MPR_TRY(vit_assemble(patches.as<float>(), cls.as<float>(), pos.as<float>(), B, g2, W, xp, s));
   MPR_TRY(layernorm(xp, W, B * T, W, lnpre_w.as<float>(), lnpre_b.as<float>(), CLIP_LN_EPS, xp, W,
                     s));
@@ -119,7 +118,7 @@ int VitModel::forward(const float* img, int B, int mode, float* out, int64_t out
                       tp, W, s));
     pj.M = B * T; pj.C = out; pj.ldc = out_dim; pj.c_rpb = T; pj.c_bs = out_bs;
   }
-  MPR_TRY(gemm_sk(pj, s));
+  MPR_TRY(gemm(pj, s));
   return MPR_OK;
 }
 
@@ -140,7 +139,7 @@ int TextModel::forward(const int32_t* tok, int B, int L, float* out, int64_t out
   GemmArgs pj;
   pj.A = pp; pj.lda = W; pj.W = projT.as<float>(); pj.ldw = W; pj.M = B; pj.N = out_dim; pj.K = W;
   pj.C = out; pj.ldc = out_bs;
-  MPR_TRY(gemm_sk(pj, s));
+  MPR_TRY(gemm(pj, s));
   return MPR_OK;
 }
 

@@ -41,10 +41,9 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
 
   // Three LDS stages: tile kt+1 is already visible while tile kt is multiplied, so its fragments
   // are read into registers under tile kt's MFMAs and the next k-step starts on the barrier
-  // without waiting for LDS.  ONE __shared__ object holds the stages and the split-K flag: a
-  // second LDS object makes hipcc drain vmcnt before every k-step's first ds_read.
-  __shared__ __attribute__((aligned(16))) float smem[3 * STAGE + 4];
-  int* last_flag = reinterpret_cast<int*>(smem + 3 * STAGE);
+  // without waiting for LDS.  ONE __shared__ object holds the stages: a second LDS object
+  // makes hipcc drain vmcnt before every k-step's first ds_read.
+  __shared__ __attribute__((aligned(16))) float smem[3 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -136,20 +135,15 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
     }
   };
 
-  // Split-K: blockIdx.z owns k-tiles [kt_lo, nk); S == 1 is the plain GEMM.
-  const int S = gridDim.z;
-  const int nk_all = (K + BK - 1) / BK;
-  const int kper = (nk_all + S - 1) / S;
-  const int kt_lo = blockIdx.z * kper;
-  const int nk = min(nk_all, kt_lo + kper);
+  const int nk = (K + BK - 1) / BK;
 
-  gload(kt_lo * BK);
+  gload(0);
   swrite(0);
-  gload((kt_lo + 1) * BK);  // clamped/zeroed when past K
+  gload(BK);  // clamped/zeroed when past K
   swrite(1);
   __syncthreads();
   sread(0, fa, fb);
-  int kt = kt_lo, st = 0;
+  int kt = 0, st = 0;
   // Steady state, branch-free (the accumulators stay in AGPRs): global loads of tile kt+2 in
   // flight across tile kt's MFMAs, LDS reads of tile kt+1 issued after its first quarter.
   for (; kt + 2 < nk; ++kt) {
@@ -176,54 +170,6 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
   }
   if (kt < nk) mfmas(0, 4);
 
-  if (S > 1) {
-    // Deterministic split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction"):
-    // every slice stores its fp32 partial tile, releases it (agent scope) and draws a ticket;
-    // the slice that draws S-1 acquires and sums the S slabs in slice order 0..S-1, so the
-    // result does not depend on which slice finishes last.
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    float* slab = a.sk_ws + (int64_t)tile * S * (BM * BN);
-#pragma unroll
-    for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < WN; ++ni)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int lr = wm * 32 * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const int lc = wn * 32 * WN + ni * 32 + li;
-          slab[(int64_t)blockIdx.z * (BM * BN) + lr * BN + lc] = acc[mi][ni][r];
-        }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int t = __hip_atomic_fetch_add(&a.sk_cnt[tile], 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      *last_flag = (t == S - 1);
-    }
-    __syncthreads();
-    if (!*last_flag) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-#pragma unroll
-    for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < WN; ++ni)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int lr = wm * 32 * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const int lc = wn * 32 * WN + ni * 32 + li;
-          float sum = slab[lr * BN + lc];
-          for (int z = 1; z < S; ++z) sum += slab[(int64_t)z * (BM * BN) + lr * BN + lc];
-          acc[mi][ni][r] = sum;
-        }
-    if (tid == 0) a.sk_cnt[tile] = 0;  // ready for the next launch (stream-ordered)
-  }
-
   // Epilogue: 32x32 accumulator, col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
 #pragma unroll
   for (int mi = 0; mi < WM; ++mi)
@@ -247,9 +193,9 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
 }
 
 template <int BM, int BN, int WM, int WN>
-int launch_gemm(const GemmArgs& a, hipStream_t s, int splits = 1) {
+int launch_gemm(const GemmArgs& a, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN));
-  dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)splits);
+  dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM));
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN>), grid, dim3(NT), 0, s, a);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -289,7 +235,7 @@ __global__ __launch_bounds__(256) void pack_rows16_kernel(const float* __restric
 // NT 16-column tiles per block share the activation slab (NT > 1 for the 32k-column lm_head,
 // which needs more bytes in flight per wave); two accumulator chains per tile halve the
 // dependent-MFMA latency of the K loop.  MAXC = chunks of 16 columns staged per pass.
-template <int MAXC, int NT>
+template <int MAXC, int NT, bool RMS>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   const GemmArgs& a = sa.g;
   constexpr int XLD = MAXC * 16 + 4;  // slab row stride (floats): conflict-free fragment reads
@@ -299,21 +245,20 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = a.M, N = a.N, K = a.K;
   const int i = lane & 15, h = lane >> 4;
-  const bool rms = sa.rms_w != nullptr;
+  // (RMS is a template flag: behind a runtime `if` hipcc sinks the norm-weight loads into the
+  // branch, after the fragments arrive, one dependent L2 round trip per chunk)
+  const float* gsrc = sa.rms_w;
 
   const int nchunk = (K + 15) / 16;
   const int ntiles = (N + 15) / 16;
   const int per = (nchunk + SK_WAVES - 1) / SK_WAVES;
   const int c_lo = wave * per, c_hi = min(nchunk, c_lo + per);
+  // (a tile past N — the lm_head's last block — re-reads the last tile; never stored)
   const f32x4* wp[NT];
-  float wmask[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int tile = blockIdx.x * NT + t;
+  for (int t = 0; t < NT; ++t)
     wp[t] = reinterpret_cast<const f32x4*>(sa.wpk) +
-            ((int64_t)min(tile, ntiles - 1) * nchunk) * 64 + lane;
-    wmask[t] = tile < ntiles ? 1.f : 0.f;
-  }
+            ((int64_t)min((int)blockIdx.x * NT + t, ntiles - 1) * nchunk) * 64 + lane;
   // Epilogue operands (residual, bias) are fetched up front by the epilogue waves.
   const int m_ep = lane & 15;
   float rres[4] = {0.f, 0.f, 0.f, 0.f}, rbias[4] = {0.f, 0.f, 0.f, 0.f};
@@ -333,17 +278,14 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   for (int c0 = c_lo; c0 < c_hi; c0 += MAXC) {
     // weights first (the long pole), then this pass's activation rows as 256-byte segments:
     // float4 q of the pass = row q / (4*MAXC), column (q % (4*MAXC)) * 4 of the pass
-    f32x4 wv[NT][MAXC], xr[MAXC];
+    f32x4 wv[NT][MAXC], xr[MAXC], gv[MAXC];
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
-      const int c = c0 + u;
-      const float km = c < c_hi ? 1.f : 0.f;
-      const int cc = c < c_hi ? c : c_lo;
+      // a chunk past the wave's slice re-reads chunk c_lo; its activation columns are zero
+      const int c = c0 + u, cc = c < c_hi ? c : c_lo;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        wv[t][u] = wp[t][(int64_t)cc * 64];
-        wv[t][u] *= km * wmask[t];
-      }
+      for (int t = 0; t < NT; ++t) wv[t][u] = wp[t][(int64_t)cc * 64];
+      if constexpr (RMS) gv[u] = *reinterpret_cast<const f32x4*>(gsrc + cc * 16 + h * 4);
     }
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
@@ -353,6 +295,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
                                               min(col, K - 4));
       if (!ok) xr[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    // every load of the pass is in flight before the first wait (hipcc otherwise sinks the
+    // weight loads next to their MFMAs, behind the activation round trip through LDS)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
       const int q = u * 64 + lane;
@@ -361,13 +306,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
       f32x4 xv = *reinterpret_cast<const f32x4*>(&xs[wave][i][u * 16 + h * 4]);
-      if (rms) {
-        const int cc = min(c0 + u, nchunk - 1);
-        const f32x4 gv = *reinterpret_cast<const f32x4*>(sa.rms_w + cc * 16 + h * 4);
+      if constexpr (RMS) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           ss += xv[e] * xv[e];
-          xv[e] = gv[e] * xv[e];
+          xv[e] = gv[u][e] * xv[e];
         }
       }
 #pragma unroll
@@ -380,7 +323,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) red[t][wave][lane] = acc[t][0] + acc[t][1];
-  if (rms) {
+  if constexpr (RMS) {
     ss += __shfl_xor(ss, 16, 64);
     ss += __shfl_xor(ss, 32, 64);
     if (lane < 16) ssq_s[wave][lane] = ss;
@@ -395,7 +338,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   // D[row = W row (n), col = A row (m)]: col = lane&15, row = (lane>>4)*4 + r.
   const int m = lane & 15;
   float scale = sa.a_scale;
-  if (rms) {
+  if constexpr (RMS) {
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][m];
@@ -488,13 +431,6 @@ int probed(int kind, const GemmArgs& a, hipStream_t s, F&& launch) {
 
 }  // namespace
 
-int SplitKWs::init() {
-  MPR_TRY(slab.ensure((size_t)kElems * sizeof(float)));
-  MPR_TRY(cnt.ensure((size_t)kTiles * sizeof(int)));
-  MPR_HIP(hipMemset(cnt.ptr, 0, (size_t)kTiles * sizeof(int)));
-  return MPR_OK;
-}
-
 int probe_enable(int kind) {
   g_probe_kind = kind;
   return MPR_OK;
@@ -526,27 +462,14 @@ int gemm(const GemmArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                   aligned16(a.W),
               "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-  // Larger tiles cut LDS/L2 traffic per FLOP but only pay while the grid still covers the 256
-  // CUs; at batch 16 many projections have N = 512..768 over M = 300..1200 rows, where a 64x64
-  // grid leaves most CUs idle, so the tile shrinks until the grid fills the chip.
-  // Measured on MI355X: below 64x64 the per-block efficiency loss outweighs the better fill
-  // (a 32x64 tile made the N=768 ViT projections slower), so 64x64 is the floor.
-  const int64_t b128 = cdiv(a.M, 128) * cdiv(a.N, 64);
-  const int64_t b64 = cdiv(a.M, 64) * cdiv(a.N, 64);
-  // Grids below ~0.75 of the CU count with a long K (the N=512/768 projections at batch 16)
-  // split K over blockIdx.z with the deterministic in-launch combine.
-  int splits = 1;
-  const int nk = (int)cdiv(a.K, 32);
-  if (a.sk_ws && a.sk_cnt && b64 < 192 && nk >= 16) {
-    splits = (int)std::min<int64_t>(4, cdiv(384, b64));
-    while (splits > 1 && nk / splits < 8) --splits;
-    if (b64 > a.sk_tiles || (int64_t)b64 * splits * 64 * 64 > a.sk_ws_elems) splits = 1;
-  }
-  return probed(PROBE_GEMM, a, s, [&]() {
-    if (splits > 1) return launch_gemm<64, 64, 1, 1>(a, s, splits);
-    if (b128 >= 512) return launch_gemm<128, 64, 2, 1>(a, s);
-    return launch_gemm<64, 64, 1, 1>(a, s);
-  });
+  // One tile shape: 64x64 (4 waves of 32x32, ~55 KB of LDS, 2 blocks per CU).  Measured on
+  // MI355X over the ViT/T5 projection shapes (tools/gbench.hip): 128x64 and 128x128 tiles are
+  // slower at every shape up to 2048^3 (fewer blocks, one per CU by LDS), 32x64 halves the
+  // waves per block without adding SIMD work.  Split-K over blockIdx.z (in-launch agent-scope
+  // combine) was slower at every shape too (800x768x768: 21.7 us plain, 30.6 at S=2, 47 at
+  // S=4): the release fence writes back the XCD L2 and a 64x64 fp32 slab per slice costs more
+  // than the idle CUs it fills.
+  return probed(PROBE_GEMM, a, s, [&]() { return launch_gemm<64, 64, 1, 1>(a, s); });
 }
 
 int64_t packed_rows16_elems(int64_t N, int64_t K) { return cdiv(N, 16) * cdiv(K, 16) * 256; }
@@ -559,6 +482,20 @@ int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, h
                      ldw, cdiv(K, 16), out);
   MPR_LAUNCHED();
   return MPR_OK;
+}
+
+template <bool RMS>
+void launch_skinny(const SkinnyArgs& sa, int64_t tiles, int per, hipStream_t s) {
+  if (tiles >= 1024 && per <= 4)  // lm_head: 4 tiles per block, more loads in flight
+    hipLaunchKernelGGL((gemm_skinny_kernel<4, 4, RMS>), dim3((unsigned)cdiv(tiles, 4)),
+                       dim3(512), 0, s, sa);
+  else if (per <= 4)
+    hipLaunchKernelGGL((gemm_skinny_kernel<4, 1, RMS>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
+  else if (per <= 8)
+    hipLaunchKernelGGL((gemm_skinny_kernel<8, 1, RMS>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<16, 1, RMS>), dim3((unsigned)tiles), dim3(512), 0, s,
+                       sa);
 }
 
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
@@ -574,15 +511,10 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
   return probed(PROBE_SKINNY, a, s, [&]() {
-    if (tiles >= 1024 && per <= 4)   // lm_head: 4 tiles per block, more loads in flight
-      hipLaunchKernelGGL((gemm_skinny_kernel<4, 4>), dim3((unsigned)cdiv(tiles, 4)), dim3(512),
-                         0, s, sa);
-    else if (per <= 4)
-      hipLaunchKernelGGL((gemm_skinny_kernel<4, 1>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
-    else if (per <= 8)
-      hipLaunchKernelGGL((gemm_skinny_kernel<8, 1>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
+    if (sa.rms_w)
+      launch_skinny<true>(sa, tiles, per, s);
     else
-      hipLaunchKernelGGL((gemm_skinny_kernel<16, 1>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
+      launch_skinny<false>(sa, tiles, per, s);
     MPR_LAUNCHED();
     return MPR_OK;
   });

@@ -24,27 +24,8 @@ struct GemmArgs {
   // Optional batched C rows: row r is stored at C + (r / c_rpb) * c_bs + (r % c_rpb) * ldc.
   int c_rpb = 0;
   int64_t c_bs = 0;
-  // Optional split-K workspace (owned by the calling model, one per stream of use): fp32 slabs
-  // and per-tile arrival counters (zeroed at allocation; each launch leaves them zeroed).
-  float* sk_ws = nullptr;
-  int* sk_cnt = nullptr;
-  int64_t sk_ws_elems = 0;
-  int64_t sk_tiles = 0;
 };
 
-// Split-K workspace a model owns and hands to its GEMMs (see GemmArgs::sk_*).
-struct SplitKWs {
-  DevBuf slab, cnt;
-  static constexpr int64_t kTiles = 256;
-  static constexpr int64_t kElems = 256 * 4 * 64 * 64;  // tiles x splits x 64x64
-  int init();
-  void attach(GemmArgs& g) const {
-    g.sk_ws = slab.as<float>();
-    g.sk_cnt = cnt.as<int>();
-    g.sk_ws_elems = slab.bytes / 4;
-    g.sk_tiles = cnt.bytes / 4;
-  }
-};
 int gemm(const GemmArgs& a, hipStream_t s);
 
 // Skinny GEMM for M <= 16 rows (decode steps): same contract as gemm() plus an optional fused

@@ -36,11 +36,6 @@ struct ClipTower {
   std::vector<std::unique_ptr<ClipBlock>> blocks;
   // workspace
   DevBuf h, qkv, ao, mlp;
-  SplitKWs sk;
-  int gemm_sk(GemmArgs& g, hipStream_t s) {
-    sk.attach(g);
-    return gemm(g, s);
-  }
   int load_blocks(const float* const* t, int width, int layers);
   // x [B*L, width] in place; causal for the text tower.
   int run(float* x, int B, int L, bool causal, hipStream_t s);
@@ -53,7 +48,6 @@ struct VitModel : mpr_model {
   ClipTower tower;
   DevBuf cols, patches, x, tmp;
   int forward(const float* img, int B, int mode, float* out, int64_t out_bs, hipStream_t s);
-  int gemm_sk(GemmArgs& g, hipStream_t s) { return tower.gemm_sk(g, s); }
 };
 
 struct TextModel : mpr_model {
@@ -63,7 +57,6 @@ struct TextModel : mpr_model {
   ClipTower tower;
   DevBuf x, pooled;
   int forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs, hipStream_t s);
-  int gemm_sk(GemmArgs& g, hipStream_t s) { return tower.gemm_sk(g, s); }
 };
 
 struct T5Layer {
@@ -86,11 +79,6 @@ struct T5Model : mpr_model {
   // workspace (every growth bumps `gen`, which invalidates captured decode graphs)
   DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, unfinished, cur_tok;
   DevBuf enc_in, mask_in, part_val, part_idx, tok_buf;
-  SplitKWs sk;
-  int gemm_sk(GemmArgs& g, hipStream_t s) {
-    sk.attach(g);
-    return gemm(g, s);
-  }
   uint64_t gen = 0;
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {

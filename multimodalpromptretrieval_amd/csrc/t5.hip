@@ -72,7 +72,7 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
     GemmArgs g;
     g.A = hp; g.lda = d; g.W = ly.qkv.as<float>(); g.ldw = d; g.C = qp; g.ldc = 3 * inner;
     g.M = M; g.N = 3 * inner; g.K = d;
-    MPR_TRY(gemm_sk(g, s));
+    MPR_TRY(gemm(g, s));
     AttnArgs at;
     at.q = qp; at.q_bs = (int64_t)L * 3 * inner; at.q_rs = 3 * inner;
     at.k = qp + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -86,16 +86,16 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
     GemmArgs o;
     o.A = ap; o.lda = inner; o.W = ly.o.as<float>(); o.ldw = inner; o.R = xp; o.ldr = d;
     o.C = xp; o.ldc = d; o.M = M; o.N = d; o.K = inner;
-    MPR_TRY(gemm_sk(o, s));
+    MPR_TRY(gemm(o, s));
     MPR_TRY(rmsnorm(xp, d, M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
     GemmArgs f;
     f.A = hp; f.lda = d; f.W = ly.wi.as<float>(); f.ldw = d; f.C = fp; f.ldc = dff;
     f.M = M; f.N = dff; f.K = d; f.act = ACT_RELU;
-    MPR_TRY(gemm_sk(f, s));
+    MPR_TRY(gemm(f, s));
     GemmArgs w;
     w.A = fp; w.lda = dff; w.W = ly.wo.as<float>(); w.ldw = dff; w.R = xp; w.ldr = d;
     w.C = xp; w.ldc = d; w.M = M; w.N = d; w.K = dff;
-    MPR_TRY(gemm_sk(w, s));
+    MPR_TRY(gemm(w, s));
   }
   MPR_TRY(rmsnorm(xp, d, M, d, enc_final.as<float>(), T5_EPS, out, d, s));
   return MPR_OK;
@@ -106,7 +106,7 @@ int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
   GemmArgs g;
   g.A = enc_out.as<float>(); g.lda = d; g.W = cross_kv_w.as<float>(); g.ldw = d;
   g.C = cross_kv.as<float>(); g.ldc = N; g.M = M; g.N = N; g.K = d;
-  return gemm_sk(g, s);
+  return gemm(g, s);
 }
 
 // Everything generate() enqueues after its inputs sit in enc_in / mask_in.  Only model-owned
@@ -300,7 +300,7 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
     GemmArgs g;
     g.A = hp; g.lda = d; g.W = ly.qkv.as<float>(); g.ldw = d; g.C = qp; g.ldc = 3 * inner;
     g.M = M; g.N = 3 * inner; g.K = d;
-    MPR_TRY(gemm_sk(g, s));
+    MPR_TRY(gemm(g, s));
     AttnArgs at;
     at.q = qp; at.q_bs = (int64_t)T * 3 * inner; at.q_rs = 3 * inner;
     at.k = qp + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -313,12 +313,12 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
     GemmArgs o;
     o.A = ap; o.lda = inner; o.W = ly.o.as<float>(); o.ldw = inner; o.R = xp; o.ldr = d;
     o.C = xp; o.ldc = d; o.M = M; o.N = d; o.K = inner;
-    MPR_TRY(gemm_sk(o, s));
+    MPR_TRY(gemm(o, s));
     MPR_TRY(rmsnorm(xp, d, M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
     GemmArgs cq;
     cq.A = hp; cq.lda = d; cq.W = ly.cq.as<float>(); cq.ldw = d; cq.C = cqp; cq.ldc = inner;
     cq.M = M; cq.N = inner; cq.K = d;
-    MPR_TRY(gemm_sk(cq, s));
+    MPR_TRY(gemm(cq, s));
     AttnArgs ca;
     ca.q = cqp; ca.q_bs = (int64_t)T * inner; ca.q_rs = inner;
     ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -330,16 +330,16 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
     GemmArgs co;
     co.A = ap; co.lda = inner; co.W = ly.co.as<float>(); co.ldw = inner; co.R = xp; co.ldr = d;
     co.C = xp; co.ldc = d; co.M = M; co.N = d; co.K = inner;
-    MPR_TRY(gemm_sk(co, s));
+    MPR_TRY(gemm(co, s));
     MPR_TRY(rmsnorm(xp, d, M, d, ly.ln2.as<float>(), T5_EPS, hp, d, s));
     GemmArgs f;
     f.A = hp; f.lda = d; f.W = ly.wi.as<float>(); f.ldw = d; f.C = fp; f.ldc = dff;
     f.M = M; f.N = dff; f.K = d; f.act = ACT_RELU;
-    MPR_TRY(gemm_sk(f, s));
+    MPR_TRY(gemm(f, s));
     GemmArgs w;
     w.A = fp; w.lda = dff; w.W = ly.wo.as<float>(); w.ldw = dff; w.R = xp; w.ldr = d;
     w.C = xp; w.ldc = d; w.M = M; w.N = d; w.K = dff;
-    MPR_TRY(gemm_sk(w, s));
+    MPR_TRY(gemm(w, s));
   }
   // final norm, then * d^-0.5 (the reference's op order, modeling_t5.py scale_decoder_outputs)
   MPR_TRY(rmsnorm(xp, d, M, d, dec_final.as<float>(), T5_EPS, hp, d, s));
@@ -347,7 +347,7 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
   GemmArgs hd;
   hd.A = hp; hd.lda = d; hd.W = lm_head.as<float>(); hd.ldw = d; hd.C = logits_out; hd.ldc = V;
   hd.M = M; hd.N = V; hd.K = d;
-  MPR_TRY(gemm_sk(hd, s));
+  MPR_TRY(gemm(hd, s));
   return MPR_OK;
 }
 

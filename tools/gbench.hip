@@ -48,8 +48,6 @@ int main() {
   (void)hipMalloc(&C, 64 << 20);
   (void)hipMemset(A, 0, 64 << 20);
   (void)hipMemset(W, 0, 64 << 20);
-  SplitKWs sk;
-  if (sk.init() != MPR_OK) return 1;
   struct Shape { const char* name; int M, N, K; };
   const Shape shapes[] = {
       {"vit qkv   800x2304x768", 800, 2304, 768},  {"vit out   800x768x768", 800, 768, 768},
@@ -57,29 +55,25 @@ int main() {
       {"t5e qkv  1136x1536x512", 1136, 1536, 512}, {"t5e wo   1136x512x2048", 1136, 512, 2048},
       {"sq 2048", 2048, 2048, 2048},
   };
-  using L = std::function<int(const GemmArgs&, hipStream_t, int)>;
-  struct Var { const char* name; L fn; int bm, bn; bool split; };
+  using L = std::function<int(const GemmArgs&, hipStream_t)>;
+  struct Var { const char* name; L fn; int bm, bn; };
   const Var vars[] = {
-      {"64x64 1x1", launch_gemm<64, 64, 1, 1>, 64, 64, true},
-      {"32x64 1x1", launch_gemm<32, 64, 1, 1>, 32, 64, false},
-      {"128x64 2x1", launch_gemm<128, 64, 2, 1>, 128, 64, false},
-      {"128x128 2x2", launch_gemm<128, 128, 2, 2>, 128, 128, false},
+      {"64x64 1x1", launch_gemm<64, 64, 1, 1>, 64, 64},
+      {"32x64 1x1", launch_gemm<32, 64, 1, 1>, 32, 64},
+      {"128x64 2x1", launch_gemm<128, 64, 2, 1>, 128, 64},
+      {"128x128 2x2", launch_gemm<128, 128, 2, 2>, 128, 128},
   };
   for (const Shape& sh : shapes) {
     const double gf = 2.0 * sh.M * sh.N * sh.K * 1e-9;
     printf("%s  (%.2f GFLOP)\n", sh.name, gf);
     for (const Var& v : vars) {
-      for (int splits = 1; splits <= (v.split ? 4 : 1); splits *= 2) {
-        const int64_t tiles = cdiv(sh.M, v.bm) * cdiv(sh.N, v.bn);
-        if (splits > 1 && (tiles > sk.kTiles || tiles * splits * 4096 > sk.kElems)) continue;
-        GemmArgs g;
-        g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.C = C; g.ldc = sh.N;
-        g.M = sh.M; g.N = sh.N; g.K = sh.K;
-        sk.attach(g);
-        const double us = time_graph(s, [&]() { v.fn(g, s, splits); }, 200);
-        printf("   %-22s split %d  blocks %5lld  %8.2f us  %6.1f TF/s\n", v.name, splits,
-               (long long)tiles * splits, us, gf / us * 1e3);
-      }
+      const int64_t tiles = cdiv(sh.M, v.bm) * cdiv(sh.N, v.bn);
+      GemmArgs g;
+      g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.C = C; g.ldc = sh.N;
+      g.M = sh.M; g.N = sh.N; g.K = sh.K;
+      const double us = time_graph(s, [&]() { v.fn(g, s); }, 200);
+      printf("   %-22s blocks %5lld  %8.2f us  %6.1f TF/s\n", v.name, (long long)tiles, us,
+             gf / us * 1e3);
     }
   }
   return 0;
