@@ -45,7 +45,8 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
   // makes hipcc drain vmcnt before every k-step's first ds_read.
   __shared__ __attribute__((aligned(16))) float smem[3 * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int M = a.M, N = a.N, K = a.K;
@@ -232,60 +233,67 @@ __global__ __launch_bounds__(256) void pack_rows16_kernel(const float* __restric
   reinterpret_cast<f32x4*>(out)[q] = v;
 }
 
+// Every option is a template flag: measured on MI355X, each runtime-optional part of this
+// kernel (a residual/bias branch, an argmax branch, a K loop) added 0.4-0.6 us to a ~3 us
+// launch, so each launch carries only the code its call needs, straight-line.
+enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8 };
+
 // NT 16-column tiles per block share the activation slab (NT > 1 for the 32k-column lm_head,
 // which needs more bytes in flight per wave); two accumulator chains per tile halve the
-// dependent-MFMA latency of the K loop.  MAXC = chunks of 16 columns staged per pass.
-template <int MAXC, int NT, bool RMS>
+// dependent-MFMA latency.  MAXC = chunks of 16 columns staged per pass; LOOP = more than one
+// pass (K > 16 * 8 * MAXC).
+template <int MAXC, int NT, int F, bool LOOP>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
+  constexpr bool RMS = (F & SKF_RMS) != 0, RES = (F & SKF_RES) != 0,
+                 RELU = (F & SKF_RELU) != 0, AMAX = (F & SKF_AMAX) != 0;
   const GemmArgs& a = sa.g;
   constexpr int XLD = MAXC * 16 + 4;  // slab row stride (floats): conflict-free fragment reads
-  __shared__ __attribute__((aligned(16))) float xs[SK_WAVES][16][XLD];
-  __shared__ __attribute__((aligned(16))) f32x4 red[NT][SK_WAVES][64];
-  __shared__ float ssq_s[SK_WAVES][16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int XS = SK_WAVES * 16 * XLD, RED = NT * SK_WAVES * 256;
+  // one LDS object: activation slabs | partial tiles | per-wave sums of squares
+  __shared__ __attribute__((aligned(16))) float smem[XS + RED + SK_WAVES * 16];
+  float(*xs)[16][XLD] = reinterpret_cast<float(*)[16][XLD]>(smem);
+  f32x4(*red)[SK_WAVES][64] = reinterpret_cast<f32x4(*)[SK_WAVES][64]>(smem + XS);
+  float(*ssq_s)[16] = reinterpret_cast<float(*)[16]>(smem + XS + RED);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int M = a.M, N = a.N, K = a.K;
   const int i = lane & 15, h = lane >> 4;
-  // (RMS is a template flag: behind a runtime `if` hipcc sinks the norm-weight loads into the
-  // branch, after the fragments arrive, one dependent L2 round trip per chunk)
-  const float* gsrc = sa.rms_w;
 
   const int nchunk = (K + 15) / 16;
   const int ntiles = (N + 15) / 16;
   const int per = (nchunk + SK_WAVES - 1) / SK_WAVES;
   const int c_lo = wave * per, c_hi = min(nchunk, c_lo + per);
+  const int c_safe = min(c_lo, nchunk - 1);  // an in-range chunk for padding reads
   // (a tile past N — the lm_head's last block — re-reads the last tile; never stored)
   const f32x4* wp[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
     wp[t] = reinterpret_cast<const f32x4*>(sa.wpk) +
             ((int64_t)min((int)blockIdx.x * NT + t, ntiles - 1) * nchunk) * 64 + lane;
-  // Epilogue operands (residual, bias) are fetched up front by the epilogue waves.
-  const int m_ep = lane & 15;
-  float rres[4] = {0.f, 0.f, 0.f, 0.f}, rbias[4] = {0.f, 0.f, 0.f, 0.f};
-  if (wave < NT) {
-    const int n0e = (blockIdx.x * NT + wave) * 16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = min(n0e + (lane >> 4) * 4 + r, N - 1);
-      if (a.R) rres[r] = a.R[(int64_t)min(m_ep, M - 1) * a.ldr + n];
-      if (a.bias) rbias[r] = a.bias[n];
-    }
+  // The lane's 4 outputs are row i, columns n0 + 4h .. +3 (16x16 D layout): its residual is
+  // one float4, fetched before the main loads.
+  f32x4 rres = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RES) {
+    if (wave < NT)
+      rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)min(i, M - 1) * a.ldr +
+                                             (blockIdx.x * NT + wave) * 16 + h * 4);
   }
   f32x4 acc[NT][2];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
-  for (int c0 = c_lo; c0 < c_hi; c0 += MAXC) {
+#pragma unroll 1
+  for (int c0 = c_lo; LOOP ? c0 < c_hi : c0 == c_lo; c0 += MAXC) {
     // weights first (the long pole), then this pass's activation rows as 256-byte segments:
     // float4 q of the pass = row q / (4*MAXC), column (q % (4*MAXC)) * 4 of the pass
     f32x4 wv[NT][MAXC], xr[MAXC], gv[MAXC];
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
-      // a chunk past the wave's slice re-reads chunk c_lo; its activation columns are zero
-      const int c = c0 + u, cc = c < c_hi ? c : c_lo;
+      // a chunk past the wave's slice re-reads an in-range chunk; its activations are zero
+      const int c = c0 + u, cc = c < c_hi ? c : c_safe;
 #pragma unroll
       for (int t = 0; t < NT; ++t) wv[t][u] = wp[t][(int64_t)cc * 64];
-      if constexpr (RMS) gv[u] = *reinterpret_cast<const f32x4*>(gsrc + cc * 16 + h * 4);
+      if constexpr (RMS) gv[u] = *reinterpret_cast<const f32x4*>(sa.rms_w + cc * 16 + h * 4);
     }
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
@@ -336,21 +344,20 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
 #pragma unroll
   for (int w = 1; w < SK_WAVES; ++w) sum += red[wave][w][lane];
   // D[row = W row (n), col = A row (m)]: col = lane&15, row = (lane>>4)*4 + r.
-  const int m = lane & 15;
   float scale = sa.a_scale;
   if constexpr (RMS) {
     float t = 0.f;
 #pragma unroll
-    for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][m];
+    for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][i];
     scale = (1.0f / sqrtf(t / (float)K + sa.rms_eps)) * sa.a_scale;
   }
-  if (sa.amax_val) {
+  if constexpr (AMAX) {
     // greedy head: per (row m, block) best column, lowest index on ties (torch.argmax)
     float bv = -INFINITY;
     int bi = 0x7fffffff;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int n = n0 + (lane >> 4) * 4 + r;
+      const int n = n0 + h * 4 + r;
       const float v = sum[r] * scale;
       if (n < N && (v > bv || (v == bv && n < bi))) {
         bv = v;
@@ -367,19 +374,17 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       }
     }
     if (lane < 16 && n0 < N) {
-      sa.amax_val[(int64_t)tile * 16 + m] = bv;
-      sa.amax_idx[(int64_t)tile * 16 + m] = bi;
+      sa.amax_val[(int64_t)tile * 16 + i] = bv;
+      sa.amax_idx[(int64_t)tile * 16 + i] = bi;
     }
-    if (!a.C) return;
-  }
-  if (m >= M) return;
+  } else {
+    f32x4 v = sum * scale;
+    if constexpr (RELU) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int n = n0 + (lane >> 4) * 4 + r;
-    if (n >= N) continue;
-    float v = act_exact(sum[r] * scale + rbias[r], a.act);
-    if (a.R) v = rres[r] + v;
-    a.C[(int64_t)m * a.ldc + n] = v;
+      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+    }
+    if constexpr (RES) v = rres + v;
+    if (i < M) *reinterpret_cast<f32x4*>(a.C + (int64_t)i * a.ldc + n0 + h * 4) = v;
   }
 }
 
@@ -484,18 +489,22 @@ int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, h
   return MPR_OK;
 }
 
-template <bool RMS>
-void launch_skinny(const SkinnyArgs& sa, int64_t tiles, int per, hipStream_t s) {
-  if (tiles >= 1024 && per <= 4)  // lm_head: 4 tiles per block, more loads in flight
-    hipLaunchKernelGGL((gemm_skinny_kernel<4, 4, RMS>), dim3((unsigned)cdiv(tiles, 4)),
-                       dim3(512), 0, s, sa);
-  else if (per <= 4)
-    hipLaunchKernelGGL((gemm_skinny_kernel<4, 1, RMS>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
-  else if (per <= 8)
-    hipLaunchKernelGGL((gemm_skinny_kernel<8, 1, RMS>), dim3((unsigned)tiles), dim3(512), 0, s, sa);
-  else
-    hipLaunchKernelGGL((gemm_skinny_kernel<16, 1, RMS>), dim3((unsigned)tiles), dim3(512), 0, s,
-                       sa);
+template <int MAXC, int NT, bool LOOP>
+void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s) {
+#define MPR_SK(f)                                                                          \
+  case f:                                                                                  \
+    hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP>), dim3(grid), dim3(512), 0, s, sa); \
+    break;
+  if constexpr (NT > 1) {
+    switch (F) { MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS) default: break; }
+  } else {
+    switch (F) {
+      MPR_SK(0) MPR_SK(1) MPR_SK(2) MPR_SK(3) MPR_SK(4) MPR_SK(5) MPR_SK(6) MPR_SK(7)
+      MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS)
+      default: break;
+    }
+  }
+#undef MPR_SK
 }
 
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
@@ -506,15 +515,29 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && aligned16(a.A) &&
                   (!sa.rms_w || aligned16(sa.rms_w)),
               "gemm_skinny: K/lda must be multiples of 4, operands 16-byte aligned");
-  MPR_REQUIRE(!sa.amax_val || (sa.amax_idx && !a.R && !a.bias && a.act == ACT_NONE),
-              "gemm_skinny: argmax mode takes plain logits");
+  MPR_REQUIRE(!a.bias && (a.act == ACT_NONE || a.act == ACT_RELU),
+              "gemm_skinny: no bias, activation none or relu (the T5 decoder's projections)");
+  const bool amax = sa.amax_val != nullptr;
+  MPR_REQUIRE(!amax || (sa.amax_idx && !a.R && !a.C && a.act == ACT_NONE),
+              "gemm_skinny: argmax mode takes plain logits and stores no C");
+  MPR_REQUIRE(amax || (a.C && a.N % 16 == 0 && a.ldc % 4 == 0 && aligned16(a.C) &&
+                       (!a.R || (a.ldr % 4 == 0 && aligned16(a.R)))),
+              "gemm_skinny: N must be a multiple of 16, C/R rows 16-byte aligned");
+  const int F = (sa.rms_w ? SKF_RMS : 0) | (a.R ? SKF_RES : 0) |
+                (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0);
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
   return probed(PROBE_SKINNY, a, s, [&]() {
-    if (sa.rms_w)
-      launch_skinny<true>(sa, tiles, per, s);
+    if (amax && tiles >= 1024 && per <= 4)  // lm_head: 4 tiles per block, more loads in flight
+      launch_skinny<4, 4, false>(sa, F, (unsigned)cdiv(tiles, 4), s);
+    else if (per <= 4)
+      launch_skinny<4, 1, false>(sa, F, (unsigned)tiles, s);
+    else if (per <= 8)
+      launch_skinny<8, 1, false>(sa, F, (unsigned)tiles, s);
+    else if (per <= 16)
+      launch_skinny<16, 1, false>(sa, F, (unsigned)tiles, s);
     else
-      launch_skinny<false>(sa, tiles, per, s);
+      launch_skinny<16, 1, true>(sa, F, (unsigned)tiles, s);
     MPR_LAUNCHED();
     return MPR_OK;
   });

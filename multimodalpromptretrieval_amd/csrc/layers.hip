@@ -93,7 +93,8 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ps[4][4][ATT_KC];
 
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * ATT_QR;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   {
     const int r = tid >> 4, c4 = (tid & 15) * 4, i = q0 + r;
     f32x4 qv = {0.f, 0.f, 0.f, 0.f};
@@ -201,7 +202,8 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
   __shared__ float red[2][4];
   __shared__ float Ps[DEC_KC];
   __shared__ __attribute__((aligned(16))) float Os[16][ATT_D];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const float* qp = a.q + (int64_t)b * a.q_bs + h * ATT_D;
   const int qpos = a.q_pos0;

@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X,
   float* Qs = lds;
   __shared__ float qn_s[QG];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int g = blockIdx.y, qbase = g * QG;
   // Stage the query group (zero rows past b).
   for (int idx = tid; idx < QG * (d / 4); idx += 256) {

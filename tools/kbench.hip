@@ -71,11 +71,12 @@ int main() {
   (void)hipMemcpy(mask, ones.data(), 1 << 20, hipMemcpyHostToDevice);
 
   time_chain("fill_i32 (1 block)", s, [&](int) { fill_i32(unf, 1, 16, s); });
+  size_t wstride = 4 << 20;
   auto skinny = [&](int N, int K, bool rms, bool res, int i) {
     SkinnyArgs a;
     a.g.A = (i & 1) ? y : x;
     a.g.lda = K;
-    a.wpk = W + (size_t)(i % 6) * (4 << 20);
+    a.wpk = W + (size_t)(i % 6) * wstride;
     a.g.C = (i & 1) ? x : y;
     a.g.ldc = N;
     a.g.M = 16;
@@ -89,6 +90,10 @@ int main() {
     gemm_skinny(a, s);
   };
   time_chain("skinny N512 K512 plain", s, [&](int i) { skinny(512, 512, false, false, i); });
+  wstride = 1 << 20;
+  time_chain("skinny N512 K512 plain, 4MB stride", s, [&](int i) { skinny(512, 512, false, false, i); });
+  time_chain("skinny N512 K512 +res, 4MB stride", s, [&](int i) { skinny(512, 512, false, true, i); });
+  wstride = 4 << 20;
   time_chain("skinny N512 K512 rms", s, [&](int i) { skinny(512, 512, true, false, i); });
   time_chain("skinny N512 K512 +res", s, [&](int i) { skinny(512, 512, false, true, i); });
   time_chain("skinny N1536 K512 rms", s, [&](int i) { skinny(1536, 512, true, false, i); });

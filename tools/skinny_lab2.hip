@@ -6,6 +6,13 @@
 #include <cstdio>
 #include <functional>
 
+#include "../multimodalpromptretrieval_amd/csrc/api.hip"
+#include "../multimodalpromptretrieval_amd/csrc/encoders.hip"
+#include "../multimodalpromptretrieval_amd/csrc/gemm.hip"
+#include "../multimodalpromptretrieval_amd/csrc/layers.hip"
+#include "../multimodalpromptretrieval_amd/csrc/scan.hip"
+#include "../multimodalpromptretrieval_amd/csrc/t5.hip"
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct Args {
@@ -150,5 +157,18 @@ int main() {
   RUN("stage + epi + residual", 1, 1, 1, true);
   RUN("direct + epi + residual", 0, 1, 1, true);
   RUN("stage, no red", 1, 0, 0, false);
+  auto lib = [&](int i, bool res) {
+    mpr::SkinnyArgs a;
+    a.wpk = W + (size_t)(i % 6) * (1 << 20);
+    a.g.A = (i & 1) ? y : x;
+    a.g.C = (i & 1) ? x : y;
+    if (res) { a.g.R = a.g.C; a.g.ldr = 512; }
+    a.g.M = 16; a.g.N = 512; a.g.K = 512; a.g.lda = 512; a.g.ldc = 512;
+    return a;
+  };
+  printf("%-34s %.3f us\n", "library gemm_skinny()", time_graph(s, [&](int i) {
+           mpr::gemm_skinny(lib(i, false), s); }));
+  printf("%-34s %.3f us\n", "library gemm_skinny() +res", time_graph(s, [&](int i) {
+           mpr::gemm_skinny(lib(i, true), s); }));
   return 0;
 }
