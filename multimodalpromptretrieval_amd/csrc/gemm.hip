@@ -373,9 +373,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
         bi = oi;
       }
     }
-    if (lane < 16 && n0 < N) {
-      sa.amax_val[(int64_t)tile * 16 + i] = bv;
-      sa.amax_idx[(int64_t)tile * 16 + i] = bi;
+    if (lane < 16 && n0 < N) {  // row-major [16][ntiles]: greedy_step reads rows coalesced
+      sa.amax_val[(int64_t)i * ntiles + tile] = bv;
+      sa.amax_idx[(int64_t)i * ntiles + tile] = bi;
     }
   } else {
     f32x4 v = sum * scale;
@@ -528,8 +528,8 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
   return probed(PROBE_SKINNY, a, s, [&]() {
-    if (amax && tiles >= 1024 && per <= 4)  // lm_head: 4 tiles per block, more loads in flight
-      launch_skinny<4, 4, false>(sa, F, (unsigned)cdiv(tiles, 4), s);
+    if (amax && tiles >= 1024 && per <= 4)  // lm_head: 2 tiles per block (NT 1/2/4/8 measured
+      launch_skinny<4, 2, false>(sa, F, (unsigned)cdiv(tiles, 2), s);  // 14.5/13.1/13.8/14.5 us)
     else if (per <= 4)
       launch_skinny<4, 1, false>(sa, F, (unsigned)tiles, s);
     else if (per <= 8)

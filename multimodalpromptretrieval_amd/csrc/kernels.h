@@ -43,7 +43,8 @@ struct SkinnyArgs {
   const float* rms_w = nullptr;  // fuse RMSNorm prologue when non-null
   float rms_eps = 1e-6f;
   float a_scale = 1.f;           // A' = (ln_w * (A * rstd)) * a_scale (T5 tied-head d^-0.5)
-  // Greedy head: per (block, row) best column -> amax_val/idx[block*16 + row] (C may be null).
+  // Greedy head: per (16-column tile, row) best column -> amax_val/idx[row * cdiv(N,16) + tile]
+  // (C must be null).
   float* amax_val = nullptr;
   int32_t* amax_idx = nullptr;
 };
@@ -100,7 +101,7 @@ int eot_gather(const float* x, const int32_t* tok, int B, int L, int ctx, int D,
 // Row argmax (first maximal index, torch.argmax semantics).
 int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hipStream_t s);
 // Greedy-search step (GenerationMixin._sample, do_sample=False): next = argmax over the
-// lm_head's per-block partials part_*[p*16 + b] (first maximal index); finished rows emit pad;
+// lm_head's per-tile partials part_*[b*nparts + p] (first maximal index); finished rows emit pad;
 // tokens[b*tok_ld + col] = next; unfinished[b] &= next != eos;
 // x[b, :] = table[next, :] (decoder input embedding of the next step, may be null).
 int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int M,

@@ -367,18 +367,22 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(const float* part_val,
                                                           int64_t tok_ld, int col, int eos,
                                                           int pad, const float* table, int D,
                                                           float* x) {
-  const int row = blockIdx.x;
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int unf = unfinished[row];  // issued with the partial loads, not after the argmax
+  const float* pv = part_val + (int64_t)row * nparts;
+  const int32_t* pi = part_idx + (int64_t)row * nparts;
   float best = -INFINITY;
   int bi = 0x7fffffff;
   for (int p0 = 0; p0 < nparts; p0 += 256 * 8) {
     float v[8];
     int c[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {  // all loads first: one round trip per 2048 partials
-      const int p = p0 + u * 256 + threadIdx.x;
+    for (int u = 0; u < 8; ++u) {  // all loads first, lane-contiguous
+      const int p = p0 + u * 256 + tid;
       const int pc = p < nparts ? p : 0;
-      v[u] = part_val[(int64_t)pc * 16 + row];
-      c[u] = part_idx[(int64_t)pc * 16 + row];
+      v[u] = pv[pc];
+      c[u] = pi[pc];
       if (p >= nparts) v[u] = -INFINITY;
     }
 #pragma unroll
@@ -389,35 +393,40 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(const float* part_val,
       }
     }
   }
-  __shared__ float bv[256];
-  __shared__ int bix[256];
-  __shared__ int next_s;
-  bv[threadIdx.x] = best;
-  bix[threadIdx.x] = bi;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      const float ov = bv[threadIdx.x + s];
-      const int oi = bix[threadIdx.x + s];
-      if (ov > bv[threadIdx.x] || (ov == bv[threadIdx.x] && oi < bix[threadIdx.x])) {
-        bv[threadIdx.x] = ov;
-        bix[threadIdx.x] = oi;
-      }
+  // wave argmax by shuffles, then the 4 wave results through LDS (one barrier)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(best, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ov > best || (ov == best && oi < bi)) {
+      best = ov;
+      bi = oi;
     }
-    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    int next = bix[0] == 0x7fffffff ? 0 : bix[0];
-    const int unf = unfinished[row];
-    next = unf ? next : pad;
+  __shared__ float wb[4];
+  __shared__ int wi[4];
+  if (lane == 0) {
+    wb[wave] = best;
+    wi[wave] = bi;
+  }
+  __syncthreads();
+  best = wb[0];
+  bi = wi[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (wb[w] > best || (wb[w] == best && wi[w] < bi)) {
+      best = wb[w];
+      bi = wi[w];
+    }
+  int next = bi == 0x7fffffff ? 0 : bi;
+  next = unf ? next : pad;
+  if (tid == 0) {
     tokens[(int64_t)row * tok_ld + col] = next;
     unfinished[row] = (unf && next != eos) ? 1 : 0;
-    next_s = next;
   }
-  __syncthreads();
   if (x) {
-    const float* src = table + (int64_t)next_s * D;
-    for (int c = threadIdx.x; c < D; c += 256) x[(int64_t)row * D + c] = src[c];
+    const float* src = table + (int64_t)next * D;
+    for (int c = tid; c < D; c += 256) x[(int64_t)row * D + c] = src[c];
   }
 }
 

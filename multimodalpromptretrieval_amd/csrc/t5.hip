@@ -210,6 +210,12 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
   MPR_REQUIRE(max_new + 1 <= lut_radius, "t5 generate: max_new exceeds lut radius");
   MPR_REQUIRE(2 * L <= lut_radius && L >= 1, "t5 generate: L=%d", L);
   if (B == 0) return MPR_OK;
+  // The source length is bucketed to a multiple of 8 (zero rows, mask 0) so a serving loop
+  // with varying prompt lengths replays a few captured graphs instead of capturing one per
+  // length.  Masked keys add exact zeros to every softmax sum and rows are independent in
+  // every other op, so the real rows' results are bit-identical.
+  const int Lsrc = L;
+  L = std::min((int)cdiv(L, 8) * 8, lut_radius / 2);
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int M = B * L, nparts = (int)cdiv(V, 16);
   // Every buffer the body touches is sized before capture (no allocation inside a graph).
@@ -230,8 +236,17 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
   MPR_TRY(grow(unfinished, (size_t)16 * 4));
   MPR_TRY(grow(cur_tok, (size_t)16 * 4));
   MPR_TRY(grow(tok_buf, (size_t)B * T1 * 4));
-  MPR_HIP(hipMemcpyAsync(enc_in.ptr, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
-  MPR_HIP(hipMemcpyAsync(mask_in.ptr, mask, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
+  if (L == Lsrc) {
+    MPR_HIP(hipMemcpyAsync(enc_in.ptr, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
+    MPR_HIP(hipMemcpyAsync(mask_in.ptr, mask, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
+  } else {
+    MPR_HIP(hipMemsetAsync(enc_in.ptr, 0, (size_t)M * d * 4, s));
+    MPR_HIP(hipMemsetAsync(mask_in.ptr, 0, (size_t)M * 4, s));
+    MPR_HIP(hipMemcpy2DAsync(enc_in.ptr, (size_t)L * d * 4, embeds, (size_t)Lsrc * d * 4,
+                             (size_t)Lsrc * d * 4, B, hipMemcpyDeviceToDevice, s));
+    MPR_HIP(hipMemcpy2DAsync(mask_in.ptr, (size_t)L * 4, mask, (size_t)Lsrc * 4,
+                             (size_t)Lsrc * 4, B, hipMemcpyDeviceToDevice, s));
+  }
   if (!graphs_enabled()) {
     MPR_TRY(generate_body(B, L, max_new, start, eos, pad, s));
   } else {

@@ -278,6 +278,42 @@ class T5VisionModel(nn.Module):
                                           do_sample=False, max_new_tokens=self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
+    def predict_many(self, batches):
+        """predict() over an iterable of batches as a two-deep pipeline (a serving loop): while
+        batch i's T5 generate runs on the device (its decode steps occupy few CUs), batch i+1's
+        image towers, question tower and index scan run beside it on other streams and the host
+        builds batch i+1's prompts.  Yields each batch's answers in order; every batch gets
+        exactly the work and the result predict() gives it."""
+        if not hasattr(self, "_s_main"):
+            self._s_main = torch.cuda.Stream(self.device)
+        if not hasattr(self, "_s_prep"):
+            self._s_prep = torch.cuda.Stream(self.device)
+        pending = None
+        for batch in batches:
+            self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._s_prep):
+                combined, mask, _ = self.prepare_input(batch)
+            self._s_main.wait_stream(self._s_prep)
+            with torch.cuda.stream(self._s_main):
+                combined.record_stream(self._s_main)
+                mask.record_stream(self._s_main)
+                t5 = self._device_t5()
+                toks = t5.generate_padded(combined, mask, self.max_new_tokens)
+                host = torch.empty(toks.shape, dtype=toks.dtype, pin_memory=True)
+                host.copy_(toks, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(self._s_main)
+            if pending is not None:
+                yield self._finish(*pending)
+            pending = (host, done)
+        if pending is not None:
+            yield self._finish(*pending)
+
+    def _finish(self, host_tokens, done):
+        done.synchronize()  # this batch's tokens only; the next batch keeps running
+        seqs = DeviceT5.trim(host_tokens)
+        return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
+
     def forward(self, batch):
         """architectures/T5VisionModel.py:219-234 (loss value; no autograd)."""
         combined, mask, _ = self.prepare_input(batch)

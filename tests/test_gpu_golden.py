@@ -123,6 +123,34 @@ def test_g2_pipeline_product(device):
     assert m3.cpu().tolist() == z["mask_txt"].tolist()
 
 
+def test_g2_predict_many_matches_predict(device):
+    """The two-deep serving pipeline returns, per batch, exactly predict()'s answers (batches
+    of different prompt lengths and images in flight together; the first is the golden one)."""
+    from multimodalpromptretrieval_amd.dataset import VQARetrieval
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    with open(os.path.join(GOLD, "g2_pipeline.json")) as f:
+        j = json.load(f)
+    ccfg, clip_sd, tcfg, tok_sd, t5cfg, t5_sd = gi.g2_models()
+    X, answers, info = gi.g2_index(ccfg)
+    retr = VQARetrieval(device, clip_state_dict=clip_sd, clip_tokenizer=syn.hash_clip_tokenize)
+    retr.set_index(X, answers, info, gi.G2["k"], False)
+    model = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=t5_sd,
+                          tokenizer=syn.HashT5Tokenizer(),
+                          retrieval_function=retr.retrieve_closest_qa_pairs).eval()
+    b0 = gi.g2_batch()
+    batches = [b0]
+    for i in (1, 2, 3):
+        b = dict(b0)
+        b["image"] = syn.images(900 + i, len(b0["question"]), gi.G2["clip_cfg"]["image_size"])
+        b["question"] = [q + " which" * (i * k % 5) for k, q in enumerate(b0["question"])]
+        batches.append(b)
+    want = [model.predict(b) for b in batches]
+    assert want[0] == j["predictions"]
+    assert list(model.predict_many(batches)) == want
+    assert list(model.predict_many(iter(batches[:1]))) == want[:1]
+    assert list(model.predict_many([])) == []
+
+
 def test_g2_state_dict_roundtrip_refreshes_device_weights(device):
     from multimodalpromptretrieval_amd.model import T5VisionModel
     _, _, tcfg, tok_sd, t5cfg, t5_sd = gi.g2_models()

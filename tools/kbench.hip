@@ -105,6 +105,21 @@ int main() {
     a.g.N = 32101; a.g.K = 512; a.rms_w = g; a.amax_val = pv; a.amax_idx = pi;
     gemm_skinny(a, s);
   }, 200);
+  for (int nt : {1, 2, 4, 8}) {
+    char name[64];
+    snprintf(name, sizeof name, "lm_head argmax NT=%d", nt);
+    time_chain(name, s, [&](int i) {
+      SkinnyArgs a;
+      a.g.A = x; a.g.lda = 512; a.wpk = W; a.g.C = nullptr; a.g.M = 16;
+      a.g.N = 32101; a.g.K = 512; a.rms_w = g; a.amax_val = pv; a.amax_idx = pi;
+      const int F = SKF_AMAX | SKF_RMS;
+      const unsigned tiles = (unsigned)cdiv(32101, 16);
+      if (nt == 1) launch_skinny<4, 1, false>(a, F, tiles, s);
+      if (nt == 2) launch_skinny<4, 2, false>(a, F, (unsigned)cdiv(tiles, 2), s);
+      if (nt == 4) launch_skinny<4, 4, false>(a, F, (unsigned)cdiv(tiles, 4), s);
+      if (nt == 8) launch_skinny<4, 8, false>(a, F, (unsigned)cdiv(tiles, 8), s);
+    }, 200);
+  }
   time_chain("greedy_step", s, [&](int i) {
     greedy_step(pv, pi, 2007, 16, unf, tok, 21, 1 + (i % 20), 1, 0, W, 512, x, s);
   });
