@@ -86,6 +86,13 @@ int mpr_vit_create(const int32_t* cfg, int32_t n_cfg, const float* const* tensor
  * mode 1: token path (ln_post on all tokens, @proj) -> out[b*out_bstride + t*out_dim + c]. */
 int mpr_vit_forward(mpr_model* m, const float* img_dev, int32_t b, int32_t mode, float* out_dev,
                     int64_t out_bstride, void* stream);
+/* Two ViTs of the same geometry over the same images in one pass (the reference runs the
+ * retrieval encode_image, dataset/VQAFeatureDataset.py:189, and get_image_token_features,
+ * architectures/T5VisionModel.py:112-139, on every batch): results identical to two
+ * mpr_vit_forward calls; the towers' projections share launches.  a != b. */
+int mpr_vit_forward_pair(mpr_model* a, int32_t mode_a, float* out_a_dev, int64_t out_a_bstride,
+                         mpr_model* b, int32_t mode_b, float* out_b_dev, int64_t out_b_bstride,
+                         const float* img_dev, int32_t b_images, void* stream);
 
 /* ---- CLIP text encoder: dataset/VQAFeatureDataset.py:190 (clip_model.encode_text) -----------
  * cfg = {width, layers, heads, context_length, vocab, out_dim}.  tensors: token_embedding

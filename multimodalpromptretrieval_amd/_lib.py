@@ -37,6 +37,8 @@ SIGNATURES = [
     ("mpr_vit_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32, POINTER(c_void_p)]),
     ("mpr_vit_forward", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64,
                                   c_void_p]),
+    ("mpr_vit_forward_pair", c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int32,
+                                       c_void_p, c_int64, c_void_p, c_int32, c_void_p]),
     ("mpr_clip_text_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32,
                                        POINTER(c_void_p)]),
     ("mpr_clip_text_forward", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64,

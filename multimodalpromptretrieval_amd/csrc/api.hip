@@ -195,6 +195,21 @@ int mpr_vit_forward(mpr_model* m, const float* img, int32_t b, int32_t mode, flo
   });
 }
 
+int mpr_vit_forward_pair(mpr_model* a, int32_t mode_a, float* out_a, int64_t out_a_bs,
+                         mpr_model* b, int32_t mode_b, float* out_b, int64_t out_b_bs,
+                         const float* img, int32_t batch, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(a && a->kind == mpr_model::VIT && b && b->kind == mpr_model::VIT,
+                "vit_forward_pair: not ViT handles");
+    MPR_REQUIRE(a != b, "vit_forward_pair: the two handles must differ (workspaces)");
+    VitModel* v[2] = {static_cast<VitModel*>(a), static_cast<VitModel*>(b)};
+    const int modes[2] = {mode_a, mode_b};
+    float* outs[2] = {out_a, out_b};
+    const int64_t bs[2] = {out_a_bs, out_b_bs};
+    return VitModel::forward_group(v, img, batch, modes, outs, bs, 2, S(stream));
+  });
+}
+
 // ---- CLIP text ------------------------------------------------------------------------------------
 int mpr_clip_text_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int32_t nt,
                          mpr_model** out) {

@@ -44,81 +44,147 @@ int ClipTower::load_blocks(const float* const* t, int w, int nl) {
 }
 
 int ClipTower::run(float* x, int B, int L, bool causal, hipStream_t s) {
-  const int W = width, M = B * L;
-  MPR_TRY(h.ensure((size_t)M * W * 4));
-  MPR_TRY(qkv.ensure((size_t)M * 3 * W * 4));
-  MPR_TRY(ao.ensure((size_t)M * W * 4));
-  MPR_TRY(mlp.ensure((size_t)M * 4 * W * 4));
-  float* hp = h.as<float>();
-  float* qp = qkv.as<float>();
-  float* ap = ao.as<float>();
-  float* mp = mlp.as<float>();
-  for (auto& bp : blocks) {
-    const ClipBlock& b = *bp;
-    MPR_TRY(layernorm(x, W, M, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(), CLIP_LN_EPS, hp, W, s));
-    GemmArgs g;
-    g.A = hp; g.lda = W; g.W = b.in_w.as<float>(); g.ldw = W; g.bias = b.in_b.as<float>();
-    g.C = qp; g.ldc = 3 * W; g.M = M; g.N = 3 * W; g.K = W;
-    MPR_TRY(gemm(g, s));
-    AttnArgs at;
-    at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
-    at.k = qp + W; at.k_bs = at.q_bs; at.k_rs = 3 * W;
-    at.v = qp + 2 * W; at.v_bs = at.q_bs; at.v_rs = 3 * W;
-    at.o = ap; at.o_bs = (int64_t)L * W; at.o_rs = W;
-    at.B = B; at.H = heads; at.Lq = L; at.Lk = L;
-    at.scale = 0.125f;  // 64 ** -0.5, exact power of two
-    at.causal = causal ? 1 : 0;
-    MPR_TRY(attention(at, s));
-    GemmArgs o;
-    o.A = ap; o.lda = W; o.W = b.out_w.as<float>(); o.ldw = W; o.bias = b.out_b.as<float>();
-    o.R = x; o.ldr = W; o.C = x; o.ldc = W; o.M = M; o.N = W; o.K = W;
-    MPR_TRY(gemm(o, s));
-    MPR_TRY(layernorm(x, W, M, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(), CLIP_LN_EPS, hp, W, s));
-    GemmArgs f;
-    f.A = hp; f.lda = W; f.W = b.fc_w.as<float>(); f.ldw = W; f.bias = b.fc_b.as<float>();
-    f.C = mp; f.ldc = 4 * W; f.M = M; f.N = 4 * W; f.K = W; f.act = ACT_QUICKGELU;
-    MPR_TRY(gemm(f, s));
-    GemmArgs pj;
-    pj.A = mp; pj.lda = 4 * W; pj.W = b.pj_w.as<float>(); pj.ldw = 4 * W; pj.bias = b.pj_b.as<float>();
-    pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M; pj.N = W; pj.K = 4 * W;
-    MPR_TRY(gemm(pj, s));
+  ClipTower* t = this;
+  return run_group(&t, &x, 1, B, L, causal, s);
+}
+
+// n towers of one geometry (n <= 2: the retrieval and token-feature ViTs of a batch) stepped in
+// lockstep; every projection of layer l is one grouped GEMM launch over the n towers.
+int ClipTower::run_group(ClipTower* const* t, float* const* xs, int n, int B, int L, bool causal,
+                         hipStream_t s) {
+  MPR_REQUIRE(n >= 1 && n <= 2, "clip tower group: n=%d", n);
+  const int W = t[0]->width, M = B * L;
+  for (int i = 0; i < n; ++i) {
+    MPR_REQUIRE(t[i]->width == W && t[i]->layers == t[0]->layers,
+                "clip tower group: towers differ in geometry");
+    MPR_TRY(t[i]->h.ensure((size_t)M * W * 4));
+    MPR_TRY(t[i]->qkv.ensure((size_t)M * 3 * W * 4));
+    MPR_TRY(t[i]->ao.ensure((size_t)M * W * 4));
+    MPR_TRY(t[i]->mlp.ensure((size_t)M * 4 * W * 4));
+  }
+  const int heads = t[0]->heads;
+  for (int l = 0; l < t[0]->layers; ++l) {
+    GemmGroup gq, go, gf, gp;
+    gq.n = go.n = gf.n = gp.n = n;
+    for (int i = 0; i < n; ++i) {
+      const ClipBlock& b = *t[i]->blocks[l];
+      float* x = xs[i];
+      float* hp = t[i]->h.as<float>();
+      float* qp = t[i]->qkv.as<float>();
+      float* ap = t[i]->ao.as<float>();
+      float* mp = t[i]->mlp.as<float>();
+      GemmArgs& g = gq.g[i];
+      g.A = hp; g.lda = W; g.W = b.in_w.as<float>(); g.ldw = W; g.bias = b.in_b.as<float>();
+      g.C = qp; g.ldc = 3 * W; g.M = M; g.N = 3 * W; g.K = W;
+      GemmArgs& o = go.g[i];
+      o.A = ap; o.lda = W; o.W = b.out_w.as<float>(); o.ldw = W; o.bias = b.out_b.as<float>();
+      o.R = x; o.ldr = W; o.C = x; o.ldc = W; o.M = M; o.N = W; o.K = W;
+      GemmArgs& f = gf.g[i];
+      f.A = hp; f.lda = W; f.W = b.fc_w.as<float>(); f.ldw = W; f.bias = b.fc_b.as<float>();
+      f.C = mp; f.ldc = 4 * W; f.M = M; f.N = 4 * W; f.K = W; f.act = ACT_QUICKGELU;
+      GemmArgs& pj = gp.g[i];
+      pj.A = mp; pj.lda = 4 * W; pj.W = b.pj_w.as<float>(); pj.ldw = 4 * W;
+      pj.bias = b.pj_b.as<float>(); pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M;
+      pj.N = W; pj.K = 4 * W;
+    }
+    for (int i = 0; i < n; ++i) {
+      const ClipBlock& b = *t[i]->blocks[l];
+      MPR_TRY(layernorm(xs[i], W, M, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(), CLIP_LN_EPS,
+                        t[i]->h.as<float>(), W, s));
+    }
+    MPR_TRY(gemm_group(gq, s));
+    for (int i = 0; i < n; ++i) {
+      float* qp = t[i]->qkv.as<float>();
+      AttnArgs at;
+      at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
+      at.k = qp + W; at.k_bs = at.q_bs; at.k_rs = 3 * W;
+      at.v = qp + 2 * W; at.v_bs = at.q_bs; at.v_rs = 3 * W;
+      at.o = t[i]->ao.as<float>(); at.o_bs = (int64_t)L * W; at.o_rs = W;
+      at.B = B; at.H = heads; at.Lq = L; at.Lk = L;
+      at.scale = 0.125f;  // 64 ** -0.5, exact power of two
+      at.causal = causal ? 1 : 0;
+      MPR_TRY(attention(at, s));
+    }
+    MPR_TRY(gemm_group(go, s));
+    for (int i = 0; i < n; ++i) {
+      const ClipBlock& b = *t[i]->blocks[l];
+      MPR_TRY(layernorm(xs[i], W, M, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(), CLIP_LN_EPS,
+                        t[i]->h.as<float>(), W, s));
+    }
+    MPR_TRY(gemm_group(gf, s));
+    MPR_TRY(gemm_group(gp, s));
   }
   return MPR_OK;
 }
 
 int VitModel::forward(const float* img, int B, int mode, float* out, int64_t out_bs,
                       hipStream_t s) {
-  MPR_REQUIRE(mode == 0 || mode == 1, "vit: mode must be 0 (CLS) or 1 (tokens)");
-  if (B == 0) return MPR_OK;
-  const int W = width, g2 = grid * grid, T = g2 + 1, P = 3 * patch * patch;
-  MPR_TRY(cols.ensure((size_t)B * g2 * P * 4));
-  MPR_TRY(patches.ensure((size_t)B * g2 * W * 4));
-  MPR_TRY(x.ensure((size_t)B * T * W * 4));
-  MPR_TRY(tmp.ensure((size_t)B * T * W * 4));
-  float* xp = x.as<float>();
-  MPR_TRY(im2col_patches(img, B, image, patch, cols.as<float>(), s));
-  GemmArgs pe;
-  pe.A = cols.as<float>(); pe.lda = P; pe.W = conv_w.as<float>(); pe.ldw = P;
-  pe.C = patches.as<float>(); pe.ldc = W; pe.M = B * g2; pe.N = W; pe.K = P;
-  MPR_TRY(gemm(pe, s));
-  MPR_TRY(vit_assemble(patches.as<float>(), cls.as<float>(), pos.as<float>(), B, g2, W, xp, s));
-  MPR_TRY(layernorm(xp, W, B * T, W, lnpre_w.as<float>(), lnpre_b.as<float>(), CLIP_LN_EPS, xp, W,
-                    s));
-  MPR_TRY(tower.run(xp, B, T, /*causal=*/false, s));
-  float* tp = tmp.as<float>();
-  GemmArgs pj;
-  pj.W = projT.as<float>(); pj.ldw = W; pj.N = out_dim; pj.K = W; pj.A = tp; pj.lda = W;
-  if (mode == 0) {
-    // ln_post on the CLS rows only (x[b*T]), then @ proj
-    MPR_TRY(layernorm(xp, (int64_t)T * W, B, W, lnpost_w.as<float>(), lnpost_b.as<float>(),
-                      CLIP_LN_EPS, tp, W, s));
-    pj.M = B; pj.C = out; pj.ldc = out_bs;
-  } else {
-    MPR_TRY(layernorm(xp, W, B * T, W, lnpost_w.as<float>(), lnpost_b.as<float>(), CLIP_LN_EPS,
-                      tp, W, s));
-    pj.M = B * T; pj.C = out; pj.ldc = out_dim; pj.c_rpb = T; pj.c_bs = out_bs;
+  VitModel* m = this;
+  return forward_group(&m, img, B, &mode, &out, &out_bs, 1, s);
+}
+
+// n ViTs of one geometry over the same images (the retrieval tower's CLS features and the
+// token-feature tower of T5VisionModel): im2col once, then both towers in lockstep.
+int VitModel::forward_group(VitModel* const* v, const float* img, int B, const int* modes,
+                            float* const* outs, const int64_t* out_bs, int n, hipStream_t s) {
+  MPR_REQUIRE(n >= 1 && n <= 2, "vit group: n=%d", n);
+  for (int i = 0; i < n; ++i) {
+    MPR_REQUIRE(modes[i] == 0 || modes[i] == 1, "vit: mode must be 0 (CLS) or 1 (tokens)");
+    MPR_REQUIRE(v[i]->width == v[0]->width && v[i]->patch == v[0]->patch &&
+                    v[i]->image == v[0]->image && v[i]->tower.layers == v[0]->tower.layers,
+                "vit group: towers differ in geometry");
   }
-  MPR_TRY(gemm(pj, s));
+  if (B == 0) return MPR_OK;
+  VitModel& a0 = *v[0];
+  const int W = a0.width, g2 = a0.grid * a0.grid, T = g2 + 1, P = 3 * a0.patch * a0.patch;
+  MPR_TRY(a0.cols.ensure((size_t)B * g2 * P * 4));
+  for (int i = 0; i < n; ++i) {
+    MPR_TRY(v[i]->patches.ensure((size_t)B * g2 * W * 4));
+    MPR_TRY(v[i]->x.ensure((size_t)B * T * W * 4));
+    MPR_TRY(v[i]->tmp.ensure((size_t)B * T * W * 4));
+  }
+  MPR_TRY(im2col_patches(img, B, a0.image, a0.patch, a0.cols.as<float>(), s));
+  GemmGroup pe;
+  pe.n = n;
+  for (int i = 0; i < n; ++i) {
+    GemmArgs& g = pe.g[i];
+    g.A = a0.cols.as<float>(); g.lda = P; g.W = v[i]->conv_w.as<float>(); g.ldw = P;
+    g.C = v[i]->patches.as<float>(); g.ldc = W; g.M = B * g2; g.N = W; g.K = P;
+  }
+  MPR_TRY(gemm_group(pe, s));
+  ClipTower* towers[2];
+  float* xs[2];
+  for (int i = 0; i < n; ++i) {
+    VitModel& m = *v[i];
+    float* xp = m.x.as<float>();
+    MPR_TRY(vit_assemble(m.patches.as<float>(), m.cls.as<float>(), m.pos.as<float>(), B, g2, W,
+                         xp, s));
+    MPR_TRY(layernorm(xp, W, B * T, W, m.lnpre_w.as<float>(), m.lnpre_b.as<float>(), CLIP_LN_EPS,
+                      xp, W, s));
+    towers[i] = &m.tower;
+    xs[i] = xp;
+  }
+  MPR_TRY(ClipTower::run_group(towers, xs, n, B, T, /*causal=*/false, s));
+  GemmGroup pg;
+  pg.n = n;
+  for (int i = 0; i < n; ++i) {
+    VitModel& m = *v[i];
+    float* xp = m.x.as<float>();
+    float* tp = m.tmp.as<float>();
+    GemmArgs& pj = pg.g[i];
+    pj.W = m.projT.as<float>(); pj.ldw = W; pj.N = m.out_dim; pj.K = W; pj.A = tp; pj.lda = W;
+    if (modes[i] == 0) {
+      // ln_post on the CLS rows only (x[b*T]), then @ proj
+      MPR_TRY(layernorm(xp, (int64_t)T * W, B, W, m.lnpost_w.as<float>(),
+                        m.lnpost_b.as<float>(), CLIP_LN_EPS, tp, W, s));
+      pj.M = B; pj.C = outs[i]; pj.ldc = out_bs[i];
+    } else {
+      MPR_TRY(layernorm(xp, W, B * T, W, m.lnpost_w.as<float>(), m.lnpost_b.as<float>(),
+                        CLIP_LN_EPS, tp, W, s));
+      pj.M = B * T; pj.C = outs[i]; pj.ldc = m.out_dim; pj.c_rpb = T; pj.c_bs = out_bs[i];
+    }
+  }
+  MPR_TRY(gemm_group(pg, s));
   return MPR_OK;
 }
 

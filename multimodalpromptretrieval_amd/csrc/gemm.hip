@@ -13,6 +13,8 @@
 // registers as the A operand of v_mfma_f32_16x16x4_f32 (16 output columns per block), the 16
 // activation rows are the B operand, K is split across the 8 waves of a block and reduced through
 // LDS, and T5's RMSNorm of the activation rows is folded into the operand and the epilogue.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace mpr {
@@ -29,62 +31,89 @@ __device__ __forceinline__ float act_exact(float v, int act) {
   return v;
 }
 
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm_f32_kernel(
-    GemmArgs a) {
+// Tile configuration:
+//   BM x BN output tile, waves of WM x WN 32x32 accumulators, BK-deep K tiles, KW wave groups
+//   splitting each K tile (KW = 2: two waves per SIMD on the same output, summed through LDS at
+//   the end), D = global-load prefetch depth in K tiles (tile t+2+D is requested while tile t is
+//   multiplied and lands in LDS D iterations later).
+// Two LDS stages: during iteration t the waves read tile t+1's fragments from one stage while
+// tile t+2 is written into the other (tile t's stage, whose fragments were read in iteration t-1,
+// before the barrier that closed it).  Fragments of tile t+1 are read under tile t's MFMAs.
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+__global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_f32_kernel(
+    const GemmGroup grp) {
   constexpr int WAVES_N = BN / (32 * WN);
-  constexpr int NT = 64 * (BM / (32 * WM)) * WAVES_N;
-  constexpr int BK = 32, LDK = BK + 4, KQ = BK / 4;  // KQ float4 per row of a K tile
+  constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
+  constexpr int NT = 64 * WAVES_MN * KW;
+  constexpr int LDK = BK + 4, KQ = BK / 4;  // LDS row stride (floats), float4 per tile row
   constexpr int LA = BM * KQ / NT, LB = BN * KQ / NT;
   constexpr int STAGE = (BM + BN) * LDK;  // floats per LDS stage (A rows then W rows)
+  constexpr int KPW = BK / KW;            // k per tile and wave
+  constexpr int NF = KPW / 8;             // float4 fragments per lane, operand and tile
   static_assert(LA * NT == BM * KQ && LB * NT == BN * KQ, "loader split");
+  static_assert(NF >= 2 && KPW % 8 == 0, "k split");
+  static_assert(KW == 1 || 2 * STAGE >= KW * BM * BN, "LDS reduction space");
 
-  // Three LDS stages: tile kt+1 is already visible while tile kt is multiplied, so its fragments
-  // are read into registers under tile kt's MFMAs and the next k-step starts on the barrier
-  // without waiting for LDS.  ONE __shared__ object holds the stages: a second LDS object
-  // makes hipcc drain vmcnt before every k-step's first ds_read.
-  __shared__ __attribute__((aligned(16))) float smem[3 * STAGE];
+  // ONE __shared__ object: a second LDS object makes hipcc drain vmcnt before every k-step's
+  // first ds_read.
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  // wave-uniform selection of this block's problem (no dynamic indexing of the kernarg struct)
+  const int z = blockIdx.z;
+#define MPR_SEL(f) (z == 0 ? grp.g[0].f : z == 1 ? grp.g[1].f : z == 2 ? grp.g[2].f : grp.g[3].f)
+  GemmArgs a;
+  a.A = MPR_SEL(A); a.lda = MPR_SEL(lda); a.W = MPR_SEL(W); a.ldw = MPR_SEL(ldw);
+  a.bias = MPR_SEL(bias); a.R = MPR_SEL(R); a.ldr = MPR_SEL(ldr); a.C = MPR_SEL(C);
+  a.ldc = MPR_SEL(ldc); a.M = MPR_SEL(M); a.N = MPR_SEL(N); a.K = MPR_SEL(K);
+  a.act = MPR_SEL(act); a.c_rpb = MPR_SEL(c_rpb); a.c_bs = MPR_SEL(c_bs);
+#undef MPR_SEL
+  const int M = a.M, N = a.N, K = a.K;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  if (m0 >= M || n0 >= N) return;  // grid sized for the largest problem of the group
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int M = a.M, N = a.N, K = a.K;
+  const int wmn = wave % WAVES_MN, kw = wave / WAVES_MN;
+  const int wm = wmn / WAVES_N, wn = wmn % WAVES_N;
 
-  f32x4 ra[LA], rb[LB];
-  bool oka[LA], okb[LB];
-  // Unconditional loads from clamped addresses, zeroed by a select only when written to LDS
-  // (after the MFMAs of the current tile): an exec-masked load makes hipcc branch around every
-  // load, and an early select makes it wait for the data right after issuing the load.
-  auto gload = [&](int k0) {
+  // D register slots of in-flight global loads (slot j is indexed by compile-time constants
+  // only: the k-loop is unrolled by D).
+  f32x4 ra[D][LA], rb[D][LB];
+  bool oka[D][LA], okb[D][LB];
+  // Unconditional loads from clamped addresses, zeroed by a select only when written to LDS: an
+  // exec-masked load makes hipcc branch around every load, and an early select makes it wait
+  // for the data right after issuing the load.  Tiles past K load clamped, in-range data and
+  // are written as zeros.
+  auto gload = [&](int j, int k0) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = m0 + r;
-      oka[i] = row < M && c < K;
-      ra[i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
-                                              min(c, K - 4));
+      oka[j][i] = row < M && c < K;
+      ra[j][i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
+                                                 min(c, K - 4));
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = n0 + r;
-      okb[i] = row < N && c < K;
-      rb[i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
-                                              min(c, K - 4));
+      okb[j][i] = row < N && c < K;
+      rb[j][i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
+                                                 min(c, K - 4));
     }
   };
-  auto swrite = [&](int st) {
-    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  auto swrite = [&](int st, int j) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     float* base = smem + st * STAGE;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT;
-      *reinterpret_cast<f32x4*>(base + (idx / KQ) * LDK + (idx % KQ) * 4) = oka[i] ? ra[i] : z;
+      *reinterpret_cast<f32x4*>(base + (idx / KQ) * LDK + (idx % KQ) * 4) =
+          oka[j][i] ? ra[j][i] : zero;
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT;
       *reinterpret_cast<f32x4*>(base + (BM + idx / KQ) * LDK + (idx % KQ) * 4) =
-          okb[i] ? rb[i] : z;
+          okb[j][i] ? rb[j][i] : zero;
     }
   };
 
@@ -96,22 +125,24 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
-  // Operand fragments of one K tile: lane (li, lh) holds row li's k = 16*lh .. 16*lh+15 as four
-  // float4 (the contraction order inside the tile is permuted identically for A and W).
+  // Operand fragments of one K tile: lane (li, lh) of wave group kw holds row li's
+  // k = kw*KPW + lh*KPW/2 + [0, KPW/2) as NF float4 (the contraction order inside the tile is
+  // permuted identically for A and W).  Row stride BK+4 floats: conflict-free ds_read_b128.
   const int li = lane & 31, lh = lane >> 5;
-  f32x4 fa[WM][4], fb[WN][4], na[WM][4], nb[WN][4];
-  auto sread = [&](int st, f32x4(&xa)[WM][4], f32x4(&xb)[WN][4]) {
+  const int kof = kw * KPW + lh * (KPW / 2);
+  f32x4 fa[WM][NF], fb[WN][NF], na[WM][NF], nb[WN][NF];
+  auto sread = [&](int st, f32x4(&xa)[WM][NF], f32x4(&xb)[WN][NF]) {
     const float* base = smem + st * STAGE;
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
+    for (int s4 = 0; s4 < NF; ++s4) {
 #pragma unroll
       for (int mi = 0; mi < WM; ++mi)
         xa[mi][s4] = *reinterpret_cast<const f32x4*>(
-            base + (wm * 32 * WM + mi * 32 + li) * LDK + lh * 16 + s4 * 4);
+            base + (wm * 32 * WM + mi * 32 + li) * LDK + kof + s4 * 4);
 #pragma unroll
       for (int ni = 0; ni < WN; ++ni)
         xb[ni][s4] = *reinterpret_cast<const f32x4*>(
-            base + (BM + wn * 32 * WN + ni * 32 + li) * LDK + lh * 16 + s4 * 4);
+            base + (BM + wn * 32 * WN + ni * 32 + li) * LDK + kof + s4 * 4);
     }
   };
   auto mfmas = [&](int s_lo, int s_hi) {
@@ -128,7 +159,7 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
   };
   auto advance = [&]() {
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
+    for (int s4 = 0; s4 < NF; ++s4) {
 #pragma unroll
       for (int mi = 0; mi < WM; ++mi) fa[mi][s4] = na[mi][s4];
 #pragma unroll
@@ -136,70 +167,112 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
     }
   };
 
+  // k-steps rounded up to a multiple of D (the extra steps multiply zero tiles: exact no-ops on
+  // the accumulators; every projection of this path has K % (BK * D) == 0 anyway).
   const int nk = (K + BK - 1) / BK;
+  const int nkr = (nk + D - 1) / D * D;
 
-  gload(0);
-  swrite(0);
-  gload(BK);  // clamped/zeroed when past K
-  swrite(1);
+  gload(0, 0);
+  swrite(0, 0);
+  gload(0, BK);
+  swrite(1, 0);
+#pragma unroll
+  for (int j = 0; j < D; ++j) gload(j, (2 + j) * BK);
   __syncthreads();
   sread(0, fa, fb);
-  int kt = 0, st = 0;
-  // Steady state, branch-free (the accumulators stay in AGPRs): global loads of tile kt+2 in
-  // flight across tile kt's MFMAs, LDS reads of tile kt+1 issued after its first quarter.
-  for (; kt + 2 < nk; ++kt) {
-    const int st1 = st == 2 ? 0 : st + 1, st2 = st1 == 2 ? 0 : st1 + 1;
-    gload((kt + 2) * BK);
-    __builtin_amdgcn_sched_barrier(0);
-    mfmas(0, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    sread(st1, na, nb);
-    __builtin_amdgcn_sched_barrier(0);
-    mfmas(1, 4);
-    __builtin_amdgcn_sched_barrier(0);
-    swrite(st2);
+  // Steady state, branch-free (the accumulators stay in AGPRs): iteration t multiplies tile t
+  // (fragments already in registers), reads tile t+1's fragments after the first quarter of the
+  // MFMAs, writes tile t+2 (register slot t % D) into tile t's stage and re-arms the slot with
+  // tile t+2+D.
+  for (int kt = 0; kt < nkr; kt += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int st = (kt + j) & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      sread(st ^ 1, na, nb);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(1, NF);
+      __builtin_amdgcn_sched_barrier(0);
+      swrite(st, j);
+      gload(j, (kt + j + 2 + D) * BK);
+      __syncthreads();
+      advance();
+    }
+  }
+
+  if constexpr (KW > 1) {
+    // wave groups 1.. park their partial accumulators in LDS (every stage read is complete: the
+    // loop ended on a barrier), group 0 adds them in group order.
+    f32x16* red = reinterpret_cast<f32x16*>(smem);
+    if (kw > 0) {
+#pragma unroll
+      for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni)
+          red[(((kw - 1) * WAVES_MN + wmn) * WM * WN + mi * WN + ni) * 64 + lane] = acc[mi][ni];
+    }
     __syncthreads();
-    advance();
-    st = st1;
+    if (kw > 0) return;
+#pragma unroll
+    for (int g = 1; g < KW; ++g)
+#pragma unroll
+      for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni)
+          acc[mi][ni] += red[(((g - 1) * WAVES_MN + wmn) * WM * WN + mi * WN + ni) * 64 + lane];
   }
-  if (kt + 1 < nk) {  // second-to-last tile: its successor is already in LDS
-    mfmas(0, 1);
-    sread(st == 2 ? 0 : st + 1, na, nb);
-    mfmas(1, 4);
-    advance();
-    ++kt;
-  }
-  if (kt < nk) mfmas(0, 4);
 
   // Epilogue: 32x32 accumulator, col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Bias and residual values are all loaded (clamped addresses) before the first use: a load
+  // behind a per-row bounds branch is waited for on its own, 16 dependent round trips.
 #pragma unroll
   for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
     for (int ni = 0; ni < WN; ++ni) {
-      const int col = n0 + wn * 32 * WN + ni * 32 + li;
-      if (col >= N) continue;
-      const float bv = a.bias ? a.bias[col] : 0.f;
+      const int col = n0 + wn * 32 * WN + ni * 32 + li, colc = min(col, N - 1);
+      const int rbase = m0 + wm * 32 * WM + mi * 32 + 4 * lh;
+      const float bv = a.bias ? a.bias[colc] : 0.f;
+      float rv[16];
+      if (a.R) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          rv[r] = a.R[(int64_t)min(rbase + (r & 3) + 8 * (r >> 2), M - 1) * a.ldr + colc];
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 32 * WM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= M) continue;
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
         float v = act_exact(acc[mi][ni][r] + bv, a.act);
-        if (a.R) v = a.R[(int64_t)row * a.ldr + col] + v;
+        if (a.R) v = rv[r] + v;
         const int64_t coff = a.c_rpb ? (int64_t)(row / a.c_rpb) * a.c_bs +
                                            (int64_t)(row % a.c_rpb) * a.ldc
                                      : (int64_t)row * a.ldc;
-        a.C[coff + col] = v;
+        if (row < M && col < N) a.C[coff + col] = v;
       }
     }
 }
 
-template <int BM, int BN, int WM, int WN>
-int launch_gemm(const GemmArgs& a, hipStream_t s) {
-  constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN));
-  dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM));
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN>), grid, dim3(NT), 0, s, a);
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
+  constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW;
+  int gx = 0, gy = 0;
+  for (int i = 0; i < g.n; ++i) {
+    gx = std::max(gx, (int)cdiv(g.g[i].N, BN));
+    gy = std::max(gy, (int)cdiv(g.g[i].M, BM));
+  }
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, D, KW>), dim3(gx, gy, g.n), dim3(NT),
+                     0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
+}
+
+template <int BM, int BN, int WM, int WN, int BK = 32, int D = 2, int KW = 1>
+int launch_gemm(const GemmArgs& a, hipStream_t s) {
+  GemmGroup g;
+  g.g[0] = a;
+  g.n = 1;
+  return launch_gemm_group<BM, BN, WM, WN, BK, D, KW>(g, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -423,9 +496,9 @@ double gemm_bytes(const GemmArgs& a) {
 }
 
 template <class F>
-int probed(int kind, const GemmArgs& a, hipStream_t s, F&& launch) {
+int probed(int kind, double flops, double bytes, hipStream_t s, F&& launch) {
   if (!probing(kind, s)) return launch();
-  ProbeRec r{pool_event(), pool_event(), 2.0 * a.M * a.N * a.K, gemm_bytes(a)};
+  ProbeRec r{pool_event(), pool_event(), flops, bytes};
   if (!r.a || !r.b) return launch();
   (void)hipEventRecord(r.a, s);
   const int rc = launch();
@@ -461,20 +534,48 @@ int probe_read(double* ms, int64_t* launches, double* flops, double* bytes) {
   return MPR_OK;
 }
 
+int gemm_group(const GemmGroup& g, hipStream_t s) {
+  MPR_REQUIRE(g.n >= 1 && g.n <= GEMM_GROUP, "gemm_group: %d problems", g.n);
+  int64_t tiles64 = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const GemmArgs& a = g.g[i];
+    MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N,
+                a.K);
+    MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
+                    aligned16(a.W),
+                "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
+    tiles64 = std::max(tiles64, cdiv(a.M, 64) * cdiv(a.N, 64));
+  }
+  if (tiles64 == 0) return MPR_OK;
+  double flops = 0, bytes = 0;
+  for (int i = 0; i < g.n; ++i) {
+    flops += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K;
+    bytes += gemm_bytes(g.g[i]);
+  }
+  // Tile choice (measured on MI355X over the ViT/T5/CLIP-text projection shapes, single and
+  // paired, tools/gbench.hip): 64x64 tiles (4 waves of 32x32, BK 32, 2 tiles of loads in flight)
+  // once one problem has >= 1.5 blocks per CU; below that 32x32 tiles with the K tile split over 4
+  // waves (4x the blocks, partial sums added through LDS): 800x768x3072 67 -> 54 us,
+  // 1152x512x2048 47 -> 38 us, paired 800x768x768 34 -> 29 us.  BK 64, 128-row tiles, 8-wave
+  // 64x64 blocks and split-K across blocks were slower at every shape of this path.  The
+  // choice depends on the largest single problem, not on the group: a problem gets the same
+  // tile (the same summation order, bit-identical results) alone or grouped.
+  return probed(PROBE_GEMM, flops, bytes, s, [&]() {
+    if (tiles64 >= 384) return launch_gemm_group<64, 64, 1, 1, 32, 2, 1>(g, s);
+    return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
+  });
+}
+
 int gemm(const GemmArgs& a, hipStream_t s) {
-  MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
-  if (a.M == 0 || a.N == 0) return MPR_OK;
-  MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
-                  aligned16(a.W),
-              "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-  // One tile shape: 64x64 (4 waves of 32x32, ~55 KB of LDS, 2 blocks per CU).  Measured on
-  // MI355X over the ViT/T5 projection shapes (tools/gbench.hip): 128x64 and 128x128 tiles are
-  // slower at every shape up to 2048^3 (fewer blocks, one per CU by LDS), 32x64 halves the
-  // waves per block without adding SIMD work.  Split-K over blockIdx.z (in-launch agent-scope
-  // combine) was slower at every shape too (800x768x768: 21.7 us plain, 30.6 at S=2, 47 at
-  // S=4): the release fence writes back the XCD L2 and a 64x64 fp32 slab per slice costs more
-  // than the idle CUs it fills.
-  return probed(PROBE_GEMM, a, s, [&]() { return launch_gemm<64, 64, 1, 1>(a, s); });
+  if (a.M == 0 || a.N == 0) {
+    MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N,
+                a.K);
+    return MPR_OK;
+  }
+  GemmGroup g;
+  g.g[0] = a;
+  g.n = 1;
+  return gemm_group(g, s);
 }
 
 int64_t packed_rows16_elems(int64_t N, int64_t K) { return cdiv(N, 16) * cdiv(K, 16) * 256; }
@@ -527,7 +628,7 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
                 (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0);
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
-  return probed(PROBE_SKINNY, a, s, [&]() {
+  return probed(PROBE_SKINNY, 2.0 * a.M * a.N * a.K, gemm_bytes(a), s, [&]() {
     if (amax && tiles >= 1024 && per <= 4)  // lm_head: 2 tiles per block (NT 1/2/4/8 measured
       launch_skinny<4, 2, false>(sa, F, (unsigned)cdiv(tiles, 2), s);  // 14.5/13.1/13.8/14.5 us)
     else if (per <= 4)

@@ -28,6 +28,16 @@ struct GemmArgs {
 
 int gemm(const GemmArgs& a, hipStream_t s);
 
+// Up to GEMM_GROUP independent problems in one launch (blockIdx.z picks the problem): the two
+// ViT-B/32 towers of a batch run their layer-l projections together, which doubles the blocks
+// of the 768-column GEMMs that alone fill only 156 of the 256 CUs.
+constexpr int GEMM_GROUP = 4;
+struct GemmGroup {
+  GemmArgs g[GEMM_GROUP];
+  int n = 1;
+};
+int gemm_group(const GemmGroup& g, hipStream_t s);
+
 // Skinny GEMM for M <= 16 rows (decode steps): same contract as gemm() plus an optional fused
 // T5 RMSNorm of the A rows: A'[m,k] = ln_w[k] * (A[m,k] * rsqrt(mean_k A[m,:]^2 + eps)).
 // Skinny GEMM weights live in a lane-order image of W (pack_rows16): for 16-row tile t and

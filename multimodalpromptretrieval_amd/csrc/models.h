@@ -39,6 +39,8 @@ struct ClipTower {
   int load_blocks(const float* const* t, int width, int layers);
   // x [B*L, width] in place; causal for the text tower.
   int run(float* x, int B, int L, bool causal, hipStream_t s);
+  static int run_group(ClipTower* const* t, float* const* xs, int n, int B, int L, bool causal,
+                       hipStream_t s);
 };
 
 struct VitModel : mpr_model {
@@ -48,6 +50,8 @@ struct VitModel : mpr_model {
   ClipTower tower;
   DevBuf cols, patches, x, tmp;
   int forward(const float* img, int B, int mode, float* out, int64_t out_bs, hipStream_t s);
+  static int forward_group(VitModel* const* v, const float* img, int B, const int* modes,
+                           float* const* outs, const int64_t* out_bs, int n, hipStream_t s);
 };
 
 struct TextModel : mpr_model {

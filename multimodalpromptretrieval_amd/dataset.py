@@ -82,34 +82,65 @@ class VQARetrieval:
         self._cache_ref = None
 
     # ---- encoding ------------------------------------------------------------------------------
+    def _streams(self):
+        if not hasattr(self, "_s_img"):
+            # High priority: the host blocks on these results (prompt building), while other
+            # device work queued meanwhile is not needed until later.
+            self._s_img = torch.cuda.Stream(self.device, priority=-1)
+            self._s_txt = torch.cuda.Stream(self.device, priority=-1)
+        return self._s_img, self._s_txt
+
+    def encode_image_pair(self, batch, other_vit, other_mode: int):
+        """Run this retrieval's ``encode_image`` together with a second ViT of the same geometry
+        over the batch's images (T5VisionModel's token-feature tower): one paired pass,
+        ``DeviceViT.forward_pair``.  The CLS half of the query rows is kept for the next
+        ``encode_queries(batch)`` of the same batch object; returns the other tower's output
+        and the stream it is produced on (the caller waits on that stream before using it)."""
+        s_img, _ = self._streams()
+        cur = torch.cuda.current_stream(self.device)
+        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+        B = img.shape[0]
+        q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
+        s_img.wait_stream(cur)
+        img.record_stream(s_img)
+        q.record_stream(s_img)
+        with torch.cuda.stream(s_img):
+            _, other_out = self.image_encoder.forward_pair(
+                other_vit, img, CLS, other_mode, out=q, out_bstride=self.embed_dim)
+        other_out.record_stream(cur)
+        self._pending_img = (batch["image"], q)
+        return other_out, s_img
+
     def encode_queries(self, batch) -> torch.Tensor:
         """[CLS image embedding ‖ EOT text embedding] fp32 [B, 1024] on the device
         (dataset/VQAFeatureDataset.py:189-191, 146-148).  The two towers run concurrently on
         two side streams (each fills only part of the chip at batch 16) and write their halves
-        of the query rows in place; the caller's stream waits for both."""
+        of the query rows in place; the caller's stream waits for both.  When
+        ``encode_image_pair`` already produced this batch's image half, only the text tower
+        runs."""
         cur = torch.cuda.current_stream(self.device)
-        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+        s_img, s_txt = self._streams()
+        pending = getattr(self, "_pending_img", None)
+        self._pending_img = None
         toks = self.clip_tokenize(batch["question"])
-        B = img.shape[0]
-        q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
         di = self.image_encoder.out_dim
-        if not hasattr(self, "_s_img"):
-            # High priority: the host blocks on these results (prompt building), while other
-            # device work queued meanwhile (the token-feature ViT) is not needed until later.
-            self._s_img = torch.cuda.Stream(self.device, priority=-1)
-            self._s_txt = torch.cuda.Stream(self.device, priority=-1)
-        ev = torch.cuda.Event()
-        ev.record(cur)
-        for s in (self._s_img, self._s_txt):
-            s.wait_event(ev)
-            q.record_stream(s)
-        img.record_stream(self._s_img)
-        with torch.cuda.stream(self._s_img):
-            self.image_encoder(img, CLS, out=q, out_bstride=self.embed_dim)
-        with torch.cuda.stream(self._s_txt):
+        if pending is not None and pending[0] is batch["image"]:
+            q = pending[1]
+        else:
+            img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+            q = torch.empty((img.shape[0], self.embed_dim), device=self.device,
+                            dtype=torch.float32)
+            s_img.wait_stream(cur)
+            q.record_stream(s_img)
+            img.record_stream(s_img)
+            with torch.cuda.stream(s_img):
+                self.image_encoder(img, CLS, out=q, out_bstride=self.embed_dim)
+        s_txt.wait_stream(cur)
+        q.record_stream(s_txt)
+        with torch.cuda.stream(s_txt):
             self.text_encoder(toks, out=q[:, di:], out_bstride=self.embed_dim)
-        cur.wait_stream(self._s_img)
-        cur.wait_stream(self._s_txt)
+        cur.wait_stream(s_img)
+        cur.wait_stream(s_txt)
         return q
 
     # ---- index -------------------------------------------------------------------------------

@@ -101,6 +101,33 @@ class DeviceViT(_Handle):
 
     __call__ = forward
 
+    def _out(self, B, mode, out, out_bstride):
+        if out is None:
+            shape = (B, self.out_dim) if mode == CLS else (B, self.tokens, self.out_dim)
+            out = torch.empty(shape, device=self.device, dtype=torch.float32)
+            out_bstride = self.out_dim if mode == CLS else self.tokens * self.out_dim
+        return out, out_bstride
+
+    def forward_pair(self, other: "DeviceViT", img: torch.Tensor, mode: int = CLS,
+                     other_mode: int = TOKENS, out: torch.Tensor = None, out_bstride: int = None,
+                     other_out: torch.Tensor = None, other_bstride: int = None):
+        """``self(img, mode)`` and ``other(img, other_mode)`` in one pass over the same images:
+        im2col once, the two towers' projections of each layer as one grouped launch.  Results
+        are identical to the two separate calls."""
+        if other is self or other.device != self.device:
+            raise ValueError("forward_pair needs a second ViT on the same device")
+        img = img.to(self.device, torch.float32, non_blocking=True).contiguous()
+        B = img.shape[0]
+        if tuple(img.shape[1:]) != (3, self.image_size, self.image_size):
+            raise ValueError(f"expected images [B,3,{self.image_size},{self.image_size}], "
+                             f"got {tuple(img.shape)}")
+        out, out_bstride = self._out(B, mode, out, out_bstride)
+        other_out, other_bstride = other._out(B, other_mode, other_out, other_bstride)
+        _lib.call("mpr_vit_forward_pair", self._h, mode, _lib.ptr(out), int(out_bstride),
+                  other._h, other_mode, _lib.ptr(other_out), int(other_bstride), _lib.ptr(img),
+                  B, _lib.stream_ptr(self.device))
+        return out, other_out
+
 
 class DeviceCLIPText(_Handle):
     """CLIP text transformer (openai naming, no prefix) on one GPU."""

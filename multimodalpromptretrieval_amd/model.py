@@ -211,12 +211,21 @@ class T5VisionModel(nn.Module):
         """architectures/T5VisionModel.py:112-139 -> [B, 50, 512] fp32 on the device."""
         return self._device_vit()(x, TOKENS)
 
+    @staticmethod
+    def _pairable(retr, vit) -> bool:
+        enc = getattr(retr, "image_encoder", None)
+        return (enc is not None and enc is not vit and getattr(enc, "device", None) == vit.device
+                and (enc.width, enc.patch, enc.image_size, enc.layers)
+                == (vit.width, vit.patch, vit.image_size, vit.layers))
+
     def prepare_input(self, batch):
         """architectures/T5VisionModel.py:141-184.
 
         The token-feature ViT does not depend on retrieval, so it is enqueued first on a side
         stream and runs on the GPU while the retrieval function encodes/scans and the host
-        builds and tokenises the prompts."""
+        builds and tokenises the prompts.  With a ``VQARetrieval`` retrieval function whose
+        image tower has this tower's geometry, both ViTs run as one paired pass (their
+        projections share launches; results identical to separate calls)."""
         vit = self._device_vit()
         t5 = self._device_t5()
         if self.use_image_info and vit.out_dim != t5.d_model:
@@ -225,14 +234,23 @@ class T5VisionModel(nn.Module):
                                f"architectures/T5VisionModel.py:176)")
         cur = torch.cuda.current_stream(self.device)
         img_tok = None
+        tok_stream = None
         if self.use_image_info:
-            img = batch["image"].to(self.device, torch.float32, non_blocking=True)
-            if not hasattr(self, "_s_tok"):
-                self._s_tok = torch.cuda.Stream(self.device)
-            self._s_tok.wait_stream(cur)
-            img.record_stream(self._s_tok)
-            with torch.cuda.stream(self._s_tok):
-                img_tok = vit(img, TOKENS)
+            retr = getattr(self.retrieval_function, "__self__", None)
+            pair = getattr(retr, "encode_image_pair", None)
+            if pair is not None and self._pairable(retr, vit):
+                # the retrieval's encode_image and this tower see the same images: one paired
+                # pass (shared launches), the retrieval picks its half up in encode_queries
+                img_tok, tok_stream = pair(batch, vit, TOKENS)
+            else:
+                img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+                if not hasattr(self, "_s_tok"):
+                    self._s_tok = torch.cuda.Stream(self.device)
+                self._s_tok.wait_stream(cur)
+                img.record_stream(self._s_tok)
+                with torch.cuda.stream(self._s_tok):
+                    img_tok = vit(img, TOKENS)
+                tok_stream = self._s_tok
         if self.retrieval_function:
             if self.use_quantifier:
                 retrieved_info = self.retrieval_function(batch)
@@ -252,7 +270,7 @@ class T5VisionModel(nn.Module):
         T = vit.tokens if self.use_image_info else 0
         combined = torch.empty((B, T + L, t5.d_model), device=self.device, dtype=torch.float32)
         if self.use_image_info:
-            cur.wait_stream(self._s_tok)
+            cur.wait_stream(tok_stream)
             img_tok.record_stream(cur)
             combined[:, :T].copy_(img_tok)
         t5.embed(ids, combined, row0=T)

@@ -105,6 +105,18 @@ def test_vit_cls_and_tokens(device, clip_sd):
     assert _rel_err(tok, oclip.image_token_features(clip_sd, img)) < FP_TOL
 
 
+def test_vit_pair_matches_single(device, clip_sd):
+    """Paired pass (two towers, shared launches) == two single calls, bit for bit."""
+    from multimodalpromptretrieval_amd.encoders import CLS, TOKENS, DeviceViT
+    a = DeviceViT(clip_sd, device)
+    b = DeviceViT(syn.clip_state_dict(14), device)
+    img = syn.images(15, 16).to(device)
+    cls, tok = a.forward_pair(b, img, CLS, TOKENS)
+    assert torch.equal(cls, a(img, CLS)) and torch.equal(tok, b(img, TOKENS))
+    tok2, cls2 = b.forward_pair(a, img[:3], TOKENS, CLS)
+    assert torch.equal(cls2, a(img[:3], CLS)) and torch.equal(tok2, b(img[:3], TOKENS))
+
+
 def test_clip_text(device, clip_sd):
     from multimodalpromptretrieval_amd.encoders import DeviceCLIPText
     txt = DeviceCLIPText(clip_sd, device)

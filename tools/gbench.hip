@@ -42,38 +42,64 @@ static double time_graph(hipStream_t s, const std::function<void()>& body, int n
 int main() {
   hipStream_t s;
   (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-  float *A, *W, *C;
-  (void)hipMalloc(&A, 64 << 20);
-  (void)hipMalloc(&W, 64 << 20);
-  (void)hipMalloc(&C, 64 << 20);
-  (void)hipMemset(A, 0, 64 << 20);
-  (void)hipMemset(W, 0, 64 << 20);
-  struct Shape { const char* name; int M, N, K; };
+  float *A, *W, *C, *R;
+  const size_t bytes = 128 << 20;
+  (void)hipMalloc(&A, bytes);
+  (void)hipMalloc(&W, bytes);
+  (void)hipMalloc(&C, bytes);
+  (void)hipMalloc(&R, bytes);
+  {  // random operands (zero data runs at a higher clock and reads high)
+    std::vector<float> h(bytes / 4);
+    uint32_t x = 12345u;
+    for (auto& v : h) {
+      x = x * 1664525u + 1013904223u;
+      v = ((x >> 9) * (1.0f / 8388608.0f)) - 0.5f;
+    }
+    (void)hipMemcpy(A, h.data(), bytes, hipMemcpyHostToDevice);
+    (void)hipMemcpy(W, h.data() + 7, bytes - 64, hipMemcpyHostToDevice);
+    (void)hipMemcpy(R, h.data() + 3, bytes - 64, hipMemcpyHostToDevice);
+  }
+  struct Shape { const char* name; int M, N, K; bool res; };
   const Shape shapes[] = {
-      {"vit qkv   800x2304x768", 800, 2304, 768},  {"vit out   800x768x768", 800, 768, 768},
-      {"vit fc1   800x3072x768", 800, 3072, 768},  {"vit fc2   800x768x3072", 800, 768, 3072},
-      {"t5e qkv  1136x1536x512", 1136, 1536, 512}, {"t5e wo   1136x512x2048", 1136, 512, 2048},
-      {"sq 2048", 2048, 2048, 2048},
+      {"vit qkv   800x2304x768", 800, 2304, 768, false},
+      {"vit out   800x768x768 +R", 800, 768, 768, true},
+      {"vit fc1   800x3072x768", 800, 3072, 768, false},
+      {"vit fc2   800x768x3072 +R", 800, 768, 3072, true},
+      {"t5e qkv  1152x1536x512", 1152, 1536, 512, false},
+      {"t5e wo   1152x512x2048 +R", 1152, 512, 2048, true},
+      {"txt fc1   384x2048x512", 384, 2048, 512, false},
+      {"sq 2048", 2048, 2048, 2048, false},
   };
-  using L = std::function<int(const GemmArgs&, hipStream_t)>;
-  struct Var { const char* name; L fn; int bm, bn; };
+  using L = std::function<int(const GemmGroup&, hipStream_t)>;
+  struct Var { const char* name; L fn; };
   const Var vars[] = {
-      {"64x64 1x1", launch_gemm<64, 64, 1, 1>, 64, 64},
-      {"32x64 1x1", launch_gemm<32, 64, 1, 1>, 32, 64},
-      {"128x64 2x1", launch_gemm<128, 64, 2, 1>, 128, 64},
-      {"128x128 2x2", launch_gemm<128, 128, 2, 2>, 128, 128},
+      {"64x64 k32 D2", launch_gemm_group<64, 64, 1, 1, 32, 2, 1>},
+      {"64x64 k64 D1", launch_gemm_group<64, 64, 1, 1, 64, 1, 1>},
+      {"64x64 k64 D2", launch_gemm_group<64, 64, 1, 1, 64, 2, 1>},
+      {"64x64 k32 D2 W2", launch_gemm_group<64, 64, 1, 1, 32, 2, 2>},
+      {"64x64 k64 D1 W2", launch_gemm_group<64, 64, 1, 1, 64, 1, 2>},
+      {"64x64 k64 D2 W2", launch_gemm_group<64, 64, 1, 1, 64, 2, 2>},
+      {"32x64 k64 D2 W2", launch_gemm_group<32, 64, 1, 1, 64, 2, 2>},
+      {"32x32 k64 D2 W4", launch_gemm_group<32, 32, 1, 1, 64, 2, 4>},
+      {"128x64 k32 D2", launch_gemm_group<128, 64, 2, 1, 32, 2, 1>},
   };
   for (const Shape& sh : shapes) {
-    const double gf = 2.0 * sh.M * sh.N * sh.K * 1e-9;
-    printf("%s  (%.2f GFLOP)\n", sh.name, gf);
-    for (const Var& v : vars) {
-      const int64_t tiles = cdiv(sh.M, v.bm) * cdiv(sh.N, v.bn);
-      GemmArgs g;
-      g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.C = C; g.ldc = sh.N;
-      g.M = sh.M; g.N = sh.N; g.K = sh.K;
-      const double us = time_graph(s, [&]() { v.fn(g, s); }, 200);
-      printf("   %-22s blocks %5lld  %8.2f us  %6.1f TF/s\n", v.name, (long long)tiles, us,
-             gf / us * 1e3);
+    for (int grp = 1; grp <= 2; ++grp) {
+      const double gf = grp * 2.0 * sh.M * sh.N * sh.K * 1e-9;
+      printf("%s x%d (%.2f GFLOP)\n", sh.name, grp, gf);
+      for (const Var& v : vars) {
+        GemmGroup G;
+        G.n = grp;
+        for (int i = 0; i < grp; ++i) {
+          GemmArgs& g = G.g[i];
+          const size_t off = (size_t)i * (8 << 20);
+          g.A = A + off; g.lda = sh.K; g.W = W + off; g.ldw = sh.K; g.C = C + off; g.ldc = sh.N;
+          g.M = sh.M; g.N = sh.N; g.K = sh.K;
+          if (sh.res) { g.R = R + off; g.ldr = sh.N; }
+        }
+        const double us = time_graph(s, [&]() { v.fn(G, s); }, 100);
+        printf("   %-18s %8.2f us  %6.1f TF/s\n", v.name, us, gf / us * 1e3);
+      }
     }
   }
   return 0;
