@@ -43,6 +43,13 @@ int32_t mpr_abi_version(void);
 /* Waits for all work on `stream` (host sync).  Used by the Python host only where the
  * reference itself syncs (D2H of retrieved ids, generated tokens). */
 int mpr_stream_sync(void* stream);
+/* A stream of the current device: with mask_words > 0 restricted to the CUs whose bits are set in
+ * cu_mask (hipExtStreamCreateWithCUMask; bit i of word w = CU 32*w + i in the driver's CU order,
+ * which deals consecutive bits round-robin over the 8 XCDs), else a non-blocking stream of the
+ * given priority (lower = higher, hipDeviceGetStreamPriorityRange).  Used to give the
+ * latency-bound decode chain CUs of its own beside the encoders of the next batch. */
+int mpr_stream_create(int32_t priority, const uint32_t* cu_mask, int32_t mask_words, void** out);
+int mpr_stream_destroy(void* stream);
 
 /* ---- retrieval index: dataset/VQAFeatureDataset.py:192-197 (torch.cdist + torch.argsort) ----
  * rows: [n, d] fp32 row-major (host or device).  metric 0 = L2 (cdist, ascending distance),
@@ -134,6 +141,10 @@ int mpr_t5_generate(mpr_model* m, const float* embeds_dev, const float* mask_dev
                     int32_t L, int32_t max_new, int32_t decoder_start, int32_t eos, int32_t pad,
                     int32_t* out_tokens_dev, void* stream);
 /* Teacher-forced decoder logits: dec_in_dev [b,T] int32 decoder input ids -> logits [b,T,vocab]. */
+/* Run the greedy decode loop of subsequent mpr_t5_generate calls on decode_stream (null = the
+ * call's own stream).  The call's stream still orders everything: the loop starts after the
+ * encoder enqueued on it and the call's stream waits for the tokens. */
+int mpr_t5_set_decode_stream(mpr_model* m, void* decode_stream);
 int mpr_t5_logits(mpr_model* m, const float* embeds_dev, const float* mask_dev, int32_t b,
                   int32_t L, const int32_t* dec_in_dev, int32_t T, float* logits_dev,
                   void* stream);

@@ -83,6 +83,26 @@ int mpr_stream_sync(void* stream) {
   return MPR_OK;
 }
 
+int mpr_stream_create(int32_t priority, const uint32_t* cu_mask, int32_t mask_words,
+                      void** out) {
+  MPR_REQUIRE(out != nullptr, "stream_create: out is null");
+  MPR_REQUIRE(mask_words >= 0 && (mask_words == 0 || cu_mask), "stream_create: bad mask");
+  hipStream_t s = nullptr;
+  if (mask_words > 0) {
+    MPR_REQUIRE(priority == 0, "stream_create: a CU-masked stream has the default priority");
+    MPR_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask_words, cu_mask));
+  } else {
+    MPR_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+  }
+  *out = s;
+  return MPR_OK;
+}
+
+int mpr_stream_destroy(void* stream) {
+  if (stream) MPR_HIP(hipStreamDestroy(S(stream)));
+  return MPR_OK;
+}
+
 // ---- index -------------------------------------------------------------------------------------
 int mpr_index_create(const float* rows, int64_t n, int32_t d, int32_t metric, int64_t row_offset,
                      mpr_index** out) {
@@ -365,6 +385,13 @@ int mpr_t5_generate(mpr_model* m, const float* embeds, const float* mask, int32_
   return guarded([&]() -> int {
     T5_HANDLE(m);
     return t5->generate(embeds, mask, b, L, max_new, start, eos, pad, out_tokens, S(stream));
+  });
+}
+
+int mpr_t5_set_decode_stream(mpr_model* m, void* decode_stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    return t5->set_decode_stream(S(decode_stream));
   });
 }
 

@@ -4,7 +4,9 @@
 // butterflies; attention for the short sequences of this path (ViT 50 tokens, CLIP text <= 77,
 // T5 <= 562, decoder steps of 1 query) keeps a 64-key chunk of K and V of one (batch, head) in
 // LDS and runs an online softmax per query row, one key per lane.
+#include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -268,6 +270,122 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
   }
 }
 
+// ---- short-sequence attention on MFMA ----------------------------------------------------------
+// One wave per (batch, head, 16-query tile), Lk <= ATT_MFMA_MAXK, head dim 64, on
+// v_mfma_f32_16x16x4_f32 (exact f32 products, 4-deep k steps):
+//   S^T = K Q^T  — key tiles of 16 as the A operand, the query tile as B; the accumulator gives
+//                  lane (query j = lane&15, group g = lane>>4) the scores of keys 16t + 4g + r,
+//                  so the softmax over keys is in-lane plus two xor-shuffles (16, 32);
+//   O   = P V    — P is used straight from those accumulators as the A operand (k step (t, r):
+//                  lane group g supplies key 16t + 4g + r), V rows as B, four 16-wide d tiles.
+// The contraction order over the head dim inside a step is permuted identically for K and Q
+// (lane group g holds d = 16g .. 16g+15), so every operand load is 4 contiguous float4.
+// Softmax follows torch: p = exp(s - max) / sum, then P @ V.
+constexpr int ATT_MFMA_MAXK = 256;
+constexpr int ATT_MFMA_KT = ATT_MFMA_MAXK / 16;
+
+__global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt, int units) {
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= units) return;
+  const int qt = unit % nqt, bh = unit / nqt, h = bh % a.H, b = bh / a.H;
+  const int li = lane & 15, g = lane >> 4;
+  const int q0 = qt * 16;
+  const int qi = q0 + li;                // this lane's query (scores layout)
+  const int qpos = qi + a.q_pos0;
+  int lk = a.Lk;
+  if (a.causal) lk = min(lk, q0 + 15 + a.q_pos0 + 1);
+  const int nkt = (lk + 15) / 16;
+  const float* qp = a.q + (int64_t)b * a.q_bs + (int64_t)min(qi, a.Lq - 1) * a.q_rs + h * 64 +
+                    16 * g;
+  const float* kb = a.k + (int64_t)b * a.k_bs + h * 64 + 16 * g;
+  const float* vb = a.v + (int64_t)b * a.v_bs + h * 64 + li;
+  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
+  f32x4 qf[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *reinterpret_cast<const f32x4*>(qp + 4 * s4);
+
+  f32x4 S[ATT_MFMA_KT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < ATT_MFMA_KT; ++t) {
+    if (t < nkt) {  // wave-uniform
+      const float* kp = kb + (int64_t)min(16 * t + li, a.Lk - 1) * a.k_rs;
+      f32x4 kf[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) kf[s4] = *reinterpret_cast<const f32x4*>(kp + 4 * s4);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s4][e], qf[s4][e], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * t + 4 * g + r;
+        bool valid = key < lk && (!a.causal || key <= qpos);
+        if (maskb && valid) valid = maskb[key] != 0.f;
+        float sc = acc[r] * a.scale;
+        if (a.rel_tab && valid) sc += a.rel_tab[(int64_t)(key - qpos + a.lut_radius) * a.H + h];
+        sc = valid ? sc : -INFINITY;
+        acc[r] = sc;
+        m = fmaxf(m, sc);
+      }
+      S[t] = acc;
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < ATT_MFMA_KT; ++t) {
+    if (t < nkt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = S[t][r] == -INFINITY ? 0.f : expf(S[t][r] - m);
+        S[t][r] = p;
+        l += p;
+      }
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float linv_ok = l > 0.f ? 1.f : 0.f;  // a query with no visible key gets zeros
+  const float ld = l > 0.f ? l : 1.f;
+  f32x4 O[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) O[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < ATT_MFMA_KT; ++t) {
+    if (t < nkt) {
+      f32x4 vv[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float* vp = vb + (int64_t)min(16 * t + 4 * g + r, a.Lk - 1) * a.v_rs;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) vv[r][dt] = f32x4{vp[16 * dt], 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = (S[t][r] / ld) * linv_ok;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          O[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(p, vv[r][dt][0], O[dt], 0, 0, 0);
+      }
+    }
+  }
+  // O[dt]: lane (d = 16 dt + li, group g) holds queries q0 + 4g + r
+  float* ob = a.o + (int64_t)b * a.o_bs + h * 64 + li;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = q0 + 4 * g + r;
+    if (q < a.Lq) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) ob[(int64_t)q * a.o_rs + 16 * dt] = O[dt][r];
+    }
+  }
+}
+
 // ---- data movement ----------------------------------------------------------------------------
 __global__ void im2col_kernel(const float* img, int B, int S, int p, float* cols) {
   // one thread per float4 of a patch row (kx contiguous)
@@ -518,6 +636,14 @@ int rmsnorm(const float* x, int64_t ldx, int M, int D, const float* w, float eps
   return MPR_OK;
 }
 
+bool mfma_attention_disabled() {
+  static const bool off = [] {
+    const char* e = getenv("MPR_MFMA_ATTN");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 int attention(const AttnArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attention: bad shape");
   if (a.B == 0 || a.Lq == 0) return MPR_OK;
@@ -527,6 +653,16 @@ int attention(const AttnArgs& a, hipStream_t s) {
   if (a.Lq == 1) {
     hipLaunchKernelGGL(attention_decode_kernel, dim3((unsigned)((int64_t)a.B * a.H)), dim3(256),
                        0, s, a);
+    MPR_LAUNCHED();
+    return MPR_OK;
+  }
+  int lk = a.Lk;
+  if (a.causal) lk = std::min(lk, a.Lq + a.q_pos0);
+  if (lk <= ATT_MFMA_MAXK && !mfma_attention_disabled()) {
+    const int nqt = (int)cdiv(a.Lq, 16);
+    const int64_t units = (int64_t)a.B * a.H * nqt;
+    hipLaunchKernelGGL(attention_mfma_kernel, dim3((unsigned)cdiv(units, 4)), dim3(256), 0, s, a,
+                       nqt, (int)units);
     MPR_LAUNCHED();
     return MPR_OK;
   }

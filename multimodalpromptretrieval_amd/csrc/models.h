@@ -89,7 +89,10 @@ struct T5Model : mpr_model {
     hipGraphExec_t exec;
     uint64_t gen;
   };
-  std::map<std::tuple<int, int, int, int, int, int>, GraphEnt> graphs;
+  using GraphKey = std::tuple<int, int, int, int, int, int>;  // (part, B, L, max_new, ., .)
+  std::map<GraphKey, GraphEnt> graphs;
+  hipStream_t dec_stream = nullptr;  // not owned
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
   int encode(const float* embeds, const float* mask, int B, int L, float* out, hipStream_t s);
   int generate(const float* embeds, const float* mask, int B, int L, int max_new, int start,
@@ -98,11 +101,16 @@ struct T5Model : mpr_model {
                 int T, float* logits_out, hipStream_t s);
   int embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
             hipStream_t s);
+  // Stream for the greedy decode loop of generate() (null: the caller's stream).
+  int set_decode_stream(hipStream_t ds);
 
  private:
   int grow(DevBuf& b, size_t bytes);
   int cross_kv_project(int B, int L, hipStream_t s);
-  int generate_body(int B, int L, int max_new, int start, int eos, int pad, hipStream_t s);
+  int encode_body(int B, int L, int max_new, int start, hipStream_t s);
+  int decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s);
+  template <class F>
+  int graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body);
 };
 
 }  // namespace mpr

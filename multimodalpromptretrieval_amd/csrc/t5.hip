@@ -12,9 +12,10 @@
 // per-layer cache laid out [B][max_new][3*inner] (the fused q|k|v row of each generated position);
 // the cross-attention K/V of every decoder layer come from one GEMM over the encoder output; the
 // lm_head never materialises logits: each block emits its per-row best column and greedy_step
-// reduces those and gathers the next input embedding.  The whole generate() — encoder, cross K/V
-// projection and all decode steps, ~50 launches per step — is captured once per shape into a
-// hipGraph (private capture stream) and replayed on the caller's stream.
+// reduces those and gathers the next input embedding.  generate() is captured once per shape into
+// two hipGraphs (private capture stream): the encoder + cross K/V projection, replayed on the
+// caller's stream, and the decode loop (~50 launches per step), replayed on the decode stream when
+// one is set (a CU partition of its own) or else on the caller's stream.
 #include <cstdlib>
 
 #include "models.h"
@@ -34,6 +35,8 @@ bool graphs_enabled() {
 T5Model::~T5Model() {
   for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
   if (cap_stream) (void)hipStreamDestroy(cap_stream);
+  if (ev_fork) (void)hipEventDestroy(ev_fork);
+  if (ev_join) (void)hipEventDestroy(ev_join);
 }
 
 int T5Model::grow(DevBuf& b, size_t bytes) {
@@ -109,30 +112,38 @@ int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
   return gemm(g, s);
 }
 
-// Everything generate() enqueues after its inputs sit in enc_in / mask_in.  Only model-owned
-// buffers are touched, so the sequence can be captured into a graph and replayed.
-int T5Model::generate_body(int B, int L, int max_new, int start, int eos, int pad,
-                           hipStream_t s) {
+// Everything generate() enqueues after its inputs sit in enc_in / mask_in, in two parts: the
+// encoder (+ cross-attention K/V of every decoder layer, + the decode state reset) and the greedy
+// decode loop.  Only model-owned buffers are touched, so each part is captured into a graph and
+// replayed; the decode part can run on its own stream (a CU partition reserved for the
+// latency-bound decode chain, mpr_t5_set_decode_stream).
+int T5Model::encode_body(int B, int L, int max_new, int start, hipStream_t s) {
+  const int T1 = max_new + 1;
+  const float* maskp = mask_in.as<float>();
+  MPR_TRY(encode(enc_in.as<float>(), maskp, B, L, enc_out.as<float>(), s));
+  MPR_TRY(cross_kv_project(B, L, s));
+  MPR_TRY(fill_i32(unfinished.as<int32_t>(), 1, B, s));
+  MPR_TRY(fill_i32(cur_tok.as<int32_t>(), start, B, s));
+  MPR_TRY(fill_i32(tok_buf.as<int32_t>(), start, (int64_t)B * T1, s));  // column 0 = start
+  MPR_TRY(embed_gather(shared.as<float>(), cur_tok.as<int32_t>(), 1, B, 1, d, nullptr,
+                       dx.as<float>(), d, 0, s));
+  return MPR_OK;
+}
+
+int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s) {
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
   const int nparts = (int)cdiv(V, 16);
   const float* maskp = mask_in.as<float>();
-  MPR_TRY(encode(enc_in.as<float>(), maskp, B, L, enc_out.as<float>(), s));
-  MPR_TRY(cross_kv_project(B, L, s));
   float* xp = dx.as<float>();
   float* qp = dq.as<float>();
   float* ap = ao.as<float>();
   float* fp = ff.as<float>();
   int32_t* unf = unfinished.as<int32_t>();
-  int32_t* ct = cur_tok.as<int32_t>();
   int32_t* toks = tok_buf.as<int32_t>();
   const float* ckv = cross_kv.as<float>();
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
 
-  MPR_TRY(fill_i32(unf, 1, B, s));
-  MPR_TRY(fill_i32(ct, start, B, s));
-  MPR_TRY(fill_i32(toks, start, (int64_t)B * T1, s));  // column 0 = decoder_start
-  MPR_TRY(embed_gather(shared.as<float>(), ct, 1, B, 1, d, nullptr, xp, d, 0, s));
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
   for (int t = 0; t < max_new; ++t) {
     for (int l = 0; l < Ld; ++l) {
@@ -247,41 +258,75 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
     MPR_HIP(hipMemcpy2DAsync(mask_in.ptr, (size_t)L * 4, mask, (size_t)Lsrc * 4,
                              (size_t)Lsrc * 4, B, hipMemcpyDeviceToDevice, s));
   }
+  hipStream_t ds = dec_stream ? dec_stream : s;
   if (!graphs_enabled()) {
-    MPR_TRY(generate_body(B, L, max_new, start, eos, pad, s));
+    MPR_TRY(encode_body(B, L, max_new, start, s));
+    if (ds != s) {
+      MPR_HIP(hipEventRecord(ev_fork, s));
+      MPR_HIP(hipStreamWaitEvent(ds, ev_fork, 0));
+    }
+    MPR_TRY(decode_body(B, L, max_new, eos, pad, ds));
   } else {
-    auto key = std::make_tuple(B, L, max_new, start, eos, pad);
-    auto it = graphs.find(key);
-    if (it != graphs.end() && it->second.gen != gen) {
-      for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
-      graphs.clear();
-      it = graphs.end();
+    hipGraphExec_t enc_exec = nullptr, dec_exec = nullptr;
+    MPR_TRY(graph_for(std::make_tuple(0, B, L, max_new, start, 0), &enc_exec,
+                      [&](hipStream_t c) { return encode_body(B, L, max_new, start, c); }));
+    MPR_TRY(graph_for(std::make_tuple(1, B, L, max_new, eos, pad), &dec_exec,
+                      [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
+    MPR_HIP(hipGraphLaunch(enc_exec, s));
+    if (ds != s) {
+      MPR_HIP(hipEventRecord(ev_fork, s));
+      MPR_HIP(hipStreamWaitEvent(ds, ev_fork, 0));
     }
-    if (it == graphs.end()) {
-      if (graphs.size() >= MAX_GRAPHS) {
-        for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
-        graphs.clear();
-      }
-      if (!cap_stream) MPR_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
-      hipGraph_t graph = nullptr;
-      MPR_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
-      const int rc = generate_body(B, L, max_new, start, eos, pad, cap_stream);
-      const hipError_t ec = hipStreamEndCapture(cap_stream, &graph);
-      if (rc != MPR_OK) {
-        if (graph) (void)hipGraphDestroy(graph);
-        return rc;
-      }
-      MPR_HIP(ec);
-      hipGraphExec_t exec = nullptr;
-      const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      MPR_HIP(ei);
-      it = graphs.emplace(key, GraphEnt{exec, gen}).first;
-    }
-    MPR_HIP(hipGraphLaunch(it->second.exec, s));
+    MPR_HIP(hipGraphLaunch(dec_exec, ds));
   }
   MPR_HIP(hipMemcpyAsync(out_tokens, tok_buf.ptr, (size_t)B * T1 * 4, hipMemcpyDeviceToDevice,
-                         s));
+                         ds));
+  if (ds != s) {  // the caller's stream sees the tokens (and may reuse the buffers) after this
+    MPR_HIP(hipEventRecord(ev_join, ds));
+    MPR_HIP(hipStreamWaitEvent(s, ev_join, 0));
+  }
+  return MPR_OK;
+}
+
+int T5Model::set_decode_stream(hipStream_t ds) {
+  if (ds && !ev_fork) {
+    MPR_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    MPR_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+  }
+  dec_stream = ds;
+  return MPR_OK;
+}
+
+template <class F>
+int T5Model::graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body) {
+  auto it = graphs.find(key);
+  if (it != graphs.end() && it->second.gen != gen) {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
+    graphs.clear();
+    it = graphs.end();
+  }
+  if (it == graphs.end()) {
+    if (graphs.size() >= MAX_GRAPHS) {
+      for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
+      graphs.clear();
+    }
+    if (!cap_stream) MPR_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+    hipGraph_t graph = nullptr;
+    MPR_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
+    const int rc = body(cap_stream);
+    const hipError_t ec = hipStreamEndCapture(cap_stream, &graph);
+    if (rc != MPR_OK) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    MPR_HIP(ec);
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    MPR_HIP(ei);
+    it = graphs.emplace(key, GraphEnt{exec, gen}).first;
+  }
+  *out = it->second.exec;
   return MPR_OK;
 }
 

@@ -84,10 +84,10 @@ class VQARetrieval:
     # ---- encoding ------------------------------------------------------------------------------
     def _streams(self):
         if not hasattr(self, "_s_img"):
-            # High priority: the host blocks on these results (prompt building), while other
-            # device work queued meanwhile is not needed until later.
-            self._s_img = torch.cuda.Stream(self.device, priority=-1)
-            self._s_txt = torch.cuda.Stream(self.device, priority=-1)
+            # The encoders' CU share (_lib.role_stream): the T5 decode chain of the previous
+            # batch keeps CUs of its own while these run.
+            self._s_img = _lib.role_stream(self.device, "encode:img")
+            self._s_txt = _lib.role_stream(self.device, "encode:txt")
         return self._s_img, self._s_txt
 
     def encode_image_pair(self, batch, other_vit, other_mode: int):

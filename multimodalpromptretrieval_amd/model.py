@@ -204,7 +204,13 @@ class T5VisionModel(nn.Module):
     def _device_t5(self):
         # named_parameters() lists the tied embedding once, as shared.weight; DeviceT5 reuses it
         # for the lm_head when lm_head.weight is absent.
-        return self._handle("t5", "T5_model.", lambda sd: DeviceT5(sd, self.device))
+        def build(sd):
+            dev = DeviceT5(sd, self.device)
+            if _lib.separate_decode_stream(self.device.index if self.device.index is not None
+                                           else torch.cuda.current_device()):
+                dev.set_decode_stream(_lib.role_stream(self.device, "decode"))
+            return dev
+        return self._handle("t5", "T5_model.", build)
 
     # ---- reference surface -----------------------------------------------------------------------
     def get_image_token_features(self, x):

@@ -107,6 +107,15 @@ class DeviceT5:
     def _stream(self):
         return _lib.stream_ptr(self.device)
 
+    def set_decode_stream(self, stream=None):
+        """Run the greedy decode loop of later generate calls on ``stream`` (a torch stream,
+        e.g. ``_lib.role_stream(device, "decode")``; None = the caller's stream).  Ordering is
+        unchanged: the loop waits for the encoder on the caller's stream and the caller's stream
+        waits for the tokens."""
+        self._dec_stream = stream  # keep the stream object alive while the library uses it
+        _lib.call("mpr_t5_set_decode_stream", self._h,
+                  _lib.c_void_p(stream.cuda_stream if stream is not None else 0))
+
     def embed(self, ids: torch.Tensor, out: torch.Tensor, row0: int = 0) -> torch.Tensor:
         """out[b, row0 + t, :] = shared[ids[b, t]] (out: [B, L, d] fp32 on device)."""
         ids32 = ids.to(self.device, torch.int32, non_blocking=True).contiguous()

@@ -180,6 +180,22 @@ def test_t5_generate_graph_replay_matches_eager(device, t5_sd, monkeypatch):
     assert torch.equal(d, c[:3, :8])
 
 
+def test_t5_generate_on_decode_stream(device, t5_sd):
+    """Decode loop on a CU-partition stream: same tokens as on the caller's stream."""
+    from multimodalpromptretrieval_amd import _lib
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    m = DeviceT5(t5_sd, device)
+    ids, mask, img_tok = _t5_inputs(6, 43)
+    emb = torch.cat([img_tok, t5_sd["shared.weight"][ids]], 1).to(device)
+    fm = torch.cat([torch.ones(6, 50, dtype=torch.long), mask], 1).to(device)
+    a = m.generate_padded(emb, fm, 20).cpu()
+    m.set_decode_stream(_lib.role_stream(device, "decode"))
+    b = m.generate_padded(emb, fm, 20).cpu()
+    c = m.generate_padded(emb[:2], fm[:2], 20).cpu()
+    m.set_decode_stream(None)
+    assert torch.equal(a, b) and torch.equal(c, a[:2])
+
+
 def test_t5_embed_and_loss(device, t5_sd):
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     m = DeviceT5(t5_sd, device)

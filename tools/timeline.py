@@ -45,6 +45,8 @@ def wrap(cls, name, label):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--pipelined", action="store_true",
+                    help="time predict_many (two batches in flight) instead of predict()")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -52,9 +54,31 @@ def main():
     model, _, _ = bench.build(cfg, dev, None)
     batches = bench.make_batches(4, cfg["B"], dev, seed=100)
     wrap(encoders.DeviceViT, "forward", "vit")
+    wrap(encoders.DeviceViT, "forward_pair", "vit-pair")
     wrap(encoders.DeviceCLIPText, "forward", "text")
     wrap(index.DeviceIndex, "search", "scan")
     wrap(t5.DeviceT5, "generate_padded", "t5.generate")
+    if args.pipelined:
+        with torch.no_grad():
+            for _ in model.predict_many(batches[i % 4] for i in range(4)):
+                pass
+            torch.cuda.synchronize()
+            RECS.clear()
+            cur = torch.cuda.current_stream()
+            ref = torch.cuda.Event(enable_timing=True)
+            ref.record(cur)
+            h_ref = time.perf_counter()
+            n = 0
+            for _ in model.predict_many(batches[i % 4] for i in range(args.steps)):
+                n += 1
+                print(f"  answers of batch {n - 1} on host at {1e3 * (time.perf_counter() - h_ref):8.3f}")
+            torch.cuda.synchronize()
+            print(f"{args.steps} pipelined steps: host {1e3 * (time.perf_counter() - h_ref):.3f} ms")
+            for tag, sid, e0, e1, h0, h1 in RECS:
+                print(f"  {tag:14s} stream {sid:>4}  host {1e3 * (h0 - h_ref):8.3f}->"
+                      f"{1e3 * (h1 - h_ref):8.3f}  dev {ref.elapsed_time(e0):8.3f}->"
+                      f"{ref.elapsed_time(e1):8.3f} ms")
+        return
     with torch.no_grad():
         for i in range(3):
             model.predict(batches[i % 4])
