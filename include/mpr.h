@@ -141,10 +141,18 @@ int mpr_t5_generate(mpr_model* m, const float* embeds_dev, const float* mask_dev
                     int32_t L, int32_t max_new, int32_t decoder_start, int32_t eos, int32_t pad,
                     int32_t* out_tokens_dev, void* stream);
 /* Teacher-forced decoder logits: dec_in_dev [b,T] int32 decoder input ids -> logits [b,T,vocab]. */
-/* Run the greedy decode loop of subsequent mpr_t5_generate calls on decode_stream (null = the
+/* mpr_t5_generate on workspace slot `slot` (0 <= slot < 4; mpr_t5_generate uses slot 0).  Each
+ * slot has its own activations, decode caches and captured graphs, so calls on different slots
+ * may be in flight on the device at the same time (a serving loop decoding two batches at once);
+ * calls on one slot must be ordered by their streams. */
+int mpr_t5_generate_slot(mpr_model* m, int32_t slot, const float* embeds_dev,
+                         const float* mask_dev, int32_t b, int32_t L, int32_t max_new,
+                         int32_t decoder_start, int32_t eos, int32_t pad, int32_t* out_tokens_dev,
+                         void* stream);
+/* Run the greedy decode loop of later generate calls on a slot on decode_stream (null = the
  * call's own stream).  The call's stream still orders everything: the loop starts after the
  * encoder enqueued on it and the call's stream waits for the tokens. */
-int mpr_t5_set_decode_stream(mpr_model* m, void* decode_stream);
+int mpr_t5_set_decode_stream(mpr_model* m, int32_t slot, void* decode_stream);
 int mpr_t5_logits(mpr_model* m, const float* embeds_dev, const float* mask_dev, int32_t b,
                   int32_t L, const int32_t* dec_in_dev, int32_t T, float* logits_dev,
                   void* stream);

@@ -54,7 +54,9 @@ SIGNATURES = [
                                 c_void_p]),
     ("mpr_t5_generate", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                   c_int32, c_int32, c_int32, c_void_p, c_void_p]),
-    ("mpr_t5_set_decode_stream", c_int32, [c_void_p, c_void_p]),
+    ("mpr_t5_generate_slot", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                       c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    ("mpr_t5_set_decode_stream", c_int32, [c_void_p, c_int32, c_void_p]),
     ("mpr_t5_logits", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                                 c_int32, c_void_p, c_void_p]),
     ("mpr_cross_entropy", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),

@@ -367,6 +367,7 @@ int mpr_t5_embed(mpr_model* m, const int32_t* ids, int32_t b, int32_t len, float
                  int64_t out_bs, int32_t row0, void* stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);
+    MPR_TRY(t5->use_slot(0));
     return t5->embed(ids, b, len, out, out_bs, row0, S(stream));
   });
 }
@@ -375,6 +376,7 @@ int mpr_t5_encode(mpr_model* m, const float* embeds, const float* mask, int32_t 
                   float* out, void* stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);
+    MPR_TRY(t5->use_slot(0));
     return t5->encode(embeds, mask, b, L, out, S(stream));
   });
 }
@@ -382,16 +384,24 @@ int mpr_t5_encode(mpr_model* m, const float* embeds, const float* mask, int32_t 
 int mpr_t5_generate(mpr_model* m, const float* embeds, const float* mask, int32_t b, int32_t L,
                     int32_t max_new, int32_t start, int32_t eos, int32_t pad, int32_t* out_tokens,
                     void* stream) {
+  return mpr_t5_generate_slot(m, 0, embeds, mask, b, L, max_new, start, eos, pad, out_tokens,
+                              stream);
+}
+
+int mpr_t5_generate_slot(mpr_model* m, int32_t slot, const float* embeds, const float* mask,
+                         int32_t b, int32_t L, int32_t max_new, int32_t start, int32_t eos,
+                         int32_t pad, int32_t* out_tokens, void* stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);
-    return t5->generate(embeds, mask, b, L, max_new, start, eos, pad, out_tokens, S(stream));
+    return t5->generate(embeds, mask, b, L, max_new, start, eos, pad, out_tokens, S(stream),
+                        slot);
   });
 }
 
-int mpr_t5_set_decode_stream(mpr_model* m, void* decode_stream) {
+int mpr_t5_set_decode_stream(mpr_model* m, int32_t slot, void* decode_stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);
-    return t5->set_decode_stream(S(decode_stream));
+    return t5->set_decode_stream(slot, S(decode_stream));
   });
 }
 
@@ -399,6 +409,7 @@ int mpr_t5_logits(mpr_model* m, const float* embeds, const float* mask, int32_t 
                   const int32_t* dec_in, int32_t T, float* logits, void* stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);
+    MPR_TRY(t5->use_slot(0));
     return t5->logits_tf(embeds, mask, b, L, dec_in, T, logits, S(stream));
   });
 }

@@ -15,6 +15,8 @@ namespace mpr {
 
 void set_error(const char* fmt, ...);
 
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 #define MPR_HIP(expr)                                                                      \
   do {                                                                                     \
     hipError_t _e = (expr);                                                                \

@@ -461,8 +461,6 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   }
 }
 
-bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-
 // ---- kernel probe: hipEvent pairs around every GEMM launch of the probed kind ----------------
 struct ProbeRec {
   hipEvent_t a, b;

@@ -26,60 +26,96 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// ---- LayerNorm / RMSNorm: one wave per row, row cached in registers (D <= 64*MAXV) ---------
-template <int MAXV>
+// ---- LayerNorm / RMSNorm: 32 lanes per row (2 rows per wave), float4 accesses -----------------
+// The row, gamma and beta are all requested before the first reduction (one memory round trip);
+// rows of width D <= 128 * V4 stay in registers.  Out-of-range slots load clamped, in-range data
+// and are zeroed by a select (a guarded load makes hipcc wait for each load separately).
+__device__ __forceinline__ float half_sum(float v) {  // over the 32 lanes of a half-wave
+#pragma unroll
+  for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int V4>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t ldx, int M, int D,
                                                         const float* g, const float* b, float eps,
                                                         float* out, int64_t ldo) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= M) return;
-  const float* xr = x + (int64_t)row * ldx;
-  float v[MAXV];
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5), l32 = threadIdx.x & 31;
+  const float* xr = x + (int64_t)min(row, M - 1) * ldx;
+  const int D4 = D >> 2;
+  f32x4 v[V4], gv[V4], bv[V4];
+#pragma unroll
+  for (int j = 0; j < V4; ++j) {
+    const int c4 = min(l32 + 32 * j, D4 - 1);
+    v[j] = reinterpret_cast<const f32x4*>(xr)[c4];
+    gv[j] = reinterpret_cast<const f32x4*>(g)[c4];
+    bv[j] = reinterpret_cast<const f32x4*>(b)[c4];
+  }
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + j * 64;
-    v[j] = c < D ? xr[c] : 0.f;
-    s += v[j];
+  for (int j = 0; j < V4; ++j) {
+    if (l32 + 32 * j >= D4) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
   }
-  const float mean = wave_sum(s) / (float)D;
+  const float mean = half_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + j * 64;
-    const float d = c < D ? v[j] - mean : 0.f;
-    q += d * d;
+  for (int j = 0; j < V4; ++j) {
+    if (l32 + 32 * j < D4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[j][e] - mean;
+        q += d * d;
+      }
+    }
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+  const float rstd = 1.0f / sqrtf(half_sum(q) / (float)D + eps);
+  if (row >= M) return;
   float* orow = out + (int64_t)row * ldo;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + j * 64;
-    if (c < D) orow[c] = (v[j] - mean) * rstd * g[c] + b[c];
+  for (int j = 0; j < V4; ++j) {
+    const int c4 = l32 + 32 * j;
+    if (c4 < D4) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * gv[j][e] + bv[j][e];
+      reinterpret_cast<f32x4*>(orow)[c4] = o;
+    }
   }
 }
 
-template <int MAXV>
+template <int V4>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, int64_t ldx, int M, int D,
                                                       const float* w, float eps, float* out,
                                                       int64_t ldo) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= M) return;
-  const float* xr = x + (int64_t)row * ldx;
-  float v[MAXV];
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5), l32 = threadIdx.x & 31;
+  const float* xr = x + (int64_t)min(row, M - 1) * ldx;
+  const int D4 = D >> 2;
+  f32x4 v[V4], wv[V4];
+#pragma unroll
+  for (int j = 0; j < V4; ++j) {
+    const int c4 = min(l32 + 32 * j, D4 - 1);
+    v[j] = reinterpret_cast<const f32x4*>(xr)[c4];
+    wv[j] = reinterpret_cast<const f32x4*>(w)[c4];
+  }
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + j * 64;
-    v[j] = c < D ? xr[c] : 0.f;
-    s += v[j] * v[j];
+  for (int j = 0; j < V4; ++j) {
+    if (l32 + 32 * j >= D4) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[j][0] * v[j][0] + v[j][1] * v[j][1]) + (v[j][2] * v[j][2] + v[j][3] * v[j][3]);
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(s) / (float)D + eps);
+  const float rstd = 1.0f / sqrtf(half_sum(s) / (float)D + eps);
+  if (row >= M) return;
   float* orow = out + (int64_t)row * ldo;
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = lane + j * 64;
-    if (c < D) orow[c] = w[c] * (v[j] * rstd);
+  for (int j = 0; j < V4; ++j) {
+    const int c4 = l32 + 32 * j;
+    if (c4 < D4) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = wv[j][e] * (v[j][e] * rstd);
+      reinterpret_cast<f32x4*>(orow)[c4] = o;
+    }
   }
 }
 
@@ -233,15 +269,19 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
       const int jv = jv0 + u < lk_end ? jv0 + u : kc;
       vr[u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)jv * a.v_rs + 4 * dg);
     }
-    const float mk = (maskb && in) ? maskb[j] : 1.f;
-    const float rb = (a.rel_tab && in) ? a.rel_tab[(int64_t)(j - qpos + a.lut_radius) * a.H + h]
-                                       : 0.f;
+    // mask / bias words from a clamped, in-range key: unconditional loads (a load under a
+    // per-lane condition is waited for on its own, a second round trip)
+    const int jc = in ? j : kc;
+    const float* mp = maskb ? maskb + jc : kp;  // any valid address when there is no mask
+    const float* bp = a.rel_tab ? a.rel_tab + (int64_t)(jc - qpos + a.lut_radius) * a.H + h : kp;
+    const float mraw = *mp, braw = *bp;
+    const float mk = maskb ? mraw : 1.f, rb = a.rel_tab ? braw : 0.f;
     float s = 0.f;
 #pragma unroll
     for (int d = 0; d < ATT_D / 4; ++d)
       s += qv[d][0] * kr[d][0] + qv[d][1] * kr[d][1] + qv[d][2] * kr[d][2] + qv[d][3] * kr[d][3];
     const bool valid = in && mk != 0.f;
-    const float sc = valid ? s * a.scale + rb : -INFINITY;
+    const float sc = valid ? s * a.scale + rb : -INFINITY;  // rb is 0 without a bias table
     float wm = wave_max(sc);
     if (lane == 0) red[0][wave] = wm;
     __syncthreads();
@@ -271,46 +311,82 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
 }
 
 // ---- short-sequence attention on MFMA ----------------------------------------------------------
-// One wave per (batch, head, 16-query tile), Lk <= ATT_MFMA_MAXK, head dim 64, on
-// v_mfma_f32_16x16x4_f32 (exact f32 products, 4-deep k steps):
+// Block = one (batch, head) and up to 64 queries (4 waves x 16-query tiles), Lk <= ATT_MFMA_MAXK,
+// head dim 64, on v_mfma_f32_16x16x4_f32 (exact f32 products, 4-deep k steps).  The block stages
+// the (b, h) K and V rows into LDS with every load in flight at once (one memory round trip),
+// then each wave computes
 //   S^T = K Q^T  — key tiles of 16 as the A operand, the query tile as B; the accumulator gives
 //                  lane (query j = lane&15, group g = lane>>4) the scores of keys 16t + 4g + r,
 //                  so the softmax over keys is in-lane plus two xor-shuffles (16, 32);
 //   O   = P V    — P is used straight from those accumulators as the A operand (k step (t, r):
 //                  lane group g supplies key 16t + 4g + r), V rows as B, four 16-wide d tiles.
 // The contraction order over the head dim inside a step is permuted identically for K and Q
-// (lane group g holds d = 16g .. 16g+15), so every operand load is 4 contiguous float4.
-// Softmax follows torch: p = exp(s - max) / sum, then P @ V.
+// (lane group g holds d = 16g .. 16g+15).  Softmax follows torch: p = exp(s - max) / sum, then
+// P @ V.
 constexpr int ATT_MFMA_MAXK = 256;
 constexpr int ATT_MFMA_KT = ATT_MFMA_MAXK / 16;
+constexpr int ATT_MFMA_LD = 68;  // LDS row stride (floats)
 
-__global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt, int units) {
-  const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (unit >= units) return;
-  const int qt = unit % nqt, bh = unit / nqt, h = bh % a.H, b = bh / a.H;
+__global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt) {
+  extern __shared__ __attribute__((aligned(16))) float kv_s[];  // K rows | V rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.x, h = bh % a.H, b = bh / a.H;
+  const int qt = blockIdx.y * 4 + wave;
   const int li = lane & 15, g = lane >> 4;
   const int q0 = qt * 16;
-  const int qi = q0 + li;                // this lane's query (scores layout)
+  const int qi = q0 + li;  // this lane's query (scores layout)
   const int qpos = qi + a.q_pos0;
-  int lk = a.Lk;
-  if (a.causal) lk = min(lk, q0 + 15 + a.q_pos0 + 1);
-  const int nkt = (lk + 15) / 16;
+  int lkb = a.Lk;          // keys any query of the block can see
+  if (a.causal) lkb = min(lkb, min(a.Lq, blockIdx.y * 64 + 64) - 1 + a.q_pos0 + 1);
+  const int nkb = (lkb + 15) / 16;
+  float* Ks = kv_s;
+  float* Vs = kv_s + nkb * 16 * ATT_MFMA_LD;
+
+  // this wave's query fragments, then the block's K / V rows (keys past lkb are zero rows)
   const float* qp = a.q + (int64_t)b * a.q_bs + (int64_t)min(qi, a.Lq - 1) * a.q_rs + h * 64 +
                     16 * g;
-  const float* kb = a.k + (int64_t)b * a.k_bs + h * 64 + 16 * g;
-  const float* vb = a.v + (int64_t)b * a.v_bs + h * 64 + li;
-  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
   f32x4 qf[4];
 #pragma unroll
   for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *reinterpret_cast<const f32x4*>(qp + 4 * s4);
+  {
+    const float* kb = a.k + (int64_t)b * a.k_bs + h * 64;
+    const float* vb = a.v + (int64_t)b * a.v_bs + h * 64;
+    const int n4 = nkb * 16 * 16;  // float4 per operand
+    constexpr int PER = ATT_MFMA_MAXK * 16 / 256;
+    f32x4 kr[PER], vr[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + u * 256;
+      if (idx < n4) {
+        const int key = min(idx >> 4, a.Lk - 1), c4 = (idx & 15) * 4;
+        kr[u] = *reinterpret_cast<const f32x4*>(kb + (int64_t)key * a.k_rs + c4);
+        vr[u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)key * a.v_rs + c4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + u * 256;
+      if (idx < n4) {
+        const int key = idx >> 4, c4 = (idx & 15) * 4;
+        *reinterpret_cast<f32x4*>(Ks + key * ATT_MFMA_LD + c4) = kr[u];
+        *reinterpret_cast<f32x4*>(Vs + key * ATT_MFMA_LD + c4) = vr[u];
+      }
+    }
+  }
+  __syncthreads();
+  if (qt >= nqt) return;  // wave-uniform; no barrier follows
 
+  int lk = lkb;  // keys this wave's queries can see
+  if (a.causal) lk = min(lk, q0 + 15 + a.q_pos0 + 1);
+  const int nkt = (lk + 15) / 16;
+  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
   f32x4 S[ATT_MFMA_KT];
   float m = -INFINITY;
 #pragma unroll
   for (int t = 0; t < ATT_MFMA_KT; ++t) {
     if (t < nkt) {  // wave-uniform
-      const float* kp = kb + (int64_t)min(16 * t + li, a.Lk - 1) * a.k_rs;
+      const float* kp = Ks + (16 * t + li) * ATT_MFMA_LD + 16 * g;
       f32x4 kf[4];
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) kf[s4] = *reinterpret_cast<const f32x4*>(kp + 4 * s4);
@@ -350,7 +426,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
-  const float linv_ok = l > 0.f ? 1.f : 0.f;  // a query with no visible key gets zeros
+  const float lok = l > 0.f ? 1.f : 0.f;  // a query with no visible key gets zeros
   const float ld = l > 0.f ? l : 1.f;
   f32x4 O[4];
 #pragma unroll
@@ -358,19 +434,13 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt
 #pragma unroll
   for (int t = 0; t < ATT_MFMA_KT; ++t) {
     if (t < nkt) {
-      f32x4 vv[4][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float* vp = vb + (int64_t)min(16 * t + 4 * g + r, a.Lk - 1) * a.v_rs;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) vv[r][dt] = f32x4{vp[16 * dt], 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (S[t][r] / ld) * linv_ok;
+        const float p = (S[t][r] / ld) * lok;
+        const float* vp = Vs + (16 * t + 4 * g + r) * ATT_MFMA_LD + li;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
-          O[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(p, vv[r][dt][0], O[dt], 0, 0, 0);
+          O[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(p, vp[16 * dt], O[dt], 0, 0, 0);
       }
     }
   }
@@ -610,14 +680,17 @@ __global__ __launch_bounds__(256) void ce_reduce_kernel(const float* loss, const
 
 int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, const float* beta,
               float eps, float* out, int64_t ldo, hipStream_t s) {
-  MPR_REQUIRE(D > 0 && D <= 1024, "layernorm: D=%d unsupported", D);
+  MPR_REQUIRE(D > 0 && D <= 1024 && D % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0,
+              "layernorm: D=%d / strides unsupported (D <= 1024, multiples of 4)", D);
+  MPR_REQUIRE(aligned16(x) && aligned16(out) && aligned16(gamma) && aligned16(beta),
+              "layernorm: operands must be 16-byte aligned");
   if (M <= 0) return MPR_OK;
-  dim3 grid((unsigned)cdiv(M, 4));
+  dim3 grid((unsigned)cdiv(M, 8));
   if (D <= 512)
-    hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, M, D, gamma, beta, eps,
+    hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, s, x, ldx, M, D, gamma, beta, eps,
                        out, ldo);
   else
-    hipLaunchKernelGGL(layernorm_kernel<16>, grid, dim3(256), 0, s, x, ldx, M, D, gamma, beta,
+    hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, M, D, gamma, beta,
                        eps, out, ldo);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -625,13 +698,16 @@ int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, con
 
 int rmsnorm(const float* x, int64_t ldx, int M, int D, const float* w, float eps, float* out,
             int64_t ldo, hipStream_t s) {
-  MPR_REQUIRE(D > 0 && D <= 1024, "rmsnorm: D=%d unsupported", D);
+  MPR_REQUIRE(D > 0 && D <= 1024 && D % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0,
+              "rmsnorm: D=%d / strides unsupported (D <= 1024, multiples of 4)", D);
+  MPR_REQUIRE(aligned16(x) && aligned16(out) && aligned16(w),
+              "rmsnorm: operands must be 16-byte aligned");
   if (M <= 0) return MPR_OK;
-  dim3 grid((unsigned)cdiv(M, 4));
+  dim3 grid((unsigned)cdiv(M, 8));
   if (D <= 512)
-    hipLaunchKernelGGL(rmsnorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, M, D, w, eps, out, ldo);
+    hipLaunchKernelGGL(rmsnorm_kernel<4>, grid, dim3(256), 0, s, x, ldx, M, D, w, eps, out, ldo);
   else
-    hipLaunchKernelGGL(rmsnorm_kernel<16>, grid, dim3(256), 0, s, x, ldx, M, D, w, eps, out, ldo);
+    hipLaunchKernelGGL(rmsnorm_kernel<8>, grid, dim3(256), 0, s, x, ldx, M, D, w, eps, out, ldo);
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -660,9 +736,10 @@ int attention(const AttnArgs& a, hipStream_t s) {
   if (a.causal) lk = std::min(lk, a.Lq + a.q_pos0);
   if (lk <= ATT_MFMA_MAXK && !mfma_attention_disabled()) {
     const int nqt = (int)cdiv(a.Lq, 16);
-    const int64_t units = (int64_t)a.B * a.H * nqt;
-    hipLaunchKernelGGL(attention_mfma_kernel, dim3((unsigned)cdiv(units, 4)), dim3(256), 0, s, a,
-                       nqt, (int)units);
+    const size_t lds = (size_t)2 * cdiv(lk, 16) * 16 * ATT_MFMA_LD * sizeof(float);
+    hipLaunchKernelGGL(attention_mfma_kernel, dim3((unsigned)((int64_t)a.B * a.H),
+                                                   (unsigned)cdiv(nqt, 4)),
+                       dim3(256), lds, s, a, nqt);
     MPR_LAUNCHED();
     return MPR_OK;
   }

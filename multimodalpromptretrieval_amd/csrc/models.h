@@ -70,20 +70,14 @@ struct T5Layer {
   DevBuf pk_qkv, pk_o, pk_cq, pk_co, pk_wi, pk_wo;
 };
 
-struct T5Model : mpr_model {
-  T5Model() : mpr_model(T5) {}
-  ~T5Model() override;
-  int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
-  int inner = 0, lut_radius = 0;
-  DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
-  DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
-  // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
-  DevBuf enc_tab, dec_tab;
-  std::vector<std::unique_ptr<T5Layer>> enc, dec;
-  // workspace (every growth bumps `gen`, which invalidates captured decode graphs)
+// Per-call workspace of generate(): activations, decode caches, captured graphs and the decode
+// stream.  A model holds MAX_SLOTS of them so independent generate calls (two batches of a
+// serving loop) can be in flight on the device at once, sharing the weights.
+struct T5Work {
+  ~T5Work();
   DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, unfinished, cur_tok;
   DevBuf enc_in, mask_in, part_val, part_idx, tok_buf;
-  uint64_t gen = 0;
+  uint64_t gen = 0;  // bumped by every buffer growth: invalidates captured graphs
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {
     hipGraphExec_t exec;
@@ -93,18 +87,35 @@ struct T5Model : mpr_model {
   std::map<GraphKey, GraphEnt> graphs;
   hipStream_t dec_stream = nullptr;  // not owned
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+};
 
+struct T5Model : mpr_model {
+  static constexpr int MAX_SLOTS = 4;
+  T5Model() : mpr_model(T5) { use_slot(0); }
+  int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
+  int inner = 0, lut_radius = 0;
+  DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
+  DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
+  // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
+  DevBuf enc_tab, dec_tab;
+  std::vector<std::unique_ptr<T5Layer>> enc, dec;
+  std::vector<std::unique_ptr<T5Work>> work;
+  T5Work* ws = nullptr;  // workspace of the call being enqueued
+
+  // encode / logits / embed use workspace slot 0; generate the given slot.
   int encode(const float* embeds, const float* mask, int B, int L, float* out, hipStream_t s);
   int generate(const float* embeds, const float* mask, int B, int L, int max_new, int start,
-               int eos, int pad, int32_t* out_tokens, hipStream_t s);
+               int eos, int pad, int32_t* out_tokens, hipStream_t s, int slot = 0);
   int logits_tf(const float* embeds, const float* mask, int B, int L, const int32_t* dec_in,
                 int T, float* logits_out, hipStream_t s);
   int embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
             hipStream_t s);
-  // Stream for the greedy decode loop of generate() (null: the caller's stream).
-  int set_decode_stream(hipStream_t ds);
+  // Stream for the greedy decode loop of generate() in a slot (null: the caller's stream).
+  int set_decode_stream(int slot, hipStream_t ds);
+  int use_slot(int slot);
 
  private:
+  using GraphKey = T5Work::GraphKey;
   int grow(DevBuf& b, size_t bytes);
   int cross_kv_project(int B, int L, hipStream_t s);
   int encode_body(int B, int L, int max_new, int start, hipStream_t s);

@@ -32,7 +32,7 @@ bool graphs_enabled() {
 }
 }  // namespace
 
-T5Model::~T5Model() {
+T5Work::~T5Work() {
   for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
   if (cap_stream) (void)hipStreamDestroy(cap_stream);
   if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -42,7 +42,15 @@ T5Model::~T5Model() {
 int T5Model::grow(DevBuf& b, size_t bytes) {
   void* before = b.ptr;
   MPR_TRY(b.ensure(bytes));
-  if (b.ptr != before) ++gen;
+  if (b.ptr != before) ++ws->gen;
+  return MPR_OK;
+}
+
+int T5Model::use_slot(int slot) {
+  MPR_REQUIRE(slot >= 0 && slot < MAX_SLOTS, "t5: workspace slot %d outside [0, %d)", slot,
+              MAX_SLOTS);
+  while ((int)work.size() <= slot) work.push_back(std::make_unique<T5Work>());
+  ws = work[slot].get();
   return MPR_OK;
 }
 
@@ -58,16 +66,16 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
               lut_radius);
   if (B == 0) return MPR_OK;
   const int M = B * L;
-  MPR_TRY(grow(x, (size_t)M * d * 4));
-  MPR_TRY(grow(h, (size_t)M * d * 4));
-  MPR_TRY(grow(qkv, (size_t)M * 3 * inner * 4));
-  MPR_TRY(grow(ao, (size_t)M * inner * 4));
-  MPR_TRY(grow(ff, (size_t)M * dff * 4));
-  float* xp = x.as<float>();
-  float* hp = h.as<float>();
-  float* qp = qkv.as<float>();
-  float* ap = ao.as<float>();
-  float* fp = ff.as<float>();
+  MPR_TRY(grow(ws->x, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->h, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->qkv, (size_t)M * 3 * inner * 4));
+  MPR_TRY(grow(ws->ao, (size_t)M * inner * 4));
+  MPR_TRY(grow(ws->ff, (size_t)M * dff * 4));
+  float* xp = ws->x.as<float>();
+  float* hp = ws->h.as<float>();
+  float* qp = ws->qkv.as<float>();
+  float* ap = ws->ao.as<float>();
+  float* fp = ws->ff.as<float>();
   MPR_HIP(hipMemcpyAsync(xp, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
   for (auto& lp : enc) {
     const T5Layer& ly = *lp;
@@ -107,8 +115,8 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
 int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
   const int M = B * L, N = Ld * 2 * inner;
   GemmArgs g;
-  g.A = enc_out.as<float>(); g.lda = d; g.W = cross_kv_w.as<float>(); g.ldw = d;
-  g.C = cross_kv.as<float>(); g.ldc = N; g.M = M; g.N = N; g.K = d;
+  g.A = ws->enc_out.as<float>(); g.lda = d; g.W = cross_kv_w.as<float>(); g.ldw = d;
+  g.C = ws->cross_kv.as<float>(); g.ldc = N; g.M = M; g.N = N; g.K = d;
   return gemm(g, s);
 }
 
@@ -119,14 +127,14 @@ int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
 // latency-bound decode chain, mpr_t5_set_decode_stream).
 int T5Model::encode_body(int B, int L, int max_new, int start, hipStream_t s) {
   const int T1 = max_new + 1;
-  const float* maskp = mask_in.as<float>();
-  MPR_TRY(encode(enc_in.as<float>(), maskp, B, L, enc_out.as<float>(), s));
+  const float* maskp = ws->mask_in.as<float>();
+  MPR_TRY(encode(ws->enc_in.as<float>(), maskp, B, L, ws->enc_out.as<float>(), s));
   MPR_TRY(cross_kv_project(B, L, s));
-  MPR_TRY(fill_i32(unfinished.as<int32_t>(), 1, B, s));
-  MPR_TRY(fill_i32(cur_tok.as<int32_t>(), start, B, s));
-  MPR_TRY(fill_i32(tok_buf.as<int32_t>(), start, (int64_t)B * T1, s));  // column 0 = start
-  MPR_TRY(embed_gather(shared.as<float>(), cur_tok.as<int32_t>(), 1, B, 1, d, nullptr,
-                       dx.as<float>(), d, 0, s));
+  MPR_TRY(fill_i32(ws->unfinished.as<int32_t>(), 1, B, s));
+  MPR_TRY(fill_i32(ws->cur_tok.as<int32_t>(), start, B, s));
+  MPR_TRY(fill_i32(ws->tok_buf.as<int32_t>(), start, (int64_t)B * T1, s));  // column 0 = start
+  MPR_TRY(embed_gather(shared.as<float>(), ws->cur_tok.as<int32_t>(), 1, B, 1, d, nullptr,
+                       ws->dx.as<float>(), d, 0, s));
   return MPR_OK;
 }
 
@@ -134,21 +142,21 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
   const int nparts = (int)cdiv(V, 16);
-  const float* maskp = mask_in.as<float>();
-  float* xp = dx.as<float>();
-  float* qp = dq.as<float>();
-  float* ap = ao.as<float>();
-  float* fp = ff.as<float>();
-  int32_t* unf = unfinished.as<int32_t>();
-  int32_t* toks = tok_buf.as<int32_t>();
-  const float* ckv = cross_kv.as<float>();
+  const float* maskp = ws->mask_in.as<float>();
+  float* xp = ws->dx.as<float>();
+  float* qp = ws->dq.as<float>();
+  float* ap = ws->ao.as<float>();
+  float* fp = ws->ff.as<float>();
+  int32_t* unf = ws->unfinished.as<int32_t>();
+  int32_t* toks = ws->tok_buf.as<int32_t>();
+  const float* ckv = ws->cross_kv.as<float>();
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
 
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
   for (int t = 0; t < max_new; ++t) {
     for (int l = 0; l < Ld; ++l) {
       const T5Layer& ly = *dec[l];
-      float* cl = cache.as<float>() + l * cache_layer;
+      float* cl = ws->cache.as<float>() + l * cache_layer;
       SkinnyArgs sq;
       sq.g.A = xp; sq.g.lda = d;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
@@ -204,10 +212,10 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
     hd.g.A = xp; hd.g.lda = d; hd.g.C = nullptr;
     hd.g.M = B; hd.g.N = V; hd.g.K = d; hd.rms_w = dec_final.as<float>();
     hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
-    hd.amax_val = part_val.as<float>(); hd.amax_idx = part_idx.as<int32_t>();
+    hd.amax_val = ws->part_val.as<float>(); hd.amax_idx = ws->part_idx.as<int32_t>();
     hd.wpk = pk_lm_head.as<float>();
     MPR_TRY(gemm_skinny(hd, s));
-    MPR_TRY(greedy_step(part_val.as<float>(), part_idx.as<int32_t>(), nparts, B, unf, toks, T1,
+    MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), nparts, B, unf, toks, T1,
                         t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,
                         s));
   }
@@ -215,7 +223,9 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
 }
 
 int T5Model::generate(const float* embeds, const float* mask, int B, int L, int max_new,
-                      int start, int eos, int pad, int32_t* out_tokens, hipStream_t s) {
+                      int start, int eos, int pad, int32_t* out_tokens, hipStream_t s,
+                      int slot) {
+  MPR_TRY(use_slot(slot));
   MPR_REQUIRE(B >= 0 && B <= 16, "t5 generate: batch %d > 16 unsupported by the decode path", B);
   MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
   MPR_REQUIRE(max_new + 1 <= lut_radius, "t5 generate: max_new exceeds lut radius");
@@ -230,40 +240,40 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int M = B * L, nparts = (int)cdiv(V, 16);
   // Every buffer the body touches is sized before capture (no allocation inside a graph).
-  MPR_TRY(grow(enc_in, (size_t)M * d * 4));
-  MPR_TRY(grow(mask_in, (size_t)M * 4));
-  MPR_TRY(grow(enc_out, (size_t)M * d * 4));
-  MPR_TRY(grow(cross_kv, (size_t)M * Ld * 2 * inner * 4));
-  MPR_TRY(grow(x, (size_t)M * d * 4));
-  MPR_TRY(grow(h, (size_t)M * d * 4));
-  MPR_TRY(grow(qkv, (size_t)M * 3 * inner * 4));
-  MPR_TRY(grow(ao, (size_t)M * (inner > dff ? inner : dff) * 4));
-  MPR_TRY(grow(ff, (size_t)M * dff * 4));
-  MPR_TRY(grow(cache, (size_t)Ld * B * Tc * 3 * inner * 4));
-  MPR_TRY(grow(dx, (size_t)B * d * 4));
-  MPR_TRY(grow(dq, (size_t)B * inner * 4));
-  MPR_TRY(grow(part_val, (size_t)nparts * 16 * 4));
-  MPR_TRY(grow(part_idx, (size_t)nparts * 16 * 4));
-  MPR_TRY(grow(unfinished, (size_t)16 * 4));
-  MPR_TRY(grow(cur_tok, (size_t)16 * 4));
-  MPR_TRY(grow(tok_buf, (size_t)B * T1 * 4));
+  MPR_TRY(grow(ws->enc_in, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->mask_in, (size_t)M * 4));
+  MPR_TRY(grow(ws->enc_out, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->cross_kv, (size_t)M * Ld * 2 * inner * 4));
+  MPR_TRY(grow(ws->x, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->h, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->qkv, (size_t)M * 3 * inner * 4));
+  MPR_TRY(grow(ws->ao, (size_t)M * (inner > dff ? inner : dff) * 4));
+  MPR_TRY(grow(ws->ff, (size_t)M * dff * 4));
+  MPR_TRY(grow(ws->cache, (size_t)Ld * B * Tc * 3 * inner * 4));
+  MPR_TRY(grow(ws->dx, (size_t)B * d * 4));
+  MPR_TRY(grow(ws->dq, (size_t)B * inner * 4));
+  MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * 4));
+  MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * 4));
+  MPR_TRY(grow(ws->unfinished, (size_t)16 * 4));
+  MPR_TRY(grow(ws->cur_tok, (size_t)16 * 4));
+  MPR_TRY(grow(ws->tok_buf, (size_t)B * T1 * 4));
   if (L == Lsrc) {
-    MPR_HIP(hipMemcpyAsync(enc_in.ptr, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
-    MPR_HIP(hipMemcpyAsync(mask_in.ptr, mask, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
+    MPR_HIP(hipMemcpyAsync(ws->enc_in.ptr, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
+    MPR_HIP(hipMemcpyAsync(ws->mask_in.ptr, mask, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
   } else {
-    MPR_HIP(hipMemsetAsync(enc_in.ptr, 0, (size_t)M * d * 4, s));
-    MPR_HIP(hipMemsetAsync(mask_in.ptr, 0, (size_t)M * 4, s));
-    MPR_HIP(hipMemcpy2DAsync(enc_in.ptr, (size_t)L * d * 4, embeds, (size_t)Lsrc * d * 4,
+    MPR_HIP(hipMemsetAsync(ws->enc_in.ptr, 0, (size_t)M * d * 4, s));
+    MPR_HIP(hipMemsetAsync(ws->mask_in.ptr, 0, (size_t)M * 4, s));
+    MPR_HIP(hipMemcpy2DAsync(ws->enc_in.ptr, (size_t)L * d * 4, embeds, (size_t)Lsrc * d * 4,
                              (size_t)Lsrc * d * 4, B, hipMemcpyDeviceToDevice, s));
-    MPR_HIP(hipMemcpy2DAsync(mask_in.ptr, (size_t)L * 4, mask, (size_t)Lsrc * 4,
+    MPR_HIP(hipMemcpy2DAsync(ws->mask_in.ptr, (size_t)L * 4, mask, (size_t)Lsrc * 4,
                              (size_t)Lsrc * 4, B, hipMemcpyDeviceToDevice, s));
   }
-  hipStream_t ds = dec_stream ? dec_stream : s;
+  hipStream_t ds = ws->dec_stream ? ws->dec_stream : s;
   if (!graphs_enabled()) {
     MPR_TRY(encode_body(B, L, max_new, start, s));
     if (ds != s) {
-      MPR_HIP(hipEventRecord(ev_fork, s));
-      MPR_HIP(hipStreamWaitEvent(ds, ev_fork, 0));
+      MPR_HIP(hipEventRecord(ws->ev_fork, s));
+      MPR_HIP(hipStreamWaitEvent(ds, ws->ev_fork, 0));
     }
     MPR_TRY(decode_body(B, L, max_new, eos, pad, ds));
   } else {
@@ -274,33 +284,35 @@ int T5Model::generate(const float* embeds, const float* mask, int B, int L, int 
                       [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
     MPR_HIP(hipGraphLaunch(enc_exec, s));
     if (ds != s) {
-      MPR_HIP(hipEventRecord(ev_fork, s));
-      MPR_HIP(hipStreamWaitEvent(ds, ev_fork, 0));
+      MPR_HIP(hipEventRecord(ws->ev_fork, s));
+      MPR_HIP(hipStreamWaitEvent(ds, ws->ev_fork, 0));
     }
     MPR_HIP(hipGraphLaunch(dec_exec, ds));
   }
-  MPR_HIP(hipMemcpyAsync(out_tokens, tok_buf.ptr, (size_t)B * T1 * 4, hipMemcpyDeviceToDevice,
+  MPR_HIP(hipMemcpyAsync(out_tokens, ws->tok_buf.ptr, (size_t)B * T1 * 4, hipMemcpyDeviceToDevice,
                          ds));
   if (ds != s) {  // the caller's stream sees the tokens (and may reuse the buffers) after this
-    MPR_HIP(hipEventRecord(ev_join, ds));
-    MPR_HIP(hipStreamWaitEvent(s, ev_join, 0));
+    MPR_HIP(hipEventRecord(ws->ev_join, ds));
+    MPR_HIP(hipStreamWaitEvent(s, ws->ev_join, 0));
   }
   return MPR_OK;
 }
 
-int T5Model::set_decode_stream(hipStream_t ds) {
-  if (ds && !ev_fork) {
-    MPR_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-    MPR_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+int T5Model::set_decode_stream(int slot, hipStream_t ds) {
+  MPR_TRY(use_slot(slot));
+  if (ds && !ws->ev_fork) {
+    MPR_HIP(hipEventCreateWithFlags(&ws->ev_fork, hipEventDisableTiming));
+    MPR_HIP(hipEventCreateWithFlags(&ws->ev_join, hipEventDisableTiming));
   }
-  dec_stream = ds;
+  ws->dec_stream = ds;
   return MPR_OK;
 }
 
 template <class F>
 int T5Model::graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body) {
+  auto& graphs = ws->graphs;
   auto it = graphs.find(key);
-  if (it != graphs.end() && it->second.gen != gen) {
+  if (it != graphs.end() && it->second.gen != ws->gen) {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
     graphs.clear();
     it = graphs.end();
@@ -310,11 +322,12 @@ int T5Model::graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body) {
       for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
       graphs.clear();
     }
-    if (!cap_stream) MPR_HIP(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+    if (!ws->cap_stream)
+      MPR_HIP(hipStreamCreateWithFlags(&ws->cap_stream, hipStreamNonBlocking));
     hipGraph_t graph = nullptr;
-    MPR_HIP(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
-    const int rc = body(cap_stream);
-    const hipError_t ec = hipStreamEndCapture(cap_stream, &graph);
+    MPR_HIP(hipStreamBeginCapture(ws->cap_stream, hipStreamCaptureModeThreadLocal));
+    const int rc = body(ws->cap_stream);
+    const hipError_t ec = hipStreamEndCapture(ws->cap_stream, &graph);
     if (rc != MPR_OK) {
       if (graph) (void)hipGraphDestroy(graph);
       return rc;
@@ -324,7 +337,7 @@ int T5Model::graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body) {
     const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     MPR_HIP(ei);
-    it = graphs.emplace(key, GraphEnt{exec, gen}).first;
+    it = graphs.emplace(key, T5Work::GraphEnt{exec, ws->gen}).first;
   }
   *out = it->second.exec;
   return MPR_OK;
@@ -334,24 +347,24 @@ int T5Model::logits_tf(const float* embeds, const float* mask, int B, int L,
                        const int32_t* dec_in, int T, float* logits_out, hipStream_t s) {
   MPR_REQUIRE(T >= 1 && T <= lut_radius, "t5 logits: T=%d", T);
   if (B == 0) return MPR_OK;
-  MPR_TRY(grow(enc_out, (size_t)B * L * d * 4));
-  MPR_TRY(grow(cross_kv, (size_t)B * L * Ld * 2 * inner * 4));
-  MPR_TRY(encode(embeds, mask, B, L, enc_out.as<float>(), s));
+  MPR_TRY(grow(ws->enc_out, (size_t)B * L * d * 4));
+  MPR_TRY(grow(ws->cross_kv, (size_t)B * L * Ld * 2 * inner * 4));
+  MPR_TRY(encode(embeds, mask, B, L, ws->enc_out.as<float>(), s));
   MPR_TRY(cross_kv_project(B, L, s));
   const int M = B * T;
-  MPR_TRY(grow(x, (size_t)M * d * 4));
-  MPR_TRY(grow(h, (size_t)M * d * 4));
-  MPR_TRY(grow(qkv, (size_t)M * 3 * inner * 4));
-  MPR_TRY(grow(ao, (size_t)M * inner * 4));
-  MPR_TRY(grow(dq, (size_t)M * inner * 4));
-  MPR_TRY(grow(ff, (size_t)M * dff * 4));
-  float* xp = x.as<float>();
-  float* hp = h.as<float>();
-  float* qp = qkv.as<float>();
-  float* ap = ao.as<float>();
-  float* cqp = dq.as<float>();
-  float* fp = ff.as<float>();
-  const float* ckv = cross_kv.as<float>();
+  MPR_TRY(grow(ws->x, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->h, (size_t)M * d * 4));
+  MPR_TRY(grow(ws->qkv, (size_t)M * 3 * inner * 4));
+  MPR_TRY(grow(ws->ao, (size_t)M * inner * 4));
+  MPR_TRY(grow(ws->dq, (size_t)M * inner * 4));
+  MPR_TRY(grow(ws->ff, (size_t)M * dff * 4));
+  float* xp = ws->x.as<float>();
+  float* hp = ws->h.as<float>();
+  float* qp = ws->qkv.as<float>();
+  float* ap = ws->ao.as<float>();
+  float* cqp = ws->dq.as<float>();
+  float* fp = ws->ff.as<float>();
+  const float* ckv = ws->cross_kv.as<float>();
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
   MPR_TRY(embed_gather(shared.as<float>(), dec_in, T, B, T, d, nullptr, xp, (int64_t)T * d, 0, s));
   for (int l = 0; l < Ld; ++l) {

@@ -302,36 +302,43 @@ class T5VisionModel(nn.Module):
                                           do_sample=False, max_new_tokens=self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
-    def predict_many(self, batches):
-        """predict() over an iterable of batches as a two-deep pipeline (a serving loop): while
-        batch i's T5 generate runs on the device (its decode steps occupy few CUs), batch i+1's
-        image towers, question tower and index scan run beside it on other streams and the host
-        builds batch i+1's prompts.  Yields each batch's answers in order; every batch gets
-        exactly the work and the result predict() gives it."""
-        if not hasattr(self, "_s_main"):
-            self._s_main = torch.cuda.Stream(self.device)
+    def predict_many(self, batches, decodes_in_flight: int = 2):
+        """predict() over an iterable of batches as a serving pipeline: up to
+        ``decodes_in_flight`` batches decode at once (each on its own stream and T5 workspace
+        slot; a greedy decode is a chain of small latency-bound launches that leaves most of the
+        chip idle), while the next batch's image towers, question tower and index scan run beside
+        them and the host builds its prompts.  Yields each batch's answers in order; every batch
+        gets exactly the work and the result predict() gives it."""
+        from collections import deque
+        depth = max(1, min(int(decodes_in_flight), 4))
         if not hasattr(self, "_s_prep"):
             self._s_prep = torch.cuda.Stream(self.device)
-        pending = None
-        for batch in batches:
+        if not hasattr(self, "_s_gen"):
+            self._s_gen = []
+        while len(self._s_gen) < depth:
+            self._s_gen.append(torch.cuda.Stream(self.device))
+        pending = deque()
+        for i, batch in enumerate(batches):
             self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self._s_prep):
                 combined, mask, _ = self.prepare_input(batch)
-            self._s_main.wait_stream(self._s_prep)
-            with torch.cuda.stream(self._s_main):
-                combined.record_stream(self._s_main)
-                mask.record_stream(self._s_main)
+            slot = i % depth
+            sg = self._s_gen[slot]
+            sg.wait_stream(self._s_prep)
+            with torch.cuda.stream(sg):
+                combined.record_stream(sg)
+                mask.record_stream(sg)
                 t5 = self._device_t5()
-                toks = t5.generate_padded(combined, mask, self.max_new_tokens)
+                toks = t5.generate_padded(combined, mask, self.max_new_tokens, slot=slot)
                 host = torch.empty(toks.shape, dtype=toks.dtype, pin_memory=True)
                 host.copy_(toks, non_blocking=True)
                 done = torch.cuda.Event()
-                done.record(self._s_main)
-            if pending is not None:
-                yield self._finish(*pending)
-            pending = (host, done)
-        if pending is not None:
-            yield self._finish(*pending)
+                done.record(sg)
+            pending.append((host, done))
+            if len(pending) > depth:  # batch i - depth is (nearly) done by now
+                yield self._finish(*pending.popleft())
+        while pending:
+            yield self._finish(*pending.popleft())
 
     def _finish(self, host_tokens, done):
         done.synchronize()  # this batch's tokens only; the next batch keeps running

@@ -107,13 +107,15 @@ class DeviceT5:
     def _stream(self):
         return _lib.stream_ptr(self.device)
 
-    def set_decode_stream(self, stream=None):
+    def set_decode_stream(self, stream=None, slot: int = 0):
         """Run the greedy decode loop of later generate calls on ``stream`` (a torch stream,
         e.g. ``_lib.role_stream(device, "decode")``; None = the caller's stream).  Ordering is
         unchanged: the loop waits for the encoder on the caller's stream and the caller's stream
         waits for the tokens."""
-        self._dec_stream = stream  # keep the stream object alive while the library uses it
-        _lib.call("mpr_t5_set_decode_stream", self._h,
+        if not hasattr(self, "_dec_streams"):
+            self._dec_streams = {}
+        self._dec_streams[slot] = stream  # keep the stream alive while the library uses it
+        _lib.call("mpr_t5_set_decode_stream", self._h, int(slot),
                   _lib.c_void_p(stream.cuda_stream if stream is not None else 0))
 
     def embed(self, ids: torch.Tensor, out: torch.Tensor, row0: int = 0) -> torch.Tensor:
@@ -143,13 +145,15 @@ class DeviceT5:
         return out
 
     def generate_padded(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
-                        eos_token_id=1, pad_token_id=0) -> torch.Tensor:
-        """All max_new_tokens greedy steps on device: int32 [B, 1+max_new] (no host sync)."""
+                        eos_token_id=1, pad_token_id=0, slot: int = 0) -> torch.Tensor:
+        """All max_new_tokens greedy steps on device: int32 [B, 1+max_new] (no host sync).
+        ``slot`` picks one of the model's independent workspaces (two batches of a serving
+        loop decode concurrently on different slots and streams)."""
         embeds, mask = self._inputs(embeds, mask)
         B, L, _ = embeds.shape
         out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
-        _lib.call("mpr_t5_generate", self._h, _lib.ptr(embeds), _lib.ptr(mask), B, L,
-                  int(max_new_tokens), int(decoder_start_token_id), int(eos_token_id),
+        _lib.call("mpr_t5_generate_slot", self._h, int(slot), _lib.ptr(embeds), _lib.ptr(mask),
+                  B, L, int(max_new_tokens), int(decoder_start_token_id), int(eos_token_id),
                   int(pad_token_id), _lib.ptr(out), self._stream())
         return out
 

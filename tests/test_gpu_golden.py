@@ -124,7 +124,7 @@ def test_g2_pipeline_product(device):
 
 
 def test_g2_predict_many_matches_predict(device):
-    """The two-deep serving pipeline returns, per batch, exactly predict()'s answers (batches
+    """The serving pipeline (1-3 decodes in flight) returns, per batch, exactly predict()'s answers (batches
     of different prompt lengths and images in flight together; the first is the golden one)."""
     from multimodalpromptretrieval_amd.dataset import VQARetrieval
     from multimodalpromptretrieval_amd.model import T5VisionModel
@@ -147,6 +147,8 @@ def test_g2_predict_many_matches_predict(device):
     want = [model.predict(b) for b in batches]
     assert want[0] == j["predictions"]
     assert list(model.predict_many(batches)) == want
+    for depth in (1, 3):  # decodes in flight on separate workspace slots
+        assert list(model.predict_many(batches, depth)) == want
     assert list(model.predict_many(iter(batches[:1]))) == want[:1]
     assert list(model.predict_many([])) == []
 
