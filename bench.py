@@ -14,9 +14,11 @@ scaling); the retrieval index is row-sharded over the ranks and every batch exch
 (all_gather) and per-shard top-k candidates (all_to_all) over RCCL.
 
 Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel (the tiled f32-MFMA
-GEMM), timed with hipEvents around each of its launches on its own stream during a probed pass
-over the same steps; ``cpu_baseline`` is the CPU oracle pipeline (torch-CPU fp32, KV-cached
-greedy decode) on a bounded sample of the same workload.
+GEMM): the launches of a pass over the same steps are recorded and replayed back to back with
+hipEvents around each launch (its ``in_serving_loop`` entry times the same launches inside the
+pipeline, sharing the chip with the decodes); ``traffic`` comes from the committed rocprofv3
+PMC summary of this command (profiles/*pmc_gemm.json).  ``cpu_baseline`` is the CPU oracle
+pipeline (torch-CPU fp32, KV-cached greedy decode) on a bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -51,6 +53,19 @@ WORDS = ("what is the organ shown in this image does picture contain lung liver 
 TASKS = ["organ", "modality", "position", "abnormality", "plane", "quantity", "color", "size"]
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 HBM_PEAK_GBS = 8000.0
+
+
+def _pmc_traffic():
+    """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary of this command
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 half-count of wide streaming reads) +
+    WRITE_SIZE, separate --pmc passes, windowed to the replay).  (bytes, source) or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gemm.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        j = json.load(f)
+    return j.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
 def make_batches(n_batches: int, B: int, device, seed: int):
@@ -186,22 +201,46 @@ def main():
 
     roofline = None
     if not args.no_probe:
-        # Probed pass over the same steps: hipEvents around every tiled-GEMM launch.
-        _lib.probe_enable(1)
-        torch.cuda.synchronize()
+        # (1) The dominant kernel on its own: every tiled-GEMM launch of `steps` pipelined steps
+        # is recorded, then re-launched back to back on this stream with hipEvents around each
+        # launch (mpr_probe_replay; two marker kernels bracket the replay so a rocprofv3 trace
+        # of this same command can be windowed to it, tools/prof_summary.py --replay).
+        _lib.probe_clear()
+        _lib.probe_enable(3)
         run(args.steps)
         torch.cuda.synchronize()
-        ms, launches, flops, _ = _lib.probe_read()
+        _lib.probe_enable(0)
+        ms, launches, flops, abytes = _lib.probe_replay(1, device)
+        _lib.probe_clear()
+        # (2) The same kernel inside the serving loop: hipEvents around each launch on its own
+        # stream while the decodes of earlier batches share the chip.
+        _lib.probe_enable(1)
+        run(args.steps)
+        torch.cuda.synchronize()
+        ms_live, launches_live, flops_live, _ = _lib.probe_read()
         _lib.probe_enable(0)
         if launches:
             ach = flops / (ms * 1e-3) / 1e12
+            traffic, traffic_src = _pmc_traffic()
             roofline = {"bound": "mfma", "achieved": round(ach, 2),
                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                        "kernel": "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)",
-                        "launches_per_step": launches // args.steps,
+                        "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                        "traffic": traffic,
+                        "kernel": "gemm_f32_kernel (v_mfma_f32_32x32x2_f32 / 16x16x4)",
+                        "measured": "replay of one pass's launches back to back, hipEvents "
+                                    "around each launch",
+                        "launches_per_step": round(launches / args.steps, 1),
+                        "avg_launch_us": round(ms * 1e3 / launches, 2),
                         "kernel_ms_per_step": round(ms / args.steps, 3),
-                        "algorithmic_gflop_per_launch": round(flops / launches / 1e9, 4)}
+                        "algorithmic_gflop_per_launch": round(flops / launches / 1e9, 4),
+                        "algorithmic_mb_per_launch": round(abytes / launches / 1e6, 3),
+                        "traffic_source": traffic_src}
+            if launches_live:
+                ach_live = flops_live / (ms_live * 1e-3) / 1e12
+                roofline["in_serving_loop"] = {
+                    "achieved": round(ach_live, 2),
+                    "frac": round(ach_live / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "avg_launch_us": round(ms_live * 1e3 / launches_live, 2)}
         barrier()
 
     cpu = None

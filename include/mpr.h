@@ -167,9 +167,17 @@ int mpr_model_destroy(mpr_model* m);
  * kind 1 = tiled f32-MFMA GEMM, 2 = skinny (decode) GEMM, 0 = off.  While enabled, every launch
  * of that kernel (outside graph capture) is bracketed by hipEvents on its own stream.
  * mpr_probe_read waits for the recorded events and returns the summed kernel time (ms), the
- * launch count and the summed algorithmic FLOPs and bytes of those launches, then resets. */
+ * launch count and the summed algorithmic FLOPs and bytes of those launches, then resets.
+ * kind 3 = record: every tiled-GEMM launch (outside capture) is kept; mpr_probe_replay launches
+ * the recorded problems again `iters` times back to back on `stream` (outputs to a scratch
+ * buffer), hipEvents around each launch, bracketed by two launches of probe_marker_kernel (so a
+ * rocprofv3 kernel trace of the same process can be windowed to the replay), and returns the
+ * same totals; mpr_probe_clear drops the recording. */
 int mpr_probe_enable(int32_t kind);
 int mpr_probe_read(double* total_ms, int64_t* launches, double* flops, double* bytes);
+int mpr_probe_replay(int32_t iters, void* stream, double* total_ms, int64_t* launches,
+                     double* flops, double* bytes);
+int mpr_probe_clear(void);
 
 #ifdef __cplusplus
 }

@@ -64,6 +64,9 @@ SIGNATURES = [
     ("mpr_probe_enable", c_int32, [c_int32]),
     ("mpr_probe_read", c_int32, [POINTER(ctypes.c_double), I64P, POINTER(ctypes.c_double),
                                  POINTER(ctypes.c_double)]),
+    ("mpr_probe_replay", c_int32, [c_int32, c_void_p, POINTER(ctypes.c_double), I64P,
+                                   POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
+    ("mpr_probe_clear", c_int32, []),
 ]
 
 
@@ -76,6 +79,19 @@ def probe_read():
     ms, n, fl, by = ctypes.c_double(), c_int64(), ctypes.c_double(), ctypes.c_double()
     call("mpr_probe_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl), ctypes.byref(by))
     return ms.value, n.value, fl.value, by.value
+
+def probe_replay(iters: int = 1, device=None):
+    """Replay the GEMM launches recorded under probe_enable(3) back to back on the current
+    stream: (kernel ms, launches, algorithmic flops, algorithmic bytes)."""
+    ms, n, fl, by = ctypes.c_double(), c_int64(), ctypes.c_double(), ctypes.c_double()
+    call("mpr_probe_replay", int(iters), stream_ptr(device), ctypes.byref(ms), ctypes.byref(n),
+         ctypes.byref(fl), ctypes.byref(by))
+    return ms.value, n.value, fl.value, by.value
+
+
+def probe_clear() -> None:
+    call("mpr_probe_clear")
+
 
 _lib = None
 

@@ -429,12 +429,23 @@ int mpr_model_destroy(mpr_model* m) {
 }
 
 int mpr_probe_enable(int32_t kind) {
-  MPR_REQUIRE(kind >= 0 && kind <= 2, "probe: kind %d", kind);
+  MPR_REQUIRE(kind >= 0 && kind <= 3, "probe: kind %d", kind);
   return probe_enable(kind);
 }
 
 int mpr_probe_read(double* ms, int64_t* launches, double* flops, double* bytes) {
   return guarded([&]() -> int { return probe_read(ms, launches, flops, bytes); });
+}
+
+int mpr_probe_replay(int32_t iters, void* stream, double* ms, int64_t* launches, double* flops,
+                     double* bytes) {
+  return guarded([&]() -> int {
+    return probe_replay(iters, S(stream), ms, launches, flops, bytes);
+  });
+}
+
+int mpr_probe_clear(void) {
+  return guarded([&]() -> int { return probe_clear(); });
 }
 
 }  // extern "C"

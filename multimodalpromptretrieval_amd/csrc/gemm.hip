@@ -493,6 +493,9 @@ double gemm_bytes(const GemmArgs& a) {
                 (a.bias ? a.N : 0));
 }
 
+// PROBE_RECORD: every tiled-GEMM launch group (outside capture) is kept for probe_replay().
+std::vector<GemmGroup> g_recorded;
+
 template <class F>
 int probed(int kind, double flops, double bytes, hipStream_t s, F&& launch) {
   if (!probing(kind, s)) return launch();
@@ -509,6 +512,73 @@ int probed(int kind, double flops, double bytes, hipStream_t s, F&& launch) {
 
 int probe_enable(int kind) {
   g_probe_kind = kind;
+  return MPR_OK;
+}
+
+__global__ void probe_marker_kernel(int tag, int* sink) {
+  if (tag < 0) sink[0] = tag;  // never true: the launch itself is the marker
+}
+
+int probe_replay(int iters, hipStream_t s, double* ms, int64_t* launches, double* flops,
+                 double* bytes) {
+  MPR_REQUIRE(iters >= 1, "probe_replay: iters=%d", iters);
+  // Outputs go to a scratch buffer (the recorded C pointers may be tensors the caller freed);
+  // inputs are read where they were (library workspaces, still mapped).
+  size_t cmax = 0;
+  for (const GemmGroup& g : g_recorded)
+    for (int i = 0; i < g.n; ++i) {
+      const GemmArgs& a = g.g[i];
+      const int64_t r = a.M - 1;
+      const int64_t last = a.c_rpb ? (r / a.c_rpb) * a.c_bs + (r % a.c_rpb) * a.ldc + a.N
+                                   : r * a.ldc + a.N;
+      cmax = std::max(cmax, (size_t)last * sizeof(float));
+    }
+  static DevBuf scratch;
+  MPR_TRY(scratch.ensure(std::max<size_t>(cmax, 256)));
+  std::vector<ProbeRec> recs;
+  hipLaunchKernelGGL(probe_marker_kernel, dim3(1), dim3(64), 0, s, 1, scratch.as<int>());
+  for (int it = 0; it < iters; ++it)
+    for (const GemmGroup& g0 : g_recorded) {
+      GemmGroup g = g0;
+      double f = 0, by = 0;
+      for (int i = 0; i < g.n; ++i) {
+        g.g[i].C = scratch.as<float>();
+        if (g.g[i].R == g0.g[i].C) g.g[i].R = scratch.as<float>();  // in-place residual
+        f += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K;
+        by += gemm_bytes(g.g[i]);
+      }
+      ProbeRec r{pool_event(), pool_event(), f, by};
+      MPR_REQUIRE(r.a && r.b, "probe_replay: no events");
+      MPR_HIP(hipEventRecord(r.a, s));
+      const int saved = g_probe_kind;
+      g_probe_kind = PROBE_OFF;
+      const int rc = gemm_group(g, s);
+      g_probe_kind = saved;
+      MPR_TRY(rc);
+      MPR_HIP(hipEventRecord(r.b, s));
+      recs.push_back(r);
+    }
+  hipLaunchKernelGGL(probe_marker_kernel, dim3(1), dim3(64), 0, s, 2, scratch.as<int>());
+  double t = 0, f = 0, by = 0;
+  for (auto& r : recs) {
+    float e = 0.f;
+    MPR_HIP(hipEventSynchronize(r.b));
+    MPR_HIP(hipEventElapsedTime(&e, r.a, r.b));
+    t += e;
+    f += r.flops;
+    by += r.bytes;
+    g_pool.push_back(r.a);
+    g_pool.push_back(r.b);
+  }
+  if (ms) *ms = t;
+  if (launches) *launches = (int64_t)recs.size();
+  if (flops) *flops = f;
+  if (bytes) *bytes = by;
+  return MPR_OK;
+}
+
+int probe_clear() {
+  g_recorded.clear();
   return MPR_OK;
 }
 
@@ -558,6 +628,11 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // 64x64 blocks and split-K across blocks were slower at every shape of this path.  The
   // choice depends on the largest single problem, not on the group: a problem gets the same
   // tile (the same summation order, bit-identical results) alone or grouped.
+  if (g_probe_kind == PROBE_RECORD) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone)
+      g_recorded.push_back(g);
+  }
   return probed(PROBE_GEMM, flops, bytes, s, [&]() {
     if (tiles64 >= 384) return launch_gemm_group<64, 64, 1, 1, 32, 2, 1>(g, s);
     return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);

@@ -61,9 +61,14 @@ struct SkinnyArgs {
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
 // Kernel probe (bench roofline): hipEvent pairs around every launch of one GEMM kind.
-enum ProbeKind : int { PROBE_OFF = 0, PROBE_GEMM = 1, PROBE_SKINNY = 2 };
+enum ProbeKind : int { PROBE_OFF = 0, PROBE_GEMM = 1, PROBE_SKINNY = 2, PROBE_RECORD = 3 };
 int probe_enable(int kind);
 int probe_read(double* ms, int64_t* launches, double* flops, double* bytes);
+// Re-launch the tiled-GEMM groups recorded under PROBE_RECORD back to back on one stream
+// (outputs to a scratch buffer), hipEvents around each; marker kernels bracket the replay.
+int probe_replay(int iters, hipStream_t s, double* ms, int64_t* launches, double* flops,
+                 double* bytes);
+int probe_clear();
 
 // LayerNorm over rows of width D (eps, affine), out may alias x.  ld in floats.
 int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, const float* beta,

@@ -1,6 +1,7 @@
 #!/bin/bash
-# GPU-box round: tests -> smoke -> bench -> rocprofv3 kernel stats.  Each GPU step has its own
-# time limit; anything but a clean exit (or plain test failures, rc 1) ends the script.
+# GPU-box round: tests -> smoke -> bench -> rocprofv3 kernel stats -> two PMC passes (GEMM HBM
+# traffic).  Each GPU step has its own time limit; anything but a clean exit (or plain test
+# failures, rc 1) ends the script.
 # usage: bash tools/gpu_round.sh <tag> [steps]
 TAG=${1:-r}
 STEPS=${2:-10}
@@ -18,17 +19,24 @@ ok_or_stop() {  # $1 = rc, $2 = step name, $3 = allow-rc-1
 }
 
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -m pytest tests -q -m gpu -rf > "$OUT/pytest.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu -rf --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
   ok_or_stop $? pytest 1
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+  ok_or_stop $? smoke 0
 fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
-ok_or_stop $? smoke 0
 timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
 ok_or_stop $? bench 0
 if [ -z "$SKIP_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-    -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe \
+    -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline \
     > "$OUT/prof.log" 2>&1
   ok_or_stop $? rocprof 0
+  python tools/prof_summary.py --replay "$OUT/prof/run_kernel_trace.csv" "$OUT/replay_window.json" >> "$OUT/prof.log" 2>&1
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_f32_kernel|probe_marker_kernel" \
+      -d "$OUT/pmc_$c" -o run --output-format csv \
+      -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1
+    ok_or_stop $? pmc_$c 0
+  done
 fi
 echo done >> "$OUT/steps.log"
