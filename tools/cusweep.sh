@@ -1,8 +1,9 @@
-# Serving-pipeline sweep: decodes in flight (bench c2, no cpu baseline / probe).
-# Measured (4 HW queues, the box default): 1 -> 1702, 2 -> 2105/2116, 3 -> 1216-1455 QA pairs/s;
-# GPU_MAX_HW_QUEUES 8 / 16 with 2 in flight: 1651 / 1658.
+# Contention sweep: LDS residency of encoder GEMM blocks vs decode GEMV blocks (bench c2).
 set -e
 mkdir -p gpurun_out/cus
-for n in 1 2 3; do
-  timeout -k 10 200 python bench.py --steps 12 --warmup 4 --inflight $n --no-cpu-baseline --no-probe > gpurun_out/cus/bench_if$n.json 2> gpurun_out/cus/bench_if$n.err
-done
+run() { timeout -k 10 200 env "$@" python bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-probe > gpurun_out/cus/bench_$TAG.json 2> gpurun_out/cus/bench_$TAG.err; }
+TAG=base run X=0
+TAG=sl run MPR_SKINNY_SMALL_LDS=1
+TAG=cb3 run MPR_GEMM_CU_BLOCKS=3
+TAG=cb3sl run MPR_GEMM_CU_BLOCKS=3 MPR_SKINNY_SMALL_LDS=1
+TAG=cb2sl run MPR_GEMM_CU_BLOCKS=2 MPR_SKINNY_SMALL_LDS=1
