@@ -68,6 +68,56 @@ def _pmc_traffic():
     return j.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+C5 = dict(N=1 << 20, D=512, B=256, k=5)
+
+
+def c5_scan(world, rank, device, group, iters=20):
+    """Config C5's retrieval core: a 1,048,576 x 512 fp32 index row-sharded
+    over the ranks (rows/W each, built on device from chunk-seeded streams, so the global index
+    is the same at every W), 256 queries in total (256/W per rank), k = 5.  One search = the
+    ShardedIndex exchange: all_gather of the query blocks, the local large-batch scan
+    (scan_mm_kernel), all_to_all of the per-shard top-k, merge.  Strong scaling (fixed index and
+    query set); the ids checksum is identical at every W."""
+    from multimodalpromptretrieval_amd.distributed import ShardedIndex, shard_bounds
+    from multimodalpromptretrieval_amd.index import DeviceIndex
+    n, d, B, k = C5["N"], C5["D"], C5["B"], C5["k"]
+    lo, hi = shard_bounds(n, world, rank)
+    rows = syn.index_rows_device(7, lo, hi, d, device)
+    gq = torch.Generator(device=device).manual_seed(8)
+    q_all = torch.randn((B, d), device=device, generator=gq) * 0.3
+    bq = B // world
+    q = q_all[rank * bq:(rank + 1) * bq].contiguous()
+    if world > 1:
+        ix = ShardedIndex(rows, device, group=group, rows_are_local=True, row_offset=lo)
+    else:
+        ix = DeviceIndex(rows, device)
+    del rows
+    for _ in range(3):
+        ix.search(q, k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist_k, ids = ix.search(q, k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    chk = torch.tensor([float(ids.sum())], device=device, dtype=torch.float64)
+    if world > 1:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        dist.all_reduce(chk)
+    ms = el / iters * 1e3
+    tf = 2.0 * n * d * B / (ms * 1e-3) / 1e12
+    del ix
+    torch.cuda.empty_cache()
+    return {"workload": "C5: 1,048,576 x 512 fp32 index, 256 queries, k=5, rows/W per rank",
+            "ms_per_search": round(ms, 3), "queries_per_s": round(B / (ms * 1e-3), 1),
+            "scan_tflops_aggregate": round(tf, 2), "scaling": "strong",
+            "ids_checksum": int(chk.item())}
+
+
 def make_batches(n_batches: int, B: int, device, seed: int):
     rng = np.random.Generator(np.random.PCG64(seed))
     out = []
@@ -139,6 +189,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 sharded-scan line")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches decoding concurrently in the serving loop (predict_many)")
     args = ap.parse_args()
@@ -243,6 +294,11 @@ def main():
                     "avg_launch_us": round(ms_live * 1e3 / launches_live, 2)}
         barrier()
 
+    c5 = None
+    if not args.no_c5:
+        c5 = c5_scan(world, rank, device, group)
+        barrier()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, weights, batches, args.cpu_seconds)
@@ -267,6 +323,7 @@ def main():
                        else "single", "parallelism": f"dp{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "c5_scan": c5,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -18,8 +18,10 @@
 // Ordering contract (ids parity with the reference): keys are the reported values — L2 distance
 // sqrt(max(|q|^2 + |x|^2 - 2 q.x, 0)) (the cdist mm-path formula) or minus the cosine similarity —
 // sorted ascending, exact ties broken by the lowest row id (argsort(stable=True) semantics).
+#include <algorithm>
 #include <cfloat>
 #include <climits>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -27,6 +29,7 @@ namespace mpr {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int QG = 16;  // queries per group (MFMA N)
 constexpr float COS_EPS = 1e-8f;
@@ -190,6 +193,210 @@ __global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X,
       oi[t] = bidx == INT_MAX ? -1 : (int64_t)bidx + row_offset;
     }
   }
+}
+
+// ---- large-batch scan (b >= 64): the similarity GEMM with a top-k epilogue ------------------
+// At b = 256 the scan is MFMA-bound in fp32 (2 FLOP per index byte per query),
+// and the 16-query kernel above would stream the index once per query group.  Here a block owns
+// a 64-query tile (Q rows, L2-resident) and a strided set of 64-row index tiles; each k-step stages
+// a 64 x 32 slice of X and of Q through LDS (register prefetch SM_D tiles ahead, two LDS stages:
+// the tiled-GEMM pipeline of gemm.hip) into v_mfma_f32_32x32x2_f32 (4 waves, 2 x 2 of 32x32).
+// At the end of each row tile the accumulators become keys in registers (row norms are summed
+// from the same staged fragments) and enter per-lane sorted top-K lists; scores never reach HBM.
+// Blocks of one row-tile set are adjacent after an XCD-aware remap, so they share an XCD's L2
+// and the index is fetched from HBM about once.  Keys, order and ties as scan_kernel.
+constexpr int SM_B = 64, SM_BK = 32, SM_D = 2, SM_LDK = SM_BK + 4;
+constexpr int SM_STAGE = 2 * SM_B * SM_LDK;  // floats: X rows then Q rows
+
+template <int K>
+__global__ __launch_bounds__(256) void scan_mm_kernel(const float* __restrict__ X, int64_t n,
+                                                      int d, int64_t row_offset, int metric,
+                                                      const float* __restrict__ Q,
+                                                      const float* __restrict__ qnorm, int b,
+                                                      int nqt, int RB, float* cand_key,
+                                                      int64_t* cand_id) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * SM_STAGE];
+  constexpr int KQ = SM_BK / 4, LA = SM_B * KQ / 256;  // float4 per thread and operand: 2
+  int qt, rb;
+  {
+    const int total = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, slot = hw >> 3, q8 = total >> 3, r8 = total & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+    qt = t % nqt;
+    rb = t / nqt;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int64_t ntile = (n + SM_B - 1) / SM_B;
+  const int ntb = (int)((ntile - rb + RB - 1) / RB);  // row tiles of this block
+  const int KS = (d + SM_BK - 1) / SM_BK;
+  const int S = ntb * KS, Sr = (S + SM_D - 1) / SM_D * SM_D;
+  const int q0 = qt * SM_B;
+
+  f32x4 ra[SM_D][LA], rq[SM_D][LA];
+  bool oka[SM_D][LA], okq[SM_D][LA];
+  auto gload = [&](int j, int step) {
+    const int tt = step / KS, ks = step - tt * KS;
+    const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * SM_B;
+    const int k0 = ks * SM_BK;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + i * 256, r = idx / KQ, c = k0 + (idx % KQ) * 4;
+      const int64_t row = row0 + r;
+      oka[j][i] = row < n && c < d && tt < ntb;
+      ra[j][i] = *reinterpret_cast<const f32x4*>(X + (row < n ? row : n - 1) * (int64_t)d +
+                                                 min(c, d - 4));
+      const int q = q0 + r;
+      okq[j][i] = q < b && c < d;
+      rq[j][i] = *reinterpret_cast<const f32x4*>(Q + (int64_t)min(q, b - 1) * d + min(c, d - 4));
+    }
+  };
+  auto swrite = [&](int st, int j) {
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    float* base = smem + st * SM_STAGE;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + i * 256, r = idx / KQ, c4 = (idx % KQ) * 4;
+      *reinterpret_cast<f32x4*>(base + r * SM_LDK + c4) = oka[j][i] ? ra[j][i] : z;
+      *reinterpret_cast<f32x4*>(base + (SM_B + r) * SM_LDK + c4) = okq[j][i] ? rq[j][i] : z;
+    }
+  };
+  // fragments: lane (li, lh) holds row li's k = 16 lh .. 16 lh + 15 of the tile (as gemm.hip)
+  f32x4 fa[4], fb[4], na[4], nb[4];
+  auto sread = [&](int st, f32x4(&xa)[4], f32x4(&xb)[4]) {
+    const float* base = smem + st * SM_STAGE;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      xa[s4] = *reinterpret_cast<const f32x4*>(base + (wm * 32 + li) * SM_LDK + lh * 16 + s4 * 4);
+      xb[s4] = *reinterpret_cast<const f32x4*>(base + (SM_B + wn * 32 + li) * SM_LDK + lh * 16 +
+                                               s4 * 4);
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float ssq = 0.f;  // this lane's half of row (wm*32 + li)'s squared norm, current tile
+  const int jq = q0 + wn * 32 + li;  // this lane's query in the accumulator
+  const float qn = qnorm[min(jq, b - 1)];
+  float bk[K];
+  int bi[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    bk[t] = INFINITY;
+    bi[t] = INT_MAX;
+  }
+
+  gload(0, 0);
+  swrite(0, 0);
+  gload(0, 1);
+  swrite(1, 0);
+#pragma unroll
+  for (int j = 0; j < SM_D; ++j) gload(j, 2 + j);
+  __syncthreads();
+  sread(0, fa, fb);
+  for (int s0 = 0; s0 < Sr; s0 += SM_D) {
+#pragma unroll
+    for (int j = 0; j < SM_D; ++j) {
+      const int step = s0 + j, st = step & 1;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s4][c], fb[s4][c], acc, 0, 0, 0);
+          ssq += fa[s4][c] * fa[s4][c];
+        }
+      sread(st ^ 1, na, nb);
+      swrite(st, j);
+      gload(j, step + 2 + SM_D);
+      const int tt = step / KS;
+      if (step - tt * KS == KS - 1 && tt < ntb) {  // last k-step of a row tile: keys -> top-K
+        const float full = ssq + __shfl_xor(ssq, 32, 64);  // norm of row wm*32 + li
+        const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * SM_B + wm * 32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const float xn = __shfl(full, rr, 64);
+          const int64_t row = row0 + rr;
+          const float key = score_key(metric, acc[r], qn, xn);
+          if (row < n && key < bk[K - 1]) {
+            float ck = key;
+            int ci = (int)row;
+#pragma unroll
+            for (int t = 0; t < K; ++t) {
+              const bool sw = ck < bk[t];
+              const float tk = sw ? bk[t] : ck;
+              const int ti = sw ? bi[t] : ci;
+              bk[t] = sw ? ck : bk[t];
+              bi[t] = sw ? ci : bi[t];
+              ck = tk;
+              ci = ti;
+            }
+          }
+          acc[r] = 0.f;
+        }
+        ssq = 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        fa[s4] = na[s4];
+        fb[s4] = nb[s4];
+      }
+    }
+  }
+
+  // Block merge: per query 4 sorted lists (lh x wm) -> best K, written as this block's
+  // candidates (the stages are free: the loop ended on a barrier).
+  float* Lk = smem;                                         // [64 q][4][K]
+  int* Li = reinterpret_cast<int*>(smem + SM_B * 4 * K);    // [64 q][4][K]
+  {
+    const int ql = wn * 32 + li, list = wm * 2 + lh;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      Lk[(ql * 4 + list) * K + t] = bk[t];
+      Li[(ql * 4 + list) * K + t] = bi[t];
+    }
+  }
+  __syncthreads();
+  if (tid < SM_B && q0 + tid < b) {
+    const int ql = tid;
+    int head[4] = {0, 0, 0, 0};
+    float* ok = cand_key + ((int64_t)(q0 + ql) * RB + rb) * K;
+    int64_t* oi = cand_id + ((int64_t)(q0 + ql) * RB + rb) * K;
+    for (int t = 0; t < K; ++t) {
+      float best = INFINITY;
+      int bidx = INT_MAX, bs = 0;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        if (head[l] < K) {
+          const float kk = Lk[(ql * 4 + l) * K + head[l]];
+          const int ii = Li[(ql * 4 + l) * K + head[l]];
+          if (kk < best || (kk == best && ii < bidx)) {
+            best = kk;
+            bidx = ii;
+            bs = l;
+          }
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < 4; ++l) head[l] += (l == bs) ? 1 : 0;
+      ok[t] = best;
+      oi[t] = bidx == INT_MAX ? -1 : (int64_t)bidx + row_offset;
+    }
+  }
+}
+
+__global__ void qnorm_kernel(const float* Q, int b, int d, float* out) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= b) return;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) s += Q[(int64_t)q * d + c] * Q[(int64_t)q * d + c];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[q] = s;
 }
 
 // Final selection: per query, best k of n_cand (key, id) candidates.  Thread-local sorted lists
@@ -363,9 +570,33 @@ int merge_dispatch(const float* ck, const int64_t* ci, int b, int64_t n_cand, in
 
 }  // namespace
 
+// The large-batch path: b >= SM_MIN_B queries, k <= 16, d >= 64 (two k-steps per row tile).
+constexpr int SM_MIN_B = 64;
+bool use_scan_mm(int64_t n, int d, int b, int k) {
+  return b >= SM_MIN_B && k <= 16 && d >= 2 * SM_BK && d % 4 == 0 && n >= SM_B;
+}
+int scan_mm_rowblocks(int64_t n, int b) {
+  const int64_t ntile = (n + SM_B - 1) / SM_B;
+  const int nqt = (int)cdiv(b, SM_B);
+  const int64_t rb = std::max<int64_t>(1, 512 / nqt);  // ~2 blocks per CU
+  return (int)std::min(rb, ntile);
+}
+
+template <int K>
+int launch_scan_mm(const float* X, int64_t n, int d, int64_t row_offset, int metric,
+                   const float* Q, float* qn, int b, float* ck, int64_t* ci, hipStream_t s) {
+  const int nqt = (int)cdiv(b, SM_B), RB = scan_mm_rowblocks(n, b);
+  hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d, qn);
+  hipLaunchKernelGGL((scan_mm_kernel<K>), dim3((unsigned)(nqt * RB)), dim3(256), 0, s, X, n, d,
+                     row_offset, metric, Q, qn, b, nqt, RB, ck, ci);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
 size_t scan_topk_workspace(int64_t n, int b, int k) {
   const int K = list_cap(k);
-  return (size_t)b * scan_blocks(n) * K * (sizeof(float) + sizeof(int64_t)) + 256;
+  const int64_t per_q = std::max<int64_t>(scan_blocks(n), scan_mm_rowblocks(n, b));
+  return (size_t)b * per_q * K * (sizeof(float) + sizeof(int64_t)) + (size_t)b * 4 + 512;
 }
 
 int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
@@ -378,6 +609,23 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
   if (b == 0) return MPR_OK;
   MPR_REQUIRE(ws_bytes >= scan_topk_workspace(n, b, k), "search: workspace too small");
   const int K = list_cap(k);
+  if (use_scan_mm(n, d, b, k) && !getenv("MPR_SCAN_MM_OFF")) {
+    const int RB = scan_mm_rowblocks(n, b);
+    int64_t* ci = reinterpret_cast<int64_t*>(ws);
+    float* ck = reinterpret_cast<float*>(ci + (size_t)b * RB * K);
+    float* qn = ck + (size_t)b * RB * K;
+    int rc = MPR_EUNSUP;
+    switch (K) {
+      case 1: rc = launch_scan_mm<1>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
+      case 2: rc = launch_scan_mm<2>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
+      case 4: rc = launch_scan_mm<4>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
+      case 8: rc = launch_scan_mm<8>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
+      case 16: rc = launch_scan_mm<16>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
+    }
+    if (rc != MPR_OK) return rc;
+    return merge_dispatch(ck, ci, b, (int64_t)RB * K, k, /*keys_are_values=*/0, metric, out_dist,
+                          out_ids, s);
+  }
   const int64_t nb = scan_blocks(n);
   int64_t* ci = reinterpret_cast<int64_t*>(ws);
   float* ck = reinterpret_cast<float*>(ci + (size_t)b * nb * K);

@@ -207,6 +207,23 @@ def index_rows(seed: int, n: int, d: int, sigma: float = 0.3) -> torch.Tensor:
     return _normal(_rng(seed), (n, d), sigma)
 
 
+def index_rows_device(seed: int, lo: int, hi: int, d: int, device, sigma: float = 0.3,
+                      chunk: int = 1 << 16) -> torch.Tensor:
+    """Rows [lo, hi) of a large synthetic index generated on the device in fixed chunks of
+    `chunk` rows (chunk c seeded with seed * 1_000_003 + c), so a row's content does not depend
+    on how the index is sharded (C5: 1,048,576 x 512 split over 1/2/4/8 ranks)."""
+    out = torch.empty((hi - lo, d), device=device, dtype=torch.float32)
+    g = torch.Generator(device=device)
+    c = lo // chunk
+    while c * chunk < hi:
+        a, b = max(lo, c * chunk), min(hi, (c + 1) * chunk)
+        g.manual_seed(seed * 1_000_003 + c)
+        full = torch.randn((chunk, d), device=device, generator=g) * sigma
+        out[a - lo:b - lo] = full[a - c * chunk:b - c * chunk]
+        c += 1
+    return out
+
+
 def answers(n: int, vocab: int = 50) -> list:
     return [f"a{j % vocab}" for j in range(n)]
 

@@ -32,7 +32,10 @@ def index_mod():
 
 @pytest.mark.parametrize("n,d,b,k", [(6500, 1024, 16, 1), (6500, 1024, 16, 3),
                                      (6500, 1024, 16, 5), (10000, 1024, 16, 15),
-                                     (512, 512, 33, 64), (7, 16, 3, 7), (65536, 1024, 16, 5)])
+                                     (512, 512, 33, 64), (7, 16, 3, 7), (65536, 1024, 16, 5),
+                                     # large batches: the GEMM-shaped scan (b >= 64, k <= 16)
+                                     (20000, 512, 256, 5), (5003, 1024, 64, 16),
+                                     (999, 64, 100, 1), (70, 512, 300, 3)])
 def test_scan_topk_l2(device, index_mod, n, d, b, k):
     X = syn.index_rows(1, n, d)
     q = syn.index_rows(2, b, d)
@@ -57,6 +60,27 @@ def test_scan_ties_lowest_id(device, index_mod):
     ref_ids = oret.topk_ids(oret.cdist(q, X), 6, skip_first=False)
     assert torch.equal(ids.cpu(), ref_ids)
     assert ids[0, :4].tolist() == [17, 101, 200, 250]
+
+
+def test_scan_large_batch_ties_and_cosine(device, index_mod):
+    """Large-batch path: exact duplicates resolve to the lowest id; cosine ids match too."""
+    g = np.random.Generator(np.random.PCG64(9))
+    X = torch.from_numpy(g.integers(-3, 4, size=(3000, 128)).astype(np.float32))
+    X[[17, 1101, 2950]] = X[2000].clone()
+    q = torch.cat([X[[2000, 5, 17]], torch.from_numpy(
+        g.integers(-3, 4, size=(125, 128)).astype(np.float32))], 0)
+    ix = index_mod.DeviceIndex(X, device)
+    dist, ids = ix.search(q.to(device), 6)
+    ref_ids = oret.topk_ids(oret.cdist(q, X), 6, skip_first=False)
+    assert torch.equal(ids.cpu(), ref_ids)
+    assert ids[0, :4].tolist() == [17, 1101, 2000, 2950]
+    Xc = syn.index_rows(3, 4000, 512)
+    qc = syn.index_rows(4, 96, 512)
+    ixc = index_mod.DeviceIndex(Xc, device, metric=index_mod.COSINE)
+    sim, idc = ixc.search(qc.to(device), 5)
+    ref_idc, ref_sim = oret.cosine_topk(qc, Xc, 5)
+    assert torch.equal(idc.cpu(), ref_idc)
+    assert torch.allclose(sim.cpu(), ref_sim, rtol=1e-5, atol=1e-6)
 
 
 def test_scan_cosine(device, index_mod):
