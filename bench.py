@@ -71,7 +71,7 @@ def _pmc_traffic():
 C5 = dict(N=1 << 20, D=512, B=256, k=5)
 
 
-def c5_scan(world, rank, device, group, iters=20):
+def c5_scan(world, rank, device, group, rdev, iters=20):
     """Config C5's retrieval core: a 1,048,576 x 512 fp32 index row-sharded
     over the ranks (rows/W each, built on device from chunk-seeded streams, so the global index
     is the same at every W), 256 queries in total (256/W per rank), k = 5.  One search = the
@@ -102,9 +102,9 @@ def c5_scan(world, rank, device, group, iters=20):
         dist_k, ids = ix.search(q, k)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    chk = torch.tensor([float(ids.sum())], device=device, dtype=torch.float64)
+    chk = torch.tensor([float(ids.sum())], device=rdev, dtype=torch.float64)
     if world > 1:
-        t = torch.tensor([el], device=device, dtype=torch.float64)
+        t = torch.tensor([el], device=rdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
         dist.all_reduce(chk)
@@ -201,11 +201,18 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
                          f"torch.distributed.run --nproc-per-node {args.gpus}")
-    device = torch.device(f"cuda:{local_rank}")
+    # MPR_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin,
+    # collectives staged through host memory); the driver's runs use nccl (RCCL), one GPU per rank.
+    backend = os.environ.get("MPR_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    device = torch.device(f"cuda:{local_rank % ndev if backend == 'gloo' else local_rank}")
     torch.cuda.set_device(device)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
         group = dist.group.WORLD
 
     model, retr, weights = build(cfg, device, group)
@@ -237,8 +244,9 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    rdev = device if backend == "nccl" else "cpu"
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=rdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -296,7 +304,7 @@ def main():
 
     c5 = None
     if not args.no_c5:
-        c5 = c5_scan(world, rank, device, group)
+        c5 = c5_scan(world, rank, device, group, rdev)
         barrier()
 
     cpu = None

@@ -52,13 +52,20 @@ class ShardedIndex:
             self._search = lambda q, k: searcher(local, lo, q, k)
         self._merge = merger or (lambda d, i, k: topk_merge(d, i, k, metric))
 
+    def _host_staged(self) -> bool:
+        # gloo (CPU tests, or a one-GPU rehearsal of N ranks) moves host tensors only
+        return dist.get_backend(self.group) == "gloo" and self.device.type == "cuda"
+
     def search(self, q: torch.Tensor, k: int):
         """q: this rank's [b, d] queries (same b on every rank).  Returns (dist, ids) [b, k]."""
         b = q.shape[0]
         kk = min(k, self.n_local)
         q = q.to(self.device, torch.float32).contiguous()
-        q_all = torch.empty((self.world * b, self.d), device=q.device, dtype=q.dtype)
-        dist.all_gather_into_tensor(q_all, q, group=self.group)
+        stage = self._host_staged()
+        qx = q.cpu() if stage else q
+        q_all = torch.empty((self.world * b, self.d), device=qx.device, dtype=qx.dtype)
+        dist.all_gather_into_tensor(q_all, qx, group=self.group)
+        q_all = q_all.to(self.device)
         d_loc, i_loc = self._search(q_all, kk)                  # [W*b, kk]
         if kk < k:                                              # tiny shard: pad with sentinels
             pad = k - kk
@@ -67,10 +74,13 @@ class ShardedIndex:
                                                  device=d_loc.device)], 1)
             i_loc = torch.cat([i_loc, torch.full((i_loc.shape[0], pad), -1, dtype=torch.int64,
                                                  device=i_loc.device)], 1)
+        if stage:
+            d_loc, i_loc = d_loc.cpu(), i_loc.cpu()
         d_recv = torch.empty_like(d_loc)
         i_recv = torch.empty_like(i_loc)
         dist.all_to_all_single(d_recv, d_loc.contiguous(), group=self.group)
         dist.all_to_all_single(i_recv, i_loc.contiguous(), group=self.group)
+        d_recv, i_recv = d_recv.to(self.device), i_recv.to(self.device)
         # [W(src shard), b, k] -> [b, W*k]
         cd = d_recv.view(self.world, b, k).permute(1, 0, 2).reshape(b, self.world * k)
         ci = i_recv.view(self.world, b, k).permute(1, 0, 2).reshape(b, self.world * k)
