@@ -42,6 +42,9 @@ SIGNATURES = [
                                   c_void_p]),
     ("mpr_vit_forward_pair", c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int32,
                                        c_void_p, c_int64, c_void_p, c_int32, c_void_p]),
+    ("mpr_encode_towers", c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int32,
+                                    c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p,
+                                    c_int32, c_int32, c_void_p, c_int64, c_void_p]),
     ("mpr_clip_text_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32,
                                        POINTER(c_void_p)]),
     ("mpr_clip_text_forward", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64,
@@ -160,20 +163,22 @@ def decode_cus(idx: int) -> int:
 
 
 def stream_priorities() -> tuple:
-    """(encoder streams, decode stream) priorities, MPR_STREAM_PRIO = "enc" (default: the
-    retrieval encoders first — the host waits on their result to build prompts), "dec" or
-    "none".  Lower is higher (-1 = high)."""
+    """(retrieval-encoder streams, generate streams) priorities, MPR_STREAM_PRIO = "enc"
+    (default: the retrieval encoders first — the host waits on their result to build prompts),
+    "gen", "both" or "none".  Lower is higher (-1 = high)."""
     mode = os.environ.get("MPR_STREAM_PRIO", "enc")
-    return {"enc": (-1, 0), "dec": (0, -1)}.get(mode, (0, 0))
+    return {"enc": (-1, 0), "gen": (0, -1), "both": (-1, -1)}.get(mode, (0, 0))
 
 
 def separate_decode_stream(idx: int) -> bool:
-    return bool(decode_cus(idx)) or stream_priorities()[1] != 0
+    """The decode loop gets a stream of its own only with a CU partition."""
+    return bool(decode_cus(idx))
 
 
 def role_stream(device, role: str):
     """A process-lifetime stream for one role of the serving pipeline: ``"decode"`` (the T5
-    greedy loop) or ``"encode:<tag>"`` (retrieval towers).  With a CU partition
+    greedy loop, CU partition only), ``"gen:<slot>"`` (a batch's T5 generate in the serving loop)
+    or ``"encode:<tag>"`` (retrieval towers).  With a CU partition
     (decode_cus() > 0) the decode stream is restricted to the first n CUs (mask bits [0, n)) and
     the encoder streams to the rest; otherwise plain non-blocking streams with
     stream_priorities().  Returned as torch.cuda.ExternalStream so torch work can be enqueued on
@@ -198,8 +203,9 @@ def role_stream(device, role: str):
                 mask[b // 32] |= 1 << (b % 32)
             call("mpr_stream_create", 0, mask, words, ctypes.byref(h))
         else:
-            pe, pd = stream_priorities()
-            call("mpr_stream_create", pd if role == "decode" else pe, None, 0, ctypes.byref(h))
+            pe, pg = stream_priorities()
+            call("mpr_stream_create", pe if role.startswith("encode") else pg, None, 0,
+                 ctypes.byref(h))
     st = torch.cuda.ExternalStream(h.value, device=dev)
     _role_streams[key] = st
     return st

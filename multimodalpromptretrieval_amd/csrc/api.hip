@@ -218,15 +218,28 @@ int mpr_vit_forward(mpr_model* m, const float* img, int32_t b, int32_t mode, flo
 int mpr_vit_forward_pair(mpr_model* a, int32_t mode_a, float* out_a, int64_t out_a_bs,
                          mpr_model* b, int32_t mode_b, float* out_b, int64_t out_b_bs,
                          const float* img, int32_t batch, void* stream) {
+  return mpr_encode_towers(a, mode_a, out_a, out_a_bs, b, mode_b, out_b, out_b_bs, img, batch,
+                           nullptr, nullptr, 0, 0, nullptr, 0, stream);
+}
+
+int mpr_encode_towers(mpr_model* vit_a, int32_t mode_a, float* out_a, int64_t out_a_bs,
+                      mpr_model* vit_b, int32_t mode_b, float* out_b, int64_t out_b_bs,
+                      const float* img, int32_t n_images, mpr_model* text, const int32_t* tok,
+                      int32_t n_texts, int32_t seq_len, float* out_t, int64_t out_t_bs,
+                      void* stream) {
   return guarded([&]() -> int {
-    MPR_REQUIRE(a && a->kind == mpr_model::VIT && b && b->kind == mpr_model::VIT,
-                "vit_forward_pair: not ViT handles");
-    MPR_REQUIRE(a != b, "vit_forward_pair: the two handles must differ (workspaces)");
-    VitModel* v[2] = {static_cast<VitModel*>(a), static_cast<VitModel*>(b)};
+    MPR_REQUIRE(!vit_a || vit_a->kind == mpr_model::VIT, "encode_towers: vit_a not a ViT");
+    MPR_REQUIRE(!vit_b || vit_b->kind == mpr_model::VIT, "encode_towers: vit_b not a ViT");
+    MPR_REQUIRE(!vit_b || vit_a, "encode_towers: vit_b without vit_a");
+    MPR_REQUIRE(!vit_b || vit_a != vit_b, "encode_towers: the two ViT handles must differ");
+    MPR_REQUIRE(!text || text->kind == mpr_model::CLIP_TEXT, "encode_towers: not a text handle");
+    VitModel* v[2] = {static_cast<VitModel*>(vit_a), static_cast<VitModel*>(vit_b)};
     const int modes[2] = {mode_a, mode_b};
     float* outs[2] = {out_a, out_b};
     const int64_t bs[2] = {out_a_bs, out_b_bs};
-    return VitModel::forward_group(v, img, batch, modes, outs, bs, 2, S(stream));
+    const int nv = vit_b ? 2 : (vit_a ? 1 : 0);
+    return encode_towers(v, modes, outs, bs, nv, img, n_images, static_cast<TextModel*>(text),
+                         tok, n_texts, seq_len, out_t, out_t_bs, S(stream));
   });
 }
 

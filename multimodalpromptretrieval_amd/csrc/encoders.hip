@@ -44,35 +44,37 @@ int ClipTower::load_blocks(const float* const* t, int w, int nl) {
 }
 
 int ClipTower::run(float* x, int B, int L, bool causal, hipStream_t s) {
-  ClipTower* t = this;
-  return run_group(&t, &x, 1, B, L, causal, s);
+  TowerRun r{this, x, B, L, causal};
+  return run_group(&r, 1, s);
 }
 
-// n towers of one geometry (n <= 2: the retrieval and token-feature ViTs of a batch) stepped in
-// lockstep; every projection of layer l is one grouped GEMM launch over the n towers.
-int ClipTower::run_group(ClipTower* const* t, float* const* xs, int n, int B, int L, bool causal,
-                         hipStream_t s) {
-  MPR_REQUIRE(n >= 1 && n <= 2, "clip tower group: n=%d", n);
-  const int W = t[0]->width, M = B * L;
+// n CLIP transformers with the same layer count stepped in lockstep (the retrieval ViT, the
+// token-feature ViT and the CLIP text tower of a batch): every projection of layer l is one
+// grouped GEMM launch over the towers (split by tile choice, gemm_group); per tower its own
+// width, batch, sequence length and causality.
+int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
+  MPR_REQUIRE(n >= 1 && n <= GEMM_GROUP, "clip tower group: n=%d", n);
   for (int i = 0; i < n; ++i) {
-    MPR_REQUIRE(t[i]->width == W && t[i]->layers == t[0]->layers,
-                "clip tower group: towers differ in geometry");
-    MPR_TRY(t[i]->h.ensure((size_t)M * W * 4));
-    MPR_TRY(t[i]->qkv.ensure((size_t)M * 3 * W * 4));
-    MPR_TRY(t[i]->ao.ensure((size_t)M * W * 4));
-    MPR_TRY(t[i]->mlp.ensure((size_t)M * 4 * W * 4));
+    ClipTower& t = *r[i].t;
+    MPR_REQUIRE(t.layers == r[0].t->layers, "clip tower group: towers differ in depth");
+    const size_t M = (size_t)r[i].B * r[i].L, W = t.width;
+    MPR_TRY(t.h.ensure(M * W * 4));
+    MPR_TRY(t.qkv.ensure(M * 3 * W * 4));
+    MPR_TRY(t.ao.ensure(M * W * 4));
+    MPR_TRY(t.mlp.ensure(M * 4 * W * 4));
   }
-  const int heads = t[0]->heads;
-  for (int l = 0; l < t[0]->layers; ++l) {
+  for (int l = 0; l < r[0].t->layers; ++l) {
     GemmGroup gq, go, gf, gp;
     gq.n = go.n = gf.n = gp.n = n;
     for (int i = 0; i < n; ++i) {
-      const ClipBlock& b = *t[i]->blocks[l];
-      float* x = xs[i];
-      float* hp = t[i]->h.as<float>();
-      float* qp = t[i]->qkv.as<float>();
-      float* ap = t[i]->ao.as<float>();
-      float* mp = t[i]->mlp.as<float>();
+      ClipTower& t = *r[i].t;
+      const ClipBlock& b = *t.blocks[l];
+      const int W = t.width, M = r[i].B * r[i].L;
+      float* x = r[i].x;
+      float* hp = t.h.as<float>();
+      float* qp = t.qkv.as<float>();
+      float* ap = t.ao.as<float>();
+      float* mp = t.mlp.as<float>();
       GemmArgs& g = gq.g[i];
       g.A = hp; g.lda = W; g.W = b.in_w.as<float>(); g.ldw = W; g.bias = b.in_b.as<float>();
       g.C = qp; g.ldc = 3 * W; g.M = M; g.N = 3 * W; g.K = W;
@@ -88,28 +90,34 @@ int ClipTower::run_group(ClipTower* const* t, float* const* xs, int n, int B, in
       pj.N = W; pj.K = 4 * W;
     }
     for (int i = 0; i < n; ++i) {
-      const ClipBlock& b = *t[i]->blocks[l];
-      MPR_TRY(layernorm(xs[i], W, M, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(), CLIP_LN_EPS,
-                        t[i]->h.as<float>(), W, s));
+      ClipTower& t = *r[i].t;
+      const ClipBlock& b = *t.blocks[l];
+      const int W = t.width;
+      MPR_TRY(layernorm(r[i].x, W, r[i].B * r[i].L, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(),
+                        CLIP_LN_EPS, t.h.as<float>(), W, s));
     }
     MPR_TRY(gemm_group(gq, s));
     for (int i = 0; i < n; ++i) {
-      float* qp = t[i]->qkv.as<float>();
+      ClipTower& t = *r[i].t;
+      const int W = t.width, L = r[i].L;
+      float* qp = t.qkv.as<float>();
       AttnArgs at;
       at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
       at.k = qp + W; at.k_bs = at.q_bs; at.k_rs = 3 * W;
       at.v = qp + 2 * W; at.v_bs = at.q_bs; at.v_rs = 3 * W;
-      at.o = t[i]->ao.as<float>(); at.o_bs = (int64_t)L * W; at.o_rs = W;
-      at.B = B; at.H = heads; at.Lq = L; at.Lk = L;
+      at.o = t.ao.as<float>(); at.o_bs = (int64_t)L * W; at.o_rs = W;
+      at.B = r[i].B; at.H = t.heads; at.Lq = L; at.Lk = L;
       at.scale = 0.125f;  // 64 ** -0.5, exact power of two
-      at.causal = causal ? 1 : 0;
+      at.causal = r[i].causal ? 1 : 0;
       MPR_TRY(attention(at, s));
     }
     MPR_TRY(gemm_group(go, s));
     for (int i = 0; i < n; ++i) {
-      const ClipBlock& b = *t[i]->blocks[l];
-      MPR_TRY(layernorm(xs[i], W, M, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(), CLIP_LN_EPS,
-                        t[i]->h.as<float>(), W, s));
+      ClipTower& t = *r[i].t;
+      const ClipBlock& b = *t.blocks[l];
+      const int W = t.width;
+      MPR_TRY(layernorm(r[i].x, W, r[i].B * r[i].L, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(),
+                        CLIP_LN_EPS, t.h.as<float>(), W, s));
     }
     MPR_TRY(gemm_group(gf, s));
     MPR_TRY(gemm_group(gp, s));
@@ -120,58 +128,85 @@ int ClipTower::run_group(ClipTower* const* t, float* const* xs, int n, int B, in
 int VitModel::forward(const float* img, int B, int mode, float* out, int64_t out_bs,
                       hipStream_t s) {
   VitModel* m = this;
-  return forward_group(&m, img, B, &mode, &out, &out_bs, 1, s);
+  return encode_towers(&m, &mode, &out, &out_bs, 1, img, B, nullptr, nullptr, 0, 0, nullptr, 0,
+                       s);
 }
 
-// n ViTs of one geometry over the same images (the retrieval tower's CLS features and the
-// token-feature tower of T5VisionModel): im2col once, then both towers in lockstep.
-int VitModel::forward_group(VitModel* const* v, const float* img, int B, const int* modes,
-                            float* const* outs, const int64_t* out_bs, int n, hipStream_t s) {
-  MPR_REQUIRE(n >= 1 && n <= 2, "vit group: n=%d", n);
-  for (int i = 0; i < n; ++i) {
+int TextModel::forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs,
+                       hipStream_t s) {
+  return encode_towers(nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, this, tok, B, L, out,
+                       out_bs, s);
+}
+
+// The CLIP towers of one batch in lockstep: nv (0..2) ViTs of one geometry over the same images
+// (im2col once) and optionally the text tower over the batch's tokens.  Results are identical to
+// separate calls (every GEMM keeps its own tile choice, every other kernel is per tower).
+int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
+                  const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
+                  const int32_t* tok, int Bt, int Lt, float* out_t, int64_t out_t_bs,
+                  hipStream_t s) {
+  MPR_REQUIRE(nv >= 0 && nv <= 2, "encode_towers: %d ViTs", nv);
+  for (int i = 0; i < nv; ++i) {
     MPR_REQUIRE(modes[i] == 0 || modes[i] == 1, "vit: mode must be 0 (CLS) or 1 (tokens)");
     MPR_REQUIRE(v[i]->width == v[0]->width && v[i]->patch == v[0]->patch &&
                     v[i]->image == v[0]->image && v[i]->tower.layers == v[0]->tower.layers,
                 "vit group: towers differ in geometry");
   }
-  if (B == 0) return MPR_OK;
-  VitModel& a0 = *v[0];
-  const int W = a0.width, g2 = a0.grid * a0.grid, T = g2 + 1, P = 3 * a0.patch * a0.patch;
-  MPR_TRY(a0.cols.ensure((size_t)B * g2 * P * 4));
-  for (int i = 0; i < n; ++i) {
-    MPR_TRY(v[i]->patches.ensure((size_t)B * g2 * W * 4));
-    MPR_TRY(v[i]->x.ensure((size_t)B * T * W * 4));
-    MPR_TRY(v[i]->tmp.ensure((size_t)B * T * W * 4));
+  if (tm) {
+    MPR_REQUIRE(Lt >= 1 && Lt <= tm->ctx, "clip text: seq_len %d outside [1, %d]", Lt, tm->ctx);
+    MPR_REQUIRE(nv == 0 || tm->tower.layers == v[0]->tower.layers,
+                "encode_towers: text and image towers differ in depth");
   }
-  MPR_TRY(im2col_patches(img, B, a0.image, a0.patch, a0.cols.as<float>(), s));
-  GemmGroup pe;
-  pe.n = n;
-  for (int i = 0; i < n; ++i) {
-    GemmArgs& g = pe.g[i];
-    g.A = a0.cols.as<float>(); g.lda = P; g.W = v[i]->conv_w.as<float>(); g.ldw = P;
-    g.C = v[i]->patches.as<float>(); g.ldc = W; g.M = B * g2; g.N = W; g.K = P;
+  if (B == 0) nv = 0;
+  if (Bt == 0) tm = nullptr;
+  if (nv == 0 && !tm) return MPR_OK;
+  TowerRun runs[3];
+  int nr = 0;
+  if (nv > 0) {
+    VitModel& a0 = *v[0];
+    const int W = a0.width, g2 = a0.grid * a0.grid, T = g2 + 1, P = 3 * a0.patch * a0.patch;
+    MPR_TRY(a0.cols.ensure((size_t)B * g2 * P * 4));
+    for (int i = 0; i < nv; ++i) {
+      MPR_TRY(v[i]->patches.ensure((size_t)B * g2 * W * 4));
+      MPR_TRY(v[i]->x.ensure((size_t)B * T * W * 4));
+      MPR_TRY(v[i]->tmp.ensure((size_t)B * T * W * 4));
+    }
+    MPR_TRY(im2col_patches(img, B, a0.image, a0.patch, a0.cols.as<float>(), s));
+    GemmGroup pe;
+    pe.n = nv;
+    for (int i = 0; i < nv; ++i) {
+      GemmArgs& g = pe.g[i];
+      g.A = a0.cols.as<float>(); g.lda = P; g.W = v[i]->conv_w.as<float>(); g.ldw = P;
+      g.C = v[i]->patches.as<float>(); g.ldc = W; g.M = B * g2; g.N = W; g.K = P;
+    }
+    MPR_TRY(gemm_group(pe, s));
+    for (int i = 0; i < nv; ++i) {
+      VitModel& m = *v[i];
+      float* xp = m.x.as<float>();
+      MPR_TRY(vit_assemble(m.patches.as<float>(), m.cls.as<float>(), m.pos.as<float>(), B, g2,
+                           W, xp, s));
+      MPR_TRY(layernorm(xp, W, B * T, W, m.lnpre_w.as<float>(), m.lnpre_b.as<float>(),
+                        CLIP_LN_EPS, xp, W, s));
+      runs[nr++] = TowerRun{&m.tower, xp, B, T, false};
+    }
   }
-  MPR_TRY(gemm_group(pe, s));
-  ClipTower* towers[2];
-  float* xs[2];
-  for (int i = 0; i < n; ++i) {
-    VitModel& m = *v[i];
-    float* xp = m.x.as<float>();
-    MPR_TRY(vit_assemble(m.patches.as<float>(), m.cls.as<float>(), m.pos.as<float>(), B, g2, W,
-                         xp, s));
-    MPR_TRY(layernorm(xp, W, B * T, W, m.lnpre_w.as<float>(), m.lnpre_b.as<float>(), CLIP_LN_EPS,
-                      xp, W, s));
-    towers[i] = &m.tower;
-    xs[i] = xp;
+  if (tm) {
+    const int W = tm->width;
+    MPR_TRY(tm->x.ensure((size_t)Bt * Lt * W * 4));
+    MPR_TRY(tm->pooled.ensure((size_t)Bt * W * 4));
+    MPR_TRY(embed_gather(tm->tok_emb.as<float>(), tok, tm->ctx, Bt, Lt, W, tm->pos.as<float>(),
+                         tm->x.as<float>(), (int64_t)Lt * W, 0, s));
+    runs[nr++] = TowerRun{&tm->tower, tm->x.as<float>(), Bt, Lt, true};
   }
-  MPR_TRY(ClipTower::run_group(towers, xs, n, B, T, /*causal=*/false, s));
+  MPR_TRY(ClipTower::run_group(runs, nr, s));
   GemmGroup pg;
-  pg.n = n;
-  for (int i = 0; i < n; ++i) {
+  pg.n = 0;
+  for (int i = 0; i < nv; ++i) {
     VitModel& m = *v[i];
+    const int W = m.width, T = m.grid * m.grid + 1;
     float* xp = m.x.as<float>();
     float* tp = m.tmp.as<float>();
-    GemmArgs& pj = pg.g[i];
+    GemmArgs& pj = pg.g[pg.n++];
     pj.W = m.projT.as<float>(); pj.ldw = W; pj.N = m.out_dim; pj.K = W; pj.A = tp; pj.lda = W;
     if (modes[i] == 0) {
       // ln_post on the CLS rows only (x[b*T]), then @ proj
@@ -184,28 +219,17 @@ int VitModel::forward_group(VitModel* const* v, const float* img, int B, const i
       pj.M = B * T; pj.C = outs[i]; pj.ldc = m.out_dim; pj.c_rpb = T; pj.c_bs = out_bs[i];
     }
   }
+  if (tm) {
+    const int W = tm->width;
+    float* pp = tm->pooled.as<float>();
+    MPR_TRY(eot_gather(tm->x.as<float>(), tok, Bt, Lt, tm->ctx, W, pp, s));
+    MPR_TRY(layernorm(pp, W, Bt, W, tm->lnf_w.as<float>(), tm->lnf_b.as<float>(), CLIP_LN_EPS,
+                      pp, W, s));
+    GemmArgs& pj = pg.g[pg.n++];
+    pj.A = pp; pj.lda = W; pj.W = tm->projT.as<float>(); pj.ldw = W; pj.M = Bt;
+    pj.N = tm->out_dim; pj.K = W; pj.C = out_t; pj.ldc = out_t_bs;
+  }
   MPR_TRY(gemm_group(pg, s));
-  return MPR_OK;
-}
-
-int TextModel::forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs,
-                       hipStream_t s) {
-  MPR_REQUIRE(L >= 1 && L <= ctx, "clip text: seq_len %d outside [1, %d]", L, ctx);
-  if (B == 0) return MPR_OK;
-  const int W = width;
-  MPR_TRY(x.ensure((size_t)B * L * W * 4));
-  MPR_TRY(pooled.ensure((size_t)B * W * 4));
-  float* xp = x.as<float>();
-  MPR_TRY(embed_gather(tok_emb.as<float>(), tok, ctx, B, L, W, pos.as<float>(), xp, (int64_t)L * W,
-                       0, s));
-  MPR_TRY(tower.run(xp, B, L, /*causal=*/true, s));
-  float* pp = pooled.as<float>();
-  MPR_TRY(eot_gather(xp, tok, B, L, ctx, W, pp, s));
-  MPR_TRY(layernorm(pp, W, B, W, lnf_w.as<float>(), lnf_b.as<float>(), CLIP_LN_EPS, pp, W, s));
-  GemmArgs pj;
-  pj.A = pp; pj.lda = W; pj.W = projT.as<float>(); pj.ldw = W; pj.M = B; pj.N = out_dim; pj.K = W;
-  pj.C = out; pj.ldc = out_bs;
-  MPR_TRY(gemm(pj, s));
   return MPR_OK;
 }
 

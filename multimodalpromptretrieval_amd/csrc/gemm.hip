@@ -196,6 +196,10 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
   for (int j = 0; j < D; ++j) gload(j, (2 + j) * BK);
   __syncthreads();
   sread(0, fa, fb);
+  // Iteration 0 overwrites stage 0 (tile 2) while a slower wave may still be reading tile 0's
+  // fragments from it here: every wave's reads must land first (this race made ~3% of grouped
+  // launches nondeterministic before the barrier was added).
+  __syncthreads();
   // Steady state, branch-free (the accumulators stay in AGPRs): iteration t multiplies tile t
   // (fragments already in registers), reads tile t+1's fragments after the first quarter of the
   // MFMAs, writes tile t+2 (register slot t % D) into tile t's stage and re-arms the slot with
@@ -618,41 +622,52 @@ int probe_read(double* ms, int64_t* launches, double* flops, double* bytes) {
   return MPR_OK;
 }
 
-int gemm_group(const GemmGroup& g, hipStream_t s) {
-  MPR_REQUIRE(g.n >= 1 && g.n <= GEMM_GROUP, "gemm_group: %d problems", g.n);
-  int64_t tiles64 = 0;
-  for (int i = 0; i < g.n; ++i) {
-    const GemmArgs& a = g.g[i];
-    MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N,
-                a.K);
-    MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
-                    aligned16(a.W),
-                "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-    tiles64 = std::max(tiles64, cdiv(a.M, 64) * cdiv(a.N, 64));
-  }
-  if (tiles64 == 0) return MPR_OK;
+namespace {
+// One launch of problems that share a tile configuration (probed / recorded as one launch).
+int gemm_launch(const GemmGroup& g, bool big, hipStream_t s) {
   double flops = 0, bytes = 0;
   for (int i = 0; i < g.n; ++i) {
     flops += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K;
     bytes += gemm_bytes(g.g[i]);
   }
-  // Tile choice (measured on MI355X over the ViT/T5/CLIP-text projection shapes, single and
-  // paired, tools/gbench.hip): 64x64 tiles (4 waves of 32x32, BK 32, 2 tiles of loads in flight)
-  // once one problem has >= 1.5 blocks per CU; below that 32x32 tiles with the K tile split over 4
-  // waves (4x the blocks, partial sums added through LDS): 800x768x3072 67 -> 54 us,
-  // 1152x512x2048 47 -> 38 us, paired 800x768x768 34 -> 29 us.  BK 64, 128-row tiles, 8-wave
-  // 64x64 blocks and split-K across blocks were slower at every shape of this path.  The
-  // choice depends on the largest single problem, not on the group: a problem gets the same
-  // tile (the same summation order, bit-identical results) alone or grouped.
   if (g_probe_kind == PROBE_RECORD) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone)
       g_recorded.push_back(g);
   }
   return probed(PROBE_GEMM, flops, bytes, s, [&]() {
-    if (tiles64 >= 384) return launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>(g, s);
+    if (big) return launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>(g, s);
     return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
   });
+}
+}  // namespace
+
+int gemm_group(const GemmGroup& g, hipStream_t s) {
+  MPR_REQUIRE(g.n >= 1 && g.n <= GEMM_GROUP, "gemm_group: %d problems", g.n);
+  // Tile choice, per problem (measured on MI355X over the ViT/T5/CLIP-text projection shapes,
+  // single and paired, tools/gbench.hip): 64x64 tiles (4 waves of 32x32, BK 32, 2 tiles of
+  // loads in flight) once the problem has >= 1.5 blocks per CU; below that 32x32 tiles with the
+  // K tile split over 4 waves (4x the blocks, partial sums added through LDS): 800x768x3072
+  // 67 -> 54 us, 1152x512x2048 47 -> 38 us, paired 800x768x768 34 -> 29 us.  BK 64, 128-row
+  // tiles, 8-wave 64x64 blocks and split-K across blocks were slower at every shape of this
+  // path.  Problems of a group with different choices go to two launches, so a problem gets the
+  // same tile (the same summation order, bit-identical results) alone or grouped.
+  GemmGroup big, small;
+  big.n = small.n = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const GemmArgs& a = g.g[i];
+    MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N,
+                a.K);
+    if (a.M == 0 || a.N == 0) continue;
+    MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
+                    aligned16(a.W),
+                "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
+    GemmGroup& dst = cdiv(a.M, 64) * cdiv(a.N, 64) >= 384 ? big : small;
+    dst.g[dst.n++] = a;
+  }
+  if (big.n) MPR_TRY(gemm_launch(big, true, s));
+  if (small.n) MPR_TRY(gemm_launch(small, false, s));
+  return MPR_OK;
 }
 
 int gemm(const GemmArgs& a, hipStream_t s) {

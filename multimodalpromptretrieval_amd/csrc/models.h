@@ -31,6 +31,14 @@ struct ClipBlock {
   DevBuf ln1_w, ln1_b, in_w, in_b, out_w, out_b, ln2_w, ln2_b, fc_w, fc_b, pj_w, pj_b;
 };
 
+struct ClipTower;
+struct TowerRun {
+  ClipTower* t;
+  float* x;  // [B*L, width], updated in place
+  int B, L;
+  bool causal;
+};
+
 struct ClipTower {
   int width = 0, layers = 0, heads = 0;
   std::vector<std::unique_ptr<ClipBlock>> blocks;
@@ -39,8 +47,7 @@ struct ClipTower {
   int load_blocks(const float* const* t, int width, int layers);
   // x [B*L, width] in place; causal for the text tower.
   int run(float* x, int B, int L, bool causal, hipStream_t s);
-  static int run_group(ClipTower* const* t, float* const* xs, int n, int B, int L, bool causal,
-                       hipStream_t s);
+  static int run_group(const TowerRun* r, int n, hipStream_t s);
 };
 
 struct VitModel : mpr_model {
@@ -50,8 +57,6 @@ struct VitModel : mpr_model {
   ClipTower tower;
   DevBuf cols, patches, x, tmp;
   int forward(const float* img, int B, int mode, float* out, int64_t out_bs, hipStream_t s);
-  static int forward_group(VitModel* const* v, const float* img, int B, const int* modes,
-                           float* const* outs, const int64_t* out_bs, int n, hipStream_t s);
 };
 
 struct TextModel : mpr_model {
@@ -62,6 +67,13 @@ struct TextModel : mpr_model {
   DevBuf x, pooled;
   int forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs, hipStream_t s);
 };
+
+// The CLIP towers of one batch in lockstep (encoders.hip): nv <= 2 ViTs over the same images,
+// optionally the text tower; identical results to separate calls.
+int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
+                  const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
+                  const int32_t* tok, int Bt, int Lt, float* out_t, int64_t out_t_bs,
+                  hipStream_t s);
 
 struct T5Layer {
   DevBuf ln0, qkv, o, ln1, wi, wo;         // encoder layer / decoder self-attn + ffn

@@ -297,6 +297,10 @@ __global__ __launch_bounds__(256) void scan_mm_kernel(const float* __restrict__ 
   for (int j = 0; j < SM_D; ++j) gload(j, 2 + j);
   __syncthreads();
   sread(0, fa, fb);
+  // Iteration 0 overwrites stage 0 (tile 2) while a slower wave may still be reading tile 0's
+  // fragments from it here: every wave's reads must land first (this race made ~3% of grouped
+  // launches nondeterministic before the barrier was added).
+  __syncthreads();
   for (int s0 = 0; s0 < Sr; s0 += SM_D) {
 #pragma unroll
     for (int j = 0; j < SM_D; ++j) {

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .encoders import CLS, DeviceCLIPText, DeviceViT
+from .encoders import CLS, DeviceCLIPText, DeviceViT, encode_towers  # noqa: F401
 from .index import L2, DeviceIndex
 
 BUCKETS = ["very unlikely", "unlikely", "maybe", "likely", "very likely", "certainly"]
@@ -83,64 +83,65 @@ class VQARetrieval:
 
     # ---- encoding ------------------------------------------------------------------------------
     def _streams(self):
+        """The retrieval stream (_lib.role_stream "encode:towers": high priority by default —
+        the host waits on the retrieval result to build prompts)."""
         if not hasattr(self, "_s_img"):
-            # The encoders' CU share (_lib.role_stream): the T5 decode chain of the previous
-            # batch keeps CUs of its own while these run.
-            self._s_img = _lib.role_stream(self.device, "encode:img")
-            self._s_txt = _lib.role_stream(self.device, "encode:txt")
-        return self._s_img, self._s_txt
+            self._s_img = _lib.role_stream(self.device, "encode:towers")
+        return self._s_img
 
     def encode_image_pair(self, batch, other_vit, other_mode: int):
-        """Run this retrieval's ``encode_image`` together with a second ViT of the same geometry
-        over the batch's images (T5VisionModel's token-feature tower): one paired pass,
-        ``DeviceViT.forward_pair``.  The CLS half of the query rows is kept for the next
-        ``encode_queries(batch)`` of the same batch object; returns the other tower's output
-        and the stream it is produced on (the caller waits on that stream before using it)."""
-        s_img, _ = self._streams()
+        """Run this retrieval's query encoders (``encode_image`` on the batch's images and
+        ``encode_text`` on its questions) together with a second ViT of the same geometry over
+        the same images (T5VisionModel's token-feature tower): one lockstep pass over the three
+        CLIP towers (``encoders.encode_towers``).  The query rows are kept for the next
+        ``encode_queries(batch)`` of the same batch object; returns the other tower's output and
+        the stream it is produced on (the caller waits on that stream before using it)."""
+        s_img = self._streams()
         cur = torch.cuda.current_stream(self.device)
         img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+        toks = self.clip_tokenize(batch["question"])
         B = img.shape[0]
         q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
+        di = self.image_encoder.out_dim
         s_img.wait_stream(cur)
         img.record_stream(s_img)
         q.record_stream(s_img)
         with torch.cuda.stream(s_img):
-            _, other_out = self.image_encoder.forward_pair(
-                other_vit, img, CLS, other_mode, out=q, out_bstride=self.embed_dim)
+            _, other_out, _ = encode_towers(
+                self.image_encoder, img, CLS, out_a=q, out_a_bstride=self.embed_dim,
+                vit_b=other_vit, mode_b=other_mode, text=self.text_encoder, tokens=toks,
+                out_t=q[:, di:], out_t_bstride=self.embed_dim)
         other_out.record_stream(cur)
-        self._pending_img = (batch["image"], q)
+        self._pending_img = (batch["image"], q, tuple(batch["question"]))
         return other_out, s_img
 
     def encode_queries(self, batch) -> torch.Tensor:
         """[CLS image embedding ‖ EOT text embedding] fp32 [B, 1024] on the device
-        (dataset/VQAFeatureDataset.py:189-191, 146-148).  The two towers run concurrently on
-        two side streams (each fills only part of the chip at batch 16) and write their halves
-        of the query rows in place; the caller's stream waits for both.  When
-        ``encode_image_pair`` already produced this batch's image half, only the text tower
-        runs."""
+        (dataset/VQAFeatureDataset.py:189-191, 146-148): the image and text towers in one
+        lockstep pass (``encoders.encode_towers``, their projections share launches) on the
+        retrieval stream, writing their halves of the query rows in place; the caller's stream
+        waits for it.  When ``encode_image_pair`` already encoded this batch, its rows are
+        returned."""
         cur = torch.cuda.current_stream(self.device)
-        s_img, s_txt = self._streams()
+        s_img = self._streams()
         pending = getattr(self, "_pending_img", None)
         self._pending_img = None
+        if (pending is not None and pending[0] is batch["image"]
+                and pending[2] == tuple(batch["question"])):
+            cur.wait_stream(s_img)
+            return pending[1]
+        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
         toks = self.clip_tokenize(batch["question"])
+        q = torch.empty((img.shape[0], self.embed_dim), device=self.device, dtype=torch.float32)
         di = self.image_encoder.out_dim
-        if pending is not None and pending[0] is batch["image"]:
-            q = pending[1]
-        else:
-            img = batch["image"].to(self.device, torch.float32, non_blocking=True)
-            q = torch.empty((img.shape[0], self.embed_dim), device=self.device,
-                            dtype=torch.float32)
-            s_img.wait_stream(cur)
-            q.record_stream(s_img)
-            img.record_stream(s_img)
-            with torch.cuda.stream(s_img):
-                self.image_encoder(img, CLS, out=q, out_bstride=self.embed_dim)
-        s_txt.wait_stream(cur)
-        q.record_stream(s_txt)
-        with torch.cuda.stream(s_txt):
-            self.text_encoder(toks, out=q[:, di:], out_bstride=self.embed_dim)
+        s_img.wait_stream(cur)
+        q.record_stream(s_img)
+        img.record_stream(s_img)
+        with torch.cuda.stream(s_img):
+            encode_towers(self.image_encoder, img, CLS, out_a=q, out_a_bstride=self.embed_dim,
+                          text=self.text_encoder, tokens=toks, out_t=q[:, di:],
+                          out_t_bstride=self.embed_dim)
         cur.wait_stream(s_img)
-        cur.wait_stream(s_txt)
         return q
 
     # ---- index -------------------------------------------------------------------------------

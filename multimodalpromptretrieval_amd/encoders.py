@@ -129,6 +129,45 @@ class DeviceViT(_Handle):
         return out, other_out
 
 
+def encode_towers(vit_a: "DeviceViT" = None, img: torch.Tensor = None, mode_a: int = CLS,
+                  out_a=None, out_a_bstride=None, vit_b: "DeviceViT" = None,
+                  mode_b: int = TOKENS, out_b=None, out_b_bstride=None,
+                  text: "DeviceCLIPText" = None, tokens: torch.Tensor = None, out_t=None,
+                  out_t_bstride=None):
+    """One lockstep pass over a batch's CLIP towers (mpr_encode_towers): up to two ViTs over
+    the same images and the text tower over clip.tokenize ids; each layer's projections share
+    launches.  Bit-identical to the separate calls.  Returns (out_a, out_b, out_t)."""
+    dev = (vit_a or text).device
+    B = 0
+    if vit_a is not None:
+        img = img.to(dev, torch.float32, non_blocking=True).contiguous()
+        B = img.shape[0]
+        if tuple(img.shape[1:]) != (3, vit_a.image_size, vit_a.image_size):
+            raise ValueError(f"expected images [B,3,{vit_a.image_size},{vit_a.image_size}], "
+                             f"got {tuple(img.shape)}")
+        out_a, out_a_bstride = vit_a._out(B, mode_a, out_a, out_a_bstride)
+    if vit_b is not None:
+        if vit_a is None or vit_b is vit_a or vit_b.device != dev:
+            raise ValueError("vit_b needs a different vit_a on the same device")
+        out_b, out_b_bstride = vit_b._out(B, mode_b, out_b, out_b_bstride)
+    Bt, L, tok = 0, 0, None
+    if text is not None:
+        tok, L = text._tokens(tokens)
+        Bt = tok.shape[0]
+        if out_t is None:
+            out_t = torch.empty((Bt, text.out_dim), device=dev, dtype=torch.float32)
+            out_t_bstride = text.out_dim
+    _lib.call("mpr_encode_towers",
+              vit_a._h if vit_a is not None else None, mode_a, _lib.ptr(out_a),
+              int(out_a_bstride or 0),
+              vit_b._h if vit_b is not None else None, mode_b, _lib.ptr(out_b),
+              int(out_b_bstride or 0),
+              _lib.ptr(img if vit_a is not None else None), B,
+              text._h if text is not None else None, _lib.ptr(tok), Bt, L, _lib.ptr(out_t),
+              int(out_t_bstride or 0), _lib.stream_ptr(dev))
+    return out_a, out_b, out_t
+
+
 class DeviceCLIPText(_Handle):
     """CLIP text transformer (openai naming, no prefix) on one GPU."""
 
@@ -153,11 +192,10 @@ class DeviceCLIPText(_Handle):
                   _lib.tensor_array(host), len(host), _lib.ctypes.byref(h))
         self._h = h
 
-    def forward(self, tokens: torch.Tensor, out: torch.Tensor = None,
-                out_bstride: int = None) -> torch.Tensor:
-        """tokens int [B, ctx] (host or device).  Runs only the leading positions up to the
-        last EOT of the batch (causal attention makes the pooled output independent of the
-        positions after each row's EOT)."""
+    def _tokens(self, tokens: torch.Tensor):
+        """(device int32 ids, positions to run): only the leading positions up to the last EOT
+        of the batch when the ids are on the host (causal attention makes the pooled output
+        independent of later positions)."""
         if tokens.shape[1] != self.context_length:
             raise ValueError(f"expected tokens [B,{self.context_length}], got "
                              f"{tuple(tokens.shape)}")
@@ -166,7 +204,15 @@ class DeviceCLIPText(_Handle):
             seq_len = int(tokens.argmax(dim=1).max()) + 1 if B else 1
         else:
             seq_len = self.context_length
-        tok = tokens.to(self.device, torch.int32, non_blocking=True).contiguous()
+        return tokens.to(self.device, torch.int32, non_blocking=True).contiguous(), seq_len
+
+    def forward(self, tokens: torch.Tensor, out: torch.Tensor = None,
+                out_bstride: int = None) -> torch.Tensor:
+        """tokens int [B, ctx] (host or device).  Runs only the leading positions up to the
+        last EOT of the batch (causal attention makes the pooled output independent of the
+        positions after each row's EOT)."""
+        tok, seq_len = self._tokens(tokens)
+        B = tok.shape[0]
         if out is None:
             out = torch.empty((B, self.out_dim), device=self.device, dtype=torch.float32)
             out_bstride = self.out_dim

@@ -316,7 +316,7 @@ class T5VisionModel(nn.Module):
         if not hasattr(self, "_s_gen"):
             self._s_gen = []
         while len(self._s_gen) < depth:
-            self._s_gen.append(torch.cuda.Stream(self.device))
+            self._s_gen.append(_lib.role_stream(self.device, f"gen:{len(self._s_gen)}"))
         pending = deque()
         for i, batch in enumerate(batches):
             self._s_prep.wait_stream(torch.cuda.current_stream(self.device))

@@ -139,6 +139,27 @@ def test_vit_pair_matches_single(device, clip_sd):
     assert torch.equal(cls, a(img, CLS)) and torch.equal(tok, b(img, TOKENS))
     tok2, cls2 = b.forward_pair(a, img[:3], TOKENS, CLS)
     assert torch.equal(cls2, a(img[:3], CLS)) and torch.equal(tok2, b(img[:3], TOKENS))
+    # determinism of grouped launches (a stage-reuse race once made ~3% of them differ)
+    for _ in range(12):
+        c_i, t_i = a.forward_pair(b, img, CLS, TOKENS)
+        assert torch.equal(c_i, cls) and torch.equal(t_i, tok)
+
+
+def test_encode_towers_matches_separate(device, clip_sd):
+    """ViT pair + text tower in one lockstep pass == the three separate calls, bit for bit."""
+    from multimodalpromptretrieval_amd.encoders import (CLS, TOKENS, DeviceCLIPText, DeviceViT,
+                                                         encode_towers)
+    a, b = DeviceViT(clip_sd, device), DeviceViT(syn.clip_state_dict(14), device)
+    txt = DeviceCLIPText(clip_sd, device)
+    img = syn.images(16, 16).to(device)
+    toks = syn.clip_tokens(17, 16)
+    ca, tb, tt = encode_towers(a, img, CLS, vit_b=b, mode_b=TOKENS, text=txt, tokens=toks)
+    assert torch.equal(ca, a(img, CLS)) and torch.equal(tb, b(img, TOKENS))
+    assert torch.equal(tt, txt(toks))
+    ca1, _, tt1 = encode_towers(a, img[:5], CLS, text=txt, tokens=toks[:5])
+    assert torch.equal(ca1, a(img[:5], CLS)) and torch.equal(tt1, txt(toks[:5]))
+    _, _, t_only = encode_towers(text=txt, tokens=toks[:3])
+    assert torch.equal(t_only, txt(toks[:3]))
 
 
 def test_clip_text(device, clip_sd):
