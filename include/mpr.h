@@ -160,6 +160,16 @@ int mpr_t5_generate_slot(mpr_model* m, int32_t slot, const float* embeds_dev,
                          const float* mask_dev, int32_t b, int32_t L, int32_t max_new,
                          int32_t decoder_start, int32_t eos, int32_t pad, int32_t* out_tokens_dev,
                          void* stream);
+/* Two batches (b_a, b_b <= 16 rows, own source lengths) generated with one shared decode loop of
+ * b_a + b_b rows on workspace slot `slot`: each batch is encoded as mpr_t5_generate_slot would,
+ * the greedy steps run once for both (every decode-step weight is read once per step for 32 rows
+ * instead of twice for 16).  out_a [b_a, 1+max_new] / out_b [b_b, 1+max_new] are bit-identical
+ * to two mpr_t5_generate_slot calls.  b_b = 0 is a plain generate of batch a. */
+int mpr_t5_generate_pair(mpr_model* m, int32_t slot, const float* embeds_a_dev,
+                         const float* mask_a_dev, int32_t b_a, int32_t L_a,
+                         const float* embeds_b_dev, const float* mask_b_dev, int32_t b_b,
+                         int32_t L_b, int32_t max_new, int32_t decoder_start, int32_t eos,
+                         int32_t pad, int32_t* out_a_dev, int32_t* out_b_dev, void* stream);
 /* Run the greedy decode loop of later generate calls on a slot on decode_stream (null = the
  * call's own stream).  The call's stream still orders everything: the loop starts after the
  * encoder enqueued on it and the call's stream waits for the tokens. */

@@ -59,6 +59,9 @@ SIGNATURES = [
                                   c_int32, c_int32, c_int32, c_void_p, c_void_p]),
     ("mpr_t5_generate_slot", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                        c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    ("mpr_t5_generate_pair", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                       c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32,
+                                       c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     ("mpr_t5_set_decode_stream", c_int32, [c_void_p, c_int32, c_void_p]),
     ("mpr_t5_logits", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                                 c_int32, c_void_p, c_void_p]),

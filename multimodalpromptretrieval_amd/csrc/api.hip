@@ -411,6 +411,20 @@ int mpr_t5_generate_slot(mpr_model* m, int32_t slot, const float* embeds, const 
   });
 }
 
+int mpr_t5_generate_pair(mpr_model* m, int32_t slot, const float* embeds_a, const float* mask_a,
+                         int32_t b_a, int32_t L_a, const float* embeds_b, const float* mask_b,
+                         int32_t b_b, int32_t L_b, int32_t max_new, int32_t start, int32_t eos,
+                         int32_t pad, int32_t* out_a, int32_t* out_b, void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    const float* e[2] = {embeds_a, embeds_b};
+    const float* k[2] = {mask_a, mask_b};
+    const int bs[2] = {b_a, b_b}, ls[2] = {L_a, L_b};
+    int32_t* o[2] = {out_a, out_b};
+    return t5->generate_groups(2, e, k, bs, ls, max_new, start, eos, pad, o, S(stream), slot);
+  });
+}
+
 int mpr_t5_set_decode_stream(mpr_model* m, int32_t slot, void* decode_stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);

@@ -335,18 +335,24 @@ enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8 };
 // which needs more bytes in flight per wave); two accumulator chains per tile halve the
 // dependent-MFMA latency.  MAXC = chunks of 16 columns staged per pass; LOOP = more than one
 // pass (K > 16 * 8 * MAXC).
-template <int MAXC, int NT, int F, bool LOOP>
+template <int MAXC, int NT, int F, bool LOOP, int MR>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   constexpr bool RMS = (F & SKF_RMS) != 0, RES = (F & SKF_RES) != 0,
                  RELU = (F & SKF_RELU) != 0, AMAX = (F & SKF_AMAX) != 0;
+  constexpr int MROWS = 16 * MR;      // activation rows: MR 16-row groups share each weight load
   const GemmArgs& a = sa.g;
   constexpr int XLD = MAXC * 16 + 4;  // slab row stride (floats): conflict-free fragment reads
-  constexpr int XS = SK_WAVES * 16 * XLD, RED = NT * SK_WAVES * 256;
-  // one LDS object: activation slabs | partial tiles | per-wave sums of squares
-  __shared__ __attribute__((aligned(16))) float smem[XS + RED + SK_WAVES * 16];
-  float(*xs)[16][XLD] = reinterpret_cast<float(*)[16][XLD]>(smem);
-  f32x4(*red)[SK_WAVES][64] = reinterpret_cast<f32x4(*)[SK_WAVES][64]>(smem + XS);
-  float(*ssq_s)[16] = reinterpret_cast<float(*)[16]>(smem + XS + RED);
+  constexpr int XS = SK_WAVES * MROWS * XLD;
+  // one LDS object: activation slabs | per-wave sums of squares.  After its K slice a wave
+  // parks its NT * MR partial tiles in its own slab (wave-private until the block barrier), so
+  // the partials cost no LDS of their own: more blocks stay resident per CU.
+  static_assert(NT * MR * 256 <= MROWS * XLD, "partial tiles must fit the wave's slab");
+  __shared__ __attribute__((aligned(16))) float smem[XS + SK_WAVES * MROWS];
+  float(*xs)[MROWS][XLD] = reinterpret_cast<float(*)[MROWS][XLD]>(smem);
+  auto red = [&](int slot, int w) -> f32x4* {  // partial tile `slot` of wave w, 64 lanes
+    return reinterpret_cast<f32x4*>(smem + w * MROWS * XLD) + slot * 64;
+  };
+  float(*ssq_s)[MROWS] = reinterpret_cast<float(*)[MROWS]>(smem + XS);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int M = a.M, N = a.N, K = a.K;
@@ -363,23 +369,29 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   for (int t = 0; t < NT; ++t)
     wp[t] = reinterpret_cast<const f32x4*>(sa.wpk) +
             ((int64_t)min((int)blockIdx.x * NT + t, ntiles - 1) * nchunk) * 64 + lane;
-  // The lane's 4 outputs are row i, columns n0 + 4h .. +3 (16x16 D layout): its residual is
-  // one float4, fetched before the main loads.
+  // Epilogue wave w finishes tile w % NT for row group w / NT.  The lane's 4 outputs are row
+  // 16 * group + i, columns n0 + 4h .. +3 (16x16 D layout): its residual is one float4, fetched
+  // before the main loads.
+  const int et = wave % NT, er = wave / NT;
   f32x4 rres = {0.f, 0.f, 0.f, 0.f};
   if constexpr (RES) {
-    if (wave < NT)
-      rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)min(i, M - 1) * a.ldr +
-                                             (blockIdx.x * NT + wave) * 16 + h * 4);
+    if (wave < NT * MR)
+      rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)min(er * 16 + i, M - 1) * a.ldr +
+                                             (blockIdx.x * NT + et) * 16 + h * 4);
   }
-  f32x4 acc[NT][2];
+  f32x4 acc[NT][MR][2];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss = 0.f;
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < MR; ++r) acc[t][r][0] = acc[t][r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[MR];
+#pragma unroll
+  for (int r = 0; r < MR; ++r) ss[r] = 0.f;
 #pragma unroll 1
   for (int c0 = c_lo; LOOP ? c0 < c_hi : c0 == c_lo; c0 += MAXC) {
     // weights first (the long pole), then this pass's activation rows as 256-byte segments:
     // float4 q of the pass = row q / (4*MAXC), column (q % (4*MAXC)) * 4 of the pass
-    f32x4 wv[NT][MAXC], xr[MAXC], gv[MAXC];
+    f32x4 wv[NT][MAXC], xr[MR * MAXC], gv[MAXC];
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
       // a chunk past the wave's slice re-reads an in-range chunk; its activations are zero
@@ -389,7 +401,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       if constexpr (RMS) gv[u] = *reinterpret_cast<const f32x4*>(sa.rms_w + cc * 16 + h * 4);
     }
 #pragma unroll
-    for (int u = 0; u < MAXC; ++u) {
+    for (int u = 0; u < MR * MAXC; ++u) {
       const int q = u * 64 + lane, row = q / (4 * MAXC), col = c0 * 16 + (q % (4 * MAXC)) * 4;
       const bool ok = row < M && col < c_hi * 16 && col < K;
       xr[u] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
@@ -400,48 +412,60 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     // weight loads next to their MFMAs, behind the activation round trip through LDS)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < MAXC; ++u) {
+    for (int u = 0; u < MR * MAXC; ++u) {
       const int q = u * 64 + lane;
       *reinterpret_cast<f32x4*>(&xs[wave][q / (4 * MAXC)][(q % (4 * MAXC)) * 4]) = xr[u];
     }
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
-      f32x4 xv = *reinterpret_cast<const f32x4*>(&xs[wave][i][u * 16 + h * 4]);
-      if constexpr (RMS) {
+      f32x4 xv[MR];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ss += xv[e] * xv[e];
-          xv[e] = gv[u][e] * xv[e];
+      for (int r = 0; r < MR; ++r) {
+        xv[r] = *reinterpret_cast<const f32x4*>(&xs[wave][r * 16 + i][u * 16 + h * 4]);
+        if constexpr (RMS) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ss[r] += xv[r][e] * xv[r][e];
+            xv[r][e] = gv[u][e] * xv[r][e];
+          }
         }
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          acc[t][u & 1] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][u][e], xv[e], acc[t][u & 1], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < MR; ++r)
+            acc[t][r][u & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][u][e], xv[r][e],
+                                                                    acc[t][r][u & 1], 0, 0, 0);
     }
   }
 #pragma unroll
-  for (int t = 0; t < NT; ++t) red[t][wave][lane] = acc[t][0] + acc[t][1];
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < MR; ++r) red(r * NT + t, wave)[lane] = acc[t][r][0] + acc[t][r][1];
   if constexpr (RMS) {
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if (lane < 16) ssq_s[wave][lane] = ss;
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+      float v = ss[r];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) ssq_s[wave][r * 16 + lane] = v;
+    }
   }
   __syncthreads();
-  if (wave >= NT) return;
-  const int tile = blockIdx.x * NT + wave;
-  const int n0 = tile * 16;
-  f32x4 sum = red[wave][0][lane];
+  if (wave >= NT * MR) return;
+  const int tile = blockIdx.x * NT + et;
+  const int n0 = tile * 16, m = er * 16 + i;
+  f32x4 sum = red(wave, 0)[lane];  // partial slot er * NT + et == wave
 #pragma unroll
-  for (int w = 1; w < SK_WAVES; ++w) sum += red[wave][w][lane];
+  for (int w = 1; w < SK_WAVES; ++w) sum += red(wave, w)[lane];
   // D[row = W row (n), col = A row (m)]: col = lane&15, row = (lane>>4)*4 + r.
   float scale = sa.a_scale;
   if constexpr (RMS) {
     float t = 0.f;
 #pragma unroll
-    for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][i];
+    for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][m];
     scale = (1.0f / sqrtf(t / (float)K + sa.rms_eps)) * sa.a_scale;
   }
   if constexpr (AMAX) {
@@ -466,9 +490,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
         bi = oi;
       }
     }
-    if (lane < 16 && n0 < N) {  // row-major [16][ntiles]: greedy_step reads rows coalesced
-      sa.amax_val[(int64_t)i * ntiles + tile] = bv;
-      sa.amax_idx[(int64_t)i * ntiles + tile] = bi;
+    if (lane < 16 && n0 < N) {  // row-major [rows][ntiles]: greedy_step reads rows coalesced
+      sa.amax_val[(int64_t)m * ntiles + tile] = bv;
+      sa.amax_idx[(int64_t)m * ntiles + tile] = bi;
     }
   } else {
     f32x4 v = sum * scale;
@@ -477,7 +501,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
     }
     if constexpr (RES) v = rres + v;
-    if (i < M) *reinterpret_cast<f32x4*>(a.C + (int64_t)i * a.ldc + n0 + h * 4) = v;
+    if (m < M) *reinterpret_cast<f32x4*>(a.C + (int64_t)m * a.ldc + n0 + h * 4) = v;
   }
 }
 
@@ -694,11 +718,11 @@ int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, h
   return MPR_OK;
 }
 
-template <int MAXC, int NT, bool LOOP>
+template <int MAXC, int NT, bool LOOP, int MR = 1>
 void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s) {
 #define MPR_SK(f)                                                                          \
   case f:                                                                                  \
-    hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP>), dim3(grid), dim3(512), 0, s, sa); \
+    hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP, MR>), dim3(grid), dim3(512), 0, s, sa); \
     break;
   if constexpr (NT > 1) {
     switch (F) { MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS) default: break; }
@@ -717,7 +741,7 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s) {
 // blocks, made the two-decodes-in-flight serving loop 1-6% slower.)
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const GemmArgs& a = sa.g;
-  MPR_REQUIRE(a.M >= 0 && a.M <= 16 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
+  MPR_REQUIRE(a.M >= 0 && a.M <= 32 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
   if (a.M == 0 || a.N == 0) return MPR_OK;
   MPR_REQUIRE(sa.wpk && aligned16(sa.wpk), "gemm_skinny: needs the 16-byte aligned packed weight");
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && aligned16(a.A) &&
@@ -736,7 +760,16 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
   return probed(PROBE_SKINNY, 2.0 * a.M * a.N * a.K, gemm_bytes(a), s, [&]() {
-    if (amax && tiles >= 1024 && per <= 4)  // lm_head: 2 tiles per block (NT 1/2/4/8 measured
+    if (a.M > 16) {  // two row groups per weight load (a paired decode: 2 batches of <= 16)
+      if (amax && tiles >= 1024 && per <= 4)
+        launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s);
+      else if (per <= 4)
+        launch_skinny<4, 1, false, 2>(sa, F, (unsigned)tiles, s);
+      else if (per <= 8)
+        launch_skinny<8, 1, false, 2>(sa, F, (unsigned)tiles, s);
+      else  // a 16-chunk slab for 32 rows would not fit the 160 KiB LDS
+        launch_skinny<8, 1, true, 2>(sa, F, (unsigned)tiles, s);
+    } else if (amax && tiles >= 1024 && per <= 4)  // lm_head: 2 tiles per block (NT 1/2/4/8
       launch_skinny<4, 2, false>(sa, F, (unsigned)cdiv(tiles, 2), s);  // 14.5/13.1/13.8/14.5 us)
     else if (per <= 4)
       launch_skinny<4, 1, false>(sa, F, (unsigned)tiles, s);

@@ -89,6 +89,7 @@ struct T5Work {
   ~T5Work();
   DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, unfinished, cur_tok;
   DevBuf enc_in, mask_in, part_val, part_idx, tok_buf;
+  DevBuf mask_enc, enc_tmp;  // a group's encoder mask / output when several groups share a decode
   uint64_t gen = 0;  // bumped by every buffer growth: invalidates captured graphs
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {
@@ -118,6 +119,12 @@ struct T5Model : mpr_model {
   int encode(const float* embeds, const float* mask, int B, int L, float* out, hipStream_t s);
   int generate(const float* embeds, const float* mask, int B, int L, int max_new, int start,
                int eos, int pad, int32_t* out_tokens, hipStream_t s, int slot = 0);
+  // generate() of ng <= 2 independent batches (<= 16 rows each) with one shared decode loop of
+  // up to 32 rows: each batch is encoded on its own (as generate() would), the decode runs
+  // over both; every batch's tokens are bit-identical to its own generate() call.
+  int generate_groups(int ng, const float* const* embeds, const float* const* masks,
+                      const int* Bs, const int* Ls, int max_new, int start, int eos, int pad,
+                      int32_t* const* outs, hipStream_t s, int slot = 0);
   int logits_tf(const float* embeds, const float* mask, int B, int L, const int32_t* dec_in,
                 int T, float* logits_out, hipStream_t s);
   int embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
@@ -131,6 +138,7 @@ struct T5Model : mpr_model {
   int grow(DevBuf& b, size_t bytes);
   int cross_kv_project(int B, int L, hipStream_t s);
   int encode_body(int B, int L, int max_new, int start, hipStream_t s);
+  int init_body(int B, int L, int max_new, int start, hipStream_t s);
   int decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s);
   template <class F>
   int graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body);

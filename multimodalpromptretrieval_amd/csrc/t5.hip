@@ -123,12 +123,16 @@ int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
 // Everything generate() enqueues after its inputs sit in enc_in / mask_in, in two parts: the
 // encoder (+ cross-attention K/V of every decoder layer, + the decode state reset) and the greedy
 // decode loop.  Only model-owned buffers are touched, so each part is captured into a graph and
-// replayed; the decode part can run on its own stream (a CU partition reserved for the
-// latency-bound decode chain, mpr_t5_set_decode_stream).
+// replayed; the decode part can run on its own stream (mpr_t5_set_decode_stream).
 int T5Model::encode_body(int B, int L, int max_new, int start, hipStream_t s) {
+  MPR_TRY(encode(ws->enc_in.as<float>(), ws->mask_in.as<float>(), B, L, ws->enc_out.as<float>(),
+                 s));
+  return init_body(B, L, max_new, start, s);
+}
+
+// Cross-attention K/V over enc_out [B, L] and the decode state reset.
+int T5Model::init_body(int B, int L, int max_new, int start, hipStream_t s) {
   const int T1 = max_new + 1;
-  const float* maskp = ws->mask_in.as<float>();
-  MPR_TRY(encode(ws->enc_in.as<float>(), maskp, B, L, ws->enc_out.as<float>(), s));
   MPR_TRY(cross_kv_project(B, L, s));
   MPR_TRY(fill_i32(ws->unfinished.as<int32_t>(), 1, B, s));
   MPR_TRY(fill_i32(ws->cur_tok.as<int32_t>(), start, B, s));
@@ -225,72 +229,129 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
 int T5Model::generate(const float* embeds, const float* mask, int B, int L, int max_new,
                       int start, int eos, int pad, int32_t* out_tokens, hipStream_t s,
                       int slot) {
+  return generate_groups(1, &embeds, &mask, &B, &L, max_new, start, eos, pad, &out_tokens, s,
+                         slot);
+}
+
+namespace {
+// [B, Lsrc] rows (row length `w` floats per position) into [B, Ldst] rows, zero beyond Lsrc.
+int stage_rows(float* dst, const float* src, int B, int Lsrc, int Ldst, int64_t w,
+               hipStream_t s) {
+  const size_t row = (size_t)w * 4;
+  if (Lsrc == Ldst)
+    MPR_HIP(hipMemcpyAsync(dst, src, (size_t)B * Lsrc * row, hipMemcpyDeviceToDevice, s));
+  else {
+    MPR_HIP(hipMemsetAsync(dst, 0, (size_t)B * Ldst * row, s));
+    MPR_HIP(hipMemcpy2DAsync(dst, (size_t)Ldst * row, src, (size_t)Lsrc * row, (size_t)Lsrc * row,
+                             B, hipMemcpyDeviceToDevice, s));
+  }
+  return MPR_OK;
+}
+}  // namespace
+
+int T5Model::generate_groups(int ng, const float* const* embeds, const float* const* masks,
+                             const int* Bs, const int* Ls, int max_new, int start, int eos,
+                             int pad, int32_t* const* outs, hipStream_t s, int slot) {
   MPR_TRY(use_slot(slot));
-  MPR_REQUIRE(B >= 0 && B <= 16, "t5 generate: batch %d > 16 unsupported by the decode path", B);
+  MPR_REQUIRE(ng >= 1 && ng <= 2, "t5 generate: %d batch groups (1 or 2)", ng);
   MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
   MPR_REQUIRE(max_new + 1 <= lut_radius, "t5 generate: max_new exceeds lut radius");
-  MPR_REQUIRE(2 * L <= lut_radius && L >= 1, "t5 generate: L=%d", L);
-  if (B == 0) return MPR_OK;
   // The source length is bucketed to a multiple of 8 (zero rows, mask 0) so a serving loop
   // with varying prompt lengths replays a few captured graphs instead of capturing one per
   // length.  Masked keys add exact zeros to every softmax sum and rows are independent in
-  // every other op, so the real rows' results are bit-identical.
-  const int Lsrc = L;
-  L = std::min((int)cdiv(L, 8) * 8, lut_radius / 2);
+  // every other op, so the real rows' results are bit-identical.  Groups sharing a decode are
+  // each encoded at their own bucket (the same launches as a generate() of their own) and
+  // then padded the same way to the longest one.
+  struct Grp {
+    const float *e, *m;
+    int B, L, Lb, row0;
+    int32_t* out;
+  } gr[2];
+  int n = 0, Btot = 0, Lp = 0;
+  int64_t Mg = 0;
+  for (int g = 0; g < ng; ++g) {
+    MPR_REQUIRE(Bs[g] >= 0 && Bs[g] <= 16, "t5 generate: batch %d > 16 unsupported by the decode path", Bs[g]);
+    if (Bs[g] == 0) continue;
+    MPR_REQUIRE(2 * Ls[g] <= lut_radius && Ls[g] >= 1, "t5 generate: L=%d", Ls[g]);
+    const int Lb = std::min((int)cdiv(Ls[g], 8) * 8, lut_radius / 2);
+    gr[n++] = Grp{embeds[g], masks[g], Bs[g], Ls[g], Lb, Btot, outs[g]};
+    Btot += Bs[g];
+    Lp = std::max(Lp, Lb);
+    Mg = std::max(Mg, (int64_t)Bs[g] * Lb);
+  }
+  if (n == 0) return MPR_OK;
+  const int L = Lp, B = Btot;
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
-  const int M = B * L, nparts = (int)cdiv(V, 16);
-  // Every buffer the body touches is sized before capture (no allocation inside a graph).
-  MPR_TRY(grow(ws->enc_in, (size_t)M * d * 4));
+  const int64_t M = (int64_t)B * L, Mx = std::max(M, Mg);
+  const int nparts = (int)cdiv(V, 16);
+  // Every buffer the bodies touch is sized before capture (no allocation inside a graph).
+  MPR_TRY(grow(ws->enc_in, (size_t)Mx * d * 4));
   MPR_TRY(grow(ws->mask_in, (size_t)M * 4));
   MPR_TRY(grow(ws->enc_out, (size_t)M * d * 4));
   MPR_TRY(grow(ws->cross_kv, (size_t)M * Ld * 2 * inner * 4));
-  MPR_TRY(grow(ws->x, (size_t)M * d * 4));
-  MPR_TRY(grow(ws->h, (size_t)M * d * 4));
-  MPR_TRY(grow(ws->qkv, (size_t)M * 3 * inner * 4));
-  MPR_TRY(grow(ws->ao, (size_t)M * (inner > dff ? inner : dff) * 4));
-  MPR_TRY(grow(ws->ff, (size_t)M * dff * 4));
+  MPR_TRY(grow(ws->x, (size_t)Mx * d * 4));
+  MPR_TRY(grow(ws->h, (size_t)Mx * d * 4));
+  MPR_TRY(grow(ws->qkv, (size_t)Mx * 3 * inner * 4));
+  MPR_TRY(grow(ws->ao, (size_t)Mx * (inner > dff ? inner : dff) * 4));
+  MPR_TRY(grow(ws->ff, (size_t)Mx * dff * 4));
   MPR_TRY(grow(ws->cache, (size_t)Ld * B * Tc * 3 * inner * 4));
   MPR_TRY(grow(ws->dx, (size_t)B * d * 4));
   MPR_TRY(grow(ws->dq, (size_t)B * inner * 4));
-  MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * 4));
-  MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * 4));
-  MPR_TRY(grow(ws->unfinished, (size_t)16 * 4));
-  MPR_TRY(grow(ws->cur_tok, (size_t)16 * 4));
+  MPR_TRY(grow(ws->part_val, (size_t)nparts * 32 * 4));
+  MPR_TRY(grow(ws->part_idx, (size_t)nparts * 32 * 4));
+  MPR_TRY(grow(ws->unfinished, (size_t)32 * 4));
+  MPR_TRY(grow(ws->cur_tok, (size_t)32 * 4));
   MPR_TRY(grow(ws->tok_buf, (size_t)B * T1 * 4));
-  if (L == Lsrc) {
-    MPR_HIP(hipMemcpyAsync(ws->enc_in.ptr, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
-    MPR_HIP(hipMemcpyAsync(ws->mask_in.ptr, mask, (size_t)M * 4, hipMemcpyDeviceToDevice, s));
+  if (n > 1) {
+    MPR_TRY(grow(ws->mask_enc, (size_t)Mg * 4));
+    MPR_TRY(grow(ws->enc_tmp, (size_t)Mg * d * 4));
+  }
+  const bool graphs = graphs_enabled();
+  auto run = [&](const GraphKey& key, hipStream_t st, auto&& body) -> int {
+    if (!graphs) return body(st);
+    hipGraphExec_t exec = nullptr;
+    MPR_TRY(graph_for(key, &exec, body));
+    MPR_HIP(hipGraphLaunch(exec, st));
+    return MPR_OK;
+  };
+  if (n == 1) {
+    const Grp& g = gr[0];
+    MPR_TRY(stage_rows(ws->enc_in.as<float>(), g.e, B, g.L, L, d, s));
+    MPR_TRY(stage_rows(ws->mask_in.as<float>(), g.m, B, g.L, L, 1, s));
+    MPR_TRY(run(std::make_tuple(0, B, L, max_new, start, 0), s,
+                [&](hipStream_t c) { return encode_body(B, L, max_new, start, c); }));
   } else {
-    MPR_HIP(hipMemsetAsync(ws->enc_in.ptr, 0, (size_t)M * d * 4, s));
+    float* eo = ws->enc_out.as<float>();
     MPR_HIP(hipMemsetAsync(ws->mask_in.ptr, 0, (size_t)M * 4, s));
-    MPR_HIP(hipMemcpy2DAsync(ws->enc_in.ptr, (size_t)L * d * 4, embeds, (size_t)Lsrc * d * 4,
-                             (size_t)Lsrc * d * 4, B, hipMemcpyDeviceToDevice, s));
-    MPR_HIP(hipMemcpy2DAsync(ws->mask_in.ptr, (size_t)L * 4, mask, (size_t)Lsrc * 4,
-                             (size_t)Lsrc * 4, B, hipMemcpyDeviceToDevice, s));
+    if (gr[0].Lb != gr[1].Lb) MPR_HIP(hipMemsetAsync(eo, 0, (size_t)M * d * 4, s));
+    for (int k = 0; k < n; ++k) {
+      const Grp& g = gr[k];
+      MPR_TRY(stage_rows(ws->enc_in.as<float>(), g.e, g.B, g.L, g.Lb, d, s));
+      MPR_TRY(stage_rows(ws->mask_enc.as<float>(), g.m, g.B, g.L, g.Lb, 1, s));
+      MPR_HIP(hipMemcpy2DAsync(ws->mask_in.as<float>() + (int64_t)g.row0 * L, (size_t)L * 4, g.m,
+                               (size_t)g.L * 4, (size_t)g.L * 4, g.B, hipMemcpyDeviceToDevice,
+                               s));
+      MPR_TRY(run(std::make_tuple(2, g.B, g.Lb, 0, 0, 0), s, [&](hipStream_t c) {
+        return encode(ws->enc_in.as<float>(), ws->mask_enc.as<float>(), g.B, g.Lb,
+                      ws->enc_tmp.as<float>(), c);
+      }));
+      MPR_HIP(hipMemcpy2DAsync(eo + (int64_t)g.row0 * L * d, (size_t)L * d * 4, ws->enc_tmp.ptr,
+                               (size_t)g.Lb * d * 4, (size_t)g.Lb * d * 4, g.B,
+                               hipMemcpyDeviceToDevice, s));
+    }
+    MPR_TRY(run(std::make_tuple(3, B, L, max_new, start, 0), s,
+                [&](hipStream_t c) { return init_body(B, L, max_new, start, c); }));
   }
   hipStream_t ds = ws->dec_stream ? ws->dec_stream : s;
-  if (!graphs_enabled()) {
-    MPR_TRY(encode_body(B, L, max_new, start, s));
-    if (ds != s) {
-      MPR_HIP(hipEventRecord(ws->ev_fork, s));
-      MPR_HIP(hipStreamWaitEvent(ds, ws->ev_fork, 0));
-    }
-    MPR_TRY(decode_body(B, L, max_new, eos, pad, ds));
-  } else {
-    hipGraphExec_t enc_exec = nullptr, dec_exec = nullptr;
-    MPR_TRY(graph_for(std::make_tuple(0, B, L, max_new, start, 0), &enc_exec,
-                      [&](hipStream_t c) { return encode_body(B, L, max_new, start, c); }));
-    MPR_TRY(graph_for(std::make_tuple(1, B, L, max_new, eos, pad), &dec_exec,
-                      [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
-    MPR_HIP(hipGraphLaunch(enc_exec, s));
-    if (ds != s) {
-      MPR_HIP(hipEventRecord(ws->ev_fork, s));
-      MPR_HIP(hipStreamWaitEvent(ds, ws->ev_fork, 0));
-    }
-    MPR_HIP(hipGraphLaunch(dec_exec, ds));
+  if (ds != s) {
+    MPR_HIP(hipEventRecord(ws->ev_fork, s));
+    MPR_HIP(hipStreamWaitEvent(ds, ws->ev_fork, 0));
   }
-  MPR_HIP(hipMemcpyAsync(out_tokens, ws->tok_buf.ptr, (size_t)B * T1 * 4, hipMemcpyDeviceToDevice,
-                         ds));
+  MPR_TRY(run(std::make_tuple(1, B, L, max_new, eos, pad), ds,
+              [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
+  for (int k = 0; k < n; ++k)
+    MPR_HIP(hipMemcpyAsync(gr[k].out, ws->tok_buf.as<int32_t>() + (int64_t)gr[k].row0 * T1,
+                           (size_t)gr[k].B * T1 * 4, hipMemcpyDeviceToDevice, ds));
   if (ds != s) {  // the caller's stream sees the tokens (and may reuse the buffers) after this
     MPR_HIP(hipEventRecord(ws->ev_join, ds));
     MPR_HIP(hipStreamWaitEvent(s, ws->ev_join, 0));

@@ -77,6 +77,7 @@ class VQARetrieval:
         self.is_training_phase = False
         self.index = None
         self.cache_enabled = True
+        self._prefetched = {}  # serving-loop lookahead: batch key -> enqueued search (prefetch)
         self._cache_key = None
         self._cache_val = None
         self._cache_ref = None
@@ -114,6 +115,56 @@ class VQARetrieval:
         other_out.record_stream(cur)
         self._pending_img = (batch["image"], q, tuple(batch["question"]))
         return other_out, s_img
+
+    def _key(self, batch):
+        # the batch's image tensor is kept alive by whoever holds the key, so an equal id() means
+        # the same object
+        return (id(batch["image"]), tuple(batch["question"]), self.retrieval_k,
+                self.is_training_phase)
+
+    def prefetch(self, batch, other_vit=None, other_mode: int = CLS):
+        """Serving-loop lookahead: enqueue all of ``batch``'s device-side retrieval work — the
+        query towers (in lockstep with ``other_vit`` over the same images when given, as
+        ``encode_image_pair``), the index scan, and the copy of its top-k into pinned host
+        memory — on the retrieval stream, and return without waiting.  The next
+        ``retrieve_closest_qa_pairs(batch)`` waits for that copy only, so a caller can enqueue
+        batch i+1's towers before it blocks on batch i's retrieval result.  Returns
+        (``other_vit``'s output or None, an event recorded after the towers: wait on it, not on
+        the stream, which by then may hold the next batch's work)."""
+        if self.index is None:
+            raise RuntimeError("create_retrieval_dataset() / set_index() first")
+        s_img = self._streams()
+        cur = torch.cuda.current_stream(self.device)
+        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+        toks = self.clip_tokenize(batch["question"])
+        B = img.shape[0]
+        q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
+        di = self.image_encoder.out_dim
+        kk = self.retrieval_k + (1 if self.is_training_phase else 0)
+        s_img.wait_stream(cur)
+        img.record_stream(s_img)
+        q.record_stream(s_img)
+        host = done = None
+        with torch.cuda.stream(s_img):
+            _, other_out, _ = encode_towers(
+                self.image_encoder, img, CLS, out_a=q, out_a_bstride=self.embed_dim,
+                vit_b=other_vit, mode_b=other_mode, text=self.text_encoder, tokens=toks,
+                out_t=q[:, di:], out_t_bstride=self.embed_dim)
+            towers = torch.cuda.Event()
+            towers.record(s_img)
+            if isinstance(self.index, DeviceIndex):  # a sharded search exchanges: done in _topk
+                dist, ids = self.index.search(q, kk)
+                both = torch.cat([ids.to(torch.float64), dist.to(torch.float64)], 1)
+                host = torch.empty(both.shape, dtype=torch.float64, pin_memory=True)
+                host.copy_(both, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(s_img)
+        if other_out is not None:
+            other_out.record_stream(cur)
+        while len(self._prefetched) >= 8:  # never consumed (an abandoned loop): drop the oldest
+            self._prefetched.pop(next(iter(self._prefetched)))
+        self._prefetched[self._key(batch)] = (host, done, q, towers, kk, batch["image"])
+        return other_out, towers
 
     def encode_queries(self, batch) -> torch.Tensor:
         """[CLS image embedding ‖ EOT text embedding] fp32 [B, 1024] on the device
@@ -208,17 +259,24 @@ class VQARetrieval:
     def _topk(self, batch):
         """(dists [B, s+k], ids [B, s+k]) as host numpy, s = 1 in the training phase.  Cached
         while the same batch object (same images, same questions) is queried again."""
-        # the cached image tensor is kept alive, so an equal id() means the same object
-        key = (id(batch["image"]), tuple(batch["question"]), self.retrieval_k,
-               self.is_training_phase)
+        key = self._key(batch)
         if self.cache_enabled and key == self._cache_key:
             return self._cache_val
         if self.index is None:
             raise RuntimeError("create_retrieval_dataset() / set_index() first")
-        q = self.encode_queries(batch)
         kk = self.retrieval_k + (1 if self.is_training_phase else 0)
-        dist, ids = self.index.search(q, kk)
-        both = torch.cat([ids.to(torch.float64), dist.to(torch.float64)], 1).cpu().numpy()
+        pre = self._prefetched.pop(key, None)
+        if pre is not None and pre[0] is not None:  # prefetch(): scan + copy already enqueued
+            pre[1].synchronize()
+            both = pre[0].numpy()
+        else:
+            if pre is not None:  # towers enqueued by prefetch(), the (sharded) search here
+                q = pre[2]
+                torch.cuda.current_stream(self.device).wait_event(pre[3])
+            else:
+                q = self.encode_queries(batch)
+            dist, ids = self.index.search(q, kk)
+            both = torch.cat([ids.to(torch.float64), dist.to(torch.float64)], 1).cpu().numpy()
         val = (both[:, kk:].astype(np.float32), both[:, :kk].astype(np.int64))
         self._cache_key, self._cache_val, self._cache_ref = key, val, batch["image"]
         return val

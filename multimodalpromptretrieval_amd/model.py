@@ -17,6 +17,8 @@ untrained 512->1024 projection raise NotImplementedError; ``predict(output_atten
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -224,7 +226,20 @@ class T5VisionModel(nn.Module):
                 and (enc.width, enc.patch, enc.image_size, enc.layers)
                 == (vit.width, vit.patch, vit.image_size, vit.layers))
 
-    def prepare_input(self, batch):
+    def _prefetch(self, batch):
+        """Serving-loop lookahead: with a ``VQARetrieval`` retrieval function, enqueue the
+        batch's towers (the token-feature ViT paired with the retrieval's when pairable), index
+        scan and top-k copy now (``VQARetrieval.prefetch``); ``prepare_input(batch, _pre=...)``
+        then only waits for them.  None when there is nothing to prefetch."""
+        retr = getattr(self.retrieval_function, "__self__", None)
+        fn = getattr(retr, "prefetch", None)
+        if fn is None or getattr(retr, "index", None) is None:
+            return None
+        vit = self._device_vit()
+        other = vit if self.use_image_info and self._pairable(retr, vit) else None
+        return fn(batch, other, TOKENS)
+
+    def prepare_input(self, batch, _pre=None):
         """architectures/T5VisionModel.py:141-184.
 
         The token-feature ViT does not depend on retrieval, so it is enqueued first on a side
@@ -241,10 +256,13 @@ class T5VisionModel(nn.Module):
         cur = torch.cuda.current_stream(self.device)
         img_tok = None
         tok_stream = None
+        tok_event = None
         if self.use_image_info:
             retr = getattr(self.retrieval_function, "__self__", None)
             pair = getattr(retr, "encode_image_pair", None)
-            if pair is not None and self._pairable(retr, vit):
+            if _pre is not None and _pre[0] is not None:
+                img_tok, tok_event = _pre  # enqueued by _prefetch with the retrieval towers
+            elif pair is not None and self._pairable(retr, vit):
                 # the retrieval's encode_image and this tower see the same images: one paired
                 # pass (shared launches), the retrieval picks its half up in encode_queries
                 img_tok, tok_stream = pair(batch, vit, TOKENS)
@@ -276,7 +294,10 @@ class T5VisionModel(nn.Module):
         T = vit.tokens if self.use_image_info else 0
         combined = torch.empty((B, T + L, t5.d_model), device=self.device, dtype=torch.float32)
         if self.use_image_info:
-            cur.wait_stream(tok_stream)
+            if tok_event is not None:
+                cur.wait_event(tok_event)
+            else:
+                cur.wait_stream(tok_stream)
             img_tok.record_stream(cur)
             combined[:, :T].copy_(img_tok)
         t5.embed(ids, combined, row0=T)
@@ -302,43 +323,98 @@ class T5VisionModel(nn.Module):
                                           do_sample=False, max_new_tokens=self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
-    def predict_many(self, batches, decodes_in_flight: int = 2):
-        """predict() over an iterable of batches as a serving pipeline: up to
-        ``decodes_in_flight`` batches decode at once (each on its own stream and T5 workspace
-        slot; a greedy decode is a chain of small latency-bound launches that leaves most of the
-        chip idle), while the next batch's image towers, question tower and index scan run beside
-        them and the host builds its prompts.  Yields each batch's answers in order; every batch
-        gets exactly the work and the result predict() gives it."""
+    def predict_many(self, batches, decodes_in_flight: int = 2, pair_decodes=None,
+                     lookahead=None):
+        """predict() over an iterable of batches as a serving pipeline.  A greedy decode is a
+        chain of small latency-bound launches that leaves most of the chip idle, so
+        (1) with ``pair_decodes`` (default on; MPR_PAIR_DECODE=0 turns it off) two consecutive
+        batches share one decode loop: each is encoded as predict() would, then their rows step
+        together, reading every decode weight once per step for both (mpr_t5_generate_pair);
+        (2) up to ``decodes_in_flight`` of those generate calls run at once, each on its own
+        stream and T5 workspace slot, while the next batches' image towers, question tower and
+        index scan run beside them and the host builds its prompts;
+        (3) with ``lookahead`` (default on; MPR_LOOKAHEAD=0 turns it off), batch i+1's towers, scan and top-k copy are enqueued before the
+        host blocks on batch i's retrieval result, so the towers never wait on the host.
+        Yields each batch's answers in order; every batch gets exactly the result predict()
+        gives it."""
         from collections import deque
         depth = max(1, min(int(decodes_in_flight), 4))
+        if pair_decodes is None:
+            pair_decodes = os.environ.get("MPR_PAIR_DECODE", "1") != "0"
+        if lookahead is None:
+            lookahead = os.environ.get("MPR_LOOKAHEAD", "1") != "0"
         if not hasattr(self, "_s_prep"):
             self._s_prep = torch.cuda.Stream(self.device)
         if not hasattr(self, "_s_gen"):
             self._s_gen = []
         while len(self._s_gen) < depth:
             self._s_gen.append(_lib.role_stream(self.device, f"gen:{len(self._s_gen)}"))
-        pending = deque()
-        for i, batch in enumerate(batches):
-            self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self._s_prep):
-                combined, mask, _ = self.prepare_input(batch)
-            slot = i % depth
+        pending = deque()  # one entry per generate call: [(host tokens, done event), ...]
+        held = None        # a prepared batch waiting for its decode partner
+        calls = 0
+
+        def launch(inputs):
+            nonlocal calls
+            slot = calls % depth
+            calls += 1
             sg = self._s_gen[slot]
             sg.wait_stream(self._s_prep)
             with torch.cuda.stream(sg):
-                combined.record_stream(sg)
-                mask.record_stream(sg)
+                for combined, mask in inputs:
+                    combined.record_stream(sg)
+                    mask.record_stream(sg)
                 t5 = self._device_t5()
-                toks = t5.generate_padded(combined, mask, self.max_new_tokens, slot=slot)
-                host = torch.empty(toks.shape, dtype=toks.dtype, pin_memory=True)
-                host.copy_(toks, non_blocking=True)
+                if len(inputs) == 2:
+                    toks = t5.generate_pair_padded(*inputs[0], *inputs[1], self.max_new_tokens,
+                                                   slot=slot)
+                else:
+                    toks = (t5.generate_padded(*inputs[0], self.max_new_tokens, slot=slot),)
+                hosts = []
+                for t in toks:
+                    host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                    host.copy_(t, non_blocking=True)
+                    hosts.append(host)
                 done = torch.cuda.Event()
                 done.record(sg)
-            pending.append((host, done))
-            if len(pending) > depth:  # batch i - depth is (nearly) done by now
-                yield self._finish(*pending.popleft())
+            pending.append([(h, done) for h in hosts])
+
+        def prefetch(b):
+            self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._s_prep):
+                return self._prefetch(b)
+
+        it = iter(batches)
+        nxt = next(it, None)
+        nxt_pre = prefetch(nxt) if nxt is not None and lookahead else None
+        while nxt is not None:
+            batch, pre = nxt, nxt_pre
+            nxt = next(it, None)
+            # the next batch's towers and scan go on the device before the host blocks on this
+            # batch's retrieval result
+            nxt_pre = prefetch(nxt) if nxt is not None and lookahead else None
+            self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._s_prep):
+                combined, mask, _ = self.prepare_input(batch, _pre=pre)
+            cur = (combined, mask)
+            if pair_decodes and combined.shape[0] <= 16:
+                if held is None:
+                    held = cur
+                    continue
+                launch([held, cur])
+                held = None
+            else:
+                if held is not None:
+                    launch([held])
+                    held = None
+                launch([cur])
+            while len(pending) > depth:  # the oldest call is (nearly) done by now
+                for item in pending.popleft():
+                    yield self._finish(*item)
+        if held is not None:
+            launch([held])
         while pending:
-            yield self._finish(*pending.popleft())
+            for item in pending.popleft():
+                yield self._finish(*item)
 
     def _finish(self, host_tokens, done):
         done.synchronize()  # this batch's tokens only; the next batch keeps running

@@ -157,6 +157,24 @@ class DeviceT5:
                   int(pad_token_id), _lib.ptr(out), self._stream())
         return out
 
+    def generate_pair_padded(self, embeds_a, mask_a, embeds_b, mask_b, max_new_tokens=20,
+                             decoder_start_token_id=0, eos_token_id=1, pad_token_id=0,
+                             slot: int = 0):
+        """generate_padded() of two batches with one shared decode loop (mpr_t5_generate_pair):
+        ([B_a, 1+max_new], [B_b, 1+max_new]) int32, each bit-identical to its own call."""
+        ea, ma = self._inputs(embeds_a, mask_a)
+        eb, mb = self._inputs(embeds_b, mask_b)
+        (Ba, La, _), (Bb, Lb, _) = ea.shape, eb.shape
+        if Ba > 16 or Bb > 16:
+            raise ValueError(f"generate_pair: batches of {Ba} and {Bb} rows (at most 16 each)")
+        oa = torch.empty((Ba, max_new_tokens + 1), device=self.device, dtype=torch.int32)
+        ob = torch.empty((Bb, max_new_tokens + 1), device=self.device, dtype=torch.int32)
+        _lib.call("mpr_t5_generate_pair", self._h, int(slot), _lib.ptr(ea), _lib.ptr(ma), Ba, La,
+                  _lib.ptr(eb), _lib.ptr(mb), Bb, Lb, int(max_new_tokens),
+                  int(decoder_start_token_id), int(eos_token_id), int(pad_token_id),
+                  _lib.ptr(oa), _lib.ptr(ob), self._stream())
+        return oa, ob
+
     @staticmethod
     def trim(tokens: torch.Tensor, eos_token_id: int = 1) -> torch.Tensor:
         """Cut the padded token matrix where GenerationMixin stops (all rows finished)."""

@@ -124,8 +124,9 @@ def test_g2_pipeline_product(device):
 
 
 def test_g2_predict_many_matches_predict(device):
-    """The serving pipeline (1-3 decodes in flight) returns, per batch, exactly predict()'s answers (batches
-    of different prompt lengths and images in flight together; the first is the golden one)."""
+    """The serving pipeline (1-3 generate calls in flight, batch pairs sharing a decode loop or
+    not) returns, per batch, exactly predict()'s answers (batches of different prompt lengths
+    and images in flight together; the first is the golden one)."""
     from multimodalpromptretrieval_amd.dataset import VQARetrieval
     from multimodalpromptretrieval_amd.model import T5VisionModel
     with open(os.path.join(GOLD, "g2_pipeline.json")) as f:
@@ -149,6 +150,9 @@ def test_g2_predict_many_matches_predict(device):
     assert list(model.predict_many(batches)) == want
     for depth in (1, 3):  # decodes in flight on separate workspace slots
         assert list(model.predict_many(batches, depth)) == want
+        assert list(model.predict_many(batches, depth, pair_decodes=False)) == want
+        assert list(model.predict_many(batches, depth, lookahead=False)) == want
+    assert list(model.predict_many(batches[:3])) == want[:3]  # an unpaired last batch
     assert list(model.predict_many(iter(batches[:1]))) == want[:1]
     assert list(model.predict_many([])) == []
 

@@ -241,6 +241,44 @@ def test_t5_generate_on_decode_stream(device, t5_sd):
     assert torch.equal(a, b) and torch.equal(c, a[:2])
 
 
+def _t5_batch(t5_sd, b, seed, extra=0):
+    ids, mask, img_tok = _t5_inputs(b, seed)
+    if extra:  # a longer prompt (another length bucket): trailing padding tokens, mask 0
+        ids = torch.cat([ids, torch.zeros(b, extra, dtype=ids.dtype)], 1)
+        mask = torch.cat([mask, torch.zeros(b, extra, dtype=mask.dtype)], 1)
+    emb = torch.cat([img_tok, t5_sd["shared.weight"][ids]], 1)
+    fm = torch.cat([torch.ones(b, 50, dtype=torch.long), mask], 1)
+    return emb, fm
+
+
+@pytest.mark.parametrize("graphs", ["1", "0"])
+def test_t5_generate_pair_matches_single(device, t5_sd, monkeypatch, graphs):
+    """Two batches through one shared decode loop (up to 32 rows: the two-row-group skinny
+    GEMMs, a 32-row greedy step): each batch's tokens are bit-identical to its own generate,
+    with equal and different source-length buckets, either batch the longer, 16 + 16 rows, and an
+    empty second batch."""
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    monkeypatch.setenv("MPR_GRAPHS", graphs)
+    m = DeviceT5(t5_sd, device)
+    A = _t5_batch(t5_sd, 7, 61)
+    B = _t5_batch(t5_sd, 9, 62, extra=19)
+    C = _t5_batch(t5_sd, 16, 63)
+    D = _t5_batch(t5_sd, 16, 64, extra=8)
+    single = {k: m.generate_padded(*v, 20).cpu() for k, v in
+              {"A": A, "B": B, "C": C, "D": D}.items()}
+    assert A[0].shape[1] != B[0].shape[1]
+    for x, y in (("A", "B"), ("B", "A"), ("C", "D"), ("A", "A")):
+        va, vb = {"A": A, "B": B, "C": C, "D": D}[x], {"A": A, "B": B, "C": C, "D": D}[y]
+        oa, ob = m.generate_pair_padded(*va, *vb, 20, slot=1)
+        assert torch.equal(oa.cpu(), single[x]), (x, y)
+        assert torch.equal(ob.cpu(), single[y]), (x, y)
+    e = (A[0][:0], A[1][:0])
+    oa, ob = m.generate_pair_padded(*A, *e, 20)
+    assert torch.equal(oa.cpu(), single["A"]) and ob.shape == (0, 21)
+    oa, ob = m.generate_pair_padded(*B, *A, 5, slot=2)  # fewer steps: a prefix of the same greedy run
+    assert torch.equal(oa.cpu(), single["B"][:, :6]) and torch.equal(ob.cpu(), single["A"][:, :6])
+
+
 def test_t5_embed_and_loss(device, t5_sd):
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     m = DeviceT5(t5_sd, device)

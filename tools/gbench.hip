@@ -73,15 +73,17 @@ int main() {
   using L = std::function<int(const GemmGroup&, hipStream_t)>;
   struct Var { const char* name; L fn; };
   const Var vars[] = {
-      {"64x64 k32 D2", launch_gemm_group<64, 64, 1, 1, 32, 2, 1>},
-      {"64x64 k64 D1", launch_gemm_group<64, 64, 1, 1, 64, 1, 1>},
-      {"64x64 k64 D2", launch_gemm_group<64, 64, 1, 1, 64, 2, 1>},
-      {"64x64 k32 D2 W2", launch_gemm_group<64, 64, 1, 1, 32, 2, 2>},
-      {"64x64 k64 D1 W2", launch_gemm_group<64, 64, 1, 1, 64, 1, 2>},
-      {"64x64 k64 D2 W2", launch_gemm_group<64, 64, 1, 1, 64, 2, 2>},
-      {"32x64 k64 D2 W2", launch_gemm_group<32, 64, 1, 1, 64, 2, 2>},
+      {"64x64 k32 D2 XR", launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>},
       {"32x32 k64 D2 W4", launch_gemm_group<32, 32, 1, 1, 64, 2, 4>},
-      {"128x64 k32 D2", launch_gemm_group<128, 64, 2, 1, 32, 2, 1>},
+      {"64x64 2x2/w k32 D2", launch_gemm_group<64, 64, 2, 2, 32, 2, 1, true>},
+      {"64x64 2x2/w k32 D2 W2", launch_gemm_group<64, 64, 2, 2, 32, 2, 2, true>},
+      {"64x64 2x2/w k64 D2 W4", launch_gemm_group<64, 64, 2, 2, 64, 2, 4, true>},
+      {"64x64 1x2/w k32 D2", launch_gemm_group<64, 64, 1, 2, 32, 2, 1, true>},
+      {"64x64 1x2/w k32 D2 W2", launch_gemm_group<64, 64, 1, 2, 32, 2, 2, true>},
+      {"64x128 1x2/w k32 D2", launch_gemm_group<64, 128, 1, 2, 32, 2, 1, true>},
+      {"128x64 2x1/w k32 D2", launch_gemm_group<128, 64, 2, 1, 32, 2, 1, true>},
+      {"128x128 2x2/w k32 D2", launch_gemm_group<128, 128, 2, 2, 32, 2, 1, true>},
+      {"64x64 2x2/w k16 D2 W1", launch_gemm_group<64, 64, 2, 2, 16, 2, 1, true>},
   };
   for (const Shape& sh : shapes) {
     for (int grp = 1; grp <= 2; ++grp) {

@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from multimodalpromptretrieval_amd import encoders, index, t5  # noqa: E402
+from multimodalpromptretrieval_amd import dataset, encoders, index, t5  # noqa: E402
+from multimodalpromptretrieval_amd import model as model_mod  # noqa: E402
 
 RECS = []
 
@@ -42,11 +43,41 @@ def wrap(cls, name, label):
         cls.__call__ = f
 
 
+def wrap_fn(mod, name, label):
+    """Same for a module-level function (looked up through `mod` by its callers)."""
+    orig = getattr(mod, name)
+
+    def f(*a, **kw):
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        h0 = time.perf_counter()
+        e0.record(s)
+        out = orig(*a, **kw)
+        e1.record(s)
+        RECS.append((label, s.stream_id, e0, e1, h0, time.perf_counter()))
+        return out
+
+    setattr(mod, name, f)
+
+
+def wrap_host(cls, name, label):
+    """Host time only (no events): e.g. prepare_input, which blocks on the retrieval result."""
+    orig = getattr(cls, name)
+
+    def f(self, *a, **kw):
+        h0 = time.perf_counter()
+        out = orig(self, *a, **kw)
+        RECS.append((label, None, None, None, h0, time.perf_counter()))
+        return out
+
+    setattr(cls, name, f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pipelined", action="store_true",
-                    help="time predict_many (two batches in flight) instead of predict()")
+                    help="time predict_many (the serving loop) instead of predict()")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -58,6 +89,9 @@ def main():
     wrap(encoders.DeviceCLIPText, "forward", "text")
     wrap(index.DeviceIndex, "search", "scan")
     wrap(t5.DeviceT5, "generate_padded", "t5.generate")
+    wrap(t5.DeviceT5, "generate_pair_padded", "t5.gen-pair")
+    wrap_fn(dataset, "encode_towers", "towers")
+    wrap_host(model_mod.T5VisionModel, "prepare_input", "prepare(host)")
     if args.pipelined:
         with torch.no_grad():
             for _ in model.predict_many(batches[i % 4] for i in range(4)):
@@ -75,9 +109,10 @@ def main():
             torch.cuda.synchronize()
             print(f"{args.steps} pipelined steps: host {1e3 * (time.perf_counter() - h_ref):.3f} ms")
             for tag, sid, e0, e1, h0, h1 in RECS:
-                print(f"  {tag:14s} stream {sid:>4}  host {1e3 * (h0 - h_ref):8.3f}->"
-                      f"{1e3 * (h1 - h_ref):8.3f}  dev {ref.elapsed_time(e0):8.3f}->"
-                      f"{ref.elapsed_time(e1):8.3f} ms")
+                dev = ("" if e0 is None else
+                       f"  dev {ref.elapsed_time(e0):8.3f}->{ref.elapsed_time(e1):8.3f}")
+                print(f"  {tag:14s} stream {str(sid):>4}  host {1e3 * (h0 - h_ref):8.3f}->"
+                      f"{1e3 * (h1 - h_ref):8.3f}{dev} ms")
         return
     with torch.no_grad():
         for i in range(3):
@@ -96,9 +131,10 @@ def main():
             h_end = time.perf_counter()
             print(f"step {i}: host {1e3 * (h_end - h_ref):.3f} ms")
             for tag, sid, e0, e1, h0, h1 in RECS:
-                print(f"  {tag:14s} stream {sid:>4}  host {1e3 * (h0 - h_ref):8.3f}->"
-                      f"{1e3 * (h1 - h_ref):8.3f}  dev {ref.elapsed_time(e0):8.3f}->"
-                      f"{ref.elapsed_time(e1):8.3f} ms")
+                dev = ("" if e0 is None else
+                       f"  dev {ref.elapsed_time(e0):8.3f}->{ref.elapsed_time(e1):8.3f}")
+                print(f"  {tag:14s} stream {str(sid):>4}  host {1e3 * (h0 - h_ref):8.3f}->"
+                      f"{1e3 * (h1 - h_ref):8.3f}{dev} ms")
 
 
 if __name__ == "__main__":
