@@ -105,12 +105,15 @@ int mpr_vit_forward_pair(mpr_model* a, int32_t mode_a, float* out_a_dev, int64_t
  * (text may be null), as mpr_vit_forward_pair + mpr_clip_text_forward — the reference's
  * encode_image / get_image_token_features / encode_text of one batch
  * (dataset/VQAFeatureDataset.py:189-190, architectures/T5VisionModel.py:112-139).  Results are
- * bit-identical to the separate calls; each layer's projections share launches. */
+ * bit-identical to the separate calls; each layer's projections share launches.  `slot`
+ * (0 <= slot < 4; the single-model calls use 0) picks each model's activation workspace: passes
+ * on different slots may be in flight at once (two batches' towers on two streams); passes on
+ * one slot must be ordered by their streams. */
 int mpr_encode_towers(mpr_model* vit_a, int32_t mode_a, float* out_a_dev, int64_t out_a_bstride,
                       mpr_model* vit_b, int32_t mode_b, float* out_b_dev, int64_t out_b_bstride,
                       const float* img_dev, int32_t n_images, mpr_model* text,
                       const int32_t* tok_dev, int32_t n_texts, int32_t seq_len, float* out_t_dev,
-                      int64_t out_t_bstride, void* stream);
+                      int64_t out_t_bstride, int32_t slot, void* stream);
 
 /* ---- CLIP text encoder: dataset/VQAFeatureDataset.py:190 (clip_model.encode_text) -----------
  * cfg = {width, layers, heads, context_length, vocab, out_dim}.  tensors: token_embedding

@@ -44,7 +44,7 @@ SIGNATURES = [
                                        c_void_p, c_int64, c_void_p, c_int32, c_void_p]),
     ("mpr_encode_towers", c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int32,
                                     c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p,
-                                    c_int32, c_int32, c_void_p, c_int64, c_void_p]),
+                                    c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p]),
     ("mpr_clip_text_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32,
                                        POINTER(c_void_p)]),
     ("mpr_clip_text_forward", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64,

@@ -219,14 +219,14 @@ int mpr_vit_forward_pair(mpr_model* a, int32_t mode_a, float* out_a, int64_t out
                          mpr_model* b, int32_t mode_b, float* out_b, int64_t out_b_bs,
                          const float* img, int32_t batch, void* stream) {
   return mpr_encode_towers(a, mode_a, out_a, out_a_bs, b, mode_b, out_b, out_b_bs, img, batch,
-                           nullptr, nullptr, 0, 0, nullptr, 0, stream);
+                           nullptr, nullptr, 0, 0, nullptr, 0, 0, stream);
 }
 
 int mpr_encode_towers(mpr_model* vit_a, int32_t mode_a, float* out_a, int64_t out_a_bs,
                       mpr_model* vit_b, int32_t mode_b, float* out_b, int64_t out_b_bs,
                       const float* img, int32_t n_images, mpr_model* text, const int32_t* tok,
                       int32_t n_texts, int32_t seq_len, float* out_t, int64_t out_t_bs,
-                      void* stream) {
+                      int32_t slot, void* stream) {
   return guarded([&]() -> int {
     MPR_REQUIRE(!vit_a || vit_a->kind == mpr_model::VIT, "encode_towers: vit_a not a ViT");
     MPR_REQUIRE(!vit_b || vit_b->kind == mpr_model::VIT, "encode_towers: vit_b not a ViT");
@@ -239,7 +239,7 @@ int mpr_encode_towers(mpr_model* vit_a, int32_t mode_a, float* out_a, int64_t ou
     const int64_t bs[2] = {out_a_bs, out_b_bs};
     const int nv = vit_b ? 2 : (vit_a ? 1 : 0);
     return encode_towers(v, modes, outs, bs, nv, img, n_images, static_cast<TextModel*>(text),
-                         tok, n_texts, seq_len, out_t, out_t_bs, S(stream));
+                         tok, n_texts, seq_len, out_t, out_t_bs, S(stream), slot);
   });
 }
 

@@ -43,11 +43,6 @@ int ClipTower::load_blocks(const float* const* t, int w, int nl) {
   return MPR_OK;
 }
 
-int ClipTower::run(float* x, int B, int L, bool causal, hipStream_t s) {
-  TowerRun r{this, x, B, L, causal};
-  return run_group(&r, 1, s);
-}
-
 // n CLIP transformers with the same layer count stepped in lockstep (the retrieval ViT, the
 // token-feature ViT and the CLIP text tower of a batch): every projection of layer l is one
 // grouped GEMM launch over the towers (split by tile choice, gemm_group); per tower its own
@@ -56,12 +51,13 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
   MPR_REQUIRE(n >= 1 && n <= GEMM_GROUP, "clip tower group: n=%d", n);
   for (int i = 0; i < n; ++i) {
     ClipTower& t = *r[i].t;
+    TowerWs& w = *r[i].w;
     MPR_REQUIRE(t.layers == r[0].t->layers, "clip tower group: towers differ in depth");
     const size_t M = (size_t)r[i].B * r[i].L, W = t.width;
-    MPR_TRY(t.h.ensure(M * W * 4));
-    MPR_TRY(t.qkv.ensure(M * 3 * W * 4));
-    MPR_TRY(t.ao.ensure(M * W * 4));
-    MPR_TRY(t.mlp.ensure(M * 4 * W * 4));
+    MPR_TRY(w.h.ensure(M * W * 4));
+    MPR_TRY(w.qkv.ensure(M * 3 * W * 4));
+    MPR_TRY(w.ao.ensure(M * W * 4));
+    MPR_TRY(w.mlp.ensure(M * 4 * W * 4));
   }
   for (int l = 0; l < r[0].t->layers; ++l) {
     GemmGroup gq, go, gf, gp;
@@ -71,10 +67,10 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       const ClipBlock& b = *t.blocks[l];
       const int W = t.width, M = r[i].B * r[i].L;
       float* x = r[i].x;
-      float* hp = t.h.as<float>();
-      float* qp = t.qkv.as<float>();
-      float* ap = t.ao.as<float>();
-      float* mp = t.mlp.as<float>();
+      float* hp = r[i].w->h.as<float>();
+      float* qp = r[i].w->qkv.as<float>();
+      float* ap = r[i].w->ao.as<float>();
+      float* mp = r[i].w->mlp.as<float>();
       GemmArgs& g = gq.g[i];
       g.A = hp; g.lda = W; g.W = b.in_w.as<float>(); g.ldw = W; g.bias = b.in_b.as<float>();
       g.C = qp; g.ldc = 3 * W; g.M = M; g.N = 3 * W; g.K = W;
@@ -94,18 +90,18 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       const ClipBlock& b = *t.blocks[l];
       const int W = t.width;
       MPR_TRY(layernorm(r[i].x, W, r[i].B * r[i].L, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(),
-                        CLIP_LN_EPS, t.h.as<float>(), W, s));
+                        CLIP_LN_EPS, r[i].w->h.as<float>(), W, s));
     }
     MPR_TRY(gemm_group(gq, s));
     for (int i = 0; i < n; ++i) {
       ClipTower& t = *r[i].t;
       const int W = t.width, L = r[i].L;
-      float* qp = t.qkv.as<float>();
+      float* qp = r[i].w->qkv.as<float>();
       AttnArgs at;
       at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
       at.k = qp + W; at.k_bs = at.q_bs; at.k_rs = 3 * W;
       at.v = qp + 2 * W; at.v_bs = at.q_bs; at.v_rs = 3 * W;
-      at.o = t.ao.as<float>(); at.o_bs = (int64_t)L * W; at.o_rs = W;
+      at.o = r[i].w->ao.as<float>(); at.o_bs = (int64_t)L * W; at.o_rs = W;
       at.B = r[i].B; at.H = t.heads; at.Lq = L; at.Lk = L;
       at.scale = 0.125f;  // 64 ** -0.5, exact power of two
       at.causal = r[i].causal ? 1 : 0;
@@ -117,7 +113,7 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       const ClipBlock& b = *t.blocks[l];
       const int W = t.width;
       MPR_TRY(layernorm(r[i].x, W, r[i].B * r[i].L, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(),
-                        CLIP_LN_EPS, t.h.as<float>(), W, s));
+                        CLIP_LN_EPS, r[i].w->h.as<float>(), W, s));
     }
     MPR_TRY(gemm_group(gf, s));
     MPR_TRY(gemm_group(gp, s));
@@ -144,8 +140,10 @@ int TextModel::forward(const int32_t* tok, int B, int L, float* out, int64_t out
 int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
                   const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
                   const int32_t* tok, int Bt, int Lt, float* out_t, int64_t out_t_bs,
-                  hipStream_t s) {
+                  hipStream_t s, int slot) {
   MPR_REQUIRE(nv >= 0 && nv <= 2, "encode_towers: %d ViTs", nv);
+  MPR_REQUIRE(slot >= 0 && slot < TOWER_SLOTS, "encode_towers: slot %d outside [0, %d)", slot,
+              TOWER_SLOTS);
   for (int i = 0; i < nv; ++i) {
     MPR_REQUIRE(modes[i] == 0 || modes[i] == 1, "vit: mode must be 0 (CLS) or 1 (tokens)");
     MPR_REQUIRE(v[i]->width == v[0]->width && v[i]->patch == v[0]->patch &&
@@ -165,38 +163,42 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
   if (nv > 0) {
     VitModel& a0 = *v[0];
     const int W = a0.width, g2 = a0.grid * a0.grid, T = g2 + 1, P = 3 * a0.patch * a0.patch;
-    MPR_TRY(a0.cols.ensure((size_t)B * g2 * P * 4));
+    DevBuf& cols = a0.ws[slot].cols;
+    MPR_TRY(cols.ensure((size_t)B * g2 * P * 4));
     for (int i = 0; i < nv; ++i) {
-      MPR_TRY(v[i]->patches.ensure((size_t)B * g2 * W * 4));
-      MPR_TRY(v[i]->x.ensure((size_t)B * T * W * 4));
-      MPR_TRY(v[i]->tmp.ensure((size_t)B * T * W * 4));
+      TowerWs& w = v[i]->ws[slot];
+      MPR_TRY(w.patches.ensure((size_t)B * g2 * W * 4));
+      MPR_TRY(w.x.ensure((size_t)B * T * W * 4));
+      MPR_TRY(w.tmp.ensure((size_t)B * T * W * 4));
     }
-    MPR_TRY(im2col_patches(img, B, a0.image, a0.patch, a0.cols.as<float>(), s));
+    MPR_TRY(im2col_patches(img, B, a0.image, a0.patch, cols.as<float>(), s));
     GemmGroup pe;
     pe.n = nv;
     for (int i = 0; i < nv; ++i) {
       GemmArgs& g = pe.g[i];
-      g.A = a0.cols.as<float>(); g.lda = P; g.W = v[i]->conv_w.as<float>(); g.ldw = P;
-      g.C = v[i]->patches.as<float>(); g.ldc = W; g.M = B * g2; g.N = W; g.K = P;
+      g.A = cols.as<float>(); g.lda = P; g.W = v[i]->conv_w.as<float>(); g.ldw = P;
+      g.C = v[i]->ws[slot].patches.as<float>(); g.ldc = W; g.M = B * g2; g.N = W; g.K = P;
     }
     MPR_TRY(gemm_group(pe, s));
     for (int i = 0; i < nv; ++i) {
       VitModel& m = *v[i];
-      float* xp = m.x.as<float>();
-      MPR_TRY(vit_assemble(m.patches.as<float>(), m.cls.as<float>(), m.pos.as<float>(), B, g2,
+      TowerWs& w = m.ws[slot];
+      float* xp = w.x.as<float>();
+      MPR_TRY(vit_assemble(w.patches.as<float>(), m.cls.as<float>(), m.pos.as<float>(), B, g2,
                            W, xp, s));
       MPR_TRY(layernorm(xp, W, B * T, W, m.lnpre_w.as<float>(), m.lnpre_b.as<float>(),
                         CLIP_LN_EPS, xp, W, s));
-      runs[nr++] = TowerRun{&m.tower, xp, B, T, false};
+      runs[nr++] = TowerRun{&m.tower, &w, xp, B, T, false};
     }
   }
   if (tm) {
     const int W = tm->width;
-    MPR_TRY(tm->x.ensure((size_t)Bt * Lt * W * 4));
-    MPR_TRY(tm->pooled.ensure((size_t)Bt * W * 4));
+    TowerWs& w = tm->ws[slot];
+    MPR_TRY(w.x.ensure((size_t)Bt * Lt * W * 4));
+    MPR_TRY(w.pooled.ensure((size_t)Bt * W * 4));
     MPR_TRY(embed_gather(tm->tok_emb.as<float>(), tok, tm->ctx, Bt, Lt, W, tm->pos.as<float>(),
-                         tm->x.as<float>(), (int64_t)Lt * W, 0, s));
-    runs[nr++] = TowerRun{&tm->tower, tm->x.as<float>(), Bt, Lt, true};
+                         w.x.as<float>(), (int64_t)Lt * W, 0, s));
+    runs[nr++] = TowerRun{&tm->tower, &w, w.x.as<float>(), Bt, Lt, true};
   }
   MPR_TRY(ClipTower::run_group(runs, nr, s));
   GemmGroup pg;
@@ -204,8 +206,8 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
   for (int i = 0; i < nv; ++i) {
     VitModel& m = *v[i];
     const int W = m.width, T = m.grid * m.grid + 1;
-    float* xp = m.x.as<float>();
-    float* tp = m.tmp.as<float>();
+    float* xp = m.ws[slot].x.as<float>();
+    float* tp = m.ws[slot].tmp.as<float>();
     GemmArgs& pj = pg.g[pg.n++];
     pj.W = m.projT.as<float>(); pj.ldw = W; pj.N = m.out_dim; pj.K = W; pj.A = tp; pj.lda = W;
     if (modes[i] == 0) {
@@ -221,8 +223,8 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
   }
   if (tm) {
     const int W = tm->width;
-    float* pp = tm->pooled.as<float>();
-    MPR_TRY(eot_gather(tm->x.as<float>(), tok, Bt, Lt, tm->ctx, W, pp, s));
+    float* pp = tm->ws[slot].pooled.as<float>();
+    MPR_TRY(eot_gather(tm->ws[slot].x.as<float>(), tok, Bt, Lt, tm->ctx, W, pp, s));
     MPR_TRY(layernorm(pp, W, Bt, W, tm->lnf_w.as<float>(), tm->lnf_b.as<float>(), CLIP_LN_EPS,
                       pp, W, s));
     GemmArgs& pj = pg.g[pg.n++];

@@ -31,9 +31,20 @@ struct ClipBlock {
   DevBuf ln1_w, ln1_b, in_w, in_b, out_w, out_b, ln2_w, ln2_b, fc_w, fc_b, pj_w, pj_b;
 };
 
+// Per-call scratch of one CLIP model (activations of its tower, patch/pooling buffers).  A model
+// holds TOWER_SLOTS of them: passes on different slots may be in flight at once (two batches'
+// towers of a serving loop on two streams), sharing the weights.
+constexpr int TOWER_SLOTS = 4;
+struct TowerWs {
+  DevBuf h, qkv, ao, mlp;             // transformer layer activations
+  DevBuf cols, patches, x, tmp, pooled;  // ViT im2col / patch embeddings / residual stream;
+                                         // text residual stream / pooled EOT rows
+};
+
 struct ClipTower;
 struct TowerRun {
   ClipTower* t;
+  TowerWs* w;
   float* x;  // [B*L, width], updated in place
   int B, L;
   bool causal;
@@ -42,11 +53,7 @@ struct TowerRun {
 struct ClipTower {
   int width = 0, layers = 0, heads = 0;
   std::vector<std::unique_ptr<ClipBlock>> blocks;
-  // workspace
-  DevBuf h, qkv, ao, mlp;
   int load_blocks(const float* const* t, int width, int layers);
-  // x [B*L, width] in place; causal for the text tower.
-  int run(float* x, int B, int L, bool causal, hipStream_t s);
   static int run_group(const TowerRun* r, int n, hipStream_t s);
 };
 
@@ -55,7 +62,7 @@ struct VitModel : mpr_model {
   int width = 0, patch = 0, image = 0, out_dim = 0, grid = 0;
   DevBuf conv_w, cls, pos, lnpre_w, lnpre_b, lnpost_w, lnpost_b, projT;
   ClipTower tower;
-  DevBuf cols, patches, x, tmp;
+  TowerWs ws[TOWER_SLOTS];
   int forward(const float* img, int B, int mode, float* out, int64_t out_bs, hipStream_t s);
 };
 
@@ -64,16 +71,17 @@ struct TextModel : mpr_model {
   int width = 0, ctx = 0, vocab = 0, out_dim = 0;
   DevBuf tok_emb, pos, lnf_w, lnf_b, projT;
   ClipTower tower;
-  DevBuf x, pooled;
+  TowerWs ws[TOWER_SLOTS];
   int forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs, hipStream_t s);
 };
 
 // The CLIP towers of one batch in lockstep (encoders.hip): nv <= 2 ViTs over the same images,
-// optionally the text tower; identical results to separate calls.
+// optionally the text tower; identical results to separate calls.  `slot` picks every model's
+// workspace (calls on different slots may run concurrently; calls on one slot must be ordered).
 int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
                   const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
                   const int32_t* tok, int Bt, int Lt, float* out_t, int64_t out_t_bs,
-                  hipStream_t s);
+                  hipStream_t s, int slot = 0);
 
 struct T5Layer {
   DevBuf ln0, qkv, o, ln1, wi, wo;         // encoder layer / decoder self-attn + ffn

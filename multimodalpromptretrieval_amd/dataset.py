@@ -84,11 +84,26 @@ class VQARetrieval:
 
     # ---- encoding ------------------------------------------------------------------------------
     def _streams(self):
-        """The retrieval stream (_lib.role_stream "encode:towers": high priority by default —
-        the host waits on the retrieval result to build prompts)."""
+        """The retrieval stream (_lib.role_stream "encode:towers"; tower workspace slot 0)."""
         if not hasattr(self, "_s_img"):
             self._s_img = _lib.role_stream(self.device, "encode:towers")
         return self._s_img
+
+    def _slot_stream(self, slot: int):
+        """Stream of tower workspace slot `slot` (slot 0 = the retrieval stream, so that every
+        use of a slot stays ordered on one stream)."""
+        if slot == 0:
+            return self._streams()
+        if not hasattr(self, "_s_slot"):
+            self._s_slot = {}
+        if slot not in self._s_slot:
+            self._s_slot[slot] = _lib.role_stream(self.device, f"encode:towers{slot}")
+        return self._s_slot[slot]
+
+    def _scan_stream(self):
+        """Every prefetched search runs on the slot-0 stream (the index keeps one search
+        workspace; one more stream would also alias a hardware queue, 4 per process)."""
+        return self._streams()
 
     def encode_image_pair(self, batch, other_vit, other_mode: int):
         """Run this retrieval's query encoders (``encode_image`` on the batch's images and
@@ -122,7 +137,7 @@ class VQARetrieval:
         return (id(batch["image"]), tuple(batch["question"]), self.retrieval_k,
                 self.is_training_phase)
 
-    def prefetch(self, batch, other_vit=None, other_mode: int = CLS):
+    def prefetch(self, batch, other_vit=None, other_mode: int = CLS, slot: int = 0):
         """Serving-loop lookahead: enqueue all of ``batch``'s device-side retrieval work — the
         query towers (in lockstep with ``other_vit`` over the same images when given, as
         ``encode_image_pair``), the index scan, and the copy of its top-k into pinned host
@@ -130,10 +145,12 @@ class VQARetrieval:
         ``retrieve_closest_qa_pairs(batch)`` waits for that copy only, so a caller can enqueue
         batch i+1's towers before it blocks on batch i's retrieval result.  Returns
         (``other_vit``'s output or None, an event recorded after the towers: wait on it, not on
-        the stream, which by then may hold the next batch's work)."""
+        the stream, which by then may hold the next batch's work).  ``slot`` (0-3) runs the
+        towers on that workspace slot and its own stream, so consecutive batches' towers can
+        overlap; the searches of all slots are ordered on one scan stream."""
         if self.index is None:
             raise RuntimeError("create_retrieval_dataset() / set_index() first")
-        s_img = self._streams()
+        s_img = self._slot_stream(int(slot))
         cur = torch.cuda.current_stream(self.device)
         img = batch["image"].to(self.device, torch.float32, non_blocking=True)
         toks = self.clip_tokenize(batch["question"])
@@ -149,16 +166,20 @@ class VQARetrieval:
             _, other_out, _ = encode_towers(
                 self.image_encoder, img, CLS, out_a=q, out_a_bstride=self.embed_dim,
                 vit_b=other_vit, mode_b=other_mode, text=self.text_encoder, tokens=toks,
-                out_t=q[:, di:], out_t_bstride=self.embed_dim)
+                out_t=q[:, di:], out_t_bstride=self.embed_dim, slot=int(slot))
             towers = torch.cuda.Event()
             towers.record(s_img)
-            if isinstance(self.index, DeviceIndex):  # a sharded search exchanges: done in _topk
+        if isinstance(self.index, DeviceIndex):  # a sharded search exchanges: done in _topk
+            s_scan = self._scan_stream()
+            s_scan.wait_event(towers)
+            q.record_stream(s_scan)
+            with torch.cuda.stream(s_scan):
                 dist, ids = self.index.search(q, kk)
                 both = torch.cat([ids.to(torch.float64), dist.to(torch.float64)], 1)
                 host = torch.empty(both.shape, dtype=torch.float64, pin_memory=True)
                 host.copy_(both, non_blocking=True)
                 done = torch.cuda.Event()
-                done.record(s_img)
+                done.record(s_scan)
         if other_out is not None:
             other_out.record_stream(cur)
         while len(self._prefetched) >= 8:  # never consumed (an abandoned loop): drop the oldest

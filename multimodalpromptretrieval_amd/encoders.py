@@ -133,10 +133,12 @@ def encode_towers(vit_a: "DeviceViT" = None, img: torch.Tensor = None, mode_a: i
                   out_a=None, out_a_bstride=None, vit_b: "DeviceViT" = None,
                   mode_b: int = TOKENS, out_b=None, out_b_bstride=None,
                   text: "DeviceCLIPText" = None, tokens: torch.Tensor = None, out_t=None,
-                  out_t_bstride=None):
+                  out_t_bstride=None, slot: int = 0):
     """One lockstep pass over a batch's CLIP towers (mpr_encode_towers): up to two ViTs over
     the same images and the text tower over clip.tokenize ids; each layer's projections share
-    launches.  Bit-identical to the separate calls.  Returns (out_a, out_b, out_t)."""
+    launches.  Bit-identical to the separate calls.  ``slot`` (0-3) picks the models'
+    activation workspaces: passes on different slots may run concurrently on different streams.
+    Returns (out_a, out_b, out_t)."""
     dev = (vit_a or text).device
     B = 0
     if vit_a is not None:
@@ -164,7 +166,7 @@ def encode_towers(vit_a: "DeviceViT" = None, img: torch.Tensor = None, mode_a: i
               int(out_b_bstride or 0),
               _lib.ptr(img if vit_a is not None else None), B,
               text._h if text is not None else None, _lib.ptr(tok), Bt, L, _lib.ptr(out_t),
-              int(out_t_bstride or 0), _lib.stream_ptr(dev))
+              int(out_t_bstride or 0), int(slot), _lib.stream_ptr(dev))
     return out_a, out_b, out_t
 
 

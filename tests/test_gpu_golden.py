@@ -152,6 +152,7 @@ def test_g2_predict_many_matches_predict(device):
         assert list(model.predict_many(batches, depth)) == want
         assert list(model.predict_many(batches, depth, pair_decodes=False)) == want
         assert list(model.predict_many(batches, depth, lookahead=False)) == want
+        assert list(model.predict_many(batches, depth, tower_slots=1)) == want
     assert list(model.predict_many(batches[:3])) == want[:3]  # an unpaired last batch
     assert list(model.predict_many(iter(batches[:1]))) == want[:1]
     assert list(model.predict_many([])) == []

@@ -162,6 +162,33 @@ def test_encode_towers_matches_separate(device, clip_sd):
     assert torch.equal(t_only, txt(toks[:3]))
 
 
+def test_encode_towers_slots_run_concurrently(device, clip_sd):
+    """Two batches' lockstep passes on workspace slots 0 and 1 on two streams at once (repeated,
+    so the passes overlap): each equals its pass run alone, bit for bit."""
+    from multimodalpromptretrieval_amd.encoders import CLS, TOKENS, DeviceCLIPText, DeviceViT, \
+        encode_towers
+    a, b = DeviceViT(clip_sd, device), DeviceViT(syn.clip_state_dict(14), device)
+    txt = DeviceCLIPText(clip_sd, device)
+    imgs = [syn.images(30 + i, 16).to(device) for i in range(2)]
+    toks = [syn.clip_tokens(40 + i, 16) for i in range(2)]
+    want = [encode_towers(a, imgs[i], CLS, vit_b=b, mode_b=TOKENS, text=txt, tokens=toks[i])
+            for i in range(2)]
+    streams = [torch.cuda.Stream(device) for _ in range(2)]
+    for _ in range(4):
+        got = []
+        for i, st in enumerate(streams):
+            st.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(st):
+                got.append(encode_towers(a, imgs[i], CLS, vit_b=b, mode_b=TOKENS, text=txt,
+                                         tokens=toks[i], slot=i))
+        for st in streams:
+            torch.cuda.current_stream(device).wait_stream(st)
+        for g, w in zip(got, want):
+            assert all(torch.equal(x, y) for x, y in zip(g, w))
+    with pytest.raises(RuntimeError):
+        encode_towers(a, imgs[0], CLS, slot=4)
+
+
 def test_clip_text(device, clip_sd):
     from multimodalpromptretrieval_amd.encoders import DeviceCLIPText
     txt = DeviceCLIPText(clip_sd, device)

@@ -7,7 +7,7 @@ STEPS=${2:-16}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
-  tests/test_gpu_kernels.py::test_t5_generate_pair_matches_single tests/test_gpu_golden.py \
+  tests/test_gpu_kernels.py::test_t5_generate_pair_matches_single tests/test_gpu_kernels.py::test_encode_towers_slots_run_concurrently tests/test_gpu_golden.py \
   > "$OUT/pytest.log" 2>&1 || exit $?
 # "pair in-flight lookahead" per run; CFGS (';'-separated) overrides
 IFS=';' read -r -a RUNS <<< "${CFGS:-1 2 1;0 2 1;1 1 1;0 1 1;0 2 0}"
