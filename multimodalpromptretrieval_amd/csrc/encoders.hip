@@ -48,7 +48,7 @@ int ClipTower::load_blocks(const float* const* t, int w, int nl) {
 // grouped GEMM launch over the towers (split by tile choice, gemm_group); per tower its own
 // width, batch, sequence length and causality.
 int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
-  MPR_REQUIRE(n >= 1 && n <= GEMM_GROUP, "clip tower group: n=%d", n);
+  MPR_REQUIRE(n >= 1 && n <= ATTN_GROUP && n <= LN_GROUP, "clip tower group: n=%d", n);
   for (int i = 0; i < n; ++i) {
     ClipTower& t = *r[i].t;
     TowerWs& w = *r[i].w;
@@ -85,19 +85,20 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       pj.bias = b.pj_b.as<float>(); pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M;
       pj.N = W; pj.K = 4 * W;
     }
+    // the towers' LayerNorms and attentions are grouped launches too (one kernel each)
+    LnGroup n1, n2;
+    AttnGroup ag;
+    n1.n = n2.n = ag.n = n;
     for (int i = 0; i < n; ++i) {
       ClipTower& t = *r[i].t;
       const ClipBlock& b = *t.blocks[l];
-      const int W = t.width;
-      MPR_TRY(layernorm(r[i].x, W, r[i].B * r[i].L, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(),
-                        CLIP_LN_EPS, r[i].w->h.as<float>(), W, s));
-    }
-    MPR_TRY(gemm_group(gq, s));
-    for (int i = 0; i < n; ++i) {
-      ClipTower& t = *r[i].t;
-      const int W = t.width, L = r[i].L;
+      const int W = t.width, L = r[i].L, M = r[i].B * L;
+      n1.p[i] = LnArgs{r[i].x, W, M, W, b.ln1_w.as<float>(), b.ln1_b.as<float>(),
+                       r[i].w->h.as<float>(), W};
+      n2.p[i] = LnArgs{r[i].x, W, M, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(),
+                       r[i].w->h.as<float>(), W};
       float* qp = r[i].w->qkv.as<float>();
-      AttnArgs at;
+      AttnArgs& at = ag.a[i];
       at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
       at.k = qp + W; at.k_bs = at.q_bs; at.k_rs = 3 * W;
       at.v = qp + 2 * W; at.v_bs = at.q_bs; at.v_rs = 3 * W;
@@ -105,16 +106,12 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       at.B = r[i].B; at.H = t.heads; at.Lq = L; at.Lk = L;
       at.scale = 0.125f;  // 64 ** -0.5, exact power of two
       at.causal = r[i].causal ? 1 : 0;
-      MPR_TRY(attention(at, s));
     }
+    MPR_TRY(layernorm_group(n1, CLIP_LN_EPS, s));
+    MPR_TRY(gemm_group(gq, s));
+    MPR_TRY(attention_group(ag, s));
     MPR_TRY(gemm_group(go, s));
-    for (int i = 0; i < n; ++i) {
-      ClipTower& t = *r[i].t;
-      const ClipBlock& b = *t.blocks[l];
-      const int W = t.width;
-      MPR_TRY(layernorm(r[i].x, W, r[i].B * r[i].L, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(),
-                        CLIP_LN_EPS, r[i].w->h.as<float>(), W, s));
-    }
+    MPR_TRY(layernorm_group(n2, CLIP_LN_EPS, s));
     MPR_TRY(gemm_group(gf, s));
     MPR_TRY(gemm_group(gp, s));
   }

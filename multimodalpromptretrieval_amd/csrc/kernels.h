@@ -71,6 +71,21 @@ int probe_replay(int iters, hipStream_t s, double* ms, int64_t* launches, double
 int probe_clear();
 
 // LayerNorm over rows of width D (eps, affine), out may alias x.  ld in floats.
+// Up to LN_GROUP LayerNorms (one per tower of a lockstep pass) in one launch; identical results.
+constexpr int LN_GROUP = 3;
+struct LnArgs {
+  const float* x = nullptr;
+  int64_t ldx = 0;
+  int M = 0, D = 0;
+  const float *g = nullptr, *b = nullptr;
+  float* out = nullptr;
+  int64_t ldo = 0;
+};
+struct LnGroup {
+  LnArgs p[LN_GROUP];
+  int n = 0;
+};
+int layernorm_group(const LnGroup& g, float eps, hipStream_t s);
 int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, const float* beta,
               float eps, float* out, int64_t ldo, hipStream_t s);
 // T5LayerNorm (RMSNorm, weight only).
@@ -100,6 +115,14 @@ struct AttnArgs {
   int lut_radius = 0;
 };
 int attention(const AttnArgs& a, hipStream_t s);
+// The attentions of up to ATTN_GROUP towers of a lockstep pass in one launch (when all take the
+// MFMA prefill path; otherwise one attention() each).  Identical results to separate calls.
+constexpr int ATTN_GROUP = 3;
+struct AttnGroup {
+  AttnArgs a[ATTN_GROUP];
+  int n = 0;
+};
+int attention_group(const AttnGroup& g, hipStream_t s);
 
 // ViT patch extraction: img [B,3,S,S] -> cols [B*g*g, 3*p*p] in (c, kh, kw) order (conv1 weight
 // flattening).

@@ -37,9 +37,9 @@ __device__ __forceinline__ float half_sum(float v) {  // over the 32 lanes of a 
 }
 
 template <int V4>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t ldx, int M, int D,
-                                                        const float* g, const float* b, float eps,
-                                                        float* out, int64_t ldo) {
+__device__ __forceinline__ void layernorm_rows(const float* x, int64_t ldx, int M, int D,
+                                               const float* g, const float* b, float eps,
+                                               float* out, int64_t ldo) {
   const int row = blockIdx.x * 8 + (threadIdx.x >> 5), l32 = threadIdx.x & 31;
   const float* xr = x + (int64_t)min(row, M - 1) * ldx;
   const int D4 = D >> 2;
@@ -82,6 +82,26 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t 
       reinterpret_cast<f32x4*>(orow)[c4] = o;
     }
   }
+}
+
+template <int V4>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t ldx, int M, int D,
+                                                        const float* g, const float* b, float eps,
+                                                        float* out, int64_t ldo) {
+  layernorm_rows<V4>(x, ldx, M, D, g, b, eps, out, ldo);
+}
+
+// Up to LN_GROUP LayerNorms in one launch (blockIdx.y picks the problem).  A row's arithmetic
+// does not depend on V4 (slots past D are exact zeros), so results equal the single launches.
+template <int V4>
+__global__ __launch_bounds__(256) void layernorm_group_kernel(LnGroup grp, float eps) {
+  const int z = blockIdx.y;
+#define MPR_SEL(f) (z == 0 ? grp.p[0].f : z == 1 ? grp.p[1].f : grp.p[2].f)
+  const int M = MPR_SEL(M);
+  if ((int)blockIdx.x * 8 >= M) return;
+  layernorm_rows<V4>(MPR_SEL(x), MPR_SEL(ldx), M, MPR_SEL(D), MPR_SEL(g), MPR_SEL(b), eps,
+                     MPR_SEL(out), MPR_SEL(ldo));
+#undef MPR_SEL
 }
 
 template <int V4>
@@ -327,8 +347,7 @@ constexpr int ATT_MFMA_MAXK = 256;
 constexpr int ATT_MFMA_KT = ATT_MFMA_MAXK / 16;
 constexpr int ATT_MFMA_LD = 68;  // LDS row stride (floats)
 
-__global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt) {
-  extern __shared__ __attribute__((aligned(16))) float kv_s[];  // K rows | V rows
+__device__ __forceinline__ void attention_mfma_body(const AttnArgs& a, int nqt, float* kv_s) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.x, h = bh % a.H, b = bh / a.H;
@@ -454,6 +473,34 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt
       for (int dt = 0; dt < 4; ++dt) ob[(int64_t)q * a.o_rs + 16 * dt] = O[dt][r];
     }
   }
+}
+
+__global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt) {
+  extern __shared__ __attribute__((aligned(16))) float kv_s[];  // K rows | V rows
+  attention_mfma_body(a, nqt, kv_s);
+}
+
+// The attentions of up to ATTN_GROUP towers in one launch (blockIdx.z picks the problem; the
+// grid covers the largest, blocks past a problem's heads / query tiles exit).  Per block the same
+// code and data as attention_mfma_kernel: identical results.
+__global__ __launch_bounds__(256) void attention_mfma_group_kernel(AttnGroup grp) {
+  extern __shared__ __attribute__((aligned(16))) float kv_s[];
+  const int z = blockIdx.z;
+  // field-wise wave-uniform selection (dynamic indexing of the kernarg struct spills to scratch)
+#define MPR_SEL(f) (z == 0 ? grp.a[0].f : z == 1 ? grp.a[1].f : grp.a[2].f)
+  AttnArgs a;
+  a.q = MPR_SEL(q); a.q_bs = MPR_SEL(q_bs); a.q_rs = MPR_SEL(q_rs);
+  a.k = MPR_SEL(k); a.k_bs = MPR_SEL(k_bs); a.k_rs = MPR_SEL(k_rs);
+  a.v = MPR_SEL(v); a.v_bs = MPR_SEL(v_bs); a.v_rs = MPR_SEL(v_rs);
+  a.o = MPR_SEL(o); a.o_bs = MPR_SEL(o_bs); a.o_rs = MPR_SEL(o_rs);
+  a.B = MPR_SEL(B); a.H = MPR_SEL(H); a.Lq = MPR_SEL(Lq); a.Lk = MPR_SEL(Lk);
+  a.scale = MPR_SEL(scale); a.causal = MPR_SEL(causal); a.q_pos0 = MPR_SEL(q_pos0);
+  a.key_mask = MPR_SEL(key_mask); a.mask_bs = MPR_SEL(mask_bs);
+  a.rel_tab = MPR_SEL(rel_tab); a.lut_radius = MPR_SEL(lut_radius);
+#undef MPR_SEL
+  const int nqt = (a.Lq + 15) / 16;
+  if ((int)blockIdx.x >= a.B * a.H || (int)blockIdx.y * 4 >= nqt) return;  // whole block
+  attention_mfma_body(a, nqt, kv_s);
 }
 
 // ---- data movement ----------------------------------------------------------------------------
@@ -696,6 +743,29 @@ int layernorm(const float* x, int64_t ldx, int M, int D, const float* gamma, con
   return MPR_OK;
 }
 
+int layernorm_group(const LnGroup& g, float eps, hipStream_t s) {
+  MPR_REQUIRE(g.n >= 1 && g.n <= LN_GROUP, "layernorm_group: %d problems", g.n);
+  int64_t blocks = 0;
+  int dmax = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const LnArgs& p = g.p[i];
+    MPR_REQUIRE(p.D > 0 && p.D <= 1024 && p.D % 4 == 0 && p.ldx % 4 == 0 && p.ldo % 4 == 0,
+                "layernorm: D=%d / strides unsupported (D <= 1024, multiples of 4)", p.D);
+    MPR_REQUIRE(aligned16(p.x) && aligned16(p.out) && aligned16(p.g) && aligned16(p.b),
+                "layernorm: operands must be 16-byte aligned");
+    blocks = std::max<int64_t>(blocks, cdiv(p.M, 8));
+    dmax = std::max(dmax, p.D);
+  }
+  if (blocks == 0) return MPR_OK;
+  dim3 grid((unsigned)blocks, (unsigned)g.n);
+  if (dmax <= 512)
+    hipLaunchKernelGGL(layernorm_group_kernel<4>, grid, dim3(256), 0, s, g, eps);
+  else
+    hipLaunchKernelGGL(layernorm_group_kernel<8>, grid, dim3(256), 0, s, g, eps);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
 int rmsnorm(const float* x, int64_t ldx, int M, int D, const float* w, float eps, float* out,
             int64_t ldo, hipStream_t s) {
   MPR_REQUIRE(D > 0 && D <= 1024 && D % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0,
@@ -745,6 +815,36 @@ int attention(const AttnArgs& a, hipStream_t s) {
   }
   dim3 grid((unsigned)cdiv(a.Lq, ATT_QR), (unsigned)a.H, (unsigned)a.B);
   hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, a);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int attention_group(const AttnGroup& g, hipStream_t s) {
+  MPR_REQUIRE(g.n >= 1 && g.n <= ATTN_GROUP, "attention_group: %d problems", g.n);
+  // one launch when every problem takes the MFMA path (prefill, keys <= ATT_MFMA_MAXK)
+  bool mfma = !mfma_attention_disabled();
+  unsigned gx = 0, gy = 0;
+  size_t lds = 0;
+  for (int i = 0; i < g.n && mfma; ++i) {
+    const AttnArgs& a = g.a[i];
+    MPR_REQUIRE(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attention: bad shape");
+    if (a.rel_tab)
+      MPR_REQUIRE(a.lut_radius >= a.Lk + a.Lq + a.q_pos0,
+                  "attention: bias table radius %d too small", a.lut_radius);
+    int lk = a.Lk;
+    if (a.causal) lk = std::min(lk, a.Lq + a.q_pos0);
+    mfma = a.Lq > 1 && lk <= ATT_MFMA_MAXK;
+    gx = std::max(gx, (unsigned)((int64_t)a.B * a.H));
+    gy = std::max(gy, (unsigned)cdiv(cdiv(a.Lq, 16), 4));
+    lds = std::max(lds, (size_t)2 * cdiv(a.Lk, 16) * 16 * ATT_MFMA_LD * sizeof(float));
+  }
+  if (!mfma) {
+    for (int i = 0; i < g.n; ++i) MPR_TRY(attention(g.a[i], s));
+    return MPR_OK;
+  }
+  if (gx == 0 || gy == 0) return MPR_OK;
+  hipLaunchKernelGGL(attention_mfma_group_kernel, dim3(gx, gy, (unsigned)g.n), dim3(256), lds, s,
+                     g);
   MPR_LAUNCHED();
   return MPR_OK;
 }
