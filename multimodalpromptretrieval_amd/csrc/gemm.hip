@@ -39,9 +39,11 @@ __device__ __forceinline__ float act_exact(float v, int act) {
 // Two LDS stages: during iteration t the waves read tile t+1's fragments from one stage while
 // tile t+2 is written into the other (tile t's stage, whose fragments were read in iteration t-1,
 // before the barrier that closed it).  Fragments of tile t+1 are read under tile t's MFMAs.
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool XR>
-__global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_f32_kernel(
-    const GemmGroup grp) {
+//
+// One BM x BN output tile of problem `a` (tile column bx, row by) with this block; `smem` is the
+// kernel's single LDS object (>= 2 * (BM + BN) * (BK + 4) floats).
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+__device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, float* smem) {
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
   constexpr int NT = 64 * WAVES_MN * KW;
@@ -53,39 +55,8 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
   static_assert(LA * NT == BM * KQ && LB * NT == BN * KQ, "loader split");
   static_assert(NF >= 2 && KPW % 8 == 0, "k split");
   static_assert(KW == 1 || 2 * STAGE >= KW * BM * BN, "LDS reduction space");
-
-  // ONE __shared__ object: a second LDS object makes hipcc drain vmcnt before every k-step's
-  // first ds_read.
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
-
-  // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (hardware id % 8), each
-  // with its own L2; remap so that every XCD walks a contiguous run of tiles in column-major
-  // order (all row tiles of a column tile before the next), i.e. an XCD reads its W columns once
-  // and shares the activation rows through its L2 (bijective for any grid size).  XR = false
-  // keeps the hardware order (measured 3-5% faster for the 32x32 K-split tiles; neutral in time
-  // for 64x64, where it cuts the L2-miss traffic).
-  int z = blockIdx.z, bx = blockIdx.x, by = blockIdx.y;
-  if constexpr (XR) {
-    const int gx = gridDim.x, gy = gridDim.y, total = gx * gy * gridDim.z;
-    const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
-    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-    z = t / (gx * gy);
-    const int rem = t - z * gx * gy;
-    bx = rem / gy;
-    by = rem - bx * gy;
-  }
-  // wave-uniform selection of this block's problem (no dynamic indexing of the kernarg struct)
-#define MPR_SEL(f) (z == 0 ? grp.g[0].f : z == 1 ? grp.g[1].f : z == 2 ? grp.g[2].f : grp.g[3].f)
-  GemmArgs a;
-  a.A = MPR_SEL(A); a.lda = MPR_SEL(lda); a.W = MPR_SEL(W); a.ldw = MPR_SEL(ldw);
-  a.bias = MPR_SEL(bias); a.R = MPR_SEL(R); a.ldr = MPR_SEL(ldr); a.C = MPR_SEL(C);
-  a.ldc = MPR_SEL(ldc); a.M = MPR_SEL(M); a.N = MPR_SEL(N); a.K = MPR_SEL(K);
-  a.act = MPR_SEL(act); a.c_rpb = MPR_SEL(c_rpb); a.c_bs = MPR_SEL(c_bs);
-#undef MPR_SEL
   const int M = a.M, N = a.N, K = a.K;
   const int m0 = by * BM, n0 = bx * BN;
-  if (m0 >= M || n0 >= N) return;  // grid sized for the largest problem of the group
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
@@ -271,6 +242,49 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
         if (row < M && col < N) a.C[coff + col] = v;
       }
     }
+}
+
+// XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (hardware id % 8), each
+// with its own L2; remap so that every XCD walks a contiguous run of tiles in column-major
+// order (all row tiles of a column tile before the next), i.e. an XCD reads its W columns once
+// and shares the activation rows through its L2 (bijective for any grid size).
+__device__ __forceinline__ void xcd_remap(int& z, int& bx, int& by) {
+  const int gx = gridDim.x, gy = gridDim.y, total = gx * gy * gridDim.z;
+  const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  z = t / (gx * gy);
+  const int rem = t - z * gx * gy;
+  bx = rem / gy;
+  by = rem - bx * gy;
+}
+
+// wave-uniform selection of problem z (no dynamic indexing of the kernarg struct: it spills)
+__device__ __forceinline__ GemmArgs select_problem(const GemmGroup& grp, int z) {
+#define MPR_SEL(f) (z == 0 ? grp.g[0].f : z == 1 ? grp.g[1].f : z == 2 ? grp.g[2].f : grp.g[3].f)
+  GemmArgs a;
+  a.A = MPR_SEL(A); a.lda = MPR_SEL(lda); a.W = MPR_SEL(W); a.ldw = MPR_SEL(ldw);
+  a.bias = MPR_SEL(bias); a.R = MPR_SEL(R); a.ldr = MPR_SEL(ldr); a.C = MPR_SEL(C);
+  a.ldc = MPR_SEL(ldc); a.M = MPR_SEL(M); a.N = MPR_SEL(N); a.K = MPR_SEL(K);
+  a.act = MPR_SEL(act); a.c_rpb = MPR_SEL(c_rpb); a.c_bs = MPR_SEL(c_bs);
+#undef MPR_SEL
+  return a;
+}
+
+// Problems of one tile configuration; blockIdx.z picks the problem.  XR: XCD-aware order
+// (measured 3-5% slower for the 32x32 K-split tiles; neutral in time for 64x64, where it cuts
+// the L2-miss traffic).
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool XR>
+__global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_f32_kernel(
+    const GemmGroup grp) {
+  // ONE __shared__ object: a second LDS object makes hipcc drain vmcnt before every k-step's
+  // first ds_read.
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * (BK + 4)];
+  int z = blockIdx.z, bx = blockIdx.x, by = blockIdx.y;
+  if constexpr (XR) xcd_remap(z, bx, by);
+  const GemmArgs a = select_problem(grp, z);
+  if (by * BM >= a.M || bx * BN >= a.N) return;  // grid sized for the largest problem
+  gemm_tile<BM, BN, WM, WN, BK, D, KW>(a, bx, by, smem);
 }
 
 template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool XR = false>
@@ -673,9 +687,11 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // loads in flight) once the problem has >= 1.5 blocks per CU; below that 32x32 tiles with the
   // K tile split over 4 waves (4x the blocks, partial sums added through LDS): 800x768x3072
   // 67 -> 54 us, 1152x512x2048 47 -> 38 us, paired 800x768x768 34 -> 29 us.  BK 64, 128-row
-  // tiles, 8-wave 64x64 blocks and split-K across blocks were slower at every shape of this
-  // path.  Problems of a group with different choices go to two launches, so a problem gets the
-  // same tile (the same summation order, bit-identical results) alone or grouped.
+  // tiles, 8-wave 64x64 blocks, 2x2 or 1x2 accumulators per wave and split-K across blocks were
+  // slower at every shape of this path.  Problems of a group with different choices go to two
+  // launches, so a problem gets the same tile (the same summation order, bit-identical results)
+  // alone or grouped (one dual-configuration kernel for both measured 30% slower for the
+  // towers: 5.2 vs 4.0 ms).
   GemmGroup big, small;
   big.n = small.n = 0;
   for (int i = 0; i < g.n; ++i) {
