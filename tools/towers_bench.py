@@ -3,7 +3,7 @@ token-feature ViT + CLIP text, bench c2 weights and questions) at several batch 
 the device; CUDA events over repeated passes.  Shows how much of a pass is per-launch overhead
 and tail (time per image falling with the batch) versus MFMA work.
 
-usage: python tools/towers_bench.py
+usage: python tools/towers_bench.py [B ...]   (default 8 16 32 64, then the two-stream test)
 """
 import os
 import sys
@@ -22,7 +22,8 @@ def main():
     model, retr, _ = bench.build(bench.CONFIGS["c2"], dev, None)
     vit_tok = model._device_vit()
     batches = bench.make_batches(4, 16, dev, seed=100)
-    for B in (8, 16, 32, 64):
+    sizes = [int(a) for a in sys.argv[1:]] or [8, 16, 32, 64]
+    for B in sizes:
         reps = max(1, B // 16)
         img = torch.cat([b["image"] for b in batches] * 4)[:B].contiguous()
         qs = sum([b["question"] for b in batches] * 4, [])[:B]
@@ -49,6 +50,8 @@ def main():
         print(f"B={B:3d} (x{reps} batches of 16): {ms:7.3f} ms per pass, "
               f"{ms / B * 16:7.3f} ms per 16 images", flush=True)
 
+    if sys.argv[1:]:
+        return
     # two batches' passes on two streams at once (second model set: its own workspaces) against
     # the same two passes back to back on one stream
     model2, retr2, _ = bench.build(bench.CONFIGS["c2"], dev, None)
