@@ -252,13 +252,16 @@ class VQARetrieval:
         else:
             embs, answers = [], []
             info = {"question_type": [], "question_id": [], "question": []}
+            # query rows stay on the device until the end: the host never waits on a batch, so
+            # the tower passes of consecutive batches queue back to back on the GPU
             for batch in data_loader:
-                embs.append(self.encode_queries(batch).cpu())
+                embs.append(self.encode_queries(batch))
                 answers.extend(batch["answer"])
                 info["question_type"].extend(batch["question_type"])
                 info["question_id"].extend(batch["question_id"])
                 info["question"].extend(batch["question"])
-            emb = torch.cat(embs, 0)
+            emb = (torch.cat(embs, 0) if embs else
+                   torch.empty((0, self.embed_dim), device=self.device)).cpu()
             os.makedirs(d, exist_ok=True)
             torch.save(emb, emb_p)
             with open(ans_p, "w") as f:

@@ -189,6 +189,35 @@ def test_encode_towers_slots_run_concurrently(device, clip_sd):
         encode_towers(a, imgs[0], CLS, slot=4)
 
 
+def test_create_retrieval_dataset_builds_and_caches(device, clip_sd, tmp_path):
+    """Index build (dataset/VQAFeatureDataset.py:118-185): the rows are
+    each batch's encode_queries rows bit for bit, the lists follow the loader, the second call
+    loads the cache (safe formats) instead of encoding, and a query finds its own row."""
+    from multimodalpromptretrieval_amd.dataset import VQARetrieval
+    r = VQARetrieval(device, clip_state_dict=clip_sd, clip_tokenizer=syn.hash_clip_tokenize)
+    loader = []
+    for i, b in enumerate((5, 7, 3)):
+        loader.append({"image": syn.images(50 + i, b).to(device),
+                       "question": [f"what organ is shown {i} {j}" for j in range(b)],
+                       "answer": [f"a{i}{j}" for j in range(b)],
+                       "question_type": ["organ"] * b,
+                       "question_id": [f"{i}-{j}" for j in range(b)]})
+    want = torch.cat([r.encode_queries(bt).cpu() for bt in loader])
+    r.create_retrieval_dataset(loader, is_training_phase=False, retrieval_k=1,
+                               cache_dir=str(tmp_path))
+    assert torch.equal(r.retrieval_embeddings.cpu(), want)
+    assert r.retrieval_answers == [a for bt in loader for a in bt["answer"]]
+    assert r.retrieval_question_info["question_id"] == [q for bt in loader
+                                                          for q in bt["question_id"]]
+    r2 = VQARetrieval(device, clip_state_dict=clip_sd, clip_tokenizer=syn.hash_clip_tokenize)
+    r2.encode_queries = None  # a cache hit must not encode
+    r2.create_retrieval_dataset(loader, is_training_phase=False, retrieval_k=1,
+                                cache_dir=str(tmp_path))
+    assert torch.equal(r2.retrieval_embeddings.cpu(), want)
+    got = r.retrieve_closest_qa_pairs(loader[1], return_ans=True)
+    assert got == [[a] for a in loader[1]["answer"]]
+
+
 def test_clip_text(device, clip_sd):
     from multimodalpromptretrieval_amd.encoders import DeviceCLIPText
     txt = DeviceCLIPText(clip_sd, device)
