@@ -141,6 +141,19 @@ def ptr(t) -> c_void_p:
     return c_void_p(t.data_ptr()) if t is not None else c_void_p(0)
 
 
+def to_device_async(t, device, dtype=None):
+    """Host tensor -> device on the current stream without blocking the host: staged through
+    pinned memory (a pageable source makes the copy wait, on the host, for all earlier work on
+    the stream — and, with more streams than the 4 hardware queues, for work of other streams
+    that share its queue).  Device tensors are only converted."""
+    import torch
+    if t.device.type != "cpu":
+        return t.to(device, dtype) if dtype is not None else t.to(device)
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.contiguous().pin_memory().to(device, non_blocking=True)
+
+
 def stream_ptr(device=None) -> c_void_p:
     import torch
     return c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -206,7 +206,7 @@ class DeviceCLIPText(_Handle):
             seq_len = int(tokens.argmax(dim=1).max()) + 1 if B else 1
         else:
             seq_len = self.context_length
-        return tokens.to(self.device, torch.int32, non_blocking=True).contiguous(), seq_len
+        return _lib.to_device_async(tokens, self.device, torch.int32).contiguous(), seq_len
 
     def forward(self, tokens: torch.Tensor, out: torch.Tensor = None,
                 out_bstride: int = None) -> torch.Tensor:

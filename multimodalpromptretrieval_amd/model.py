@@ -306,7 +306,7 @@ class T5VisionModel(nn.Module):
             mask[:, T:] = encoding["attention_mask"].float()
         else:
             mask = encoding["attention_mask"]
-        return combined, mask.to(self.device), encoding
+        return combined, _lib.to_device_async(mask, self.device), encoding
 
     def predict(self, batch, output_attentions=False):
         """architectures/T5VisionModel.py:196-216 (greedy, max_new_tokens=20)."""
@@ -421,7 +421,11 @@ class T5VisionModel(nn.Module):
                     launch([held])
                     held = None
                 launch([cur])
-            while len(pending) > depth:  # the oldest call is (nearly) done by now
+            # Answers are handed out as their calls complete; the host blocks on the oldest only
+            # when more than depth + 2 calls are outstanding (a slot's next call is ordered
+            # behind its previous one by the slot's stream, so reuse needs no host wait, and a
+            # blocked host would leave the tower stream without its next pass).
+            while pending and (len(pending) > depth + 2 or pending[0][-1][1].query()):
                 for item in pending.popleft():
                     yield self._finish(*item)
         if held is not None:

@@ -120,7 +120,7 @@ class DeviceT5:
 
     def embed(self, ids: torch.Tensor, out: torch.Tensor, row0: int = 0) -> torch.Tensor:
         """out[b, row0 + t, :] = shared[ids[b, t]] (out: [B, L, d] fp32 on device)."""
-        ids32 = ids.to(self.device, torch.int32, non_blocking=True).contiguous()
+        ids32 = _lib.to_device_async(ids, self.device, torch.int32).contiguous()
         B, n = ids32.shape
         _lib.call("mpr_t5_embed", self._h, _lib.ptr(ids32), B, n, _lib.ptr(out),
                   out.shape[1] * out.shape[2], row0, self._stream())
