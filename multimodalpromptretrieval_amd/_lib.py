@@ -181,9 +181,12 @@ def decode_cus(idx: int) -> int:
 def stream_priorities() -> tuple:
     """(retrieval-encoder streams, generate streams) priorities, MPR_STREAM_PRIO = "enc"
     (the retrieval encoders first — the host waits on their result to build prompts),
-    "gen", "both" or "none" (default: all within 2% of each other in the two-decode serving
-    loop, none best at 2356 QA pairs/s).  Lower is higher (-1 = high)."""
-    mode = os.environ.get("MPR_STREAM_PRIO", "none")
+    "gen" (default: the generate streams first — with the towers back to back, the pair
+    decodes, a chain of ~1000 small launches, are the co-critical path; gen / both / enc / none
+    = 2633 / 2606 / 2590 / 2548 QA pairs/s), "both" or "none".  Lower is higher (-1 = high).
+    Leaving CUs to the generate streams through a CU mask on the encoder streams measured far
+    slower (8 / 16 / 32 CUs: 1251 / 1039 / 1391)."""
+    mode = os.environ.get("MPR_STREAM_PRIO", "gen")
     return {"enc": (-1, 0), "gen": (0, -1), "both": (-1, -1)}.get(mode, (0, 0))
 
 
