@@ -173,6 +173,15 @@ int mpr_t5_generate_pair(mpr_model* m, int32_t slot, const float* embeds_a_dev,
                          const float* embeds_b_dev, const float* mask_b_dev, int32_t b_b,
                          int32_t L_b, int32_t max_new, int32_t decoder_start, int32_t eos,
                          int32_t pad, int32_t* out_a_dev, int32_t* out_b_dev, void* stream);
+/* n (1..4) batches (b[i] <= 16 rows each, own source lengths L[i]) generated with one shared
+ * decode loop of sum(b) <= 64 rows on workspace slot `slot` (the general form of
+ * mpr_t5_generate_pair; arrays of n device pointers / sizes).  out[i] [b[i], 1+max_new] is
+ * bit-identical to mpr_t5_generate_slot on batch i. */
+int mpr_t5_generate_batches(mpr_model* m, int32_t slot, int32_t n,
+                            const float* const* embeds_dev, const float* const* masks_dev,
+                            const int32_t* b, const int32_t* L, int32_t max_new,
+                            int32_t decoder_start, int32_t eos, int32_t pad,
+                            int32_t* const* out_dev, void* stream);
 /* Run the greedy decode loop of later generate calls on a slot on decode_stream (null = the
  * call's own stream).  The call's stream still orders everything: the loop starts after the
  * encoder enqueued on it and the call's stream waits for the tokens. */

@@ -62,6 +62,9 @@ SIGNATURES = [
     ("mpr_t5_generate_pair", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                        c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32,
                                        c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    ("mpr_t5_generate_batches", c_int32, [c_void_p, c_int32, c_int32, POINTER(c_void_p),
+                                          POINTER(c_void_p), I32P, I32P, c_int32, c_int32,
+                                          c_int32, c_int32, POINTER(c_void_p), c_void_p]),
     ("mpr_t5_set_decode_stream", c_int32, [c_void_p, c_int32, c_void_p]),
     ("mpr_t5_logits", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                                 c_int32, c_void_p, c_void_p]),

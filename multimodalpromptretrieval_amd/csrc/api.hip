@@ -425,6 +425,24 @@ int mpr_t5_generate_pair(mpr_model* m, int32_t slot, const float* embeds_a, cons
   });
 }
 
+int mpr_t5_generate_batches(mpr_model* m, int32_t slot, int32_t n,
+                            const float* const* embeds, const float* const* masks,
+                            const int32_t* b, const int32_t* L, int32_t max_new, int32_t start,
+                            int32_t eos, int32_t pad, int32_t* const* outs, void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    MPR_REQUIRE(n >= 1 && n <= T5Model::MAX_GROUPS && embeds && masks && b && L && outs,
+                "t5 generate_batches: n=%d (1 to %d) and every array", n, T5Model::MAX_GROUPS);
+    int bs[T5Model::MAX_GROUPS], ls[T5Model::MAX_GROUPS];
+    for (int i = 0; i < n; ++i) {
+      bs[i] = b[i];
+      ls[i] = L[i];
+    }
+    return t5->generate_groups(n, embeds, masks, bs, ls, max_new, start, eos, pad, outs,
+                               S(stream), slot);
+  });
+}
+
 int mpr_t5_set_decode_stream(mpr_model* m, int32_t slot, void* decode_stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);

@@ -757,7 +757,7 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s) {
 // blocks, made the two-decodes-in-flight serving loop 1-6% slower.)
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const GemmArgs& a = sa.g;
-  MPR_REQUIRE(a.M >= 0 && a.M <= 32 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
+  MPR_REQUIRE(a.M >= 0 && a.M <= 64 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
   if (a.M == 0 || a.N == 0) return MPR_OK;
   MPR_REQUIRE(sa.wpk && aligned16(sa.wpk), "gemm_skinny: needs the 16-byte aligned packed weight");
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && aligned16(a.A) &&
@@ -776,7 +776,14 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
   return probed(PROBE_SKINNY, 2.0 * a.M * a.N * a.K, gemm_bytes(a), s, [&]() {
-    if (a.M > 16) {  // two row groups per weight load (a paired decode: 2 batches of <= 16)
+    if (a.M > 32) {  // four row groups per weight load (up to 4 batches of <= 16 rows)
+      if (amax && tiles >= 1024 && per <= 4)
+        launch_skinny<4, 2, false, 4>(sa, F, (unsigned)cdiv(tiles, 2), s);
+      else if (per <= 4)
+        launch_skinny<4, 1, false, 4>(sa, F, (unsigned)tiles, s);
+      else  // 4-chunk passes: a wider slab for 64 rows would not fit the 160 KiB LDS
+        launch_skinny<4, 1, true, 4>(sa, F, (unsigned)tiles, s);
+    } else if (a.M > 16) {  // two row groups per weight load (2 batches of <= 16 rows)
       if (amax && tiles >= 1024 && per <= 4)
         launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s);
       else if (per <= 4)

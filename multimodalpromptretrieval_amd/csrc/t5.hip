@@ -253,7 +253,8 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
                              const int* Bs, const int* Ls, int max_new, int start, int eos,
                              int pad, int32_t* const* outs, hipStream_t s, int slot) {
   MPR_TRY(use_slot(slot));
-  MPR_REQUIRE(ng >= 1 && ng <= 2, "t5 generate: %d batch groups (1 or 2)", ng);
+  MPR_REQUIRE(ng >= 1 && ng <= MAX_GROUPS, "t5 generate: %d batch groups (1 to %d)", ng,
+              MAX_GROUPS);
   MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
   MPR_REQUIRE(max_new + 1 <= lut_radius, "t5 generate: max_new exceeds lut radius");
   // The source length is bucketed to a multiple of 8 (zero rows, mask 0) so a serving loop
@@ -266,7 +267,7 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     const float *e, *m;
     int B, L, Lb, row0;
     int32_t* out;
-  } gr[2];
+  } gr[MAX_GROUPS];
   int n = 0, Btot = 0, Lp = 0;
   int64_t Mg = 0;
   for (int g = 0; g < ng; ++g) {
@@ -297,10 +298,10 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
   MPR_TRY(grow(ws->cache, (size_t)Ld * B * Tc * 3 * inner * 4));
   MPR_TRY(grow(ws->dx, (size_t)B * d * 4));
   MPR_TRY(grow(ws->dq, (size_t)B * inner * 4));
-  MPR_TRY(grow(ws->part_val, (size_t)nparts * 32 * 4));
-  MPR_TRY(grow(ws->part_idx, (size_t)nparts * 32 * 4));
-  MPR_TRY(grow(ws->unfinished, (size_t)32 * 4));
-  MPR_TRY(grow(ws->cur_tok, (size_t)32 * 4));
+  MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * MAX_GROUPS * 4));
+  MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * MAX_GROUPS * 4));
+  MPR_TRY(grow(ws->unfinished, (size_t)16 * MAX_GROUPS * 4));
+  MPR_TRY(grow(ws->cur_tok, (size_t)16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->tok_buf, (size_t)B * T1 * 4));
   if (n > 1) {
     MPR_TRY(grow(ws->mask_enc, (size_t)Mg * 4));
@@ -323,7 +324,9 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
   } else {
     float* eo = ws->enc_out.as<float>();
     MPR_HIP(hipMemsetAsync(ws->mask_in.ptr, 0, (size_t)M * 4, s));
-    if (gr[0].Lb != gr[1].Lb) MPR_HIP(hipMemsetAsync(eo, 0, (size_t)M * d * 4, s));
+    bool ragged = false;
+    for (int k = 1; k < n; ++k) ragged |= gr[k].Lb != gr[0].Lb;
+    if (ragged) MPR_HIP(hipMemsetAsync(eo, 0, (size_t)M * d * 4, s));
     for (int k = 0; k < n; ++k) {
       const Grp& g = gr[k];
       MPR_TRY(stage_rows(ws->enc_in.as<float>(), g.e, g.B, g.L, g.Lb, d, s));

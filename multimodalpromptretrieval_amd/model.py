@@ -324,12 +324,13 @@ class T5VisionModel(nn.Module):
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     def predict_many(self, batches, decodes_in_flight: int = 2, pair_decodes=None,
-                     lookahead=None, tower_slots=None):
+                     lookahead=None, tower_slots=None, decode_group=None):
         """predict() over an iterable of batches as a serving pipeline.  A greedy decode is a
         chain of small latency-bound launches that leaves most of the chip idle, so
-        (1) with ``pair_decodes`` (default on; MPR_PAIR_DECODE=0 turns it off) two consecutive
-        batches share one decode loop: each is encoded as predict() would, then their rows step
-        together, reading every decode weight once per step for both (mpr_t5_generate_pair);
+        (1) ``decode_group`` (1-4, default MPR_DECODE_GROUP or 4; ``pair_decodes`` = False / True
+        is 1 / 2) consecutive batches share one decode loop: each is encoded as predict() would,
+        then their rows step together, reading every decode weight once per step for all
+        (mpr_t5_generate_batches);
         (2) up to ``decodes_in_flight`` of those generate calls run at once, each on its own
         stream and T5 workspace slot, while the next batches' image towers, question tower and
         index scan run beside them and the host builds its prompts;
@@ -343,8 +344,14 @@ class T5VisionModel(nn.Module):
         gives it."""
         from collections import deque
         depth = max(1, min(int(decodes_in_flight), 4))
-        if pair_decodes is None:
-            pair_decodes = os.environ.get("MPR_PAIR_DECODE", "1") != "0"
+        if decode_group is None:
+            if pair_decodes is not None:
+                decode_group = 2 if pair_decodes else 1
+            elif os.environ.get("MPR_PAIR_DECODE") == "0":
+                decode_group = 1
+            else:
+                decode_group = int(os.environ.get("MPR_DECODE_GROUP", "4"))
+        decode_group = max(1, min(int(decode_group), 4))
         if lookahead is None:
             lookahead = os.environ.get("MPR_LOOKAHEAD", "1") != "0"
         if tower_slots is None:
@@ -357,7 +364,7 @@ class T5VisionModel(nn.Module):
         while len(self._s_gen) < depth:
             self._s_gen.append(_lib.role_stream(self.device, f"gen:{len(self._s_gen)}"))
         pending = deque()  # one entry per generate call: [(host tokens, done event), ...]
-        held = None        # a prepared batch waiting for its decode partner
+        held = []          # prepared batches waiting for the rest of their decode group
         calls = 0
 
         def launch(inputs):
@@ -371,9 +378,8 @@ class T5VisionModel(nn.Module):
                     combined.record_stream(sg)
                     mask.record_stream(sg)
                 t5 = self._device_t5()
-                if len(inputs) == 2:
-                    toks = t5.generate_pair_padded(*inputs[0], *inputs[1], self.max_new_tokens,
-                                                   slot=slot)
+                if len(inputs) > 1:
+                    toks = t5.generate_batches_padded(inputs, self.max_new_tokens, slot=slot)
                 else:
                     toks = (t5.generate_padded(*inputs[0], self.max_new_tokens, slot=slot),)
                 hosts = []
@@ -410,16 +416,16 @@ class T5VisionModel(nn.Module):
             with torch.cuda.stream(self._s_prep):
                 combined, mask, _ = self.prepare_input(batch, _pre=pre)
             cur = (combined, mask)
-            if pair_decodes and combined.shape[0] <= 16:
-                if held is None:
-                    held = cur
+            if decode_group > 1 and combined.shape[0] <= 16:
+                held.append(cur)
+                if len(held) < decode_group:
                     continue
-                launch([held, cur])
-                held = None
+                launch(held)
+                held = []
             else:
-                if held is not None:
-                    launch([held])
-                    held = None
+                if held:
+                    launch(held)
+                    held = []
                 launch([cur])
             # Answers are handed out as their calls complete; the host blocks on the oldest only
             # when more than depth + 2 calls are outstanding (a slot's next call is ordered
@@ -428,8 +434,8 @@ class T5VisionModel(nn.Module):
             while pending and (len(pending) > depth + 2 or pending[0][-1][1].query()):
                 for item in pending.popleft():
                     yield self._finish(*item)
-        if held is not None:
-            launch([held])
+        if held:
+            launch(held)
         while pending:
             for item in pending.popleft():
                 yield self._finish(*item)

@@ -157,6 +157,27 @@ class DeviceT5:
                   int(pad_token_id), _lib.ptr(out), self._stream())
         return out
 
+    def generate_batches_padded(self, batches, max_new_tokens=20, decoder_start_token_id=0,
+                                eos_token_id=1, pad_token_id=0, slot: int = 0):
+        """generate_padded() of 1-4 batches [(embeds, mask), ...] (<= 16 rows each) with one
+        shared decode loop (mpr_t5_generate_batches): a list of [B_i, 1+max_new] int32, each
+        bit-identical to its own call."""
+        if not 1 <= len(batches) <= 4:
+            raise ValueError(f"generate_batches: {len(batches)} batches (1 to 4)")
+        ins = [self._inputs(e, m) for e, m in batches]
+        for e, _ in ins:
+            if e.shape[0] > 16:
+                raise ValueError(f"generate_batches: a batch of {e.shape[0]} rows (at most 16)")
+        outs = [torch.empty((e.shape[0], max_new_tokens + 1), device=self.device,
+                            dtype=torch.int32) for e, _ in ins]
+        _lib.call("mpr_t5_generate_batches", self._h, int(slot), len(ins),
+                  _lib.tensor_array([e for e, _ in ins]), _lib.tensor_array([m for _, m in ins]),
+                  _lib.int_array([e.shape[0] for e, _ in ins]),
+                  _lib.int_array([e.shape[1] for e, _ in ins]), int(max_new_tokens),
+                  int(decoder_start_token_id), int(eos_token_id), int(pad_token_id),
+                  _lib.tensor_array(outs), self._stream())
+        return outs
+
     def generate_pair_padded(self, embeds_a, mask_a, embeds_b, mask_b, max_new_tokens=20,
                              decoder_start_token_id=0, eos_token_id=1, pad_token_id=0,
                              slot: int = 0):

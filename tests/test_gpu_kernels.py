@@ -309,10 +309,10 @@ def _t5_batch(t5_sd, b, seed, extra=0):
 
 @pytest.mark.parametrize("graphs", ["1", "0"])
 def test_t5_generate_pair_matches_single(device, t5_sd, monkeypatch, graphs):
-    """Two batches through one shared decode loop (up to 32 rows: the two-row-group skinny
-    GEMMs, a 32-row greedy step): each batch's tokens are bit-identical to its own generate,
-    with equal and different source-length buckets, either batch the longer, 16 + 16 rows, and an
-    empty second batch."""
+    """Two to four batches through one shared decode loop (up to 64 rows: the two- and
+    four-row-group skinny GEMMs, the 64-row greedy step): each batch's tokens are bit-identical
+    to its own generate, with equal and different source-length buckets, any batch the longest,
+    16 + 16 rows, and an empty second batch."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     monkeypatch.setenv("MPR_GRAPHS", graphs)
     m = DeviceT5(t5_sd, device)
@@ -333,6 +333,14 @@ def test_t5_generate_pair_matches_single(device, t5_sd, monkeypatch, graphs):
     assert torch.equal(oa.cpu(), single["A"]) and ob.shape == (0, 21)
     oa, ob = m.generate_pair_padded(*B, *A, 5, slot=2)  # fewer steps: a prefix of the same greedy run
     assert torch.equal(oa.cpu(), single["B"][:, :6]) and torch.equal(ob.cpu(), single["A"][:, :6])
+    # 3 and 4 batches in one loop (48 / 57 rows: the four-row-group GEMVs, a 64-row greedy step)
+    named = {"A": A, "B": B, "C": C, "D": D}
+    for keys in ("ACD", "CDAB", "BDCA"):
+        outs = m.generate_batches_padded([named[k] for k in keys], 20, slot=3)
+        for k, o in zip(keys, outs):
+            assert torch.equal(o.cpu(), single[k]), (keys, k)
+    with pytest.raises(ValueError):
+        m.generate_batches_padded([A, B, C, D, A], 20)
 
 
 def test_t5_embed_and_loss(device, t5_sd):
