@@ -115,9 +115,10 @@ struct AttnArgs {
   int lut_radius = 0;
 };
 int attention(const AttnArgs& a, hipStream_t s);
-// The attentions of up to ATTN_GROUP towers of a lockstep pass in one launch (when all take the
+// The attentions of up to ATTN_GROUP towers of a lockstep pass (or batches of a T5 encoder
+// group) in one launch (when all take the
 // MFMA prefill path; otherwise one attention() each).  Identical results to separate calls.
-constexpr int ATTN_GROUP = 3;
+constexpr int ATTN_GROUP = 4;
 struct AttnGroup {
   AttnArgs a[ATTN_GROUP];
   int n = 0;

@@ -480,14 +480,14 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(AttnArgs a, int nqt
   attention_mfma_body(a, nqt, kv_s);
 }
 
-// The attentions of up to ATTN_GROUP towers in one launch (blockIdx.z picks the problem; the
+// The attentions of up to ATTN_GROUP towers / batches in one launch (blockIdx.z picks the problem; the
 // grid covers the largest, blocks past a problem's heads / query tiles exit).  Per block the same
 // code and data as attention_mfma_kernel: identical results.
 __global__ __launch_bounds__(256) void attention_mfma_group_kernel(AttnGroup grp) {
   extern __shared__ __attribute__((aligned(16))) float kv_s[];
   const int z = blockIdx.z;
   // field-wise wave-uniform selection (dynamic indexing of the kernarg struct spills to scratch)
-#define MPR_SEL(f) (z == 0 ? grp.a[0].f : z == 1 ? grp.a[1].f : grp.a[2].f)
+#define MPR_SEL(f) (z == 0 ? grp.a[0].f : z == 1 ? grp.a[1].f : z == 2 ? grp.a[2].f : grp.a[3].f)
   AttnArgs a;
   a.q = MPR_SEL(q); a.q_bs = MPR_SEL(q_bs); a.q_rs = MPR_SEL(q_rs);
   a.k = MPR_SEL(k); a.k_bs = MPR_SEL(k_bs); a.k_rs = MPR_SEL(k_rs);

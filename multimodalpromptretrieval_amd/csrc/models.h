@@ -126,6 +126,10 @@ struct T5Model : mpr_model {
 
   // encode / logits / embed use workspace slot 0; generate the given slot.
   int encode(const float* embeds, const float* mask, int B, int L, float* out, hipStream_t s);
+  // the encoder over n batches stacked row-wise (batch g: Bs[g] x Ls[g] rows) in one pass of
+  // grouped launches; each batch bit-identical to encode() alone
+  int encode_multi(int n, const int* Bs, const int* Ls, const float* embeds, const float* mask,
+                   float* out, hipStream_t s);
   int generate(const float* embeds, const float* mask, int B, int L, int max_new, int start,
                int eos, int pad, int32_t* out_tokens, hipStream_t s, int slot = 0);
   // generate() of ng <= MAX_GROUPS independent batches (<= 16 rows each) with one shared

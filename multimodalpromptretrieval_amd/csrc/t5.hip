@@ -61,11 +61,27 @@ int T5Model::embed(const int32_t* ids, int B, int len, float* out, int64_t out_b
 
 int T5Model::encode(const float* embeds, const float* mask, int B, int L, float* out,
                     hipStream_t s) {
-  MPR_REQUIRE(L >= 1, "t5 encode: L=%d", L);
-  MPR_REQUIRE(2 * L <= lut_radius, "t5 encode: L=%d exceeds the bucket lut radius %d", L,
-              lut_radius);
-  if (B == 0) return MPR_OK;
-  const int M = B * L;
+  return encode_multi(1, &B, &L, embeds, mask, out, s);
+}
+
+// The T5 encoder over n <= MAX_GROUPS batches at once: batch g's rows (B[g] x L[g]) follow
+// batch g-1's in `embeds`, `mask` and `out`.  Row-wise ops run once over all rows, every GEMM is
+// one grouped launch with a problem per batch (each keeps the tile it gets alone) and the
+// attentions are one grouped launch: each batch's result is bit-identical to encoding it alone.
+int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embeds,
+                          const float* mask, float* out, hipStream_t s) {
+  MPR_REQUIRE(n >= 1 && n <= MAX_GROUPS && n <= GEMM_GROUP && n <= ATTN_GROUP,
+              "t5 encode: %d batches", n);
+  int64_t row0[MAX_GROUPS + 1];
+  row0[0] = 0;
+  for (int g = 0; g < n; ++g) {
+    MPR_REQUIRE(Ls[g] >= 1, "t5 encode: L=%d", Ls[g]);
+    MPR_REQUIRE(2 * Ls[g] <= lut_radius, "t5 encode: L=%d exceeds the bucket lut radius %d",
+                Ls[g], lut_radius);
+    row0[g + 1] = row0[g] + (int64_t)Bs[g] * Ls[g];
+  }
+  const int64_t M = row0[n];
+  if (M == 0) return MPR_OK;
   MPR_TRY(grow(ws->x, (size_t)M * d * 4));
   MPR_TRY(grow(ws->h, (size_t)M * d * 4));
   MPR_TRY(grow(ws->qkv, (size_t)M * 3 * inner * 4));
@@ -79,36 +95,47 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
   MPR_HIP(hipMemcpyAsync(xp, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
   for (auto& lp : enc) {
     const T5Layer& ly = *lp;
-    MPR_TRY(rmsnorm(xp, d, M, d, ly.ln0.as<float>(), T5_EPS, hp, d, s));
-    GemmArgs g;
-    g.A = hp; g.lda = d; g.W = ly.qkv.as<float>(); g.ldw = d; g.C = qp; g.ldc = 3 * inner;
-    g.M = M; g.N = 3 * inner; g.K = d;
-    MPR_TRY(gemm(g, s));
-    AttnArgs at;
-    at.q = qp; at.q_bs = (int64_t)L * 3 * inner; at.q_rs = 3 * inner;
-    at.k = qp + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
-    at.v = qp + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
-    at.o = ap; at.o_bs = (int64_t)L * inner; at.o_rs = inner;
-    at.B = B; at.H = H; at.Lq = L; at.Lk = L; at.scale = 1.f;
-    at.key_mask = mask; at.mask_bs = L;
-    at.rel_tab = enc_tab.as<float>();
-    at.lut_radius = lut_radius;
-    MPR_TRY(attention(at, s));
-    GemmArgs o;
-    o.A = ap; o.lda = inner; o.W = ly.o.as<float>(); o.ldw = inner; o.R = xp; o.ldr = d;
-    o.C = xp; o.ldc = d; o.M = M; o.N = d; o.K = inner;
-    MPR_TRY(gemm(o, s));
-    MPR_TRY(rmsnorm(xp, d, M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
-    GemmArgs f;
-    f.A = hp; f.lda = d; f.W = ly.wi.as<float>(); f.ldw = d; f.C = fp; f.ldc = dff;
-    f.M = M; f.N = dff; f.K = d; f.act = ACT_RELU;
-    MPR_TRY(gemm(f, s));
-    GemmArgs w;
-    w.A = fp; w.lda = dff; w.W = ly.wo.as<float>(); w.ldw = dff; w.R = xp; w.ldr = d;
-    w.C = xp; w.ldc = d; w.M = M; w.N = d; w.K = dff;
-    MPR_TRY(gemm(w, s));
+    MPR_TRY(rmsnorm(xp, d, (int)M, d, ly.ln0.as<float>(), T5_EPS, hp, d, s));
+    GemmGroup gq, go, gi, gw;
+    AttnGroup at;
+    gq.n = go.n = gi.n = gw.n = 0;
+    at.n = 0;
+    for (int g = 0; g < n; ++g) {
+      const int B = Bs[g], L = Ls[g], Mg = B * L;
+      if (Mg == 0) continue;
+      const int64_t r = row0[g];
+      GemmArgs& q = gq.g[gq.n++];
+      q.A = hp + r * d; q.lda = d; q.W = ly.qkv.as<float>(); q.ldw = d;
+      q.C = qp + r * 3 * inner; q.ldc = 3 * inner; q.M = Mg; q.N = 3 * inner; q.K = d;
+      AttnArgs& a = at.a[at.n++];
+      const float* qb = qp + r * 3 * inner;
+      a.q = qb; a.q_bs = (int64_t)L * 3 * inner; a.q_rs = 3 * inner;
+      a.k = qb + inner; a.k_bs = a.q_bs; a.k_rs = 3 * inner;
+      a.v = qb + 2 * inner; a.v_bs = a.q_bs; a.v_rs = 3 * inner;
+      a.o = ap + r * inner; a.o_bs = (int64_t)L * inner; a.o_rs = inner;
+      a.B = B; a.H = H; a.Lq = L; a.Lk = L; a.scale = 1.f;
+      a.key_mask = mask + r; a.mask_bs = L;
+      a.rel_tab = enc_tab.as<float>();
+      a.lut_radius = lut_radius;
+      GemmArgs& o = go.g[go.n++];
+      o.A = ap + r * inner; o.lda = inner; o.W = ly.o.as<float>(); o.ldw = inner;
+      o.R = xp + r * d; o.ldr = d; o.C = xp + r * d; o.ldc = d; o.M = Mg; o.N = d; o.K = inner;
+      GemmArgs& f = gi.g[gi.n++];
+      f.A = hp + r * d; f.lda = d; f.W = ly.wi.as<float>(); f.ldw = d; f.C = fp + r * dff;
+      f.ldc = dff; f.M = Mg; f.N = dff; f.K = d; f.act = ACT_RELU;
+      GemmArgs& w = gw.g[gw.n++];
+      w.A = fp + r * dff; w.lda = dff; w.W = ly.wo.as<float>(); w.ldw = dff; w.R = xp + r * d;
+      w.ldr = d; w.C = xp + r * d; w.ldc = d; w.M = Mg; w.N = d; w.K = dff;
+    }
+    if (gq.n == 0) break;
+    MPR_TRY(gemm_group(gq, s));
+    MPR_TRY(attention_group(at, s));
+    MPR_TRY(gemm_group(go, s));
+    MPR_TRY(rmsnorm(xp, d, (int)M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
+    MPR_TRY(gemm_group(gi, s));
+    MPR_TRY(gemm_group(gw, s));
   }
-  MPR_TRY(rmsnorm(xp, d, M, d, enc_final.as<float>(), T5_EPS, out, d, s));
+  MPR_TRY(rmsnorm(xp, d, (int)M, d, enc_final.as<float>(), T5_EPS, out, d, s));
   return MPR_OK;
 }
 
@@ -278,7 +305,7 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     gr[n++] = Grp{embeds[g], masks[g], Bs[g], Ls[g], Lb, Btot, outs[g]};
     Btot += Bs[g];
     Lp = std::max(Lp, Lb);
-    Mg = std::max(Mg, (int64_t)Bs[g] * Lb);
+    Mg += (int64_t)Bs[g] * Lb;  // the batches' encoder rows, stacked
   }
   if (n == 0) return MPR_OK;
   const int L = Lp, B = Btot;
@@ -327,20 +354,32 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     bool ragged = false;
     for (int k = 1; k < n; ++k) ragged |= gr[k].Lb != gr[0].Lb;
     if (ragged) MPR_HIP(hipMemsetAsync(eo, 0, (size_t)M * d * 4, s));
+    // every batch's inputs at its own bucket, back to back; one grouped encoder pass
+    int bs[MAX_GROUPS], lbs[MAX_GROUPS], pack[2] = {0, 0};
+    int64_t r = 0;
     for (int k = 0; k < n; ++k) {
       const Grp& g = gr[k];
-      MPR_TRY(stage_rows(ws->enc_in.as<float>(), g.e, g.B, g.L, g.Lb, d, s));
-      MPR_TRY(stage_rows(ws->mask_enc.as<float>(), g.m, g.B, g.L, g.Lb, 1, s));
+      MPR_TRY(stage_rows(ws->enc_in.as<float>() + r * d, g.e, g.B, g.L, g.Lb, d, s));
+      MPR_TRY(stage_rows(ws->mask_enc.as<float>() + r, g.m, g.B, g.L, g.Lb, 1, s));
       MPR_HIP(hipMemcpy2DAsync(ws->mask_in.as<float>() + (int64_t)g.row0 * L, (size_t)L * 4, g.m,
                                (size_t)g.L * 4, (size_t)g.L * 4, g.B, hipMemcpyDeviceToDevice,
                                s));
-      MPR_TRY(run(std::make_tuple(2, g.B, g.Lb, 0, 0, 0), s, [&](hipStream_t c) {
-        return encode(ws->enc_in.as<float>(), ws->mask_enc.as<float>(), g.B, g.Lb,
-                      ws->enc_tmp.as<float>(), c);
-      }));
-      MPR_HIP(hipMemcpy2DAsync(eo + (int64_t)g.row0 * L * d, (size_t)L * d * 4, ws->enc_tmp.ptr,
-                               (size_t)g.Lb * d * 4, (size_t)g.Lb * d * 4, g.B,
-                               hipMemcpyDeviceToDevice, s));
+      bs[k] = g.B;
+      lbs[k] = g.Lb;
+      pack[k / 2] |= (g.B | (g.Lb << 5)) << (16 * (k % 2));  // B <= 16, Lb <= 1024
+      r += (int64_t)g.B * g.Lb;
+    }
+    MPR_TRY(run(std::make_tuple(2, n, pack[0], pack[1], 0, 0), s, [&](hipStream_t c) {
+      return encode_multi(n, bs, lbs, ws->enc_in.as<float>(), ws->mask_enc.as<float>(),
+                          ws->enc_tmp.as<float>(), c);
+    }));
+    r = 0;
+    for (int k = 0; k < n; ++k) {
+      const Grp& g = gr[k];
+      MPR_HIP(hipMemcpy2DAsync(eo + (int64_t)g.row0 * L * d, (size_t)L * d * 4,
+                               ws->enc_tmp.as<float>() + r * d, (size_t)g.Lb * d * 4,
+                               (size_t)g.Lb * d * 4, g.B, hipMemcpyDeviceToDevice, s));
+      r += (int64_t)g.B * g.Lb;
     }
     MPR_TRY(run(std::make_tuple(3, B, L, max_new, start, 0), s,
                 [&](hipStream_t c) { return init_body(B, L, max_new, start, c); }));
