@@ -115,6 +115,18 @@ int mpr_encode_towers(mpr_model* vit_a, int32_t mode_a, float* out_a_dev, int64_
                       const int32_t* tok_dev, int32_t n_texts, int32_t seq_len, float* out_t_dev,
                       int64_t out_t_bstride, int32_t slot, void* stream);
 
+/* mpr_encode_towers with n_text_runs (0..2) separate text batches in the same pass: the towers of
+ * two serving batches at once (their images concatenated in img_dev for the ViTs, each batch's
+ * tokens / length / output as its own text run).  Every output is bit-identical to the
+ * single-batch calls.  Text run j uses the text model's workspace slot (slot + j) % 4. */
+int mpr_encode_towers_multi(mpr_model* vit_a, int32_t mode_a, float* out_a_dev,
+                            int64_t out_a_bstride, mpr_model* vit_b, int32_t mode_b,
+                            float* out_b_dev, int64_t out_b_bstride, const float* img_dev,
+                            int32_t n_images, mpr_model* text, int32_t n_text_runs,
+                            const int32_t* const* tok_dev, const int32_t* n_texts,
+                            const int32_t* seq_lens, float* const* out_t_dev,
+                            const int64_t* out_t_bstride, int32_t slot, void* stream);
+
 /* ---- CLIP text encoder: dataset/VQAFeatureDataset.py:190 (clip_model.encode_text) -----------
  * cfg = {width, layers, heads, context_length, vocab, out_dim}.  tensors: token_embedding
  * [vocab,w], positional_embedding [ctx,w], 12 per layer (as ViT), ln_final.weight,

@@ -45,6 +45,10 @@ SIGNATURES = [
     ("mpr_encode_towers", c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int32,
                                     c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p,
                                     c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p]),
+    ("mpr_encode_towers_multi", c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p,
+                                          c_int32, c_void_p, c_int64, c_void_p, c_int32,
+                                          c_void_p, c_int32, POINTER(c_void_p), I32P, I32P,
+                                          POINTER(c_void_p), I64P, c_int32, c_void_p]),
     ("mpr_clip_text_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32,
                                        POINTER(c_void_p)]),
     ("mpr_clip_text_forward", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64,

@@ -243,6 +243,39 @@ int mpr_encode_towers(mpr_model* vit_a, int32_t mode_a, float* out_a, int64_t ou
   });
 }
 
+int mpr_encode_towers_multi(mpr_model* vit_a, int32_t mode_a, float* out_a, int64_t out_a_bs,
+                            mpr_model* vit_b, int32_t mode_b, float* out_b, int64_t out_b_bs,
+                            const float* img, int32_t n_images, mpr_model* text,
+                            int32_t n_text_runs, const int32_t* const* tok,
+                            const int32_t* n_texts, const int32_t* seq_lens,
+                            float* const* out_t, const int64_t* out_t_bs, int32_t slot,
+                            void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(!vit_a || vit_a->kind == mpr_model::VIT, "encode_towers: vit_a not a ViT");
+    MPR_REQUIRE(!vit_b || vit_b->kind == mpr_model::VIT, "encode_towers: vit_b not a ViT");
+    MPR_REQUIRE(!vit_b || vit_a, "encode_towers: vit_b without vit_a");
+    MPR_REQUIRE(!vit_b || vit_a != vit_b, "encode_towers: the two ViT handles must differ");
+    MPR_REQUIRE(!text || text->kind == mpr_model::CLIP_TEXT, "encode_towers: not a text handle");
+    MPR_REQUIRE(n_text_runs >= 0 && n_text_runs <= MAX_TEXT_RUNS && (text || n_text_runs == 0),
+                "encode_towers: %d text runs", n_text_runs);
+    MPR_REQUIRE(n_text_runs == 0 || (tok && n_texts && seq_lens && out_t && out_t_bs),
+                "encode_towers: text run arrays missing");
+    VitModel* v[2] = {static_cast<VitModel*>(vit_a), static_cast<VitModel*>(vit_b)};
+    const int modes[2] = {mode_a, mode_b};
+    float* outs[2] = {out_a, out_b};
+    const int64_t bs[2] = {out_a_bs, out_b_bs};
+    const int nv = vit_b ? 2 : (vit_a ? 1 : 0);
+    int bt[MAX_TEXT_RUNS] = {0, 0}, lt[MAX_TEXT_RUNS] = {1, 1};
+    for (int j = 0; j < n_text_runs; ++j) {
+      bt[j] = n_texts[j];
+      lt[j] = seq_lens[j];
+    }
+    return encode_towers_multi(v, modes, outs, bs, nv, img, n_images,
+                               static_cast<TextModel*>(text), n_text_runs, tok, bt, lt, out_t,
+                               out_t_bs, S(stream), slot);
+  });
+}
+
 // ---- CLIP text ------------------------------------------------------------------------------------
 int mpr_clip_text_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int32_t nt,
                          mpr_model** out) {

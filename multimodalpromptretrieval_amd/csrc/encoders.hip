@@ -65,7 +65,7 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
     for (int i = 0; i < n; ++i) {
       ClipTower& t = *r[i].t;
       const ClipBlock& b = *t.blocks[l];
-      const int W = t.width, M = r[i].B * r[i].L;
+      const int W = t.width, M = r[i].B * r[i].L, TM = M / r[i].tile_div;
       float* x = r[i].x;
       float* hp = r[i].w->h.as<float>();
       float* qp = r[i].w->qkv.as<float>();
@@ -84,6 +84,7 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       pj.A = mp; pj.lda = 4 * W; pj.W = b.pj_w.as<float>(); pj.ldw = 4 * W;
       pj.bias = b.pj_b.as<float>(); pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M;
       pj.N = W; pj.K = 4 * W;
+      g.tile_m = o.tile_m = f.tile_m = pj.tile_m = TM;
     }
     // the towers' LayerNorms and attentions are grouped launches too (one kernel each)
     LnGroup n1, n2;
@@ -138,7 +139,18 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
                   const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
                   const int32_t* tok, int Bt, int Lt, float* out_t, int64_t out_t_bs,
                   hipStream_t s, int slot) {
+  return encode_towers_multi(v, modes, outs, out_bs, nv, img, B, tm, tm ? 1 : 0, &tok, &Bt, &Lt,
+                             &out_t, &out_t_bs, s, slot);
+}
+
+int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs,
+                        const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
+                        int nt, const int32_t* const* toks, const int* Bts, const int* Lts,
+                        float* const* out_ts, const int64_t* out_t_bss, hipStream_t s,
+                        int slot) {
   MPR_REQUIRE(nv >= 0 && nv <= 2, "encode_towers: %d ViTs", nv);
+  MPR_REQUIRE(nt >= 0 && nt <= MAX_TEXT_RUNS && (tm || nt == 0),
+              "encode_towers: %d text runs (at most %d)", nt, MAX_TEXT_RUNS);
   MPR_REQUIRE(slot >= 0 && slot < TOWER_SLOTS, "encode_towers: slot %d outside [0, %d)", slot,
               TOWER_SLOTS);
   for (int i = 0; i < nv; ++i) {
@@ -147,15 +159,33 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
                     v[i]->image == v[0]->image && v[i]->tower.layers == v[0]->tower.layers,
                 "vit group: towers differ in geometry");
   }
-  if (tm) {
-    MPR_REQUIRE(Lt >= 1 && Lt <= tm->ctx, "clip text: seq_len %d outside [1, %d]", Lt, tm->ctx);
+  // the text runs that have rows
+  const int32_t* tok[MAX_TEXT_RUNS];
+  int Btv[MAX_TEXT_RUNS], Ltv[MAX_TEXT_RUNS], tslot[MAX_TEXT_RUNS];
+  float* out_t[MAX_TEXT_RUNS];
+  int64_t out_t_bs[MAX_TEXT_RUNS];
+  int ntr = 0;
+  for (int j = 0; j < nt; ++j) {
+    MPR_REQUIRE(Lts[j] >= 1 && Lts[j] <= tm->ctx, "clip text: seq_len %d outside [1, %d]",
+                Lts[j], tm->ctx);
     MPR_REQUIRE(nv == 0 || tm->tower.layers == v[0]->tower.layers,
                 "encode_towers: text and image towers differ in depth");
+    if (Bts[j] == 0) continue;
+    tok[ntr] = toks[j];
+    Btv[ntr] = Bts[j];
+    Ltv[ntr] = Lts[j];
+    tslot[ntr] = (slot + j) % TOWER_SLOTS;
+    out_t[ntr] = out_ts[j];
+    out_t_bs[ntr] = out_t_bss[j];
+    ++ntr;
   }
+  // the images are `ig` equal serving batches: ViT GEMMs choose tiles for one batch's rows
+  const int ig = (nv > 0 && nt > 1) ? nt : 1;
+  MPR_REQUIRE(B % ig == 0, "encode_towers: %d images are not %d equal batches", B, ig);
   if (B == 0) nv = 0;
-  if (Bt == 0) tm = nullptr;
+  if (ntr == 0) tm = nullptr;
   if (nv == 0 && !tm) return MPR_OK;
-  TowerRun runs[3];
+  TowerRun runs[2 + MAX_TEXT_RUNS];
   int nr = 0;
   if (nv > 0) {
     VitModel& a0 = *v[0];
@@ -175,6 +205,7 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
       GemmArgs& g = pe.g[i];
       g.A = cols.as<float>(); g.lda = P; g.W = v[i]->conv_w.as<float>(); g.ldw = P;
       g.C = v[i]->ws[slot].patches.as<float>(); g.ldc = W; g.M = B * g2; g.N = W; g.K = P;
+      g.tile_m = B / ig * g2;
     }
     MPR_TRY(gemm_group(pe, s));
     for (int i = 0; i < nv; ++i) {
@@ -185,16 +216,16 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
                            W, xp, s));
       MPR_TRY(layernorm(xp, W, B * T, W, m.lnpre_w.as<float>(), m.lnpre_b.as<float>(),
                         CLIP_LN_EPS, xp, W, s));
-      runs[nr++] = TowerRun{&m.tower, &w, xp, B, T, false};
+      runs[nr++] = TowerRun{&m.tower, &w, xp, B, T, false, ig};
     }
   }
-  if (tm) {
-    const int W = tm->width;
-    TowerWs& w = tm->ws[slot];
+  for (int j = 0; tm && j < ntr; ++j) {
+    const int W = tm->width, Bt = Btv[j], Lt = Ltv[j];
+    TowerWs& w = tm->ws[tslot[j]];
     MPR_TRY(w.x.ensure((size_t)Bt * Lt * W * 4));
     MPR_TRY(w.pooled.ensure((size_t)Bt * W * 4));
-    MPR_TRY(embed_gather(tm->tok_emb.as<float>(), tok, tm->ctx, Bt, Lt, W, tm->pos.as<float>(),
-                         w.x.as<float>(), (int64_t)Lt * W, 0, s));
+    MPR_TRY(embed_gather(tm->tok_emb.as<float>(), tok[j], tm->ctx, Bt, Lt, W,
+                         tm->pos.as<float>(), w.x.as<float>(), (int64_t)Lt * W, 0, s));
     runs[nr++] = TowerRun{&tm->tower, &w, w.x.as<float>(), Bt, Lt, true};
   }
   MPR_TRY(ClipTower::run_group(runs, nr, s));
@@ -211,22 +242,24 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
       // ln_post on the CLS rows only (x[b*T]), then @ proj
       MPR_TRY(layernorm(xp, (int64_t)T * W, B, W, m.lnpost_w.as<float>(),
                         m.lnpost_b.as<float>(), CLIP_LN_EPS, tp, W, s));
-      pj.M = B; pj.C = outs[i]; pj.ldc = out_bs[i];
+      pj.M = B; pj.C = outs[i]; pj.ldc = out_bs[i]; pj.tile_m = B / ig;
     } else {
       MPR_TRY(layernorm(xp, W, B * T, W, m.lnpost_w.as<float>(), m.lnpost_b.as<float>(),
                         CLIP_LN_EPS, tp, W, s));
       pj.M = B * T; pj.C = outs[i]; pj.ldc = m.out_dim; pj.c_rpb = T; pj.c_bs = out_bs[i];
+      pj.tile_m = B / ig * T;
     }
   }
-  if (tm) {
-    const int W = tm->width;
-    float* pp = tm->ws[slot].pooled.as<float>();
-    MPR_TRY(eot_gather(tm->ws[slot].x.as<float>(), tok, Bt, Lt, tm->ctx, W, pp, s));
+  for (int j = 0; tm && j < ntr; ++j) {
+    const int W = tm->width, Bt = Btv[j], Lt = Ltv[j];
+    TowerWs& w = tm->ws[tslot[j]];
+    float* pp = w.pooled.as<float>();
+    MPR_TRY(eot_gather(w.x.as<float>(), tok[j], Bt, Lt, tm->ctx, W, pp, s));
     MPR_TRY(layernorm(pp, W, Bt, W, tm->lnf_w.as<float>(), tm->lnf_b.as<float>(), CLIP_LN_EPS,
                       pp, W, s));
     GemmArgs& pj = pg.g[pg.n++];
     pj.A = pp; pj.lda = W; pj.W = tm->projT.as<float>(); pj.ldw = W; pj.M = Bt;
-    pj.N = tm->out_dim; pj.K = W; pj.C = out_t; pj.ldc = out_t_bs;
+    pj.N = tm->out_dim; pj.K = W; pj.C = out_t[j]; pj.ldc = out_t_bs[j];
   }
   MPR_TRY(gemm_group(pg, s));
   return MPR_OK;

@@ -703,7 +703,8 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
     MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                     aligned16(a.W),
                 "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-    GemmGroup& dst = cdiv(a.M, 64) * cdiv(a.N, 64) >= 384 ? big : small;
+    const int tm = a.tile_m > 0 ? a.tile_m : a.M;
+    GemmGroup& dst = cdiv(tm, 64) * cdiv(a.N, 64) >= 384 ? big : small;
     dst.g[dst.n++] = a;
   }
   if (big.n) MPR_TRY(gemm_launch(big, true, s));

@@ -24,6 +24,10 @@ struct GemmArgs {
   // Optional batched C rows: row r is stored at C + (r / c_rpb) * c_bs + (r % c_rpb) * ldc.
   int c_rpb = 0;
   int64_t c_bs = 0;
+  // Rows the tile choice is made for (0: M).  A problem whose rows are several equal serving
+  // batches concatenated sets one batch's rows, so it gets the tile (summation order) each batch
+  // gets alone: bit-identical results.
+  int tile_m = 0;
 };
 
 int gemm(const GemmArgs& a, hipStream_t s);
@@ -72,7 +76,7 @@ int probe_clear();
 
 // LayerNorm over rows of width D (eps, affine), out may alias x.  ld in floats.
 // Up to LN_GROUP LayerNorms (one per tower of a lockstep pass) in one launch; identical results.
-constexpr int LN_GROUP = 3;
+constexpr int LN_GROUP = 4;
 struct LnArgs {
   const float* x = nullptr;
   int64_t ldx = 0;

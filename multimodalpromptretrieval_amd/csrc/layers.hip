@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t 
 template <int V4>
 __global__ __launch_bounds__(256) void layernorm_group_kernel(LnGroup grp, float eps) {
   const int z = blockIdx.y;
-#define MPR_SEL(f) (z == 0 ? grp.p[0].f : z == 1 ? grp.p[1].f : grp.p[2].f)
+#define MPR_SEL(f) (z == 0 ? grp.p[0].f : z == 1 ? grp.p[1].f : z == 2 ? grp.p[2].f : grp.p[3].f)
   const int M = MPR_SEL(M);
   if ((int)blockIdx.x * 8 >= M) return;
   layernorm_rows<V4>(MPR_SEL(x), MPR_SEL(ldx), M, MPR_SEL(D), MPR_SEL(g), MPR_SEL(b), eps,

@@ -48,6 +48,7 @@ struct TowerRun {
   float* x;  // [B*L, width], updated in place
   int B, L;
   bool causal;
+  int tile_div = 1;  // the B rows are tile_div equal batches (GemmArgs::tile_m = M / tile_div)
 };
 
 struct ClipTower {
@@ -82,6 +83,17 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
                   const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
                   const int32_t* tok, int Bt, int Lt, float* out_t, int64_t out_t_bs,
                   hipStream_t s, int slot = 0);
+// Same with up to MAX_TEXT_RUNS separate text batches (their own lengths) in the pass: several
+// serving batches' towers at once.  With ViTs and nt >= 1 text runs the B images are nt equal
+// batches concatenated (B % nt == 0): every ViT GEMM makes its tile choice for one batch's rows,
+// so each batch's outputs are bit-identical to its own pass.  Text run j uses the text model's
+// workspace slot (slot + j) % TOWER_SLOTS.
+constexpr int MAX_TEXT_RUNS = 2;
+int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs,
+                        const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
+                        int nt, const int32_t* const* tok, const int* Bt, const int* Lt,
+                        float* const* out_t, const int64_t* out_t_bs, hipStream_t s,
+                        int slot = 0);
 
 struct T5Layer {
   DevBuf ln0, qkv, o, ln1, wi, wo;         // encoder layer / decoder self-attn + ffn

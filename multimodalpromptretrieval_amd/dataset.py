@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .encoders import CLS, DeviceCLIPText, DeviceViT, encode_towers  # noqa: F401
+from .encoders import CLS, DeviceCLIPText, DeviceViT, encode_towers, encode_towers_multi  # noqa: F401,E501
 from .index import L2, DeviceIndex
 
 BUCKETS = ["very unlikely", "unlikely", "maybe", "likely", "very likely", "certainly"]
@@ -146,46 +146,64 @@ class VQARetrieval:
         batch i+1's towers before it blocks on batch i's retrieval result.  Returns
         (``other_vit``'s output or None, an event recorded after the towers: wait on it, not on
         the stream, which by then may hold the next batch's work).  ``slot`` (0-3) runs the
-        towers on that workspace slot and its own stream, so consecutive batches' towers can
-        overlap; the searches of all slots are ordered on one scan stream."""
+        towers on that workspace slot and its own stream."""
+        return self.prefetch_many([batch], other_vit, other_mode, slot)[0]
+
+    def prefetch_many(self, batches, other_vit=None, other_mode: int = CLS, slot: int = 0):
+        """``prefetch`` of 1-2 batches with ONE tower pass over all their images when they are of
+        equal size (the ViTs over the images concatenated, each batch's questions as its own
+        text run: every row bit-identical to the per-batch pass; unequal batches get a pass
+        each) and one search per batch.  Returns a list of
+        (other output or None, towers event), one per batch."""
         if self.index is None:
             raise RuntimeError("create_retrieval_dataset() / set_index() first")
+        if not 1 <= len(batches) <= 2:
+            raise ValueError(f"prefetch_many: {len(batches)} batches (1 or 2)")
+        if len({b["image"].shape[0] for b in batches}) > 1:  # one pass needs equal batches
+            return [self.prefetch_many([b], other_vit, other_mode, slot)[0] for b in batches]
         s_img = self._slot_stream(int(slot))
         cur = torch.cuda.current_stream(self.device)
-        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
-        toks = self.clip_tokenize(batch["question"])
-        B = img.shape[0]
-        q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
+        imgs = [b["image"].to(self.device, torch.float32, non_blocking=True) for b in batches]
+        img = imgs[0] if len(imgs) == 1 else torch.cat(imgs)
+        toks = [self.clip_tokenize(b["question"]) for b in batches]
+        sizes = [x.shape[0] for x in imgs]
+        rows = [sum(sizes[:j]) for j in range(len(sizes))]
+        q = torch.empty((img.shape[0], self.embed_dim), device=self.device, dtype=torch.float32)
         di = self.image_encoder.out_dim
         kk = self.retrieval_k + (1 if self.is_training_phase else 0)
         s_img.wait_stream(cur)
         img.record_stream(s_img)
         q.record_stream(s_img)
-        host = done = None
         with torch.cuda.stream(s_img):
-            _, other_out, _ = encode_towers(
+            _, other_out, _ = encode_towers_multi(
                 self.image_encoder, img, CLS, out_a=q, out_a_bstride=self.embed_dim,
                 vit_b=other_vit, mode_b=other_mode, text=self.text_encoder, tokens=toks,
-                out_t=q[:, di:], out_t_bstride=self.embed_dim, slot=int(slot))
+                out_t=[q[r:r + n, di:] for r, n in zip(rows, sizes)],
+                out_t_bstride=[self.embed_dim] * len(toks), slot=int(slot))
             towers = torch.cuda.Event()
             towers.record(s_img)
-        if isinstance(self.index, DeviceIndex):  # a sharded search exchanges: done in _topk
-            s_scan = self._scan_stream()
-            s_scan.wait_event(towers)
-            q.record_stream(s_scan)
-            with torch.cuda.stream(s_scan):
-                dist, ids = self.index.search(q, kk)
-                both = torch.cat([ids.to(torch.float64), dist.to(torch.float64)], 1)
-                host = torch.empty(both.shape, dtype=torch.float64, pin_memory=True)
-                host.copy_(both, non_blocking=True)
-                done = torch.cuda.Event()
-                done.record(s_scan)
         if other_out is not None:
             other_out.record_stream(cur)
-        while len(self._prefetched) >= 8:  # never consumed (an abandoned loop): drop the oldest
-            self._prefetched.pop(next(iter(self._prefetched)))
-        self._prefetched[self._key(batch)] = (host, done, q, towers, kk, batch["image"])
-        return other_out, towers
+        out = []
+        for b, r, n in zip(batches, rows, sizes):
+            qb = q[r:r + n]
+            host = done = None
+            if isinstance(self.index, DeviceIndex):  # a sharded search exchanges: in _topk
+                s_scan = self._scan_stream()
+                s_scan.wait_event(towers)
+                q.record_stream(s_scan)
+                with torch.cuda.stream(s_scan):
+                    dist, ids = self.index.search(qb, kk)
+                    both = torch.cat([ids.to(torch.float64), dist.to(torch.float64)], 1)
+                    host = torch.empty(both.shape, dtype=torch.float64, pin_memory=True)
+                    host.copy_(both, non_blocking=True)
+                    done = torch.cuda.Event()
+                    done.record(s_scan)
+            while len(self._prefetched) >= 8:  # never consumed (an abandoned loop): drop oldest
+                self._prefetched.pop(next(iter(self._prefetched)))
+            self._prefetched[self._key(b)] = (host, done, qb, towers, kk, b["image"])
+            out.append((None if other_out is None else other_out[r:r + n], towers))
+        return out
 
     def encode_queries(self, batch) -> torch.Tensor:
         """[CLS image embedding ‖ EOT text embedding] fp32 [B, 1024] on the device

@@ -170,6 +170,54 @@ def encode_towers(vit_a: "DeviceViT" = None, img: torch.Tensor = None, mode_a: i
     return out_a, out_b, out_t
 
 
+def encode_towers_multi(vit_a: "DeviceViT", img: torch.Tensor, mode_a: int = CLS, out_a=None,
+                        out_a_bstride=None, vit_b: "DeviceViT" = None, mode_b: int = TOKENS,
+                        out_b=None, out_b_bstride=None, text: "DeviceCLIPText" = None,
+                        tokens: list = (), out_t: list = None, out_t_bstride: list = None,
+                        slot: int = 0):
+    """encode_towers over several EQUAL-SIZED batches at once (mpr_encode_towers_multi): ``img``
+    holds the batches' images concatenated (the ViTs run over all of them, choosing GEMM tiles
+    for one batch's rows), ``tokens`` is a list of up to 2 per-batch clip.tokenize tensors (each
+    its own text run, own length).  Every output row is bit-identical to the per-batch
+    encode_towers call.  Returns (out_a, out_b, [out_t, ...])."""
+    if len(tokens) > 2:
+        raise ValueError(f"encode_towers_multi: {len(tokens)} text runs (at most 2)")
+    if len(tokens) > 1 and any(t.shape[0] * len(tokens) != img.shape[0] for t in tokens):
+        raise ValueError("encode_towers_multi: the batches must be of equal size "
+                         f"({img.shape[0]} images, text runs of {[t.shape[0] for t in tokens]})")
+    dev = vit_a.device
+    img = img.to(dev, torch.float32, non_blocking=True).contiguous()
+    B = img.shape[0]
+    if tuple(img.shape[1:]) != (3, vit_a.image_size, vit_a.image_size):
+        raise ValueError(f"expected images [B,3,{vit_a.image_size},{vit_a.image_size}], "
+                         f"got {tuple(img.shape)}")
+    out_a, out_a_bstride = vit_a._out(B, mode_a, out_a, out_a_bstride)
+    if vit_b is not None:
+        if vit_b is vit_a or vit_b.device != dev:
+            raise ValueError("vit_b needs a different vit_a on the same device")
+        out_b, out_b_bstride = vit_b._out(B, mode_b, out_b, out_b_bstride)
+    toks, lens, outs, bss = [], [], [], []
+    for j, t in enumerate(tokens):
+        tok, L = text._tokens(t)
+        toks.append(tok)
+        lens.append(L)
+        if out_t is None or out_t[j] is None:
+            o = torch.empty((tok.shape[0], text.out_dim), device=dev, dtype=torch.float32)
+            outs.append(o)
+            bss.append(text.out_dim)
+        else:
+            outs.append(out_t[j])
+            bss.append(int(out_t_bstride[j]))
+    _lib.call("mpr_encode_towers_multi", vit_a._h, mode_a, _lib.ptr(out_a),
+              int(out_a_bstride or 0), vit_b._h if vit_b is not None else None, mode_b,
+              _lib.ptr(out_b), int(out_b_bstride or 0), _lib.ptr(img), B,
+              text._h if text is not None else None, len(toks), _lib.tensor_array(toks),
+              _lib.int_array([t.shape[0] for t in toks]), _lib.int_array(lens),
+              _lib.tensor_array(outs), _lib.int_array(bss, _lib.ctypes.c_int64), int(slot),
+              _lib.stream_ptr(dev))
+    return out_a, out_b, outs
+
+
 class DeviceCLIPText(_Handle):
     """CLIP text transformer (openai naming, no prefix) on one GPU."""
 

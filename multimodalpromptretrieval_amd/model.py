@@ -226,18 +226,20 @@ class T5VisionModel(nn.Module):
                 and (enc.width, enc.patch, enc.image_size, enc.layers)
                 == (vit.width, vit.patch, vit.image_size, vit.layers))
 
-    def _prefetch(self, batch, slot: int = 0):
+    def _prefetch(self, batches, slot: int = 0):
         """Serving-loop lookahead: with a ``VQARetrieval`` retrieval function, enqueue the
-        batch's towers (the token-feature ViT paired with the retrieval's when pairable), index
-        scan and top-k copy now (``VQARetrieval.prefetch``); ``prepare_input(batch, _pre=...)``
-        then only waits for them.  None when there is nothing to prefetch."""
+        batches' towers (one pass over 1-2 batches; the token-feature ViT paired with the
+        retrieval's when pairable), index scans and top-k copies now
+        (``VQARetrieval.prefetch_many``); ``prepare_input(batch, _pre=...)`` then only waits for
+        them.  A list with one entry per batch (None entries when there is nothing to
+        prefetch)."""
         retr = getattr(self.retrieval_function, "__self__", None)
-        fn = getattr(retr, "prefetch", None)
+        fn = getattr(retr, "prefetch_many", None)
         if fn is None or getattr(retr, "index", None) is None:
-            return None
+            return [None] * len(batches)
         vit = self._device_vit()
         other = vit if self.use_image_info and self._pairable(retr, vit) else None
-        return fn(batch, other, TOKENS, slot)
+        return fn(batches, other, TOKENS, slot)
 
     def prepare_input(self, batch, _pre=None):
         """architectures/T5VisionModel.py:141-184.
@@ -324,7 +326,7 @@ class T5VisionModel(nn.Module):
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     def predict_many(self, batches, decodes_in_flight: int = 2, pair_decodes=None,
-                     lookahead=None, tower_slots=None, decode_group=None):
+                     lookahead=None, tower_slots=None, decode_group=None, tower_batches=None):
         """predict() over an iterable of batches as a serving pipeline.  A greedy decode is a
         chain of small latency-bound launches that leaves most of the chip idle, so
         (1) ``decode_group`` (1-4, default MPR_DECODE_GROUP or 4; ``pair_decodes`` = False / True
@@ -336,7 +338,9 @@ class T5VisionModel(nn.Module):
         index scan run beside them and the host builds its prompts;
         (3) with ``lookahead`` (default on; MPR_LOOKAHEAD=0 turns it off), batch i+1's
         towers, scan and top-k copy are enqueued before the host blocks on batch i's retrieval
-        result, so the towers never wait on the host.  ``tower_slots`` > 1 (MPR_TOWER_SLOTS)
+        result, so the towers never wait on the host; ``tower_batches`` (1-2, default
+        MPR_TOWER_BATCHES or 2) batches share one tower pass (the ViTs over their images
+        concatenated: fewer, fuller launches).  ``tower_slots`` > 1 (MPR_TOWER_SLOTS)
         runs consecutive batches' towers on that many workspace slots and streams at once:
         alone two passes overlap to 0.86x their back-to-back time, but beside the decodes of
         the loop it measured slower (2177-1983 vs 2300-2241 QA pairs/s), so the default is 1.
@@ -354,6 +358,9 @@ class T5VisionModel(nn.Module):
         decode_group = max(1, min(int(decode_group), 4))
         if lookahead is None:
             lookahead = os.environ.get("MPR_LOOKAHEAD", "1") != "0"
+        if tower_batches is None:
+            tower_batches = int(os.environ.get("MPR_TOWER_BATCHES", "2"))
+        tower_batches = max(1, min(int(tower_batches), 2))
         if tower_slots is None:
             tower_slots = int(os.environ.get("MPR_TOWER_SLOTS", "1"))
         tower_slots = max(1, min(int(tower_slots), 4))
@@ -392,26 +399,39 @@ class T5VisionModel(nn.Module):
             pending.append([(h, done) for h in hosts])
 
         n_pre = 0
-
-        def prefetch(b):
-            nonlocal n_pre
-            if b is None or not lookahead:
-                return None
-            self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self._s_prep):
-                pre = self._prefetch(b, n_pre % tower_slots)
-            n_pre += 1
-            return pre
-
         it = iter(batches)
-        nxt = next(it, None)
-        nxt_pre = prefetch(nxt)
-        while nxt is not None:
-            batch, pre = nxt, nxt_pre
-            nxt = next(it, None)
-            # the next batch's towers and scan go on the device before the host blocks on this
-            # batch's retrieval result
-            nxt_pre = prefetch(nxt)
+        ready = deque()  # (batch, prefetched handles) in order
+        exhausted = False
+
+        def refill():
+            # keep the next tower pass enqueued before the host blocks on a retrieval result
+            nonlocal n_pre, exhausted
+            while not exhausted and len(ready) < (tower_batches if lookahead else 1):
+                chunk = []
+                while len(chunk) < (tower_batches if lookahead else 1):
+                    b = next(it, None)
+                    if b is None:
+                        exhausted = True
+                        break
+                    chunk.append(b)
+                if not chunk:
+                    break
+                if lookahead:
+                    self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(self._s_prep):
+                        pres = self._prefetch(chunk, n_pre % tower_slots)
+                    n_pre += 1
+                else:
+                    pres = [None] * len(chunk)
+                ready.extend(zip(chunk, pres))
+
+        while True:
+            if not ready:
+                refill()
+            if not ready:
+                break
+            batch, pre = ready.popleft()
+            refill()
             self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self._s_prep):
                 combined, mask, _ = self.prepare_input(batch, _pre=pre)

@@ -152,7 +152,8 @@ def test_g2_predict_many_matches_predict(device):
         assert list(model.predict_many(batches, depth)) == want
         assert list(model.predict_many(batches, depth, pair_decodes=False)) == want
         assert list(model.predict_many(batches, depth, lookahead=False)) == want
-        assert list(model.predict_many(batches, depth, tower_slots=1)) == want
+        assert list(model.predict_many(batches, depth, tower_slots=2)) == want
+        assert list(model.predict_many(batches, depth, tower_batches=1)) == want
     assert list(model.predict_many(batches[:3])) == want[:3]  # an unpaired last batch
     for group in (3, 4):  # 3 / 4 batches per decode loop (a partial last group at 3)
         assert list(model.predict_many(batches, decode_group=group)) == want

@@ -162,6 +162,33 @@ def test_encode_towers_matches_separate(device, clip_sd):
     assert torch.equal(t_only, txt(toks[:3]))
 
 
+def test_encode_towers_multi_matches_per_batch(device, clip_sd):
+    """Two batches' towers in one pass (images concatenated for the ViTs, each batch's questions
+    a text run of its own length) == the per-batch passes, bit for bit."""
+    from multimodalpromptretrieval_amd.encoders import (CLS, TOKENS, DeviceCLIPText, DeviceViT,
+                                                         encode_towers, encode_towers_multi)
+    a, b = DeviceViT(clip_sd, device), DeviceViT(syn.clip_state_dict(14), device)
+    txt = DeviceCLIPText(clip_sd, device)
+    imgs = [syn.images(60, 11).to(device), syn.images(61, 11).to(device)]
+    toks = [syn.clip_tokens(62, 11), syn.clip_tokens(63, 11).clone()]
+    eot = int(toks[1].max())
+    toks[1][:, 9] = eot  # the second batch's prompts end earlier: a shorter text run
+    toks[1][:, 10:] = 0
+    assert int(toks[0].argmax(1).max()) != int(toks[1].argmax(1).max())
+    want = [encode_towers(a, imgs[i], CLS, vit_b=b, mode_b=TOKENS, text=txt, tokens=toks[i])
+            for i in range(2)]
+    ca, tb, tts = encode_towers_multi(a, torch.cat(imgs), CLS, vit_b=b, mode_b=TOKENS, text=txt,
+                                      tokens=toks)
+    # 11-image batches: alone some projections take the 32x32 tile that 22 images' rows would
+    # not; the per-batch tile choice keeps the pass bit-identical
+    assert torch.equal(ca[:11], want[0][0]) and torch.equal(ca[11:], want[1][0])
+    assert torch.equal(tb[:11], want[0][1]) and torch.equal(tb[11:], want[1][1])
+    assert torch.equal(tts[0], want[0][2]) and torch.equal(tts[1], want[1][2])
+    with pytest.raises(ValueError):  # unequal batches cannot share a pass
+        encode_towers_multi(a, torch.cat([imgs[0], imgs[1][:5]]), CLS, text=txt,
+                            tokens=[toks[0], toks[1][:5]])
+
+
 def test_encode_towers_slots_run_concurrently(device, clip_sd):
     """Two batches' lockstep passes on workspace slots 0 and 1 on two streams at once (repeated,
     so the passes overlap): each equals its pass run alone, bit for bit."""
