@@ -221,6 +221,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 sharded-scan line")
+    ap.add_argument("--index-sharding", choices=["auto", "shard", "replicate"], default="auto",
+                    help="N>1: row-shard the serving index over the ranks (an RCCL exchange per "
+                         "batch) or keep a replica per rank; auto shards past 1 GiB (C2's "
+                         "26.6 MB index is replicated; C5's sharded scan is always sharded)")
     ap.add_argument("--no-index-build", action="store_true",
                     help="skip the index-build line (create_retrieval_dataset throughput)")
     ap.add_argument("--inflight", type=int, default=2,
@@ -248,7 +252,10 @@ def main():
             dist.init_process_group(backend)
         group = dist.group.WORLD
 
-    model, retr, weights = build(cfg, device, group)
+    index_bytes = cfg["N"] * cfg["D"] * 4
+    shard = world > 1 and (args.index_sharding == "shard" or
+                           (args.index_sharding == "auto" and index_bytes > (1 << 30)))
+    model, retr, weights = build(cfg, device, group if shard else None)
     batches = make_batches(4, cfg["B"], device, seed=100 + rank)
 
     def barrier():
@@ -366,8 +373,9 @@ def main():
                     "random 224x224 images + random-word questions)",
             "config": {"workload": cfg["desc"], "global_batch": world * cfg["B"],
                        "index_rows": cfg["N"], "index_dim": cfg["D"], "k": cfg["k"],
-                       "decode_steps": 20, "index_sharding": f"rows/{world}" if world > 1
-                       else "single", "parallelism": f"dp{world}"},
+                       "decode_steps": 20, "index_sharding": f"rows/{world}" if shard
+                       else ("replica per rank" if world > 1 else "single"),
+                       "parallelism": f"dp{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "c5_scan": c5, "index_build": ib,

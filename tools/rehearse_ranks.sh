@@ -6,6 +6,6 @@ mkdir -p gpurun_out/rehearse
 for n in 2 4; do
   MPR_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) \
-    bench.py --gpus $n --steps 5 --warmup 2 --no-cpu-baseline --no-probe \
+    bench.py --gpus $n --steps 5 --warmup 2 --no-cpu-baseline --no-probe $EXTRA \
     > gpurun_out/rehearse/bench_n$n.json 2> gpurun_out/rehearse/bench_n$n.err
 done
