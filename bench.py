@@ -60,7 +60,8 @@ def _pmc_traffic():
     (tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 half-count of wide streaming reads) +
     WRITE_SIZE, separate --pmc passes, windowed to the replay).  (bytes, source) or (None, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gemm.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gemm.json")),
+                   key=os.path.getmtime)
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -256,6 +257,10 @@ def main():
     shard = world > 1 and (args.index_sharding == "shard" or
                            (args.index_sharding == "auto" and index_bytes > (1 << 30)))
     model, retr, weights = build(cfg, device, group if shard else None)
+    # SURVEY §8(f) rank 1, measured first: a separate retrieval object on a fresh process state
+    ib = None
+    if rank == 0 and not args.no_index_build:
+        ib = index_build(cfg, weights, device)
     batches = make_batches(4, cfg["B"], device, seed=100 + rank)
 
     def barrier():
@@ -346,10 +351,6 @@ def main():
     if not args.no_c5:
         c5 = c5_scan(world, rank, device, group, rdev)
         barrier()
-
-    ib = None
-    if rank == 0 and not args.no_index_build:
-        ib = index_build(cfg, weights, device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

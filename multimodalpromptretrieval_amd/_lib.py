@@ -154,7 +154,7 @@ def to_device_async(t, device, dtype=None):
     the stream — and, with more streams than the 4 hardware queues, for work of other streams
     that share its queue).  Device tensors are only converted."""
     import torch
-    if t.device.type != "cpu":
+    if t.device.type != "cpu" or os.environ.get("MPR_PIN_H2D") == "0":
         return t.to(device, dtype) if dtype is not None else t.to(device)
     if dtype is not None:
         t = t.to(dtype)

@@ -24,7 +24,7 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
   ok_or_stop $? smoke 0
 fi
-timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 4 > "$OUT/bench.json" 2> "$OUT/bench.err"
 ok_or_stop $? bench 0
 if [ -z "$SKIP_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
