@@ -90,6 +90,7 @@ def main():
     wrap(index.DeviceIndex, "search", "scan")
     wrap(t5.DeviceT5, "generate_padded", "t5.generate")
     wrap(t5.DeviceT5, "generate_pair_padded", "t5.gen-pair")
+    wrap(t5.DeviceT5, "generate_batches_padded", "t5.gen-group")
     wrap_fn(dataset, "encode_towers", "towers")
     wrap_fn(dataset, "encode_towers_multi", "towers")
     wrap_host(model_mod.T5VisionModel, "prepare_input", "prepare(host)")
