@@ -295,8 +295,17 @@ int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
     gx = std::max(gx, (int)cdiv(g.g[i].N, BN));
     gy = std::max(gy, (int)cdiv(g.g[i].M, BM));
   }
+  // MPR_GEMM_LDS_KB: reserve that much LDS per block (unused dynamic LDS beyond the static
+  // stages), capping the blocks per CU so the decode GEMVs of other streams fit beside them
+  // (41 KB = 3 blocks per CU measured 3012 vs 3028 QA pairs/s: off by default).
+  static const int lds_kb = [] {
+    const char* e = getenv("MPR_GEMM_LDS_KB");
+    return e ? atoi(e) : 0;
+  }();
+  constexpr int STATIC_LDS = 2 * (BM + BN) * (BK + 4) * 4;
+  const size_t pad = lds_kb * 1024 > STATIC_LDS ? (size_t)(lds_kb * 1024 - STATIC_LDS) : 0;
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, D, KW, XR>), dim3(gx, gy, g.n), dim3(NT),
-                     0, s, g);
+                     pad, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -777,7 +786,28 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
                 (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0);
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
+  static const bool small_lds = [] {
+    const char* e = getenv("MPR_SKINNY_SMALL");
+    return e && e[0] == '1';
+  }();
   return probed(PROBE_SKINNY, 2.0 * a.M * a.N * a.K, gemm_bytes(a), s, [&]() {
+    // MPR_SKINNY_SMALL=1: <= 43 KB of LDS per block (fits beside 3 GEMM blocks on a CU) at the
+    // price of more, shorter passes; in the serving loop 3086 vs 3028 QA pairs/s (within the
+    // box-to-box spread), and the MAXC change moves the summation order: off by default.
+    if (small_lds) {
+      if (a.M > 32) {
+        if (per <= 1) launch_skinny<1, 1, false, 4>(sa, F, (unsigned)tiles, s);
+        else launch_skinny<1, 1, true, 4>(sa, F, (unsigned)tiles, s);
+      } else if (a.M > 16) {
+        if (per <= 2) launch_skinny<2, 1, false, 2>(sa, F, (unsigned)tiles, s);
+        else launch_skinny<2, 1, true, 2>(sa, F, (unsigned)tiles, s);
+      } else {
+        if (per <= 4) launch_skinny<4, 1, false>(sa, F, (unsigned)tiles, s);
+        else launch_skinny<4, 1, true>(sa, F, (unsigned)tiles, s);
+      }
+      MPR_LAUNCHED();
+      return MPR_OK;
+    }
     if (a.M > 32) {  // four row groups per weight load (up to 4 batches of <= 16 rows)
       if (amax && tiles >= 1024 && per <= 4)
         launch_skinny<4, 2, false, 4>(sa, F, (unsigned)cdiv(tiles, 2), s);
