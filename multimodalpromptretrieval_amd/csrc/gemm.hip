@@ -9,9 +9,10 @@
 // that each lane reads 16 contiguous floats (4 x ds_read_b128) per operand and tile; the LDS rows
 // are padded to 36 floats, which makes those 128-bit reads bank-conflict free.
 //
-// gemm_skinny() serves decoder steps (M = batch <= 16): W streams straight from HBM/L2 into
-// registers as the A operand of v_mfma_f32_16x16x4_f32 (16 output columns per block), the 16
-// activation rows are the B operand, K is split across the 8 waves of a block and reduced through
+// gemm_skinny() serves decoder steps (M = batch rows <= 16, or up to 64 when 2-4 batches share a
+// decode loop): W streams straight from HBM/L2 into registers as the A operand of
+// v_mfma_f32_16x16x4_f32 (16 output columns per block), each 16-row group of activations is a B
+// operand for the same weight registers, K is split across the 8 waves of a block and reduced through
 // LDS, and T5's RMSNorm of the activation rows is folded into the operand and the epilogue.
 #include <algorithm>
 
