@@ -795,6 +795,10 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
     // MPR_SKINNY_SMALL=1: <= 43 KB of LDS per block (fits beside 3 GEMM blocks on a CU) at the
     // price of more, shorter passes; in the serving loop 3086 vs 3028 QA pairs/s (within the
     // box-to-box spread), and the MAXC change moves the summation order: off by default.
+    // (A K split of the K = 2048 GEMV over 4 blocks per tile, partials published with an
+    // agent-scope fence and added by the last block, made a 16-row generate 5.49 -> 5.89 ms and
+    // the serving loop 3050 -> 2830 QA pairs/s: the cross-XCD publish costs more than the
+    // 32-block launch loses.)
     if (small_lds) {
       if (a.M > 32) {
         if (per <= 1) launch_skinny<1, 1, false, 4>(sa, F, (unsigned)tiles, s);
