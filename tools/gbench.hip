@@ -61,26 +61,23 @@ int main() {
   }
   struct Shape { const char* name; int M, N, K; bool res; };
   const Shape shapes[] = {
-      {"vit out   800x768x768 +R", 800, 768, 768, true},
-      {"vit fc2   800x768x3072 +R", 800, 768, 3072, true},
-      {"t5e wo   1152x512x2048 +R", 1152, 512, 2048, true},
-      {"t5e o    1152x512x512 +R", 1152, 512, 512, true},
-      {"txt qkv   384x1536x512", 384, 1536, 512, false},
+      {"vit qkv  1600x2304x768", 1600, 2304, 768, false},
+      {"vit out  1600x768x768 +R", 1600, 768, 768, true},
+      {"vit fc1  1600x3072x768", 1600, 3072, 768, false},
+      {"vit fc2  1600x768x3072 +R", 1600, 768, 3072, true},
+      {"vit qkv   800x2304x768", 800, 2304, 768, false},
+      {"vit fc1   800x3072x768", 800, 3072, 768, false},
   };
   using L = std::function<int(const GemmGroup&, hipStream_t)>;
   struct Var { const char* name; L fn; };
   const Var vars[] = {
       {"64x64 k32 D2 XR", launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>},
       {"32x32 k64 D2 W4", launch_gemm_group<32, 32, 1, 1, 64, 2, 4>},
-      {"32x32 k64 D2 W4 XR", launch_gemm_group<32, 32, 1, 1, 64, 2, 4, true>},
-      {"32x32 k64 D3 W4", launch_gemm_group<32, 32, 1, 1, 64, 3, 4>},
-      {"32x32 k128 D2 W4", launch_gemm_group<32, 32, 1, 1, 128, 2, 4>},
-      {"32x32 k128 D2 W8", launch_gemm_group<32, 32, 1, 1, 128, 2, 8>},
-      {"32x64 k64 D2 W4", launch_gemm_group<32, 64, 1, 1, 64, 2, 4>},
+      {"128x64 2x1/w k32 D2 XR", launch_gemm_group<128, 64, 2, 1, 32, 2, 1, true>},
+      {"64x128 1x2/w k32 D2 XR", launch_gemm_group<64, 128, 1, 2, 32, 2, 1, true>},
+      {"128x128 2x2/w k32 D2 XR", launch_gemm_group<128, 128, 2, 2, 32, 2, 1, true>},
+      {"64x64 1x2/w k32 D2 W2 XR", launch_gemm_group<64, 64, 1, 2, 32, 2, 2, true>},
       {"32x64 k64 D2 W2", launch_gemm_group<32, 64, 1, 1, 64, 2, 2>},
-      {"64x32 k64 D2 W4", launch_gemm_group<64, 32, 1, 1, 64, 2, 4>},
-      {"32x64 1x2/w k64 D2 W4", launch_gemm_group<32, 64, 1, 2, 64, 2, 4>},
-      {"64x64 k64 D2 W4", launch_gemm_group<64, 64, 1, 1, 64, 2, 4>},
   };
   for (const Shape& sh : shapes) {
     for (int grp = 1; grp <= 2; ++grp) {
