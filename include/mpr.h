@@ -185,8 +185,8 @@ int mpr_t5_generate_pair(mpr_model* m, int32_t slot, const float* embeds_a_dev,
                          const float* embeds_b_dev, const float* mask_b_dev, int32_t b_b,
                          int32_t L_b, int32_t max_new, int32_t decoder_start, int32_t eos,
                          int32_t pad, int32_t* out_a_dev, int32_t* out_b_dev, void* stream);
-/* n (1..4) batches (b[i] <= 16 rows each, own source lengths L[i]) generated with one shared
- * decode loop of sum(b) <= 64 rows on workspace slot `slot` (the general form of
+/* n (1..8) batches (b[i] <= 16 rows each, own source lengths L[i]) generated with one shared
+ * decode loop of sum(b) <= 128 rows on workspace slot `slot` (the general form of
  * mpr_t5_generate_pair; arrays of n device pointers / sizes).  out[i] [b[i], 1+max_new] is
  * bit-identical to mpr_t5_generate_slot on batch i. */
 int mpr_t5_generate_batches(mpr_model* m, int32_t slot, int32_t n,

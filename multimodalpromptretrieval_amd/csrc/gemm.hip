@@ -769,7 +769,7 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s) {
 // blocks, made the two-decodes-in-flight serving loop 1-6% slower.)
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const GemmArgs& a = sa.g;
-  MPR_REQUIRE(a.M >= 0 && a.M <= 64 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
+  MPR_REQUIRE(a.M >= 0 && a.M <= 128 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
   if (a.M == 0 || a.N == 0) return MPR_OK;
   MPR_REQUIRE(sa.wpk && aligned16(sa.wpk), "gemm_skinny: needs the 16-byte aligned packed weight");
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && aligned16(a.A) &&
@@ -813,7 +813,13 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
       MPR_LAUNCHED();
       return MPR_OK;
     }
-    if (a.M > 32) {  // four row groups per weight load (up to 4 batches of <= 16 rows)
+    if (a.M > 64) {  // eight row groups per weight load (up to 8 batches): 2-chunk passes fit
+      // (one tile per block also for the lm_head: two would spill registers)
+      if (per <= 2)
+        launch_skinny<2, 1, false, 8>(sa, F, (unsigned)tiles, s);
+      else
+        launch_skinny<2, 1, true, 8>(sa, F, (unsigned)tiles, s);
+    } else if (a.M > 32) {  // four row groups per weight load (up to 4 batches of <= 16 rows)
       if (amax && tiles >= 1024 && per <= 4)
         launch_skinny<4, 2, false, 4>(sa, F, (unsigned)cdiv(tiles, 2), s);
       else if (per <= 4)

@@ -124,7 +124,7 @@ struct T5Work {
 
 struct T5Model : mpr_model {
   static constexpr int MAX_SLOTS = 4;
-  static constexpr int MAX_GROUPS = 4;  // batches (<= 16 rows each) sharing one decode loop
+  static constexpr int MAX_GROUPS = 8;  // batches (<= 16 rows each) sharing one decode loop
   T5Model() : mpr_model(T5) { use_slot(0); }
   int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
   int inner = 0, lut_radius = 0;
@@ -145,7 +145,7 @@ struct T5Model : mpr_model {
   int generate(const float* embeds, const float* mask, int B, int L, int max_new, int start,
                int eos, int pad, int32_t* out_tokens, hipStream_t s, int slot = 0);
   // generate() of ng <= MAX_GROUPS independent batches (<= 16 rows each) with one shared
-  // decode loop of up to 64 rows: each batch is encoded on its own (as generate() would), the
+  // decode loop of up to 128 rows: each batch is encoded on its own (as generate() would), the
   // decode runs over all; every batch's tokens are bit-identical to its own generate() call.
   int generate_groups(int ng, const float* const* embeds, const float* const* masks,
                       const int* Bs, const int* Ls, int max_new, int start, int eos, int pad,

@@ -70,9 +70,8 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
 // attentions are one grouped launch: each batch's result is bit-identical to encoding it alone.
 int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embeds,
                           const float* mask, float* out, hipStream_t s) {
-  MPR_REQUIRE(n >= 1 && n <= MAX_GROUPS && n <= GEMM_GROUP && n <= ATTN_GROUP,
-              "t5 encode: %d batches", n);
-  int64_t row0[MAX_GROUPS + 1];
+  MPR_REQUIRE(n >= 1 && n <= GEMM_GROUP && n <= ATTN_GROUP, "t5 encode: %d batches", n);
+  int64_t row0[GEMM_GROUP + 1];
   row0[0] = 0;
   for (int g = 0; g < n; ++g) {
     MPR_REQUIRE(Ls[g] >= 1, "t5 encode: L=%d", Ls[g]);
@@ -355,7 +354,7 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     for (int k = 1; k < n; ++k) ragged |= gr[k].Lb != gr[0].Lb;
     if (ragged) MPR_HIP(hipMemsetAsync(eo, 0, (size_t)M * d * 4, s));
     // every batch's inputs at its own bucket, back to back; one grouped encoder pass
-    int bs[MAX_GROUPS], lbs[MAX_GROUPS], pack[2] = {0, 0};
+    int bs[MAX_GROUPS], lbs[MAX_GROUPS], pack[MAX_GROUPS / 2] = {0, 0, 0, 0};
     int64_t r = 0;
     for (int k = 0; k < n; ++k) {
       const Grp& g = gr[k];
@@ -369,10 +368,19 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
       pack[k / 2] |= (g.B | (g.Lb << 5)) << (16 * (k % 2));  // B <= 16, Lb <= 1024
       r += (int64_t)g.B * g.Lb;
     }
-    MPR_TRY(run(std::make_tuple(2, n, pack[0], pack[1], 0, 0), s, [&](hipStream_t c) {
-      return encode_multi(n, bs, lbs, ws->enc_in.as<float>(), ws->mask_enc.as<float>(),
-                          ws->enc_tmp.as<float>(), c);
-    }));
+    MPR_TRY(run(std::make_tuple(2, n, pack[0], pack[1], pack[2], pack[3]), s,
+                [&](hipStream_t c) {
+                  // grouped passes of up to GEMM_GROUP batches over the stacked rows
+                  int64_t rr = 0;
+                  for (int k0 = 0; k0 < n; k0 += GEMM_GROUP) {
+                    const int nk = std::min(GEMM_GROUP, n - k0);
+                    MPR_TRY(encode_multi(nk, bs + k0, lbs + k0, ws->enc_in.as<float>() + rr * d,
+                                         ws->mask_enc.as<float>() + rr,
+                                         ws->enc_tmp.as<float>() + rr * d, c));
+                    for (int k = k0; k < k0 + nk; ++k) rr += (int64_t)bs[k] * lbs[k];
+                  }
+                  return MPR_OK;
+                }));
     r = 0;
     for (int k = 0; k < n; ++k) {
       const Grp& g = gr[k];

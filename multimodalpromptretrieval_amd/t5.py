@@ -159,11 +159,11 @@ class DeviceT5:
 
     def generate_batches_padded(self, batches, max_new_tokens=20, decoder_start_token_id=0,
                                 eos_token_id=1, pad_token_id=0, slot: int = 0):
-        """generate_padded() of 1-4 batches [(embeds, mask), ...] (<= 16 rows each) with one
+        """generate_padded() of 1-8 batches [(embeds, mask), ...] (<= 16 rows each) with one
         shared decode loop (mpr_t5_generate_batches): a list of [B_i, 1+max_new] int32, each
         bit-identical to its own call."""
-        if not 1 <= len(batches) <= 4:
-            raise ValueError(f"generate_batches: {len(batches)} batches (1 to 4)")
+        if not 1 <= len(batches) <= 8:
+            raise ValueError(f"generate_batches: {len(batches)} batches (1 to 8)")
         ins = [self._inputs(e, m) for e, m in batches]
         for e, _ in ins:
             if e.shape[0] > 16:

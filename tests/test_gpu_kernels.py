@@ -366,8 +366,11 @@ def test_t5_generate_pair_matches_single(device, t5_sd, monkeypatch, graphs):
         outs = m.generate_batches_padded([named[k] for k in keys], 20, slot=3)
         for k, o in zip(keys, outs):
             assert torch.equal(o.cpu(), single[k]), (keys, k)
+    outs = m.generate_batches_padded([named[k] for k in "ABCDDCBA"], 20, slot=3)  # 114 rows
+    for k, o in zip("ABCDDCBA", outs):
+        assert torch.equal(o.cpu(), single[k]), ("ABCDDCBA", k)
     with pytest.raises(ValueError):
-        m.generate_batches_padded([A, B, C, D, A], 20)
+        m.generate_batches_padded([A, B, C, D, A, B, C, D, A], 20)
 
 
 def test_t5_embed_and_loss(device, t5_sd):
