@@ -215,7 +215,7 @@ def cpu_baseline(cfg, weights, batches, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=80)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -365,7 +365,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "pipelining": f"serving loop (predict_many): next batch's towers + scan enqueued "
-                          f"ahead, {os.environ.get('MPR_DECODE_GROUP', '4')} batches per decode "
+                          f"ahead, {os.environ.get('MPR_DECODE_GROUP', '8')} batches per decode "
                           f"loop, {args.inflight} generate calls in flight; ramp-up and drain "
                           f"inside the timed steps",
             "sync_ms_per_step": round(sync_ms, 3),

@@ -329,7 +329,7 @@ class T5VisionModel(nn.Module):
                      lookahead=None, tower_slots=None, decode_group=None, tower_batches=None):
         """predict() over an iterable of batches as a serving pipeline.  A greedy decode is a
         chain of small latency-bound launches that leaves most of the chip idle, so
-        (1) ``decode_group`` (1-8, default MPR_DECODE_GROUP or 4; ``pair_decodes`` = False / True
+        (1) ``decode_group`` (1-8, default MPR_DECODE_GROUP or 8; ``pair_decodes`` = False / True
         is 1 / 2) consecutive batches share one decode loop: each is encoded as predict() would,
         then their rows step together, reading every decode weight once per step for all
         (mpr_t5_generate_batches);
@@ -354,7 +354,7 @@ class T5VisionModel(nn.Module):
             elif os.environ.get("MPR_PAIR_DECODE") == "0":
                 decode_group = 1
             else:
-                decode_group = int(os.environ.get("MPR_DECODE_GROUP", "4"))
+                decode_group = int(os.environ.get("MPR_DECODE_GROUP", "8"))
         decode_group = max(1, min(int(decode_group), 8))
         if lookahead is None:
             lookahead = os.environ.get("MPR_LOOKAHEAD", "1") != "0"
