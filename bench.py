@@ -224,8 +224,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 sharded-scan line")
     ap.add_argument("--index-sharding", choices=["auto", "shard", "replicate"], default="auto",
                     help="N>1: row-shard the serving index over the ranks (an RCCL exchange per "
-                         "batch) or keep a replica per rank; auto shards past 1 GiB (C2's "
-                         "26.6 MB index is replicated; C5's sharded scan is always sharded)")
+                         "batch) or keep a replica per rank; auto shards past 64 MiB (SURVEY "
+                         "§8(e): C2/C3 replicas, C4's 268 MB sharded; C5's scan always sharded)")
     ap.add_argument("--no-index-build", action="store_true",
                     help="skip the index-build line (create_retrieval_dataset throughput)")
     ap.add_argument("--inflight", type=int, default=2,
@@ -255,7 +255,7 @@ def main():
 
     index_bytes = cfg["N"] * cfg["D"] * 4
     shard = world > 1 and (args.index_sharding == "shard" or
-                           (args.index_sharding == "auto" and index_bytes > (1 << 30)))
+                           (args.index_sharding == "auto" and index_bytes > (64 << 20)))
     model, retr, weights = build(cfg, device, group if shard else None)
     # SURVEY §8(f) rank 1, measured first: a separate retrieval object on a fresh process state
     ib = None

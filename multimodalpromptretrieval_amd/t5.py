@@ -148,9 +148,18 @@ class DeviceT5:
                         eos_token_id=1, pad_token_id=0, slot: int = 0) -> torch.Tensor:
         """All max_new_tokens greedy steps on device: int32 [B, 1+max_new] (no host sync).
         ``slot`` picks one of the model's independent workspaces (two batches of a serving
-        loop decode concurrently on different slots and streams)."""
+        loop decode concurrently on different slots and streams).  A batch of more than 16 rows
+        runs as 16-row chunks sharing decode loops (up to 8 chunks per loop)."""
         embeds, mask = self._inputs(embeds, mask)
         B, L, _ = embeds.shape
+        if B > 16:
+            chunks = [(embeds[i:i + 16], mask[i:i + 16]) for i in range(0, B, 16)]
+            outs = []
+            for g in range(0, len(chunks), 8):
+                outs += self.generate_batches_padded(chunks[g:g + 8], max_new_tokens,
+                                                     decoder_start_token_id, eos_token_id,
+                                                     pad_token_id, slot)
+            return torch.cat(outs)
         out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
         _lib.call("mpr_t5_generate_slot", self._h, int(slot), _lib.ptr(embeds), _lib.ptr(mask),
                   B, L, int(max_new_tokens), int(decoder_start_token_id), int(eos_token_id),

@@ -371,6 +371,12 @@ def test_t5_generate_pair_matches_single(device, t5_sd, monkeypatch, graphs):
         assert torch.equal(o.cpu(), single[k]), ("ABCDDCBA", k)
     with pytest.raises(ValueError):
         m.generate_batches_padded([A, B, C, D, A, B, C, D, A], 20)
+    # a batch of more than 16 rows runs as 16-row chunks (here 16 + 8): each row as alone
+    big = (torch.cat([C[0], A[0][:8]]), torch.cat([C[1], A[1][:8]])) if C[0].shape[1] == \
+        A[0].shape[1] else (torch.cat([C[0], C[0][:8]]), torch.cat([C[1], C[1][:8]]))
+    want_big = torch.cat([m.generate_padded(big[0][:16], big[1][:16], 20).cpu(),
+                          m.generate_padded(big[0][16:], big[1][16:], 20).cpu()])
+    assert torch.equal(m.generate_padded(*big, 20).cpu(), want_big)
 
 
 def test_t5_embed_and_loss(device, t5_sd):
