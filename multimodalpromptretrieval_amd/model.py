@@ -17,8 +17,6 @@ untrained 512->1024 projection raise NotImplementedError; ``predict(output_atten
 """
 from __future__ import annotations
 
-import os
-
 import torch
 from torch import nn
 
@@ -336,129 +334,18 @@ class T5VisionModel(nn.Module):
         (2) up to ``decodes_in_flight`` of those generate calls run at once, each on its own
         stream and T5 workspace slot, while the next batches' image towers, question tower and
         index scan run beside them and the host builds its prompts;
-        (3) with ``lookahead`` (default on; MPR_LOOKAHEAD=0 turns it off), batch i+1's
-        towers, scan and top-k copy are enqueued before the host blocks on batch i's retrieval
-        result, so the towers never wait on the host; ``tower_batches`` (1-2, default
-        MPR_TOWER_BATCHES or 2) batches share one tower pass (the ViTs over their images
-        concatenated: fewer, fuller launches).  ``tower_slots`` > 1 (MPR_TOWER_SLOTS)
-        runs consecutive batches' towers on that many workspace slots and streams at once:
-        alone two passes overlap to 0.86x their back-to-back time, but beside the decodes of
-        the loop it measured slower (2177-1983 vs 2300-2241 QA pairs/s), so the default is 1.
+        (3) with ``lookahead`` (default on; MPR_LOOKAHEAD=0 turns it off) the next tower pass,
+        its scans and top-k copies are enqueued before the host blocks on a retrieval result, so
+        the towers never wait on the host; ``tower_batches`` (1-2, default MPR_TOWER_BATCHES or
+        2) batches share one tower pass (the ViTs over their images concatenated: fewer, fuller
+        launches); ``tower_slots`` > 1 (MPR_TOWER_SLOTS, default 1) overlaps consecutive passes
+        on workspace slots of their own (measured slower beside the decodes).
         Yields each batch's answers in order; every batch gets exactly the result predict()
-        gives it."""
-        from collections import deque
-        depth = max(1, min(int(decodes_in_flight), 4))
-        if decode_group is None:
-            if pair_decodes is not None:
-                decode_group = 2 if pair_decodes else 1
-            elif os.environ.get("MPR_PAIR_DECODE") == "0":
-                decode_group = 1
-            else:
-                decode_group = int(os.environ.get("MPR_DECODE_GROUP", "8"))
-        decode_group = max(1, min(int(decode_group), 8))
-        if lookahead is None:
-            lookahead = os.environ.get("MPR_LOOKAHEAD", "1") != "0"
-        if tower_batches is None:
-            tower_batches = int(os.environ.get("MPR_TOWER_BATCHES", "2"))
-        tower_batches = max(1, min(int(tower_batches), 2))
-        if tower_slots is None:
-            tower_slots = int(os.environ.get("MPR_TOWER_SLOTS", "1"))
-        tower_slots = max(1, min(int(tower_slots), 4))
-        if not hasattr(self, "_s_prep"):
-            self._s_prep = torch.cuda.Stream(self.device)
-        if not hasattr(self, "_s_gen"):
-            self._s_gen = []
-        while len(self._s_gen) < depth:
-            self._s_gen.append(_lib.role_stream(self.device, f"gen:{len(self._s_gen)}"))
-        pending = deque()  # one entry per generate call: [(host tokens, done event), ...]
-        held = []          # prepared batches waiting for the rest of their decode group
-        calls = 0
-
-        def launch(inputs):
-            nonlocal calls
-            slot = calls % depth
-            calls += 1
-            sg = self._s_gen[slot]
-            sg.wait_stream(self._s_prep)
-            with torch.cuda.stream(sg):
-                for combined, mask in inputs:
-                    combined.record_stream(sg)
-                    mask.record_stream(sg)
-                t5 = self._device_t5()
-                if len(inputs) > 1:
-                    toks = t5.generate_batches_padded(inputs, self.max_new_tokens, slot=slot)
-                else:
-                    toks = (t5.generate_padded(*inputs[0], self.max_new_tokens, slot=slot),)
-                hosts = []
-                for t in toks:
-                    host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-                    host.copy_(t, non_blocking=True)
-                    hosts.append(host)
-                done = torch.cuda.Event()
-                done.record(sg)
-            pending.append([(h, done) for h in hosts])
-
-        n_pre = 0
-        it = iter(batches)
-        ready = deque()  # (batch, prefetched handles) in order
-        exhausted = False
-
-        def refill():
-            # keep the next tower pass enqueued before the host blocks on a retrieval result
-            nonlocal n_pre, exhausted
-            while not exhausted and len(ready) < (tower_batches if lookahead else 1):
-                chunk = []
-                while len(chunk) < (tower_batches if lookahead else 1):
-                    b = next(it, None)
-                    if b is None:
-                        exhausted = True
-                        break
-                    chunk.append(b)
-                if not chunk:
-                    break
-                if lookahead:
-                    self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
-                    with torch.cuda.stream(self._s_prep):
-                        pres = self._prefetch(chunk, n_pre % tower_slots)
-                    n_pre += 1
-                else:
-                    pres = [None] * len(chunk)
-                ready.extend(zip(chunk, pres))
-
-        while True:
-            if not ready:
-                refill()
-            if not ready:
-                break
-            batch, pre = ready.popleft()
-            refill()
-            self._s_prep.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self._s_prep):
-                combined, mask, _ = self.prepare_input(batch, _pre=pre)
-            cur = (combined, mask)
-            if decode_group > 1 and combined.shape[0] <= 16:
-                held.append(cur)
-                if len(held) < decode_group:
-                    continue
-                launch(held)
-                held = []
-            else:
-                if held:
-                    launch(held)
-                    held = []
-                launch([cur])
-            # Answers are handed out as their calls complete; the host blocks on the oldest only
-            # when more than depth + 2 calls are outstanding (a slot's next call is ordered
-            # behind its previous one by the slot's stream, so reuse needs no host wait, and a
-            # blocked host would leave the tower stream without its next pass).
-            while pending and (len(pending) > depth + 2 or pending[0][-1][1].query()):
-                for item in pending.popleft():
-                    yield self._finish(*item)
-        if held:
-            launch(held)
-        while pending:
-            for item in pending.popleft():
-                yield self._finish(*item)
+        gives it (serving.ServingLoop)."""
+        from .serving import ServingLoop, ServingOptions
+        opts = ServingOptions.resolve(decodes_in_flight, pair_decodes, lookahead, tower_slots,
+                                      decode_group, tower_batches)
+        return ServingLoop(self, opts).run(batches)
 
     def _finish(self, host_tokens, done):
         done.synchronize()  # this batch's tokens only; the next batch keeps running

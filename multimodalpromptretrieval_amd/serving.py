@@ -1,0 +1,175 @@
+"""The serving loop behind ``T5VisionModel.predict_many`` (a pipeline over many batches).
+
+Stages per batch, as ``predict()`` runs them (architectures/T5VisionModel.py:141-216), but
+overlapped across batches on their own streams:
+
+* towers: ``VQARetrieval.prefetch_many`` enqueues one lockstep CLIP pass for 1-2 batches, each
+  batch's index scan and the copy of its top-k to pinned host memory, one pass ahead of the
+  batch the host is preparing (lookahead);
+* prompts: ``T5VisionModel.prepare_input(batch, _pre=...)`` waits for that batch's retrieval
+  copy only, builds and tokenises the prompts, gathers the T5 embeddings;
+* generate: ``decode_group`` consecutive batches share one ``mpr_t5_generate_batches`` call;
+  up to ``depth`` calls are in flight, each on a stream and T5 workspace slot of its own;
+* answers are handed out in order as their calls complete (``_finish``).
+
+Every batch gets exactly the answers ``predict()`` gives it (the grouped launches keep each
+batch's arithmetic: tests/test_gpu_golden.py).
+"""
+from __future__ import annotations
+
+import os
+from collections import deque
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class ServingOptions:
+    depth: int          # generate calls in flight
+    decode_group: int   # batches per generate call
+    lookahead: bool     # enqueue the next tower pass before blocking on a retrieval result
+    tower_batches: int  # batches per tower pass
+    tower_slots: int    # tower workspace slots used round robin
+
+    @staticmethod
+    def resolve(decodes_in_flight=2, pair_decodes=None, lookahead=None, tower_slots=None,
+                decode_group=None, tower_batches=None) -> "ServingOptions":
+        """Explicit arguments first, then the MPR_* environment, then the measured defaults."""
+        env = os.environ.get
+        if decode_group is None:
+            if pair_decodes is not None:
+                decode_group = 2 if pair_decodes else 1
+            elif env("MPR_PAIR_DECODE") == "0":
+                decode_group = 1
+            else:
+                decode_group = int(env("MPR_DECODE_GROUP", "8"))
+        if lookahead is None:
+            lookahead = env("MPR_LOOKAHEAD", "1") != "0"
+        if tower_batches is None:
+            tower_batches = int(env("MPR_TOWER_BATCHES", "2"))
+        if tower_slots is None:
+            tower_slots = int(env("MPR_TOWER_SLOTS", "1"))
+        return ServingOptions(depth=max(1, min(int(decodes_in_flight), 4)),
+                              decode_group=max(1, min(int(decode_group), 8)),
+                              lookahead=bool(lookahead),
+                              tower_batches=max(1, min(int(tower_batches), 2)),
+                              tower_slots=max(1, min(int(tower_slots), 4)))
+
+
+class ServingLoop:
+    """One pass of the pipeline over an iterable of batches (see the module docstring)."""
+
+    def __init__(self, model, opts: ServingOptions):
+        self.m = model
+        self.o = opts
+        if not hasattr(model, "_s_prep"):
+            model._s_prep = torch.cuda.Stream(model.device)
+        if not hasattr(model, "_s_gen"):
+            model._s_gen = []
+        while len(model._s_gen) < opts.depth:
+            model._s_gen.append(_lib.role_stream(model.device, f"gen:{len(model._s_gen)}"))
+        self.pending = deque()  # one entry per generate call: [(host tokens, done event), ...]
+        self.held = []          # prepared batches waiting for the rest of their decode group
+        self.ready = deque()    # (batch, prefetched handles) in order
+        self.calls = 0
+        self.passes = 0
+        self.it = None
+        self.exhausted = False
+
+    # ---- towers (one pass ahead) -----------------------------------------------------------
+    def _refill(self):
+        """Keep the next tower pass enqueued before the host blocks on a retrieval result."""
+        per_pass = self.o.tower_batches if self.o.lookahead else 1
+        while not self.exhausted and len(self.ready) < per_pass:
+            chunk = []
+            while len(chunk) < per_pass:
+                b = next(self.it, None)
+                if b is None:
+                    self.exhausted = True
+                    break
+                chunk.append(b)
+            if not chunk:
+                break
+            if self.o.lookahead:
+                m = self.m
+                m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
+                with torch.cuda.stream(m._s_prep):
+                    pres = m._prefetch(chunk, self.passes % self.o.tower_slots)
+                self.passes += 1
+            else:
+                pres = [None] * len(chunk)
+            self.ready.extend(zip(chunk, pres))
+
+    # ---- generate ----------------------------------------------------------------------------
+    def _launch(self, inputs):
+        m = self.m
+        slot = self.calls % self.o.depth
+        self.calls += 1
+        sg = m._s_gen[slot]
+        sg.wait_stream(m._s_prep)
+        with torch.cuda.stream(sg):
+            for combined, mask in inputs:
+                combined.record_stream(sg)
+                mask.record_stream(sg)
+            t5 = m._device_t5()
+            if len(inputs) > 1:
+                toks = t5.generate_batches_padded(inputs, m.max_new_tokens, slot=slot)
+            else:
+                toks = (t5.generate_padded(*inputs[0], m.max_new_tokens, slot=slot),)
+            hosts = []
+            for t in toks:
+                host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                host.copy_(t, non_blocking=True)
+                hosts.append(host)
+            done = torch.cuda.Event()
+            done.record(sg)
+        self.pending.append([(h, done) for h in hosts])
+
+    def _add(self, prepared) -> bool:
+        """Queue a prepared batch: grouped with its neighbours (<= 16 rows) or alone.  Returns
+        whether a generate call was launched."""
+        if self.o.decode_group > 1 and prepared[0].shape[0] <= 16:
+            self.held.append(prepared)
+            if len(self.held) < self.o.decode_group:
+                return False
+            self._launch(self.held)
+            self.held = []
+            return True
+        if self.held:
+            self._launch(self.held)
+            self.held = []
+        self._launch([prepared])
+        return True
+
+    def run(self, batches):
+        m = self.m
+        self.it = iter(batches)
+        while True:
+            if not self.ready:
+                self._refill()
+            if not self.ready:
+                break
+            batch, pre = self.ready.popleft()
+            self._refill()
+            m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
+            with torch.cuda.stream(m._s_prep):
+                combined, mask, _ = m.prepare_input(batch, _pre=pre)
+            if not self._add((combined, mask)):
+                continue
+            # Answers are handed out as their calls complete; the host blocks on the oldest
+            # only when more than depth + 2 calls are outstanding (a slot's next call is ordered
+            # behind its previous one by the slot's stream, so reuse needs no host wait, and a
+            # blocked host would leave the tower stream without its next pass).
+            while self.pending and (len(self.pending) > self.o.depth + 2
+                                    or self.pending[0][-1][1].query()):
+                for item in self.pending.popleft():
+                    yield m._finish(*item)
+        if self.held:
+            self._launch(self.held)
+            self.held = []
+        while self.pending:
+            for item in self.pending.popleft():
+                yield m._finish(*item)
