@@ -229,7 +229,8 @@ def main():
     ap.add_argument("--no-index-build", action="store_true",
                     help="skip the index-build line (create_retrieval_dataset throughput)")
     ap.add_argument("--inflight", type=int, default=2,
-                    help="batches decoding concurrently in the serving loop (predict_many)")
+                    help="generate calls in flight in the serving loop (predict_many; each decodes "
+                         "a group of batches)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 

@@ -673,6 +673,12 @@ int probe_read(double* ms, int64_t* launches, double* flops, double* bytes) {
 
 namespace {
 // One launch of problems that share a tile configuration (probed / recorded as one launch).
+// MPR_KSPLIT32_ONLY=1: always the 32x32 K-split blocks (A/B switch for measurements and tests)
+const bool g_ksplit32_only = [] {
+  const char* e = getenv("MPR_KSPLIT32_ONLY");
+  return e && atoi(e) != 0;
+}();
+
 int gemm_launch(const GemmGroup& g, bool big, hipStream_t s) {
   double flops = 0, bytes = 0;
   for (int i = 0; i < g.n; ++i) {
@@ -684,8 +690,16 @@ int gemm_launch(const GemmGroup& g, bool big, hipStream_t s) {
     if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone)
       g_recorded.push_back(g);
   }
+  // K-split tiles: 32x32 blocks, or 64x32 blocks (two 32x32 tiles sharing each W slice, 8 waves)
+  // once the launch has >= 2048 32x32 blocks (8 per CU: the two-batch tower passes' ViT out-proj
+  // and fc2, 54 -> 50 and 168 -> 158 us; below that the 32x32 blocks are faster).  Every 32x32
+  // sub-tile is summed by the same 4 K-slice waves in the same order in both, so the choice may
+  // depend on the launch: results are bit-identical (tools/gbench.hip checks).
+  int64_t blocks32 = 0;
+  for (int i = 0; i < g.n; ++i) blocks32 += cdiv(g.g[i].M, 32) * cdiv(g.g[i].N, 32);
   return probed(PROBE_GEMM, flops, bytes, s, [&]() {
     if (big) return launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>(g, s);
+    if (blocks32 >= 2048 && !g_ksplit32_only) return launch_gemm_group<64, 32, 1, 1, 64, 2, 4>(g, s);
     return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
   });
 }

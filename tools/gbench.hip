@@ -2,6 +2,9 @@
 // (development aid; includes the library sources so the kernel templates are visible).
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gbench.hip -o tools/gbench
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
 #include <functional>
 
 #include "../multimodalpromptretrieval_amd/csrc/api.hip"
@@ -39,7 +42,11 @@ static double time_graph(hipStream_t s, const std::function<void()>& body, int n
   return ms * 1e3 / n;
 }
 
-int main() {
+// usage: gbench [shape variant groups]  (indices into the tables below; default: all)
+int main(int argc, char** argv) {
+  const int only_shape = argc > 1 ? atoi(argv[1]) : -1;
+  const int only_var = argc > 2 ? atoi(argv[2]) : -1;
+  const int only_grp = argc > 3 ? atoi(argv[3]) : -1;
   hipStream_t s;
   (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   float *A, *W, *C, *R;
@@ -67,6 +74,9 @@ int main() {
       {"vit fc2  1600x768x3072 +R", 1600, 768, 3072, true},
       {"vit qkv   800x2304x768", 800, 2304, 768, false},
       {"vit fc1   800x3072x768", 800, 3072, 768, false},
+      {"vit out   800x768x768 +R", 800, 768, 768, true},
+      {"vit fc2   800x768x3072 +R", 800, 768, 3072, true},
+      {"txt fc2   384x512x2048 +R", 384, 512, 2048, true},
   };
   using L = std::function<int(const GemmGroup&, hipStream_t)>;
   struct Var { const char* name; L fn; };
@@ -78,12 +88,23 @@ int main() {
       {"128x128 2x2/w k32 D2 XR", launch_gemm_group<128, 128, 2, 2, 32, 2, 1, true>},
       {"64x64 1x2/w k32 D2 W2 XR", launch_gemm_group<64, 64, 1, 2, 32, 2, 2, true>},
       {"32x64 k64 D2 W2", launch_gemm_group<32, 64, 1, 1, 64, 2, 2>},
+      // bit-identical to "32x32 k64 D2 W4" (same per-wave K slices and reduction order)
+      {"64x64 k64 D2 W4", launch_gemm_group<64, 64, 1, 1, 64, 2, 4>},
+      {"64x64 k64 D2 W4 XR", launch_gemm_group<64, 64, 1, 1, 64, 2, 4, true>},
+      {"64x32 k64 D2 W4", launch_gemm_group<64, 32, 1, 1, 64, 2, 4>},
+      {"32x64 k64 D2 W4", launch_gemm_group<32, 64, 1, 1, 64, 2, 4>},
+      {"32x32 k64 D2 W4 XR", launch_gemm_group<32, 32, 1, 1, 64, 2, 4, true>},
   };
+  int si = -1;
   for (const Shape& sh : shapes) {
+    if (++si, only_shape >= 0 && si != only_shape) continue;
     for (int grp = 1; grp <= 2; ++grp) {
+      if (only_grp > 0 && grp != only_grp) continue;
       const double gf = grp * 2.0 * sh.M * sh.N * sh.K * 1e-9;
       printf("%s x%d (%.2f GFLOP)\n", sh.name, grp, gf);
+      int vi = -1;
       for (const Var& v : vars) {
+        if (++vi, only_var >= 0 && vi != only_var) continue;
         GemmGroup G;
         G.n = grp;
         for (int i = 0; i < grp; ++i) {
@@ -96,6 +117,33 @@ int main() {
         const double us = time_graph(s, [&]() { v.fn(G, s); }, 100);
         printf("   %-18s %8.2f us  %6.1f TF/s\n", v.name, us, gf / us * 1e3);
       }
+    }
+  }
+  // bit-identity of the K-split-by-4 tiles (32x32 W4 vs the larger W4 blocks) on two shapes
+  float* C2;
+  (void)hipMalloc(&C2, bytes);
+  const int same_a = 1, same_b[] = {7, 8, 9, 10, 11};
+  for (int shi : {1, 3, 6, 7, 8}) {
+    const Shape& sh = shapes[shi];
+    GemmGroup G;
+    G.n = 1;
+    GemmArgs& g = G.g[0];
+    g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.ldc = sh.N;
+    g.M = sh.M; g.N = sh.N; g.K = sh.K;
+    if (sh.res) { g.R = R; g.ldr = sh.N; }
+    g.C = C;
+    vars[same_a].fn(G, s);
+    (void)hipStreamSynchronize(s);  // s is non-blocking: hipMemcpy would not wait for it
+    std::vector<float> h1((size_t)sh.M * sh.N), h2(h1.size());
+    (void)hipMemcpy(h1.data(), C, h1.size() * 4, hipMemcpyDeviceToHost);
+    for (int vb : same_b) {
+      g.C = C2;
+      (void)hipMemsetAsync(C2, 0, h1.size() * 4, s);  // ordered before the kernel on s
+      vars[vb].fn(G, s);
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpy(h2.data(), C2, h2.size() * 4, hipMemcpyDeviceToHost);
+      printf("identity %s: %s vs %s: %s\n", sh.name, vars[same_a].name, vars[vb].name,
+             memcmp(h1.data(), h2.data(), h1.size() * 4) == 0 ? "bit-identical" : "DIFFERENT");
     }
   }
   return 0;
