@@ -60,8 +60,12 @@ def _pmc_traffic():
     (tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 half-count of wide streaming reads) +
     WRITE_SIZE, separate --pmc passes, windowed to the replay).  (bytes, source) or (None, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gemm.json")),
-                   key=os.path.getmtime)
+    import re
+
+    def _version(path):  # r<round>_v<n>_pmc_gemm.json, newest last (mtimes do not survive a checkout)
+        m = re.search(r"r(\d+)_v(\d+)_pmc_gemm\.json$", path)
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gemm.json")), key=_version)
     if not files:
         return None, None
     with open(files[-1]) as f:
