@@ -16,7 +16,8 @@ from multimodalpromptretrieval_amd.index import DeviceIndex  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(1)
-    for n, d, b, k in [(6500, 1024, 16, 1), (65536, 1024, 16, 5), (1 << 20, 512, 16, 5),
+    for n, d, b, k in [(6500, 1024, 16, 1), (10000, 1024, 16, 3), (8192, 1024, 16, 5),
+                       (32768, 1024, 16, 5), (65536, 1024, 16, 5), (1 << 20, 512, 16, 5),
                        (1 << 20, 512, 256, 5), (1 << 17, 512, 256, 5)]:
         X = torch.randn(n, d, device=dev, generator=g) * 0.3
         q = torch.randn(b, d, device=dev, generator=g) * 0.3
