@@ -190,8 +190,30 @@ def index_build(cfg, weights, device, n_batches: int = 48):
             "rows": rows, "ms": round(el * 1e3, 2), "rows_per_s": round(rows / el, 1)}
 
 
-def cpu_baseline(cfg, weights, batches, seconds: float):
-    """The CPU oracle pipeline (restated reference path, torch-CPU fp32) on a bounded sample."""
+def host_cpu():
+    """(CPU model, physical cores of the host, CPUs this process may run on)."""
+    model, cores = None, set()
+    try:
+        phys = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    cores.add((phys, v))
+    except OSError:
+        pass
+    return model, len(cores) or None, len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(cfg, weights, batches, seconds: float, gpu_answers=None):
+    """The CPU oracle pipeline (restated reference path, torch-CPU fp32) on a bounded sample of
+    the bench's own batches.  With ``gpu_answers`` (predict() on the same batches, same weights)
+    the CPU leg's prompts and answers double as a full-size C2 parity check (``parity``)."""
     from oracle import pipeline
     retr_sd, tok_sd, t5_sd, X, info = weights
     answers = syn.answers(cfg["N"], 50)
@@ -200,20 +222,41 @@ def cpu_baseline(cfg, weights, batches, seconds: float):
     heads = 8 if cfg["t5"] == "t5-small" else 12
     cpu_batches = [{**b, "image": b["image"].cpu()} for b in batches]
     n, t0 = 0, time.perf_counter()
+    cpu_out = {}
     with torch.no_grad():
         while True:
-            b = cpu_batches[n % len(cpu_batches)]
-            pipeline.predict(b, retr_sd, tok_sd, t5_sd, heads, X, answers, info, cfg["k"], False,
-                             syn.hash_clip_tokenize, tok, 20, forced_steps=True)
+            i = n % len(cpu_batches)
+            b = cpu_batches[i]
+            preds, prompts, _ = pipeline.predict(
+                b, retr_sd, tok_sd, t5_sd, heads, X, answers, info, cfg["k"], False,
+                syn.hash_clip_tokenize, tok, 20, forced_steps=True)
+            cpu_out.setdefault(i, (preds, prompts))
             n += 1
             el = time.perf_counter() - t0
             if el >= seconds or n >= 32:
                 break
     pairs = n * cfg["B"]
-    return {"value": pairs / el, "unit": "QA pairs/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{n} batches x {cfg['B']} QA pairs of the same workload ({el:.1f} s), "
-                      f"oracle/pipeline.py (torch-CPU fp32, KV-cached greedy, 20 forced steps)"}
+    model, phys, avail = host_cpu()
+    out = {"value": pairs / el, "unit": "QA pairs/s", "cores": torch.get_num_threads(),
+           "kind": "port",
+           "sample": f"{n} batches x {cfg['B']} QA pairs of the same workload ({el:.1f} s), "
+                     f"oracle/pipeline.py (torch-CPU fp32, KV-cached greedy, 20 forced steps)",
+           "cpu_model": model, "host_physical_cores": phys, "host_cpus_available": avail}
+    if gpu_answers is not None:
+        # forced steps keep finished rows on pad, as the device loop does: the decoded answers
+        # compare as strings
+        n_pairs = n_prompt = n_ans = 0
+        for i, (preds, prompts) in cpu_out.items():
+            g_preds, g_prompts = gpu_answers[i]
+            n_pairs += len(preds)
+            n_prompt += sum(a == b for a, b in zip(prompts, g_prompts))
+            n_ans += sum(a == b for a, b in zip(preds, g_preds))
+        out["parity"] = {"batches": len(cpu_out), "qa_pairs": n_pairs,
+                         "prompts_equal": n_prompt, "answers_equal": n_ans,
+                         "check": "CPU oracle vs GPU predict() on the same full-size C2 "
+                                  "batches and weights (prompts = retrieved ids, answers = "
+                                  "greedy tokens)"}
+    return out
 
 
 def main():
@@ -359,7 +402,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, weights, batches, args.cpu_seconds)
+        with torch.no_grad():
+            gpu_answers = [(model.predict(b), retr.retrieve_closest_qa_pairs(b)) for b in batches]
+        cpu = cpu_baseline(cfg, weights, batches, args.cpu_seconds, gpu_answers)
 
     if rank == 0:
         pairs = world * cfg["B"] * args.steps

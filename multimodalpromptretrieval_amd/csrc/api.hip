@@ -142,10 +142,13 @@ int mpr_index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_
     if (b == 0) return MPR_OK;
     MPR_REQUIRE(k >= 1 && k <= 64 && k <= ix->n, "search: k=%d (1..64, <= %lld rows)", k,
                 (long long)ix->n);
-    const size_t ws = scan_topk_workspace(ix->n, b, k);
-    MPR_TRY(ix->ws.ensure(ws));
+    auto& slot = ix->ws[stream];
+    if (!slot) slot = std::make_unique<DevBuf>();
+    // a growth frees the old buffer: hipFree waits for the device, so work of earlier searches
+    // on this stream that still reads it completes first
+    MPR_TRY(slot->ensure(scan_topk_workspace(ix->n, b, k)));
     return scan_topk(ix->rows.as<float>(), ix->norms.as<float>(), ix->n, ix->d, ix->row_offset,
-                     ix->metric, q, b, k, ix->ws.as<float>(), ix->ws.bytes, dist, ids, S(stream));
+                     ix->metric, q, b, k, slot->as<float>(), slot->bytes, dist, ids, S(stream));
   });
 }
 
@@ -495,9 +498,13 @@ int mpr_t5_logits(mpr_model* m, const float* embeds, const float* mask, int32_t 
 int mpr_cross_entropy(const float* logits, const int32_t* labels, int64_t n, int32_t vocab,
                       float* out, void* stream) {
   return guarded([&]() -> int {
-    static DevBuf ws;  // 2n floats of per-row partials
-    MPR_TRY(ws.ensure((size_t)n * 2 * sizeof(float)));
-    return cross_entropy(logits, labels, n, vocab, ws.as<float>(), out, S(stream));
+    // 2n floats of per-row partials, one buffer per stream (calls on different streams may be
+    // in flight together)
+    static std::map<void*, std::unique_ptr<DevBuf>> by_stream;
+    auto& ws = by_stream[stream];
+    if (!ws) ws = std::make_unique<DevBuf>();
+    MPR_TRY(ws->ensure((size_t)n * 2 * sizeof(float)));
+    return cross_entropy(logits, labels, n, vocab, ws->as<float>(), out, S(stream));
   });
 }
 

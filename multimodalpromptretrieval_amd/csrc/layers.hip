@@ -793,9 +793,10 @@ bool mfma_attention_disabled() {
 int attention(const AttnArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attention: bad shape");
   if (a.B == 0 || a.Lq == 0) return MPR_OK;
-  if (a.rel_tab)
-    MPR_REQUIRE(a.lut_radius >= a.Lk + a.Lq + a.q_pos0, "attention: bias table radius %d too small",
-                a.lut_radius);
+  if (a.rel_tab)  // offsets key - query span [-(q_pos0 + Lq - 1), Lk - 1 - q_pos0]
+    MPR_REQUIRE(std::max(a.q_pos0 + a.Lq, a.Lk) - 1 <= a.lut_radius,
+                "attention: bias table radius %d too small (Lq %d, Lk %d)", a.lut_radius, a.Lq,
+                a.Lk);
   if (a.Lq == 1) {
     hipLaunchKernelGGL(attention_decode_kernel, dim3((unsigned)((int64_t)a.B * a.H)), dim3(256),
                        0, s, a);
@@ -829,8 +830,9 @@ int attention_group(const AttnGroup& g, hipStream_t s) {
     const AttnArgs& a = g.a[i];
     MPR_REQUIRE(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attention: bad shape");
     if (a.rel_tab)
-      MPR_REQUIRE(a.lut_radius >= a.Lk + a.Lq + a.q_pos0,
-                  "attention: bias table radius %d too small", a.lut_radius);
+      MPR_REQUIRE(std::max(a.q_pos0 + a.Lq, a.Lk) - 1 <= a.lut_radius,
+                  "attention: bias table radius %d too small (Lq %d, Lk %d)", a.lut_radius, a.Lq,
+                  a.Lk);
     int lk = a.Lk;
     if (a.causal) lk = std::min(lk, a.Lq + a.q_pos0);
     mfma = a.Lq > 1 && lk <= ATT_MFMA_MAXK;

@@ -17,7 +17,9 @@ struct mpr_model {
 struct mpr_index {
   mpr::DevBuf rows;   // [n, d] fp32
   mpr::DevBuf norms;  // [n] squared L2 norms
-  mpr::DevBuf ws;     // search workspace
+  // search workspace per stream: searches enqueued on different streams (a prefetched search on
+  // the tower stream beside an analytics search on the caller's) never share candidate buffers
+  std::map<void*, std::unique_ptr<mpr::DevBuf>> ws;
   int64_t n = 0;
   int d = 0;
   int metric = 0;

@@ -75,7 +75,7 @@ int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embe
   row0[0] = 0;
   for (int g = 0; g < n; ++g) {
     MPR_REQUIRE(Ls[g] >= 1, "t5 encode: L=%d", Ls[g]);
-    MPR_REQUIRE(2 * Ls[g] <= lut_radius, "t5 encode: L=%d exceeds the bucket lut radius %d",
+    MPR_REQUIRE(Ls[g] - 1 <= lut_radius, "t5 encode: L=%d exceeds the bucket lut radius %d + 1",
                 Ls[g], lut_radius);
     row0[g + 1] = row0[g] + (int64_t)Bs[g] * Ls[g];
   }
@@ -299,8 +299,11 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
   for (int g = 0; g < ng; ++g) {
     MPR_REQUIRE(Bs[g] >= 0 && Bs[g] <= 16, "t5 generate: batch %d > 16 unsupported by the decode path", Bs[g]);
     if (Bs[g] == 0) continue;
-    MPR_REQUIRE(2 * Ls[g] <= lut_radius && Ls[g] >= 1, "t5 generate: L=%d", Ls[g]);
-    const int Lb = std::min((int)cdiv(Ls[g], 8) * 8, lut_radius / 2);
+    // every key/query offset of the (bucketed) source must have a bias-table entry
+    const int Lb = (int)cdiv(Ls[g], 8) * 8;
+    MPR_REQUIRE(Ls[g] >= 1 && Lb - 1 <= lut_radius,
+                "t5 generate: L=%d (bucketed %d) exceeds the bucket lut radius %d + 1", Ls[g], Lb,
+                lut_radius);
     gr[n++] = Grp{embeds[g], masks[g], Bs[g], Ls[g], Lb, Btot, outs[g]};
     Btot += Bs[g];
     Lp = std::max(Lp, Lb);

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import json
 import os
+import pickle
 
 import numpy as np
 import torch
@@ -53,6 +54,22 @@ def vote_prompt(row: list, use_quantifier: bool = True) -> str:
     if use_quantifier:
         return f"I believe the answer is {BUCKETS[int(certainty * (len(BUCKETS) - 1))]} {pred}"
     return f"The most frequent answer is {pred}"
+
+
+class _DataOnlyUnpickler(pickle.Unpickler):
+    """Reads pickles of plain containers only (lists, dicts, tuples, str, numbers): no global is
+    ever resolved, so nothing in the file can run."""
+
+    def find_class(self, module, name):
+        raise pickle.UnpicklingError(f"{module}.{name}: only plain lists / dicts / strings are "
+                                     f"read from an index cache")
+
+
+def read_pickled_data(path):
+    """The reference's answers.pkl / answer_types.pkl (dataset/VQAFeatureDataset.py:130-135):
+    a list of answer strings / a dict of lists.  Refuses anything that needs a global."""
+    with open(path, "rb") as f:
+        return _DataOnlyUnpickler(f).load()
 
 
 class VQARetrieval:
@@ -257,43 +274,88 @@ class VQARetrieval:
         return d, os.path.join(d, "embedding.pt"), os.path.join(d, "answers.json"), \
             os.path.join(d, "question_info.json")
 
+    @staticmethod
+    def _ref_paths(d):
+        """The reference's cache files (dataset/VQAFeatureDataset.py:122-124)."""
+        return (os.path.join(d, "embedding.pt"), os.path.join(d, "answers.pkl"),
+                os.path.join(d, "answer_types.pkl"))
+
+    def _encode_loader(self, data_loader):
+        """[img ‖ txt] rows of every batch (dataset/VQAFeatureDataset.py:145-161)."""
+        embs, answers = [], []
+        info = {"question_type": [], "question_id": [], "question": []}
+        # query rows stay on the device until the end: the host never waits on a batch, so
+        # the tower passes of consecutive batches queue back to back on the GPU
+        for batch in data_loader:
+            embs.append(self.encode_queries(batch))
+            answers.extend(batch["answer"])
+            info["question_type"].extend(batch["question_type"])
+            info["question_id"].extend(batch["question_id"])
+            info["question"].extend(batch["question"])
+        emb = (torch.cat(embs, 0) if embs else
+               torch.empty((0, self.embed_dim), device=self.device)).cpu()
+        return emb, answers, info
+
     def create_retrieval_dataset(self, data_loader, prefix=None, is_training_phase=True,
-                                 retrieval_k=15, use_additional_data=False, cache_dir="cache"):
-        """dataset/VQAFeatureDataset.py:118-185."""
-        d, emb_p, ans_p, info_p = self._cache_paths(cache_dir, data_loader)
-        if os.path.exists(emb_p) and os.path.exists(ans_p) and os.path.exists(info_p):
-            emb = torch.load(emb_p, map_location="cpu", weights_only=True).float()
-            with open(ans_p) as f:
-                answers = json.load(f)
-            with open(info_p) as f:
-                info = json.load(f)
+                                 retrieval_k=15, use_additional_data=False, cache_dir="cache",
+                                 layout="native", cache_name=None):
+        """dataset/VQAFeatureDataset.py:118-185.
+
+        ``layout="native"`` (default): cache under a key that includes the dataset name and
+        size, tensor + JSON files (the reference's class-name key collides).
+        ``layout="reference"``: the reference's own files and key, ``<cache_dir>/<cache_name>/
+        embedding.pt | answers.pkl | answer_types.pkl`` (read when embedding.pt and answers.pkl
+        exist, as :126), so a cache the reference built is served and one built here is the
+        reference's; files are read with loaders that execute nothing (``torch.load(...,
+        weights_only=True)``, ``read_pickled_data``)."""
+        if layout == "reference":
+            d = os.path.join(cache_dir, cache_name or type(self).__name__)
+            emb_p, ans_p, info_p = self._ref_paths(d)
+            if os.path.exists(emb_p) and os.path.exists(ans_p):
+                emb = torch.load(emb_p, map_location="cpu", weights_only=True).float()
+                answers = read_pickled_data(ans_p)
+                info = read_pickled_data(info_p) if os.path.exists(info_p) else {}
+            else:
+                emb, answers, info = self._encode_loader(data_loader)
+                os.makedirs(d, exist_ok=True)
+                torch.save(emb, emb_p)
+                with open(ans_p, "wb") as f:
+                    pickle.dump(answers, f)
+                with open(info_p, "wb") as f:
+                    pickle.dump(info, f)
+        elif layout == "native":
+            d, emb_p, ans_p, info_p = self._cache_paths(cache_dir, data_loader)
+            if os.path.exists(emb_p) and os.path.exists(ans_p) and os.path.exists(info_p):
+                emb = torch.load(emb_p, map_location="cpu", weights_only=True).float()
+                with open(ans_p) as f:
+                    answers = json.load(f)
+                with open(info_p) as f:
+                    info = json.load(f)
+            else:
+                emb, answers, info = self._encode_loader(data_loader)
+                os.makedirs(d, exist_ok=True)
+                torch.save(emb, emb_p)
+                with open(ans_p, "w") as f:
+                    json.dump(answers, f)
+                with open(info_p, "w") as f:
+                    json.dump(info, f)
         else:
-            embs, answers = [], []
-            info = {"question_type": [], "question_id": [], "question": []}
-            # query rows stay on the device until the end: the host never waits on a batch, so
-            # the tower passes of consecutive batches queue back to back on the GPU
-            for batch in data_loader:
-                embs.append(self.encode_queries(batch))
-                answers.extend(batch["answer"])
-                info["question_type"].extend(batch["question_type"])
-                info["question_id"].extend(batch["question_id"])
-                info["question"].extend(batch["question"])
-            emb = (torch.cat(embs, 0) if embs else
-                   torch.empty((0, self.embed_dim), device=self.device)).cpu()
-            os.makedirs(d, exist_ok=True)
-            torch.save(emb, emb_p)
-            with open(ans_p, "w") as f:
-                json.dump(answers, f)
-            with open(info_p, "w") as f:
-                json.dump(info, f)
+            raise ValueError(f"layout {layout!r} (native or reference)")
         if use_additional_data:
+            # :169-181 (ROCO synthetic corpus); question-info dicts are merged key by key where
+            # the reference calls .extend on a dict (F9)
             extra = os.path.join("synthetic_data", "cache", "ROCOFeatureDataset")
             emb = torch.cat([emb, torch.load(os.path.join(extra, "embedding.pt"),
                                              map_location="cpu", weights_only=True).float()], 0)
-            with open(os.path.join(extra, "answers.json")) as f:
-                answers = answers + json.load(f)
-            with open(os.path.join(extra, "question_info.json")) as f:
-                more = json.load(f)
+            if layout == "reference":
+                _, e_ans, e_info = self._ref_paths(extra)
+                more_ans, more = read_pickled_data(e_ans), read_pickled_data(e_info)
+            else:
+                with open(os.path.join(extra, "answers.json")) as f:
+                    more_ans = json.load(f)
+                with open(os.path.join(extra, "question_info.json")) as f:
+                    more = json.load(f)
+            answers = list(answers) + list(more_ans)
             info = {k: list(info.get(k, [])) + list(more.get(k, [])) for k in set(info) | set(more)}
         self.set_index(emb, answers, info, retrieval_k, is_training_phase)
 

@@ -56,17 +56,31 @@ class ShardedIndex:
         # gloo (CPU tests, or a one-GPU rehearsal of N ranks) moves host tensors only
         return dist.get_backend(self.group) == "gloo" and self.device.type == "cuda"
 
+    def _max_batch(self, b: int) -> int:
+        """All-reduced max of the per-rank batch sizes (a DataLoader's last partial batch gives
+        ranks different b; every collective below is sized from the common maximum)."""
+        dev = "cpu" if dist.get_backend(self.group) == "gloo" else self.device
+        t = torch.tensor([b], device=dev, dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
     def search(self, q: torch.Tensor, k: int):
-        """q: this rank's [b, d] queries (same b on every rank).  Returns (dist, ids) [b, k]."""
+        """q: this rank's [b, d] queries (b may differ between ranks).  Returns (dist, ids)
+        [b, k].  Every rank pads its block to the group's largest b with zero rows (their
+        candidates are computed and dropped before the merge), so the collectives always see
+        equal sizes."""
         b = q.shape[0]
+        bmax = self._max_batch(b)
         kk = min(k, self.n_local)
         q = q.to(self.device, torch.float32).contiguous()
+        if b < bmax:
+            q = torch.cat([q, q.new_zeros((bmax - b, self.d))], 0)
         stage = self._host_staged()
         qx = q.cpu() if stage else q
-        q_all = torch.empty((self.world * b, self.d), device=qx.device, dtype=qx.dtype)
+        q_all = torch.empty((self.world * bmax, self.d), device=qx.device, dtype=qx.dtype)
         dist.all_gather_into_tensor(q_all, qx, group=self.group)
         q_all = q_all.to(self.device)
-        d_loc, i_loc = self._search(q_all, kk)                  # [W*b, kk]
+        d_loc, i_loc = self._search(q_all, kk)                  # [W*bmax, kk]
         if kk < k:                                              # tiny shard: pad with sentinels
             pad = k - kk
             fill = float("inf") if self.metric == L2 else float("-inf")
@@ -81,7 +95,7 @@ class ShardedIndex:
         dist.all_to_all_single(d_recv, d_loc.contiguous(), group=self.group)
         dist.all_to_all_single(i_recv, i_loc.contiguous(), group=self.group)
         d_recv, i_recv = d_recv.to(self.device), i_recv.to(self.device)
-        # [W(src shard), b, k] -> [b, W*k]
-        cd = d_recv.view(self.world, b, k).permute(1, 0, 2).reshape(b, self.world * k)
-        ci = i_recv.view(self.world, b, k).permute(1, 0, 2).reshape(b, self.world * k)
+        # [W(src shard), bmax, k] -> this rank's b real queries: [b, W*k]
+        cd = d_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
+        ci = i_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
         return self._merge(cd.contiguous(), ci.contiguous(), k)

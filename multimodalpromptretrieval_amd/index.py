@@ -20,6 +20,10 @@ class DeviceIndex:
         _lib.ensure_device(device)
         self.device = torch.device(device)
         rows = rows.detach().to(torch.float32).contiguous()
+        if rows.device.type == "cuda":
+            # mpr_index_create copies with a synchronous copy on the legacy stream, which is not
+            # ordered behind torch's (possibly non-blocking) current stream: let the rows land
+            torch.cuda.current_stream(rows.device).synchronize()
         if rows.dim() != 2 or rows.shape[0] < 1:
             raise ValueError(f"index rows must be [n, d] with n >= 1, got {tuple(rows.shape)}")
         self.n, self.d = rows.shape

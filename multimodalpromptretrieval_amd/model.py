@@ -217,6 +217,13 @@ class T5VisionModel(nn.Module):
         """architectures/T5VisionModel.py:112-139 -> [B, 50, 512] fp32 on the device."""
         return self._device_vit()(x, TOKENS)
 
+    def _retrieval_obj(self):
+        """The VQARetrieval behind ``retrieval_function``: its ``__self__``, or the one a
+        reference dataset patched by ``dropin`` carries (``main.py`` passes the dataset's bound
+        ``retrieve_closest_qa_pairs``, main.py:123)."""
+        owner = getattr(self.retrieval_function, "__self__", None)
+        return getattr(owner, "__dict__", {}).get("_mpr_retrieval", owner)
+
     @staticmethod
     def _pairable(retr, vit) -> bool:
         enc = getattr(retr, "image_encoder", None)
@@ -231,7 +238,7 @@ class T5VisionModel(nn.Module):
         (``VQARetrieval.prefetch_many``); ``prepare_input(batch, _pre=...)`` then only waits for
         them.  A list with one entry per batch (None entries when there is nothing to
         prefetch)."""
-        retr = getattr(self.retrieval_function, "__self__", None)
+        retr = self._retrieval_obj()
         fn = getattr(retr, "prefetch_many", None)
         if fn is None or getattr(retr, "index", None) is None:
             return [None] * len(batches)
@@ -258,7 +265,7 @@ class T5VisionModel(nn.Module):
         tok_stream = None
         tok_event = None
         if self.use_image_info:
-            retr = getattr(self.retrieval_function, "__self__", None)
+            retr = self._retrieval_obj()
             pair = getattr(retr, "encode_image_pair", None)
             if _pre is not None and _pre[0] is not None:
                 img_tok, tok_event = _pre  # enqueued by _prefetch with the retrieval towers

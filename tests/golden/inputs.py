@@ -99,3 +99,82 @@ def g3_inputs(d_model=512):
     img_tok = syn._normal(syn._rng(G3["img_seed"]), (B, 50, d_model), 0.5)
     mask = torch.cat([torch.ones(B, 50, dtype=torch.long), tmask], 1)
     return ids, img_tok, mask
+
+
+# ---- G5: utils.cosine_similarity (reference utils.py:57-62) ----------------------------------
+G5 = {"seed": 601, "aligned": (16, 1024), "aligned3": (4, 8, 64), "pair_B": 16, "pair_N": 600,
+      "pair_D": 1024}
+
+
+def g5_inputs():
+    """(name, x1, x2, dim) cases: aligned rows (dim 1 and a middle dim), a zero row (the eps
+    clamp), the [B,1,D] x [1,N,D] retrieval-matrix pattern, and a single-query pairwise call
+    (squeeze to [N])."""
+    s = G5["seed"]
+    B, D = G5["aligned"]
+    a1, a2 = syn.index_rows(s, B, D), syn.index_rows(s + 1, B, D)
+    a1[3] = 0.0
+    t1, t2 = syn.index_rows(s + 2, 4 * 8, 64).view(4, 8, 64), \
+        syn.index_rows(s + 3, 4 * 8, 64).view(4, 8, 64)
+    pB, pN, pD = G5["pair_B"], G5["pair_N"], G5["pair_D"]
+    q = syn.index_rows(s + 4, pB, pD)[:, None, :]
+    X = syn.index_rows(s + 5, pN, pD)[None]
+    return [("aligned", a1, a2, 1), ("aligned3_dim2", t1, t2, 2),
+            ("aligned3_dim1", t1.transpose(1, 2).contiguous(), t2.transpose(1, 2).contiguous(), 1),
+            ("pairwise", q, X, 2), ("pairwise_one", q[:1], X, 2)]
+
+
+# ---- G6: retrieval off (config C1: retrieval_function=None, architectures/T5VisionModel.py:148)
+# ---- G7: t5-base behind the reference model with use_image_info=0 (config C5, SURVEY F6) -------
+G7 = {"t5_seed": 701}
+
+
+# ---- G8: a source past 256 / 512 keys (50 image tokens + 512 text tokens, max_source_length) --
+G8 = {"t5_seed": 801, "ids_seed": 802, "img_seed": 803, "B": 2, "L_txt": [512, 301]}
+
+
+def g8_inputs(d_model=512):
+    """Two rows: 50 image tokens + 512 text tokens (the longest source the reference can build,
+    L = 562) and + 301 (padded)."""
+    B = G8["B"]
+    rng = syn._rng(G8["ids_seed"])
+    L = max(G8["L_txt"])
+    ids = torch.zeros((B, L), dtype=torch.long)
+    tmask = torch.zeros((B, L), dtype=torch.long)
+    for i, n in enumerate(G8["L_txt"]):
+        ids[i, :n - 1] = torch.from_numpy(rng.integers(2, 32099, size=n - 1))
+        ids[i, n - 1] = 1
+        tmask[i, :n] = 1
+    img_tok = syn._normal(syn._rng(G8["img_seed"]), (B, 50, d_model), 0.5)
+    mask = torch.cat([torch.ones(B, 50, dtype=torch.long), tmask], 1)
+    return ids, img_tok, mask
+
+
+# ---- G9: main.py-shaped harness (create_retrieval_dataset over a loader, then per test batch
+# ---- predict + the four analytics calls, main.py:119-123, 262-270) on the G2 models ----------
+G9 = {"retr_batches": 4, "test_batches": 3, "B": 6, "k": 3, "seed": 901}
+G9_ANSWERS = ["yes", "no", "lung", "liver", "ct", "mri", "left", "brain"]
+
+
+def _g9_batch(seed, B, qid0):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    words = ["what", "is", "the", "organ", "shown", "in", "this", "image", "does", "picture",
+             "contain", "lung", "liver", "brain", "which", "modality", "used", "where", "mass"]
+    return {"image": syn.images(seed, B, G2["clip_cfg"]["image_size"]),
+            "question": [" ".join(rng.choice(words, size=int(rng.integers(4, 10))))
+                         for _ in range(B)],
+            "task": [["organ", "modality", "position", "abnormality"][int(t)]
+                     for t in rng.integers(0, 4, size=B)],
+            "answer": [G9_ANSWERS[int(a)] for a in rng.integers(0, len(G9_ANSWERS), size=B)],
+            "question_id": [str(qid0 + i) for i in range(B)],
+            "question_type": [["open", "closed"][int(t)] for t in rng.integers(0, 2, size=B)]}
+
+
+def g9_retrieval_loader():
+    return [_g9_batch(G9["seed"] + i, G9["B"], 1000 + i * G9["B"])
+            for i in range(G9["retr_batches"])]
+
+
+def g9_test_batches():
+    return [_g9_batch(G9["seed"] + 100 + i, G9["B"], 5000 + i * G9["B"])
+            for i in range(G9["test_batches"])]

@@ -298,6 +298,199 @@ def make_g2():
     print("G2 prompts:", prompts[:2], "loss:", loss.item())
 
 
+# ------------------------------------------------------------------ reference T5VisionModel shell
+def ref_model(vm_t, t5_sd, t5cfg, retrieval_function, use_image_info=True, version="t5-small"):
+    """The reference's T5VisionModel (architectures/T5VisionModel.py) built with __new__: its own
+    prepare_input / predict / forward run; vision_model.visual, T5_model and tokenizer are
+    injected (clip.load / from_pretrained need the network)."""
+    model = T5VisionModel.__new__(T5VisionModel)
+    nn.Module.__init__(model)
+    model.device = "cpu"
+    model.vision_encoder = "ViT-B/32"
+    model.T5_version = version
+    model.max_source_length = 512
+    model.max_target_length = 128
+    model.use_image_info = use_image_info
+    model.retrieval_function = retrieval_function
+    model.use_quantifier = True
+    model.use_mapping = False
+    model.map_to_large = False
+    model.vision_model = SimpleNamespace(visual=HFVisual(vm_t))
+    model.vision_model.visual.forward = model.get_image_token_features
+    tok = syn.HashT5Tokenizer()
+    tok.add_tokens(["[itk]"])
+    model.tokenizer = tok
+    model.T5_model = hf_t5(t5_sd, t5cfg)
+    model.image_token_id = tok.convert_tokens_to_ids("[itk]")
+    return model
+
+
+def _g2_retrieval():
+    ccfg, clip_sd, tcfg, tok_sd, t5cfg, t5_sd = gi.g2_models()
+    vm_r, tm_r = hf_clip_models(clip_sd, ccfg)
+    vm_t, _ = hf_clip_models(tok_sd, tcfg)
+    X, answers, info = gi.g2_index(ccfg)
+    clip_model = SimpleNamespace(
+        encode_image=lambda x: vm_r(pixel_values=x).image_embeds,
+        encode_text=lambda t: tm_r(input_ids=t).text_embeds)
+    rset = SimpleNamespace(clip_model=clip_model, device="cpu", retrieval_embeddings=X,
+                           retrieval_answers=answers, retrieval_question_info=info,
+                           retrieval_k=gi.G2["k"], is_training_phase=False)
+
+    def retrieval_function(batch, **kw):
+        return VQADataset.retrieve_closest_qa_pairs(rset, batch, **kw)
+    return vm_t, t5_sd, t5cfg, retrieval_function
+
+
+def _run_model(model, batch):
+    """prepare_input / predict (generate's sequences captured) / forward of the reference."""
+    captured = {}
+    gen = model.T5_model.generate
+
+    def gen_capture(**kw):
+        out = gen(**kw)
+        captured["sequences"] = out
+        return out
+
+    model.T5_model.generate = gen_capture
+    combined, mask, enc = model.prepare_input(batch)
+    preds = model.predict(batch)
+    model.T5_model.generate = gen
+    loss = model.forward(batch)
+    return combined, mask, enc, captured["sequences"], preds, loss
+
+
+# ------------------------------------------------------------------ G5: utils.cosine_similarity
+def make_g5():
+    import utils as ref_utils  # the reference's utils.py (imported with the stub clip above)
+    out = {}
+    for name, x1, x2, dim in gi.g5_inputs():
+        out[name] = ref_utils.cosine_similarity(x1, x2, dim=dim).numpy()
+    np.savez_compressed(os.path.join(HERE, "g5_cosine.npz"), **out)
+    print("G5:", {k: v.shape for k, v in out.items()})
+
+
+# ------------------------------------------------------------------ G6: retrieval off (C1)
+def make_g6():
+    with torch.no_grad():
+        vm_t, t5_sd, t5cfg, _ = _g2_retrieval()
+        model = ref_model(vm_t, t5_sd, t5cfg, None)
+        batch = gi.g2_batch()
+        combined, mask, enc, seqs, preds, loss = _run_model(model, batch)
+    np.savez_compressed(os.path.join(HERE, "g6_noretrieval.npz"), combined=combined.numpy(),
+                        mask=mask.numpy(), input_ids=enc["input_ids"].numpy(),
+                        sequences=seqs.numpy(), loss=np.float32(loss.item()))
+    with open(os.path.join(HERE, "g6_noretrieval.json"), "w") as f:
+        json.dump({"predictions": preds}, f, indent=1)
+    print("G6 predictions:", preds[:2], "loss:", loss.item())
+
+
+# ------------------------------------------------------------------ G7: t5-base, use_image_info=0
+def make_g7():
+    cfg = syn.T5_BASE
+    with torch.no_grad():
+        vm_t, _, _, retrieval_function = _g2_retrieval()
+        t5_sd = syn.t5_state_dict(gi.G7["t5_seed"], cfg)
+        model = ref_model(vm_t, t5_sd, cfg, retrieval_function, use_image_info=False,
+                          version="t5-base")
+        batch = gi.g2_batch()
+        combined, mask, enc, seqs, preds, loss = _run_model(model, batch)
+        m = model.T5_model
+        emb = m.shared(enc["input_ids"])
+        encd = m.encoder(inputs_embeds=emb, attention_mask=mask).last_hidden_state
+        labels = seqs[:, 1:].clone()
+        labels[labels == 0] = -100
+        lg = m(inputs_embeds=emb, attention_mask=mask, labels=labels).logits
+    sel = np.random.Generator(np.random.PCG64(gi.G7["t5_seed"] + 1)).choice(
+        cfg.vocab_size, 64, replace=False)
+    np.savez_compressed(os.path.join(HERE, "g7_t5_base.npz"), combined=combined.numpy(),
+                        mask=mask.numpy(), input_ids=enc["input_ids"].numpy(),
+                        sequences=seqs.numpy(), loss=np.float32(loss.item()),
+                        enc_head=encd[:, :8].numpy(), labels=labels.numpy(),
+                        logits_sel=lg[:, :, sel].numpy(), vocab_sel=sel,
+                        logits_argmax=lg.argmax(-1).numpy())
+    with open(os.path.join(HERE, "g7_t5_base.json"), "w") as f:
+        json.dump({"predictions": preds}, f, indent=1)
+    print("G7 predictions:", preds[:2], "loss:", loss.item(), "L:", mask.shape)
+
+
+# ------------------------------------------------------------------ G8: long source (L = 562)
+def make_g8():
+    cfg = syn.T5Config()
+    sd = syn.t5_state_dict(gi.G8["t5_seed"], cfg)
+    m = hf_t5(sd, cfg)
+    ids, img_tok, mask = gi.g8_inputs(cfg.d_model)
+    with torch.no_grad():
+        emb = torch.cat([img_tok, m.shared(ids)], 1)
+        seqs = m.generate(inputs_embeds=emb, attention_mask=mask, do_sample=False,
+                          max_new_tokens=20)
+        labels = seqs[:, 1:].clone()
+        labels[labels == 0] = -100
+        out = m(inputs_embeds=emb, attention_mask=mask, labels=labels)
+        enc = m.encoder(inputs_embeds=emb, attention_mask=mask).last_hidden_state
+    sel = np.random.Generator(np.random.PCG64(gi.G8["t5_seed"] + 1)).choice(
+        cfg.vocab_size, 64, replace=False)
+    np.savez_compressed(os.path.join(HERE, "g8_long_source.npz"), sequences=seqs.numpy(),
+                        labels=labels.numpy(), loss=np.float32(out.loss.item()),
+                        logits_sel=out.logits[:, :, sel].numpy(), vocab_sel=sel,
+                        logits_argmax=out.logits.argmax(-1).numpy(),
+                        enc_rows=enc[:, ::37].numpy())
+    print("G8 L:", emb.shape[1], "sequences:", seqs[:, :8].tolist())
+
+
+# ------------------------------------------------------------------ G9: main.py-shaped harness
+class VQASLAKEFeatureDataset:
+    """Stands in for the reference's dataset object (its class name keys the cache directory,
+    dataset/VQAFeatureDataset.py:122); the reference's own methods run on it unbound."""
+
+
+def make_g9():
+    import shutil
+    import tempfile
+    ccfg, clip_sd, tcfg, tok_sd, t5cfg, t5_sd = gi.g2_models()
+    vm_r, tm_r = hf_clip_models(clip_sd, ccfg)
+    vm_t, _ = hf_clip_models(tok_sd, tcfg)
+    ds = VQASLAKEFeatureDataset()
+    ds.device = "cpu"
+    ds.clip_model = SimpleNamespace(
+        encode_image=lambda x: vm_r(pixel_values=x).image_embeds,
+        encode_text=lambda t: tm_r(input_ids=t).text_embeds)
+    cwd = os.getcwd()
+    tmp = tempfile.mkdtemp(prefix="g9_")
+    out = {"batches": []}
+    try:
+        os.chdir(tmp)
+        with torch.no_grad():
+            # main.py:119-123: the index over the retrieval loader, test phase
+            VQADataset.create_retrieval_dataset(ds, gi.g9_retrieval_loader(), "prefix",
+                                                is_training_phase=False,
+                                                retrieval_k=gi.G9["k"])
+
+            def retrieval_function(batch, **kw):
+                return VQADataset.retrieve_closest_qa_pairs(ds, batch, **kw)
+            model = ref_model(vm_t, t5_sd, t5cfg, retrieval_function)
+            for batch in gi.g9_test_batches():   # main.py:262-270
+                rec = {"predictions": model.predict(batch),
+                       "retrieved_answers": retrieval_function(batch, return_ans=True),
+                       "retrieved_answer_types": retrieval_function(
+                           batch, return_info=["question_type"]),
+                       "retrieved_question_info": retrieval_function(
+                           batch, return_info=["question", "question_id"])}
+                dd = retrieval_function(batch, return_dists=True)
+                rec["dists_answers"] = [a for a, _ in dd]
+                rec["dists"] = [[float(v) for v in d] for _, d in dd]
+                out["batches"].append(rec)
+        cache = os.path.join(HERE, "g9_cache")
+        shutil.rmtree(cache, ignore_errors=True)
+        shutil.copytree(os.path.join(tmp, "cache", "VQASLAKEFeatureDataset"), cache)
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp, ignore_errors=True)
+    with open(os.path.join(HERE, "g9_main_loop.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("G9:", out["batches"][0]["predictions"][:2], sorted(os.listdir(cache)))
+
+
 # ------------------------------------------------------------------ G3 / G4: full-size second source
 def make_g3():
     cfg = syn.T5Config()
@@ -340,12 +533,15 @@ def make_g4():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g4"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8", "g9"]
     for w in which:
         globals()["make_" + w]()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_goldens.py", "inputs": "tests/golden/inputs.py",
                    "reference": REF, "transformers": transformers.__version__,
                    "torch": torch.__version__, "argsort": "stable=True while the reference runs",
-                   "files": sorted(n for n in os.listdir(HERE) if n.startswith("g"))}, f,
+                   "files": sorted(n for n in os.listdir(HERE) if n.startswith("g") and
+                                   n not in ("g9_cache",)),
+                   "g9_cache": "cache files written by the reference's create_retrieval_dataset "
+                               "(dataset/VQAFeatureDataset.py:163-167)"}, f,
                   indent=1)

@@ -43,28 +43,39 @@ def cpu_merger(cd, ci, k):
     return torch.tensor(out_d), torch.tensor(out_i, dtype=torch.int64)
 
 
-def _worker(rank, world, port, n, d, b, k, result_q):
+def _spans(sizes):
+    return [(sum(sizes[:r]), sum(sizes[:r + 1])) for r in range(len(sizes))]
+
+
+def _worker(rank, world, port, n, d, sizes, k, result_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         X = syn.index_rows(7, n, d)
-        q_all = syn.index_rows(8, world * b, d)
-        q = q_all[rank * b:(rank + 1) * b]
+        q_all = syn.index_rows(8, sum(sizes), d)
+        lo, hi = _spans(sizes)[rank]
         six = ShardedIndex(X, "cpu", searcher=cpu_searcher, merger=cpu_merger)
-        dd, ids = six.search(q, k)
-        result_q.put((rank, ids.tolist(), dd.tolist()))
+        out = []
+        for _ in range(2):  # a second search on the same index: the exchange stays in step
+            dd, ids = six.search(q_all[lo:hi], k)
+            out.append(ids.tolist())
+        result_q.put((rank, out, dd.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,k", [(2, 1000, 5), (3, 1001, 3), (2, 9, 7)])
-def test_sharded_search_matches_single_index(world, n, k):
-    d, b = 64, 4
+@pytest.mark.parametrize("world,n,k,sizes", [
+    (2, 1000, 5, None), (3, 1001, 3, None), (2, 9, 7, None),
+    (2, 1000, 5, [16, 5]),      # a DataLoader's partial last batch on one rank
+    (3, 1001, 3, [4, 0, 7])])   # and a rank with no queries at all
+def test_sharded_search_matches_single_index(world, n, k, sizes):
+    d = 64
+    sizes = sizes or [4] * world
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, d, b, k, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, d, sizes, k, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -76,10 +87,11 @@ def test_sharded_search_matches_single_index(world, n, k):
         p.join(timeout=60)
         assert p.exitcode == 0
     X = syn.index_rows(7, n, d)
-    q_all = syn.index_rows(8, world * b, d)
+    q_all = syn.index_rows(8, sum(sizes), d)
     ref = oret.topk_ids(oret.cdist(q_all, X), k, False)
-    for r in range(world):
-        assert res[r][0] == ref[r * b:(r + 1) * b].tolist()
+    for r, (lo, hi) in enumerate(_spans(sizes)):
+        for ids in res[r][0]:
+            assert ids == ref[lo:hi].tolist()
 
 
 def test_shard_bounds_cover_rows():

@@ -1,0 +1,96 @@
+"""CPU checks of the main.py drop-in binding (multimodalpromptretrieval_amd/dropin.py) and of the
+reference-cache reader (no GPU work: classes are patched, not run)."""
+import io
+import os
+import pickle
+import sys
+import types
+
+import pytest
+import torch
+
+from multimodalpromptretrieval_amd import dropin
+from multimodalpromptretrieval_amd.dataset import read_pickled_data
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CACHE = os.path.join(HERE, "golden", "g9_cache")
+
+
+def test_reference_cache_files_read_safely():
+    """The reference's create_retrieval_dataset wrote these (make_goldens.py make_g9)."""
+    emb = torch.load(os.path.join(CACHE, "embedding.pt"), map_location="cpu", weights_only=True)
+    answers = read_pickled_data(os.path.join(CACHE, "answers.pkl"))
+    info = read_pickled_data(os.path.join(CACHE, "answer_types.pkl"))
+    assert emb.shape[0] == len(answers) == 24
+    assert set(info) == {"question_type", "question_id", "question"}
+    assert all(len(v) == 24 for v in info.values())
+
+
+class _Evil:
+    def __reduce__(self):
+        return (os.getcwd, ())
+
+
+def test_cache_reader_refuses_globals(tmp_path):
+    p = tmp_path / "answers.pkl"
+    p.write_bytes(pickle.dumps([_Evil()]))
+    with pytest.raises(pickle.UnpicklingError):
+        read_pickled_data(str(p))
+    p.write_bytes(pickle.dumps({"a": ["x", "y"], "b": [1, 2.5]}))
+    assert read_pickled_data(str(p)) == {"a": ["x", "y"], "b": [1, 2.5]}
+
+
+def test_patch_dataset_class_routes_both_methods():
+    class VQADataset:
+        def create_retrieval_dataset(self, *a, **k):
+            raise AssertionError("reference method called")
+
+        def retrieve_closest_qa_pairs(self, *a, **k):
+            raise AssertionError("reference method called")
+
+    dropin.patch_dataset_class(VQADataset)
+    dropin.patch_dataset_class(VQADataset)  # idempotent
+    calls = []
+
+    class FakeRetrieval:
+        retrieval_embeddings = torch.zeros(3, 4)
+        retrieval_answers = ["a", "b", "c"]
+        retrieval_question_info = {"question_id": ["1", "2", "3"]}
+
+        def create_retrieval_dataset(self, loader, prefix, **kw):
+            calls.append(("create", prefix, kw))
+
+        def retrieve_closest_qa_pairs(self, batch, **kw):
+            calls.append(("retrieve", kw))
+            return ["prompt"]
+
+    ds = VQADataset()
+    ds._mpr_retrieval = FakeRetrieval()
+    ds.create_retrieval_dataset([], "pfx", is_training_phase=False, retrieval_k=3)
+    assert calls[0][0] == "create" and calls[0][2]["layout"] == "reference"
+    assert calls[0][2]["cache_name"] == "VQADataset" and ds.retrieval_k == 3
+    assert ds.retrieval_answers == ["a", "b", "c"]
+    assert ds.retrieve_closest_qa_pairs({}, return_info=["question_id"]) == ["prompt"]
+    assert calls[1] == ("retrieve", {"return_ans": False, "return_info": ["question_id"],
+                                     "return_dists": False, "use_quantifier": True})
+
+
+def test_patch_model_module_and_gpu_flag():
+    mod = types.ModuleType("architectures.T5VisionModel")
+    mod.T5VisionModel = object
+    dropin.patch_model_module(mod)
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    assert mod.T5VisionModel is T5VisionModel and mod._mpr_orig_T5VisionModel is object
+    assert dropin.wants_gpu(["--test", "--gpu_id", "0"])
+    assert dropin.wants_gpu(["--gpu_id=3"])
+    assert not dropin.wants_gpu(["--test", "--gpu_id", "cpu"])
+    assert not dropin.wants_gpu(["--test"])
+
+
+def test_launcher_leaves_cpu_runs_to_the_reference(tmp_path, capsys):
+    script = tmp_path / "main.py"
+    script.write_text("import sys\nprint('ran', sys.argv[1:])\n")
+    assert dropin.main([str(script), "--test", "--gpu_id", "cpu"]) == 0
+    out = capsys.readouterr()
+    assert "ran ['--test', '--gpu_id', 'cpu']" in out.out
+    assert not dropin._INSTALLED

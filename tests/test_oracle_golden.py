@@ -78,11 +78,38 @@ def test_vote_prompt_buckets():
     assert oret.vote_prompt(["x", "y"], False) == "The most frequent answer is x"
 
 
-def test_cosine_similarity_oracle_matches_reference_formula():
-    x1 = torch.randn(5, 7)
-    x2 = torch.randn(5, 7)
-    ref = torch.nn.functional.cosine_similarity(x1, x2, dim=1, eps=1e-8)
-    assert torch.allclose(oret.cosine_similarity(x1, x2), ref, atol=1e-6)
+def test_cosine_similarity_oracle_matches_reference_golden():
+    """G5: the reference's own utils.cosine_similarity (utils.py:57-62) outputs."""
+    z = np.load(os.path.join(GOLD, "g5_cosine.npz"))
+    for name, x1, x2, dim in gi.g5_inputs():
+        got = oret.cosine_similarity(x1, x2, dim=dim)
+        assert got.shape == z[name].shape, name
+        assert np.abs(got.numpy() - z[name]).max() <= 1e-6, name
+
+
+def test_g6_retrieval_off_oracle():
+    """G6 (config C1): the reference's prepare_input / predict / forward with
+    retrieval_function=None (retrieved_info = "", architectures/T5VisionModel.py:148-149)."""
+    z = np.load(os.path.join(GOLD, "g6_noretrieval.npz"))
+    with open(os.path.join(GOLD, "g6_noretrieval.json")) as f:
+        j = json.load(f)
+    ccfg, clip_sd, tcfg, tok_sd, t5cfg, t5_sd = gi.g2_models()
+    batch = gi.g2_batch()
+    tok = syn.HashT5Tokenizer()
+    tok.add_tokens(["[itk]"])
+    emb, mask, enc = _oracle_prepare(batch, [""] * len(batch["question"]), tok_sd, t5_sd, tok)
+    assert enc["input_ids"].tolist() == z["input_ids"].tolist()
+    assert mask.tolist() == z["mask"].tolist()
+    assert _rel(emb, z["combined"]) < FP_TOL
+    seqs, _ = ot5.generate(t5_sd, emb, mask, t5cfg.num_heads, 20)
+    assert seqs.tolist() == z["sequences"].tolist()
+    assert tok.batch_decode(seqs, skip_special_tokens=True) == j["predictions"]
+    from oracle import pipeline
+    X, answers, info = gi.g2_index(ccfg)
+    preds, prompts, _ = pipeline.predict(
+        batch, clip_sd, tok_sd, t5_sd, t5cfg.num_heads, X, answers, info, 0, False,
+        syn.hash_clip_tokenize, tok)
+    assert prompts == [""] * len(batch["question"]) and preds == j["predictions"]
 
 
 @pytest.fixture(scope="module")
@@ -170,3 +197,36 @@ def test_t5_bucket_lut_matches_reference_function():
     rel = torch.arange(-700, 701)
     for bid in (True, False):
         assert torch.equal(prod_bucket(rel, bid), ot5.relative_position_bucket(rel, bid))
+
+
+@pytest.mark.slow
+def test_g7_t5_base_oracle():
+    """G7 (config C5's model): t5-base behind the reference's T5VisionModel, use_image_info=0."""
+    z = np.load(os.path.join(GOLD, "g7_t5_base.npz"))
+    cfg = syn.T5_BASE
+    sd = syn.t5_state_dict(gi.G7["t5_seed"], cfg)
+    ids = torch.from_numpy(z["input_ids"])
+    mask = torch.from_numpy(z["mask"])
+    emb = sd["shared.weight"][ids]
+    assert _rel(emb, z["combined"]) < FP_TOL
+    enc = ot5.encode(sd, emb, mask, cfg.num_heads)
+    assert _rel(enc[:, :8], z["enc_head"]) < FP_TOL
+    assert ot5.generate_cached(sd, emb, mask, cfg.num_heads, 20).tolist() == \
+        z["sequences"].tolist()
+    labels = torch.from_numpy(z["labels"])
+    lg = ot5.decoder_logits(sd, enc, mask, ot5.shift_right(labels), cfg.num_heads)
+    assert _rel(lg[:, :, torch.from_numpy(z["vocab_sel"])], z["logits_sel"]) < FP_TOL
+
+
+@pytest.mark.slow
+def test_g8_long_source_oracle():
+    """G8: a 562-key source (50 image tokens + max_source_length 512 text tokens)."""
+    z = np.load(os.path.join(GOLD, "g8_long_source.npz"))
+    cfg = syn.T5Config()
+    sd = syn.t5_state_dict(gi.G8["t5_seed"], cfg)
+    ids, img_tok, mask = gi.g8_inputs(cfg.d_model)
+    emb = torch.cat([img_tok, sd["shared.weight"][ids]], 1)
+    enc = ot5.encode(sd, emb, mask, cfg.num_heads)
+    assert _rel(enc[:, ::37], z["enc_rows"]) < FP_TOL
+    assert ot5.generate_cached(sd, emb, mask, cfg.num_heads, 20).tolist() == \
+        z["sequences"].tolist()
