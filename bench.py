@@ -52,6 +52,7 @@ WORDS = ("what is the organ shown in this image does picture contain lung liver 
          "x-ray largest normal").split()
 TASKS = ["organ", "modality", "position", "abnormality", "plane", "quantity", "color", "size"]
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+BF16_MFMA_PEAK_TFLOPS = 2516.8  # MI355X_MICROARCH.md: bf16 dense = 16 x the f32 MFMA rate
 HBM_PEAK_GBS = 8000.0
 
 
@@ -374,11 +375,15 @@ def main():
         if launches:
             ach = flops / (ms * 1e-3) / 1e12
             traffic, traffic_src = _pmc_traffic()
+            x3 = os.environ.get("MPR_GEMM", "") != "f32"
             roofline = {"bound": "mfma", "achieved": round(ach, 2),
                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
                         "traffic": traffic,
-                        "kernel": "gemm_f32_kernel (v_mfma_f32_32x32x2_f32 / 16x16x4)",
+                        "kernel": ("gemm_x3_kernel (fp32 product as 6 bf16 v_mfma_f32_32x32x16_bf16"
+                                   " partial products of a 3-way bf16 split; achieved/peak are fp32"
+                                   " algorithmic flops against the fp32 MFMA dense peak)" if x3 else
+                                   "gemm_f32_kernel (v_mfma_f32_32x32x2_f32 / 16x16x4)"),
                         "measured": "replay of one pass's launches back to back, hipEvents "
                                     "around each launch",
                         "launches_per_step": round(launches / args.steps, 1),
@@ -387,6 +392,10 @@ def main():
                         "algorithmic_gflop_per_launch": round(flops / launches / 1e9, 4),
                         "algorithmic_mb_per_launch": round(abytes / launches / 1e6, 3),
                         "traffic_source": traffic_src}
+            if x3:  # what the bf16 pipe actually executes: 6 products per fp32 flop
+                roofline["bf16_pipe"] = {"executed": round(6 * ach, 1),
+                                         "peak": BF16_MFMA_PEAK_TFLOPS,
+                                         "frac": round(6 * ach / BF16_MFMA_PEAK_TFLOPS, 4)}
             if launches_live:
                 ach_live = flops_live / (ms_live * 1e-3) / 1e12
                 roofline["in_serving_loop"] = {

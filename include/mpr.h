@@ -64,6 +64,10 @@ int64_t mpr_index_rows(const mpr_index* index);
  * similarity.  Order: best first; exact ties broken by lowest id.  1 <= k <= 64, k <= n. */
 int mpr_index_search(mpr_index* index, const float* q_dev, int32_t b, int32_t k, int64_t* ids_dev,
                      float* dist_dev, void* stream);
+/* Queries of the last search on `stream` that took the exact fallback of the coarse large-batch
+ * path (bf16 scan + exact re-rank; see scan.hip): -1 when that search was not a coarse one.
+ * Synchronises the stream (measurement / tests; no reference counterpart). */
+int mpr_index_coarse_fallbacks(mpr_index* index, void* stream, int32_t* count);
 /* Full score matrix out_dev [b, n] (L2 distance or cosine similarity), the torch.cdist output
  * (dataset/VQAFeatureDataset.py:192) / pairwise cosine_similarity (utils.py:57-62). */
 int mpr_index_scores(mpr_index* index, const float* q_dev, int32_t b, float* out_dev, void* stream);

@@ -33,6 +33,7 @@ SIGNATURES = [
     ("mpr_index_search", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                    c_void_p]),
     ("mpr_index_scores", c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    ("mpr_index_coarse_fallbacks", c_int32, [c_void_p, c_void_p, I32P]),
     ("mpr_topk_merge", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32,
                                  c_void_p, c_void_p, c_void_p]),
     ("mpr_cosine_rows", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p,

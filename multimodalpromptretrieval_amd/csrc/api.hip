@@ -147,8 +147,41 @@ int mpr_index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_
     // a growth frees the old buffer: hipFree waits for the device, so work of earlier searches
     // on this stream that still reads it completes first
     MPR_TRY(slot->ensure(scan_topk_workspace(ix->n, b, k)));
+    const void* xb = nullptr;
+    const float* xmax = nullptr;
+    if (scan_coarse_eligible(ix->n, ix->d, b, k, ix->metric)) {
+      if (!ix->rows_bf16.ptr) {  // first large-batch search: the bf16 rows and the norm bound
+        MPR_TRY(ix->rows_bf16.ensure((size_t)ix->n * ix->d * 2));
+        MPR_TRY(ix->xmax.ensure(2 * sizeof(float)));
+        MPR_TRY(index_to_bf16(ix->rows.as<float>(), ix->n * ix->d, ix->rows_bf16.ptr, S(stream)));
+        MPR_TRY(max_of(ix->norms.as<float>(), ix->n, ix->xmax.as<float>(), S(stream)));
+        DevBuf res;  // per-row rounding residuals, reduced to their max (freed after the sync)
+        MPR_TRY(res.ensure((size_t)ix->n * sizeof(float)));
+        MPR_TRY(bf16_residuals(ix->rows.as<float>(), ix->n, ix->d, res.as<float>(), S(stream)));
+        MPR_TRY(max_of(res.as<float>(), ix->n, ix->xmax.as<float>() + 1, S(stream)));
+        MPR_HIP(hipStreamSynchronize(S(stream)));
+      }
+      xb = ix->rows_bf16.ptr;
+      xmax = ix->xmax.as<float>();
+    }
+    ix->last_coarse_b[stream] = xb ? b : 0;
     return scan_topk(ix->rows.as<float>(), ix->norms.as<float>(), ix->n, ix->d, ix->row_offset,
-                     ix->metric, q, b, k, slot->as<float>(), slot->bytes, dist, ids, S(stream));
+                     ix->metric, q, b, k, slot->as<float>(), slot->bytes, dist, ids, S(stream),
+                     xb, xmax);
+  });
+}
+
+int mpr_index_coarse_fallbacks(mpr_index* ix, void* stream, int32_t* count) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(ix != nullptr && count != nullptr, "coarse_fallbacks: null argument");
+    *count = -1;
+    auto it = ix->last_coarse_b.find(stream);
+    if (it == ix->last_coarse_b.end() || it->second == 0) return MPR_OK;
+    MPR_HIP(hipStreamSynchronize(S(stream)));
+    int c = 0;
+    MPR_TRY(coarse_flag_count(ix->ws[stream]->ptr, ix->n, ix->d, it->second, &c));
+    *count = c;
+    return MPR_OK;
   });
 }
 

@@ -15,6 +15,7 @@
 // operand for the same weight registers, K is split across the 8 waves of a block and reduced through
 // LDS, and T5's RMSNorm of the activation rows is folded into the operand and the epilogue.
 #include <algorithm>
+#include <cstring>
 
 #include "kernels.h"
 
@@ -245,6 +246,232 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, flo
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores ("x3"): every fp32 operand is split into three bf16 terms
+// with round-to-nearest residuals, a = a0 + a1 + a2 (|a - a0| <= 2^-8 |a|, |a - a0 - a1| <=
+// 2^-16 |a|, the remainder <= 2^-24 |a|: fp32 input precision), and
+//     a.b = a0.b0 + (a0.b1 + a1.b0) + (a0.b2 + a1.b1 + a2.b0)          (+ terms <= 2^-23 |a.b|)
+// — six v_mfma_f32_32x32x16_bf16 per 16-deep k step, each product of two bf16 exact in fp32 and
+// accumulated in fp32.  Six bf16 MFMAs cost 12 cycles per k per SIMD against 32 for one
+// v_mfma_f32_32x32x2_f32 (bf16 runs at 16x the f32 MFMA rate): the same tile does 2.67x the
+// arithmetic per cycle.  Error vs fp64 (tools/x3bench.hip): within a factor ~1.5 of the f32 MFMA
+// kernel's (both ~1e-7 of sum|a.b| at K <= 3072), orders below every parity tolerance.
+// Structure as gemm_tile: BM x BN block tile, WM x WN 32x32 accumulators per wave, BK-deep K
+// tiles staged fp32 global -> registers (D tiles in flight) -> split -> 3 bf16 planes in LDS (two
+// stages), KW wave groups splitting each K tile (partials summed through LDS).
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const f32x4& v, bf16x4& h0, bf16x4& h1, bf16x4& h2) {
+  h0 = __builtin_convertvector(v, bf16x4);
+  const f32x4 r1 = v - __builtin_convertvector(h0, f32x4);
+  h1 = __builtin_convertvector(r1, bf16x4);
+  const f32x4 r2 = r1 - __builtin_convertvector(h1, f32x4);
+  h2 = __builtin_convertvector(r2, bf16x4);
+}
+
+template <int BM, int BN, int BK>
+constexpr int x3_lds_floats() {
+  // per stage: 3 planes x (BM + BN) rows x (BK + 8) bf16 (16-byte row pad: conflict-free
+  // ds_read_b128 of 32 rows), two stages, in floats
+  return 2 * 3 * (BM + BN) * (BK + 8) / 2;
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+__device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
+  constexpr int WAVES_N = BN / (32 * WN);
+  constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
+  constexpr int NT = 64 * WAVES_MN * KW;
+  constexpr int LDK = BK + 8, KQ = BK / 4;      // LDS row stride (bf16), float4 per tile row
+  constexpr int LA = BM * KQ / NT, LB = BN * KQ / NT;
+  constexpr int PLANE = (BM + BN) * LDK;        // bf16 per plane (A rows then W rows)
+  constexpr int STAGE = 3 * PLANE;              // bf16 per stage
+  constexpr int KPW = BK / KW;                  // k per tile and wave group
+  constexpr int NS = KPW / 16;                  // 16-deep MFMA steps per tile and wave
+  static_assert(LA * NT == BM * KQ && LB * NT == BN * KQ, "loader split");
+  static_assert(NS >= 1 && KPW % 16 == 0, "k split");
+  static_assert(KW == 1 || 2 * STAGE / 2 >= KW * BM * BN, "LDS reduction space");
+  __bf16* smem = reinterpret_cast<__bf16*>(smem_f);
+  const int M = a.M, N = a.N, K = a.K;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wmn = wave % WAVES_MN, kw = wave / WAVES_MN;
+  const int wm = wmn / WAVES_N, wn = wmn % WAVES_N;
+
+  f32x4 ra[D][LA], rb[D][LB];
+  bool oka[D][LA], okb[D][LB];
+  auto gload = [&](int j, int k0) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = m0 + r;
+      oka[j][i] = row < M && c < K;
+      ra[j][i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
+                                                 min(c, K - 4));
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = n0 + r;
+      okb[j][i] = row < N && c < K;
+      rb[j][i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
+                                                 min(c, K - 4));
+    }
+  };
+  auto put = [&](__bf16* base, int row, int kc, const f32x4& v) {
+    bf16x4 h0, h1, h2;
+    split3(v, h0, h1, h2);
+    __bf16* p = base + row * LDK + kc;
+    *reinterpret_cast<bf16x4*>(p) = h0;
+    *reinterpret_cast<bf16x4*>(p + PLANE) = h1;
+    *reinterpret_cast<bf16x4*>(p + 2 * PLANE) = h2;
+  };
+  auto swrite = [&](int st, int j) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    __bf16* base = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + i * NT;
+      put(base, idx / KQ, (idx % KQ) * 4, oka[j][i] ? ra[j][i] : zero);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int idx = tid + i * NT;
+      put(base, BM + idx / KQ, (idx % KQ) * 4, okb[j][i] ? rb[j][i] : zero);
+    }
+  };
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  // lane (li, lh) of a 32x32x16 step reads row li, k = 16 s + 8 lh .. +7 of every plane
+  const int li = lane & 31, lh = lane >> 5;
+  const int kof = kw * KPW + 8 * lh;
+  bf16x8 fa[WM][NS][3], fb[WN][NS][3], na[WM][NS][3], nb[WN][NS][3];
+  auto sread = [&](int st, bf16x8(&xa)[WM][NS][3], bf16x8(&xb)[WN][NS][3]) {
+    const __bf16* base = smem + st * STAGE;
+#pragma unroll
+    for (int s4 = 0; s4 < NS; ++s4)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+          xa[mi][s4][p] = *reinterpret_cast<const bf16x8*>(
+              base + p * PLANE + (wm * 32 * WM + mi * 32 + li) * LDK + kof + 16 * s4);
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni)
+          xb[ni][s4][p] = *reinterpret_cast<const bf16x8*>(
+              base + p * PLANE + (BM + wn * 32 * WN + ni * 32 + li) * LDK + kof + 16 * s4);
+      }
+  };
+  // MFMA u of the tile's NS * WM * WN * 6 (u = ((s4 * WM + mi) * WN + ni) * 6 + term); terms in
+  // increasing magnitude: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
+  constexpr int NMF = NS * WM * WN * 6;
+  auto mfmas = [&](int u_lo, int u_hi) {
+#pragma unroll
+    for (int u = u_lo; u < u_hi; ++u) {
+      const int term = u % 6, t = u / 6, ni = t % WN, mi = (t / WN) % WM, s4 = t / (WN * WM);
+      constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+      acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][s4][PA[term]],
+                                                            fb[ni][s4][PB[term]], acc[mi][ni],
+                                                            0, 0, 0);
+    }
+  };
+  auto advance = [&]() {
+#pragma unroll
+    for (int s4 = 0; s4 < NS; ++s4)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi) fa[mi][s4][p] = na[mi][s4][p];
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) fb[ni][s4][p] = nb[ni][s4][p];
+      }
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  const int nkr = (nk + D - 1) / D * D;
+  gload(0, 0);
+  swrite(0, 0);
+  gload(0, BK);
+  swrite(1, 0);
+#pragma unroll
+  for (int j = 0; j < D; ++j) gload(j, (2 + j) * BK);
+  __syncthreads();
+  sread(0, fa, fb);
+  __syncthreads();  // every wave's tile-0 reads land before iteration 0 rewrites stage 0
+  // Iteration t (one barrier): multiply tile t (fragments in registers), read tile t+1's
+  // fragments from the other stage under the first MFMAs, write tile t+2 into tile t's stage
+  // (read by every wave before the previous barrier) and re-arm the register slot.
+  constexpr int U1 = NMF / 3 > 0 ? NMF / 3 : 1;
+  for (int kt = 0; kt < nkr; kt += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int st = (kt + j) & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(0, U1);
+      __builtin_amdgcn_sched_barrier(0);
+      sread(st ^ 1, na, nb);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(U1, NMF);
+      __builtin_amdgcn_sched_barrier(0);
+      swrite(st, j);
+      gload(j, (kt + j + 2 + D) * BK);
+      __syncthreads();
+      advance();
+    }
+  }
+
+  if constexpr (KW > 1) {
+    f32x16* red = reinterpret_cast<f32x16*>(smem_f);
+    if (kw > 0) {
+#pragma unroll
+      for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni)
+          red[(((kw - 1) * WAVES_MN + wmn) * WM * WN + mi * WN + ni) * 64 + lane] = acc[mi][ni];
+    }
+    __syncthreads();
+    if (kw > 0) return;
+#pragma unroll
+    for (int g = 1; g < KW; ++g)
+#pragma unroll
+      for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni)
+          acc[mi][ni] += red[(((g - 1) * WAVES_MN + wmn) * WM * WN + mi * WN + ni) * 64 + lane];
+  }
+
+#pragma unroll
+  for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+      const int col = n0 + wn * 32 * WN + ni * 32 + li, colc = min(col, N - 1);
+      const int rbase = m0 + wm * 32 * WM + mi * 32 + 4 * lh;
+      const float bv = a.bias ? a.bias[colc] : 0.f;
+      float rv[16];
+      if (a.R) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          rv[r] = a.R[(int64_t)min(rbase + (r & 3) + 8 * (r >> 2), M - 1) * a.ldr + colc];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        float v = act_exact(acc[mi][ni][r] + bv, a.act);
+        if (a.R) v = rv[r] + v;
+        const int64_t coff = a.c_rpb ? (int64_t)(row / a.c_rpb) * a.c_bs +
+                                           (int64_t)(row % a.c_rpb) * a.ldc
+                                     : (int64_t)row * a.ldc;
+        if (row < M && col < N) a.C[coff + col] = v;
+      }
+    }
+}
+
 // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (hardware id % 8), each
 // with its own L2; remap so that every XCD walks a contiguous run of tiles in column-major
 // order (all row tiles of a column tile before the next), i.e. an XCD reads its W columns once
@@ -307,6 +534,55 @@ int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
   const size_t pad = lds_kb * 1024 > STATIC_LDS ? (size_t)(lds_kb * 1024 - STATIC_LDS) : 0;
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, D, KW, XR>), dim3(gx, gy, g.n), dim3(NT),
                      pad, s, g);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+// Grid = exactly the launch's tiles (every problem's own cdiv(M, BM) x cdiv(N, BN), problems in
+// order), one dimension.  Blocks are dealt round-robin over the 8 XCDs; the index is remapped so
+// each XCD walks a contiguous run of the concatenated tile list, column-major inside a problem
+// (an XCD reads its W columns once and shares activation rows through its L2).  Sizing the grid
+// by the largest problem instead (blockIdx.z per problem) leaves the small problems' slices
+// mostly empty, and the remap then gives whole XCDs nothing to do (the tower launches' text
+// problems: fc2 231 -> see DESIGN §3).
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+__global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_x3_kernel(
+    const GemmGroup grp) {
+  __shared__ __attribute__((aligned(16))) float smem[x3_lds_floats<BM, BN, BK>()];
+  const int total = gridDim.x, hw = blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
+  int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  int z = 0, gy = 0;
+#pragma unroll
+  for (int i = 0; i < GEMM_GROUP; ++i) {
+    if (i == z && i < grp.n) {
+      const int gyi = (int)cdiv(i == 0 ? grp.g[0].M : i == 1 ? grp.g[1].M : i == 2 ? grp.g[2].M
+                                                                                  : grp.g[3].M,
+                                BM);
+      const int gxi = (int)cdiv(i == 0 ? grp.g[0].N : i == 1 ? grp.g[1].N : i == 2 ? grp.g[2].N
+                                                                                  : grp.g[3].N,
+                                BN);
+      if (t >= gxi * gyi) {
+        t -= gxi * gyi;
+        ++z;
+      } else {
+        gy = gyi;
+      }
+    }
+  }
+  const GemmArgs a = select_problem(grp, z);
+  const int bx = t / gy, by = t - bx * gy;
+  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW>(a, bx, by, smem);
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
+  constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW;
+  int64_t tiles = 0;
+  for (int i = 0; i < g.n; ++i) tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM);
+  if (tiles == 0) return MPR_OK;
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW>), dim3((unsigned)tiles), dim3(NT),
+                     0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -679,7 +955,19 @@ const bool g_ksplit32_only = [] {
   return e && atoi(e) != 0;
 }();
 
-int gemm_launch(const GemmGroup& g, bool big, hipStream_t s) {
+// Kernel families of one launch.  F32_*: exact f32 MFMA (v_mfma_f32_32x32x2_f32), the round-1
+// kernels, kept behind MPR_GEMM=f32.  X3_*: the split-bf16 kernels (default).  Within X3_WIDE /
+// X3_TALL (16-deep k steps in order, KW = 1) every output element is accumulated in the same
+// order whatever the block tile, so the tile may follow the launch (grouped or alone, one batch
+// or two concatenated: bit-identical results).
+enum GemmKind : int { F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3 };
+
+const bool g_gemm_f32 = [] {
+  const char* e = getenv("MPR_GEMM");
+  return e && strcmp(e, "f32") == 0;
+}();
+
+int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
   double flops = 0, bytes = 0;
   for (int i = 0; i < g.n; ++i) {
     flops += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K;
@@ -690,50 +978,69 @@ int gemm_launch(const GemmGroup& g, bool big, hipStream_t s) {
     if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone)
       g_recorded.push_back(g);
   }
-  // K-split tiles: 32x32 blocks, or 64x32 blocks (two 32x32 tiles sharing each W slice, 8 waves)
-  // once the launch has >= 2048 32x32 blocks (8 per CU: the two-batch tower passes' ViT out-proj
-  // and fc2, 54 -> 50 and 168 -> 158 us; below that the 32x32 blocks are faster).  Every 32x32
-  // sub-tile is summed by the same 4 K-slice waves in the same order in both, so the choice may
-  // depend on the launch: results are bit-identical (tools/gbench.hip checks).
+  // F32_SMALL: 32x32 blocks, or 64x32 blocks (two 32x32 tiles sharing each W slice, 8 waves)
+  // once the launch has >= 2048 32x32 blocks; every 32x32 sub-tile is summed by the same 4
+  // K-slice waves in the same order in both (bit-identical, tools/gbench.hip checks).
   int64_t blocks32 = 0;
   for (int i = 0; i < g.n; ++i) blocks32 += cdiv(g.g[i].M, 32) * cdiv(g.g[i].N, 32);
   return probed(PROBE_GEMM, flops, bytes, s, [&]() {
-    if (big) return launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>(g, s);
-    if (blocks32 >= 2048 && !g_ksplit32_only) return launch_gemm_group<64, 32, 1, 1, 64, 2, 4>(g, s);
-    return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
+    switch (kind) {
+      case F32_BIG: return launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>(g, s);
+      case F32_SMALL:
+        if (blocks32 >= 2048 && !g_ksplit32_only)
+          return launch_gemm_group<64, 32, 1, 1, 64, 2, 4>(g, s);
+        return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
+      case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1>(g, s);
+      default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);
+    }
   });
 }
 }  // namespace
 
 int gemm_group(const GemmGroup& g, hipStream_t s) {
   MPR_REQUIRE(g.n >= 1 && g.n <= GEMM_GROUP, "gemm_group: %d problems", g.n);
-  // Tile choice, per problem (measured on MI355X over the ViT/T5/CLIP-text projection shapes,
-  // single and paired, tools/gbench.hip): 64x64 tiles (4 waves of 32x32, BK 32, 2 tiles of
-  // loads in flight) once the problem has >= 1.5 blocks per CU; below that 32x32 tiles with the
-  // K tile split over 4 waves (4x the blocks, partial sums added through LDS): 800x768x3072
-  // 67 -> 54 us, 1152x512x2048 47 -> 38 us, paired 800x768x768 34 -> 29 us.  BK 64, 128-row
-  // tiles, 8-wave 64x64 blocks, 2x2 or 1x2 accumulators per wave and split-K across blocks were
-  // slower at every shape of this path.  Problems of a group with different choices go to two
-  // launches, so a problem gets the same tile (the same summation order, bit-identical results)
-  // alone or grouped (one dual-configuration kernel for both measured 30% slower for the
-  // towers: 5.2 vs 4.0 ms; giving the text tower's QKV / fc1 (M 384) the 64x64 tile so they
-  // join the ViT launches measured 4.46 vs 4.02 ms).
-  GemmGroup big, small;
-  big.n = small.n = 0;
   for (int i = 0; i < g.n; ++i) {
     const GemmArgs& a = g.g[i];
     MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N,
                 a.K);
-    if (a.M == 0 || a.N == 0) continue;
     MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                     aligned16(a.W),
                 "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-    const int tm = a.tile_m > 0 ? a.tile_m : a.M;
-    GemmGroup& dst = cdiv(tm, 64) * cdiv(a.N, 64) >= 384 ? big : small;
-    dst.g[dst.n++] = a;
   }
-  if (big.n) MPR_TRY(gemm_launch(big, true, s));
-  if (small.n) MPR_TRY(gemm_launch(small, false, s));
+  if (g_gemm_f32) {
+    // Round-1 f32 MFMA tiles, per problem (tools/gbench.hip): 64x64 tiles (4 waves of 32x32,
+    // BK 32) once the problem has >= 1.5 blocks per CU, else 32x32 tiles with the K tile split
+    // over 4 waves.  A problem keeps its tile alone or grouped (bit-identical results).
+    GemmGroup big, small;
+    big.n = small.n = 0;
+    for (int i = 0; i < g.n; ++i) {
+      const GemmArgs& a = g.g[i];
+      if (a.M == 0 || a.N == 0) continue;
+      const int tm = a.tile_m > 0 ? a.tile_m : a.M;
+      GemmGroup& dst = cdiv(tm, 64) * cdiv(a.N, 64) >= 384 ? big : small;
+      dst.g[dst.n++] = a;
+    }
+    if (big.n) MPR_TRY(gemm_launch(big, F32_BIG, s));
+    if (small.n) MPR_TRY(gemm_launch(small, F32_SMALL, s));
+    return MPR_OK;
+  }
+  // Split-bf16 tiles (tools/x3bench.hip: the tower launches of two batches, each ViT problem plus
+  // the text tower's problem of the same layer in one launch).  Every problem of a launch shares
+  // one KW = 1 tile, so the choice may follow the launch: 128x128 blocks of 8 waves (2x1 32x32
+  // accumulators each) once the launch has >= 160 of them — even below one block per CU they beat
+  // smaller tiles (ViT out 1600x768x768 x2 + text: 41.3 us against 50.6 for 64x64 blocks and 60.6
+  // for the f32 kernel; qkv 106 vs 158, fc1 140 vs 196, fc2 137 vs 178) — else 64x128 blocks of 8
+  // waves of 32x32 (one-batch fc2 800x768x3072 x2 + text: 93.7 vs 114 us f32).
+  GemmGroup fam;
+  fam.n = 0;
+  int64_t b128 = 0;
+  for (int i = 0; i < g.n; ++i) {
+    const GemmArgs& a = g.g[i];
+    if (a.M == 0 || a.N == 0) continue;
+    fam.g[fam.n++] = a;
+    b128 += cdiv(a.M, 128) * cdiv(a.N, 128);
+  }
+  if (fam.n) MPR_TRY(gemm_launch(fam, b128 >= 160 ? X3_WIDE : X3_TALL, s));
   return MPR_OK;
 }
 

@@ -156,10 +156,21 @@ int fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s);
 int scale_inplace(float* p, int64_t n, float scale, hipStream_t s);
 
 // Retrieval scan (scan.hip).
+// Xb / xmax (optional): the index as bf16 rows and {max_i |x_i|^2, max_i |bf16(x_i) - x_i|^2} —
+// enable the coarse bf16 scan +
+// exact re-rank for large batches (scan_coarse_eligible).
 int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
               int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
-              float* out_dist, int64_t* out_ids, hipStream_t s);
+              float* out_dist, int64_t* out_ids, hipStream_t s, const void* Xb = nullptr,
+              const float* xmax = nullptr);
 size_t scan_topk_workspace(int64_t n, int b, int k);
+bool scan_coarse_eligible(int64_t n, int d, int b, int k, int metric);
+// queries of the last coarse search on workspace `ws` that needed the exact fallback (host sync)
+int coarse_flag_count(const void* ws, int64_t n, int d, int b, int* count);
+int index_to_bf16(const float* X, int64_t count, void* out, hipStream_t s);
+// |bf16(x_i) - x_i|^2 per row
+int bf16_residuals(const float* X, int64_t n, int d, float* out, hipStream_t s);
+int max_of(const float* x, int64_t n, float* out, hipStream_t s);
 int scan_scores(const float* X, const float* xnorm, int64_t n, int d, int metric, const float* Q,
                 int b, float* out, hipStream_t s);
 int row_sqnorms(const float* X, int64_t n, int d, float* out, hipStream_t s);

@@ -17,9 +17,11 @@ struct mpr_model {
 struct mpr_index {
   mpr::DevBuf rows;   // [n, d] fp32
   mpr::DevBuf norms;  // [n] squared L2 norms
+  mpr::DevBuf rows_bf16, xmax;  // coarse-scan copy of the rows, max squared norm (built on demand)
   // search workspace per stream: searches enqueued on different streams (a prefetched search on
   // the tower stream beside an analytics search on the caller's) never share candidate buffers
   std::map<void*, std::unique_ptr<mpr::DevBuf>> ws;
+  std::map<void*, int> last_coarse_b;  // batch of the last coarse search per stream (0: none)
   int64_t n = 0;
   int d = 0;
   int metric = 0;

@@ -22,6 +22,7 @@
 #include <cfloat>
 #include <climits>
 #include <cstdlib>
+#include <vector>
 
 #include "kernels.h"
 
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256) void scan_mm_kernel(const float* __restrict__ 
                                                       const float* __restrict__ Q,
                                                       const float* __restrict__ qnorm, int b,
                                                       int nqt, int RB, float* cand_key,
-                                                      int64_t* cand_id) {
+                                                      int64_t* cand_id, const int* gate) {
   __shared__ __attribute__((aligned(16))) float smem[2 * SM_STAGE];
   constexpr int KQ = SM_BK / 4, LA = SM_B * KQ / 256;  // float4 per thread and operand: 2
   int qt, rb;
@@ -224,6 +225,11 @@ __global__ __launch_bounds__(256) void scan_mm_kernel(const float* __restrict__ 
     const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
     qt = t % nqt;
     rb = t / nqt;
+  }
+  if (gate) {  // the coarse path's exact fallback: only query tiles holding a flagged query run
+    int any = 0;
+    for (int i = 0; i < SM_B && qt * SM_B + i < b; ++i) any |= gate[qt * SM_B + i];
+    if (!any) return;
   }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -403,12 +409,447 @@ __global__ void qnorm_kernel(const float* Q, int b, int d, float* out) {
   if (lane == 0) out[q] = s;
 }
 
+// ---- coarse bf16 scan + exact fp32 re-rank (b >= 64 queries, L2, d in {256, 512}) -------------
+// At C5 (256 queries x 1,048,576 x 512) the exact scan is fp32-MFMA-bound (275 GFLOP, ~3.2 ms).
+// Here the index is also kept as bf16 (rows rounded to nearest, 1 GiB) and scanned with
+// v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate, half the bytes: the HBM regime), keeping per
+// query the best coarse keys s~ = |x|^2 - 2 q~.x~ (|x|^2 exact; |q|^2 is constant per query): a
+// sorted list of CB_L per lane (its share of the rows), then the best CB_C over all lists; every
+// one of those is re-scored exactly in fp32 and the best k returned.  The coarse error is
+// bounded: with r = x~ - x and e = q~ - q the rounding residuals, |q~.x~ - q.x| <= |e| |x| +
+// |q| |r| + |e| |r| (Cauchy-Schwarz), so with the index's max |x| and max |r| and the query's own
+// |e|, |s~ - s| <= E = 2 (|e| X + |q| R + |e| R + 2 d 2^-24 (|q| + |e|)(X + R)) (the fp32
+// accumulations of the coarse and the exact dot included; rounding residuals are <= 2^-9 of each
+// component, so E ~ 2^-8 |q| X at worst, ~2^-9 for random data).  Every row of the exact top k
+// (ties included) has s~ <= T = s~(k) + 2E, s~(k) the coarse k-th best.  The re-rank is exact
+// when no such row can be missing: the CB_C-th selected key and every lane's bound (no row the
+// lane left out has a smaller key) lie beyond T.  Otherwise the
+// query's device flag is set and
+// the exact scan recomputes the flagged queries (its blocks exit at once for query tiles without
+// a flag) — never a silently approximate id.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int CB_RT = 128;             // index rows per block tile (4 x 32-row MFMA tiles)
+constexpr int CB_QT = 128;             // queries per block: 4 waves x 32
+constexpr int CB_BK = 32;              // k per LDS stage (two 16-deep MFMA steps)
+constexpr int CB_LDK = CB_BK + 8;      // LDS row stride in bf16 (16-byte pad: conflict-free)
+constexpr int CB_D = 4;                // stages of global loads in flight (1 wave per SIMD)
+constexpr int CB_L = 8;                // coarse candidates kept per lane list
+constexpr int CB_C = 64;               // coarse candidates re-ranked per query
+constexpr int CB_STAGE = CB_RT * CB_LDK;
+
+__global__ void to_bf16_kernel(const float* __restrict__ x, int64_t n4, bf16x4* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    out[i] = __builtin_convertvector(reinterpret_cast<const f32x4*>(x)[i], bf16x4);
+}
+
+// |bf16(x) - x|^2 per row (wave per row; runs once per index)
+__global__ void bf16_residual_kernel(const float* __restrict__ X, int64_t n, int d, float* out) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    const float v = X[row * d + c];
+    const float r = (float)(__bf16)v - v;
+    s += r * r;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[row] = s;
+}
+
+// max of n floats by one block (runs once per index)
+__global__ __launch_bounds__(1024) void max_kernel(const float* __restrict__ x, int64_t n,
+                                                   float* out) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, x[i]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    for (int i = 0; i < 16; ++i) r = fmaxf(r, red[i]);
+    out[0] = r;
+  }
+}
+
+// Block = 4 waves = CB_QT queries (wave w: queries qt*128 + 32w + (lane & 31); the block's bf16
+// query rows resident in LDS, the B operand) x a strided set of 128-row index tiles (staged
+// through LDS, shared by the 4 waves, A operand).  Per row tile each lane turns its 64
+// accumulators into coarse keys and keeps a sorted list of its best CB_L; each query's two lists
+// (lane halves) leave the block.
+template <int KS>
+__global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restrict__ Xb,
+                                                         const float* __restrict__ xnorm,
+                                                         int64_t n, int64_t row_offset,
+                                                         const __bf16* __restrict__ Qb, int b,
+                                                         int nqt, int RB, float* cand_key,
+                                                         int64_t* cand_id, float* lane_bound) {
+  constexpr int d = KS * 16, KQ = CB_BK / 8;  // 16-byte loads per staged row
+  constexpr int SPT = KS / 2;                  // stages per row tile
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][CB_STAGE];
+  __shared__ float xn_s[2][CB_RT];
+  int qt, rb;
+  {
+    const int total = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, slot = hw >> 3, q8 = total >> 3, r8 = total & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+    qt = t % nqt;
+    rb = t / nqt;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int64_t ntile = (n + CB_RT - 1) / CB_RT;
+  const int ntb = (int)((ntile - rb + RB - 1) / RB);
+
+  // the block's query rows stay in LDS for the whole scan (row stride d + 8 bf16: the B-fragment
+  // reads of 32 rows are conflict-free); zero rows past b
+  extern __shared__ __attribute__((aligned(16))) __bf16 qs[];  // [CB_QT][d + 8]
+  constexpr int LDQ = d + 8;
+  const int q = qt * CB_QT + wave * 32 + li;
+  const bool qok = q < b;
+  for (int idx = tid; idx < CB_QT * (d / 8); idx += 256) {
+    const int r = idx / (d / 8), c = (idx % (d / 8)) * 8, qq = qt * CB_QT + r;
+    bf16x8 v = bf16x8{};
+    if (qq < b) v = *reinterpret_cast<const bf16x8*>(Qb + (int64_t)qq * d + c);
+    *reinterpret_cast<bf16x8*>(&qs[r * LDQ + c]) = v;
+  }
+  // B[k = 16 s + 8 lh + j][col li] = Q~[wave's query li][16 s + 8 lh + j]
+  const __bf16* qrow = qs + (wave * 32 + li) * LDQ + 8 * lh;
+
+  bf16x8 rx[CB_D][2];
+  bool okx[CB_D][2];
+  float rn[CB_D];
+  auto gload = [&](int j, int step) {
+    const int tt = step / SPT, ks = step - tt * SPT;
+    const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB_RT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + i * 256, r = idx / KQ, c = ks * CB_BK + (idx % KQ) * 8;
+      const int64_t row = row0 + r;
+      okx[j][i] = row < n && tt < ntb;
+      rx[j][i] = *reinterpret_cast<const bf16x8*>(Xb + (row < n ? row : n - 1) * (int64_t)d + c);
+    }
+    // the tile's row norms ride with its first stage
+    const int64_t nrow = row0 + (tid & (CB_RT - 1));
+    rn[j] = xnorm[nrow < n ? nrow : n - 1];
+  };
+  auto swrite = [&](int st, int j, int step) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + i * 256, r = idx / KQ, c = (idx % KQ) * 8;
+      *reinterpret_cast<bf16x8*>(&xs[st][r * CB_LDK + c]) = okx[j][i] ? rx[j][i] : bf16x8{};
+    }
+    const int tt = step / SPT;
+    if (step - tt * SPT == 0 && tid < CB_RT) xn_s[tt & 1][tid] = rn[j];
+  };
+  bf16x8 fa[4][2], na[4][2], fb[2], nb[2];
+  // fragments of stage `ks` of a row tile: the 4 row tiles' A from the staged rows, the wave's
+  // B from the resident query rows
+  auto sread = [&](int st, int ks, bf16x8(&xa)[4][2], bf16x8(&xb)[2]) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        xa[mi][u] = *reinterpret_cast<const bf16x8*>(&xs[st][(mi * 32 + li) * CB_LDK + 16 * u +
+                                                              8 * lh]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      xb[u] = *reinterpret_cast<const bf16x8*>(qrow + CB_BK * ks + 16 * u);
+  };
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[mi][r] = 0.f;
+  // the lane's sorted best-CB_L list, in registers.  Per row tile only the lane's best two rows
+  // may enter it; the tile's third-best key goes into `drop`, so every row the lane did not keep
+  // has a key >= min(list's last key, drop) — the lane's bound the re-rank tests against.
+  float bk[CB_L];
+  int bi[CB_L];
+#pragma unroll
+  for (int t = 0; t < CB_L; ++t) {
+    bk[t] = INFINITY;
+    bi[t] = INT_MAX;
+  }
+  float drop = INFINITY;
+
+  gload(0, 0);
+  swrite(0, 0, 0);
+  gload(0, 1);
+  swrite(1, 0, 1);
+#pragma unroll
+  for (int j = 0; j < CB_D; ++j) gload(j, 2 + j);
+  __syncthreads();
+  sread(0, 0, fa, fb);
+  __syncthreads();
+  static_assert(SPT % CB_D == 0 && SPT % 2 == 0, "stage slots / LDS stages repeat per row tile");
+  // one barrier per stage: multiply stage t (fragments in registers), read stage t+1's
+  // fragments, write stage t+2 into stage t's LDS buffer, re-arm the register slot
+  for (int tt = 0; tt < ntb; ++tt) {
+#pragma clang loop unroll(full)
+    for (int ks = 0; ks < SPT; ++ks) {
+      const int step = tt * SPT + ks;
+      const int st = ks & 1, j = ks % CB_D;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+          acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][u], fb[u], acc[mi], 0, 0, 0);
+      sread(st ^ 1, (ks + 1) % SPT, na, nb);
+      swrite(st, j, step + 2);
+      gload(j, step + 2 + CB_D);
+      __syncthreads();
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        fa[mi][0] = na[mi][0];
+        fa[mi][1] = na[mi][1];
+      }
+      fb[0] = nb[0];
+      fb[1] = nb[1];
+    }
+    {  // coarse keys of this row tile: best two -> the lane's list, third best -> drop
+      const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB_RT;
+      float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
+      int i1 = INT_MAX, i2 = INT_MAX;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {  // rows in increasing order: ties keep the lower id
+          const int rr = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int row = (int)(row0 + rr);
+          float key = xn_s[tt & 1][rr] - 2.0f * acc[mi][r];
+          acc[mi][r] = 0.f;
+          key = row0 + rr < n ? key : INFINITY;
+          const bool l1 = key < b1, l2 = key < b2;
+          b3 = l2 ? b2 : fminf(b3, key);
+          b2 = l1 ? b1 : (l2 ? key : b2);
+          i2 = l1 ? i1 : (l2 ? row : i2);
+          b1 = l1 ? key : b1;
+          i1 = l1 ? row : i1;
+        }
+      drop = fminf(drop, b3);
+      auto insert = [&](float ck, int ci) {
+#pragma unroll
+        for (int t = 0; t < CB_L; ++t) {
+          const bool sw = ck < bk[t];
+          const float tk = sw ? bk[t] : ck;
+          const int ti = sw ? bi[t] : ci;
+          bk[t] = sw ? ck : bk[t];
+          bi[t] = sw ? ci : bi[t];
+          ck = tk;
+          ci = ti;
+        }
+      };
+      if (b1 < bk[CB_L - 1]) insert(b1, i1);
+      if (b2 < bk[CB_L - 1]) insert(b2, i2);
+    }
+  }
+  if (!qok) return;
+  float* okp = cand_key + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
+  int64_t* oip = cand_id + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
+#pragma unroll
+  for (int t = 0; t < CB_L; ++t) {
+    okp[t] = bk[t];
+    oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
+  }
+  lane_bound[((int64_t)q * RB + rb) * 2 + lh] = fminf(bk[CB_L - 1], drop);
+}
+
+// Coarse selection: block per query, the CB_C smallest of its n_cand lane-list keys (ids
+// alongside), sorted by (key, id).  The CB_C-th key is found by a bisection over the keys' order
+// bits (counts by a block reduction), then the <= CB_C keys at or below it are ranked.
+__device__ __forceinline__ uint32_t order_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restrict__ cand_key,
+                                                            const int64_t* __restrict__ cand_id,
+                                                            int n_cand, float* sel_key,
+                                                            int64_t* sel_id) {
+  __shared__ int cnt[4];
+  __shared__ float sk[CB_C * 2];
+  __shared__ int64_t si[CB_C * 2];
+  __shared__ int nsel;
+  const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* ck = cand_key + (int64_t)qi * n_cand;
+  const int64_t* ci = cand_id + (int64_t)qi * n_cand;
+  uint32_t u[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = tid + j * 256;
+    u[j] = c < n_cand && ci[c] >= 0 ? order_bits(ck[c]) : 0xFFFFFFFFu;
+  }
+  // smallest v with count(u <= v) >= CB_C
+  uint32_t lo = 0, hi = 0xFFFFFFFFu;
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) c += u[j] <= mid ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (lane == 0) cnt[wave] = c;
+    __syncthreads();
+    const int tot = (cnt[0] + cnt[1]) + (cnt[2] + cnt[3]);
+    __syncthreads();
+    if (tot >= CB_C) hi = mid;
+    else lo = mid + 1;
+  }
+  if (tid == 0) nsel = 0;
+  __syncthreads();
+  // gather every key <= the threshold (ties past CB_C are ranked out below; at most 2 CB_C kept)
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = tid + j * 256;
+    if (u[j] <= lo && u[j] != 0xFFFFFFFFu) {
+      const int slot = atomicAdd(&nsel, 1);  // LDS atomic
+      if (slot < 2 * CB_C) {
+        sk[slot] = ck[c];
+        si[slot] = ci[c];
+      }
+    }
+  }
+  __syncthreads();
+  const int m = min(nsel, 2 * CB_C);
+  for (int c = tid; c < CB_C; c += 256) {  // pad a short list
+    sel_key[(int64_t)qi * CB_C + c] = INFINITY;
+    sel_id[(int64_t)qi * CB_C + c] = -1;
+  }
+  __syncthreads();
+  if (tid < m) {
+    const float a = sk[tid];
+    const int64_t ia = si[tid];
+    int rank = 0;
+    for (int c = 0; c < m; ++c) rank += key_less(sk[c], si[c], a, ia) ? 1 : 0;
+    if (rank < CB_C) {
+      sel_key[(int64_t)qi * CB_C + rank] = a;
+      sel_id[(int64_t)qi * CB_C + rank] = ia;
+    }
+  }
+}
+
+// Exact re-rank: block per query over its CB_C coarse candidates (sorted coarse keys, global ids):
+// the sufficiency test (against the selected list and every lane's bound), the fp32 key
+// of every candidate (the exact scan's formula), the best k by (key, id); gate[q] = 1 asks the
+// exact scan for this query.
+__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X,
+                                                     const float* __restrict__ xnorm, int d,
+                                                     int64_t row_offset,
+                                                     const float* __restrict__ Q,
+                                                     const float* sel_key, const int64_t* sel_id,
+                                                     const float* lane_bound, int n_lists, int k,
+                                                     const float* xmax, float* out_dist,
+                                                     int64_t* out_id, int* gate) {
+  __shared__ float qs[512];
+  __shared__ float keys[CB_C];
+  __shared__ int64_t ids[CB_C];
+  __shared__ float part[4], epart[4], lmin[4];
+  const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* qp = Q + (int64_t)qi * d;
+  float ss = 0.f, ee = 0.f;
+  for (int c = tid; c < d; c += 256) {
+    const float v = qp[c];
+    const float r = (float)(__bf16)v - v;  // the coarse scan's rounding of this component
+    qs[c] = v;
+    ss += v * v;
+    ee += r * r;
+  }
+  // the smallest last key over the query's lane lists
+  float lm = INFINITY;
+  const float* lb = lane_bound + (int64_t)qi * n_lists;
+  for (int l = tid; l < n_lists; l += 256) lm = fminf(lm, lb[l]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    ss += __shfl_xor(ss, off, 64);
+    ee += __shfl_xor(ee, off, 64);
+    lm = fminf(lm, __shfl_xor(lm, off, 64));
+  }
+  if (lane == 0) {
+    part[wave] = ss;
+    epart[wave] = ee;
+    lmin[wave] = lm;
+  }
+  __syncthreads();
+  const float qn = (part[0] + part[1]) + (part[2] + part[3]);
+  const float* sk = sel_key + (int64_t)qi * CB_C;
+  const int64_t* si = sel_id + (int64_t)qi * CB_C;
+  // candidates round-robin over the 4 waves, 4 at a time with every load of the group in flight
+  // (d <= 512: 8 components per lane), 64 lanes over the row
+  constexpr int G = 4;
+  for (int c0 = wave * G; c0 < CB_C; c0 += 4 * G) {
+    float xv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t id = si[c0 + g];
+      const float* xp = X + (id >= 0 ? id - row_offset : 0) * (int64_t)d;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = lane + 64 * j;
+        xv[g][j] = e < d ? xp[e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int c = c0 + g;
+      const int64_t id = si[c];
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = lane + 64 * j;
+        dot += e < d ? qs[e] * xv[g][j] : 0.f;
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) dot += __shfl_xor(dot, off, 64);
+      if (lane == 0) {
+        keys[c] = id >= 0 ? sqrtf(fmaxf(qn + xnorm[id - row_offset] - 2.0f * dot, 0.0f))
+                          : INFINITY;
+        ids[c] = id >= 0 ? id : INT64_MAX;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int nvalid = 0;
+    for (int c = 0; c < CB_C; ++c) nvalid += si[c] >= 0 ? 1 : 0;
+    const float qa = sqrtf(qn), ea = sqrtf((epart[0] + epart[1]) + (epart[2] + epart[3]));
+    const float X = sqrtf(xmax[0]), R = sqrtf(xmax[1]);
+    const float E = 2.0f * (ea * X + qa * R + ea * R + 2.0f * d * 5.9604645e-8f * (qa + ea) *
+                                                      (X + R)) * 1.01f +
+                    4.0f * 5.9604645e-8f * (X * X + 2.0f * qa * X);
+    const float T = sk[k - 1] + 2.0f * E;
+    const float lists_last = fminf(fminf(lmin[0], lmin[1]), fminf(lmin[2], lmin[3]));
+    const bool enough = (nvalid < CB_C || sk[CB_C - 1] > T) && lists_last > T;
+    gate[qi] = enough ? 0 : 1;
+  }
+  // rank of each candidate among the CB_C by (exact key, id): the best k are written in order
+  if (tid < CB_C) {
+    const float a = keys[tid];
+    const int64_t ia = ids[tid];
+    int rank = 0;
+    for (int c = 0; c < CB_C; ++c) rank += key_less(keys[c], ids[c], a, ia) ? 1 : 0;
+    if (rank < k) {
+      out_dist[(int64_t)qi * k + rank] = ia == INT64_MAX ? NAN : a;
+      out_id[(int64_t)qi * k + rank] = ia == INT64_MAX ? -1 : ia;
+    }
+  }
+}
+
 // Final selection: per query, best k of n_cand (key, id) candidates.  Thread-local sorted lists
 // over a strided slice, then a pairwise tree merge through LDS.
 template <int K, int NT>
 __global__ __launch_bounds__(NT) void merge_kernel(const float* cand_key, const int64_t* cand_id,
                                                    int64_t n_cand, int k, int keys_are_values,
-                                                   int metric, float* out_val, int64_t* out_id) {
+                                                   int metric, float* out_val, int64_t* out_id,
+                                                   const int* gate) {
+  if (gate && gate[blockIdx.x] == 0) return;  // coarse path fallback: flagged queries only
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* Sk = lds;                                            // [NT][K]
   int64_t* Si = reinterpret_cast<int64_t*>(lds + NT * K);     // [NT][K]
@@ -548,26 +989,25 @@ int launch_scan(const float* X, const float* xnorm, int64_t n, int d, int64_t ro
 
 template <int K>
 int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
-                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s) {
+                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
+                 const int* gate) {
   constexpr int NT = K >= 64 ? 128 : 256;
   const size_t lds = (size_t)NT * K * (sizeof(float) + sizeof(int64_t));
   hipLaunchKernelGGL((merge_kernel<K, NT>), dim3(b), dim3(NT), lds, s, ck, ci, n_cand, k,
-                     keys_are_values, metric, od, oi);
+                     keys_are_values, metric, od, oi, gate);
   MPR_LAUNCHED();
   return MPR_OK;
 }
 
 int merge_dispatch(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
-                   int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s) {
+                   int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
+                   const int* gate = nullptr) {
+#define MPR_MG(K) \
+  case K: return launch_merge<K>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate);
   switch (list_cap(k)) {
-    case 1: return launch_merge<1>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s);
-    case 2: return launch_merge<2>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s);
-    case 4: return launch_merge<4>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s);
-    case 8: return launch_merge<8>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s);
-    case 16: return launch_merge<16>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s);
-    case 32: return launch_merge<32>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s);
-    case 64: return launch_merge<64>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s);
+    MPR_MG(1) MPR_MG(2) MPR_MG(4) MPR_MG(8) MPR_MG(16) MPR_MG(32) MPR_MG(64)
   }
+#undef MPR_MG
   set_error("top-k: k=%d unsupported (1..64)", k);
   return MPR_EUNSUP;
 }
@@ -588,24 +1028,106 @@ int scan_mm_rowblocks(int64_t n, int b) {
 
 template <int K>
 int launch_scan_mm(const float* X, int64_t n, int d, int64_t row_offset, int metric,
-                   const float* Q, float* qn, int b, float* ck, int64_t* ci, hipStream_t s) {
+                   const float* Q, float* qn, int b, float* ck, int64_t* ci, hipStream_t s,
+                   const int* gate) {
   const int nqt = (int)cdiv(b, SM_B), RB = scan_mm_rowblocks(n, b);
   hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d, qn);
   hipLaunchKernelGGL((scan_mm_kernel<K>), dim3((unsigned)(nqt * RB)), dim3(256), 0, s, X, n, d,
-                     row_offset, metric, Q, qn, b, nqt, RB, ck, ci);
+                     row_offset, metric, Q, qn, b, nqt, RB, ck, ci, gate);
   MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+// ---- coarse path launchers --------------------------------------------------------------------
+int coarse_rowblocks(int64_t n, int b) {
+  // ~2 blocks per CU, but every lane sees >= 8 row tiles (its bound gets tight: few fallbacks)
+  const int64_t ntile = (n + CB_RT - 1) / CB_RT;
+  const int nqt = (int)cdiv(b, CB_QT);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(1, 512 / nqt), ntile / 8));
+}
+
+bool scan_coarse_eligible(int64_t n, int d, int b, int k, int metric) {
+  static const bool off = [] {
+    const char* e = getenv("MPR_SCAN_COARSE");
+    return e && e[0] == '0';
+  }();
+  return !off && metric == 0 && b >= SM_MIN_B && k <= CB_C / 2 && (d == 256 || d == 512) &&
+         n >= CB_C;
+}
+
+int bf16_residuals(const float* X, int64_t n, int d, float* out, hipStream_t s) {
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(bf16_residual_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, s, X, n, d,
+                     out);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int index_to_bf16(const float* X, int64_t count, void* out, hipStream_t s) {
+  MPR_REQUIRE(count % 4 == 0, "to_bf16: count %lld", (long long)count);
+  if (count == 0) return MPR_OK;
+  const int64_t n4 = count / 4;
+  hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n4, 256), 8192)),
+                     dim3(256), 0, s, X, n4, reinterpret_cast<bf16x4*>(out));
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int max_of(const float* x, int64_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(max_kernel, dim3(1), dim3(1024), 0, s, x, n, out);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+namespace {
+struct CoarseWs {
+  float *ck, *sk, *qn, *lb;
+  int64_t *ci, *si;
+  __bf16* qb;
+  int* gate;
+  size_t bytes;
+};
+CoarseWs coarse_ws(void* base, int64_t n, int d, int b) {
+  const int RB = coarse_rowblocks(n, b);
+  const size_t nc = (size_t)b * RB * 2 * CB_L, ns = (size_t)b * CB_C;
+  char* p = reinterpret_cast<char*>(base);
+  CoarseWs w;
+  w.ci = reinterpret_cast<int64_t*>(p); p += nc * 8;
+  w.si = reinterpret_cast<int64_t*>(p); p += ns * 8;
+  w.ck = reinterpret_cast<float*>(p); p += nc * 4;
+  w.sk = reinterpret_cast<float*>(p); p += ns * 4;
+  w.lb = reinterpret_cast<float*>(p); p += ((size_t)b * RB * 2 * 4 + 15) / 16 * 16;
+  w.qn = reinterpret_cast<float*>(p); p += ((size_t)b * 4 + 15) / 16 * 16;
+  w.qb = reinterpret_cast<__bf16*>(p); p += ((size_t)b * d * 2 + 15) / 16 * 16;
+  w.gate = reinterpret_cast<int*>(p); p += ((size_t)b * 4 + 15) / 16 * 16;
+  w.bytes = (size_t)(p - reinterpret_cast<char*>(base));
+  return w;
+}
+}  // namespace
+
+int coarse_flag_count(const void* ws, int64_t n, int d, int b, int* count) {
+  CoarseWs w = coarse_ws(const_cast<void*>(ws), n, d, b);
+  std::vector<int> h(b);
+  MPR_HIP(hipMemcpy(h.data(), w.gate, (size_t)b * sizeof(int), hipMemcpyDeviceToHost));
+  int c = 0;
+  for (int v : h) c += v != 0;
+  *count = c;
   return MPR_OK;
 }
 
 size_t scan_topk_workspace(int64_t n, int b, int k) {
   const int K = list_cap(k);
   const int64_t per_q = std::max<int64_t>(scan_blocks(n), scan_mm_rowblocks(n, b));
-  return (size_t)b * per_q * K * (sizeof(float) + sizeof(int64_t)) + (size_t)b * 4 + 512;
+  const size_t exact = (size_t)b * per_q * K * (sizeof(float) + sizeof(int64_t)) + (size_t)b * 4 +
+                       512;
+  // the coarse path's buffers (d <= 512) ahead of the exact path's (its gated fallback)
+  return exact + coarse_ws(nullptr, n, 512, b).bytes + 256;
 }
 
 int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
               int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
-              float* out_dist, int64_t* out_ids, hipStream_t s) {
+              float* out_dist, int64_t* out_ids, hipStream_t s, const void* Xb,
+              const float* xmax) {
   MPR_REQUIRE(k >= 1 && k <= 64, "search: k=%d must be in [1, 64]", k);
   MPR_REQUIRE(k <= n, "search: k=%d exceeds index rows %lld", k, (long long)n);
   MPR_REQUIRE(d % 16 == 0 && d <= 8192, "search: d=%d must be a multiple of 16", d);
@@ -613,6 +1135,37 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
   if (b == 0) return MPR_OK;
   MPR_REQUIRE(ws_bytes >= scan_topk_workspace(n, b, k), "search: workspace too small");
   const int K = list_cap(k);
+  const int* gate = nullptr;
+  if (Xb && xmax && scan_coarse_eligible(n, d, b, k, metric)) {
+    // coarse bf16 scan -> top CB_C per query -> exact re-rank (+ the gated exact fallback below)
+    CoarseWs w = coarse_ws(ws, n, d, b);
+    ws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + (w.bytes + 255) / 256 * 256);
+    const int nqt = (int)cdiv(b, CB_QT), RB = coarse_rowblocks(n, b);
+    MPR_TRY(index_to_bf16(Q, (int64_t)b * d, w.qb, s));
+    const size_t qlds = (size_t)CB_QT * (d + 8) * 2;
+    if (d == 512)
+      hipLaunchKernelGGL(scan_bf_kernel<32>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s,
+                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b, nqt,
+                         RB, w.ck, w.ci, w.lb);
+    else
+      hipLaunchKernelGGL(scan_bf_kernel<16>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s,
+                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b, nqt,
+                         RB, w.ck, w.ci, w.lb);
+    MPR_LAUNCHED();
+    const int n_cand = RB * 2 * CB_L;
+    if (n_cand <= 256 * 16)
+      hipLaunchKernelGGL(coarse_select_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck, w.ci,
+                         n_cand, w.sk, w.si);
+    else
+      MPR_TRY(merge_dispatch(w.ck, w.ci, b, n_cand, CB_C, /*keys_are_values=*/0, /*metric=*/0,
+                             w.sk, w.si, s));
+    MPR_LAUNCHED();
+    hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)b), dim3(256), 0, s, X, xnorm, d,
+                       row_offset, Q, w.sk, w.si, w.lb, RB * 2, k, xmax, out_dist, out_ids,
+                       w.gate);
+    MPR_LAUNCHED();
+    gate = w.gate;
+  }
   if (use_scan_mm(n, d, b, k) && !getenv("MPR_SCAN_MM_OFF")) {
     const int RB = scan_mm_rowblocks(n, b);
     int64_t* ci = reinterpret_cast<int64_t*>(ws);
@@ -620,16 +1173,16 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     float* qn = ck + (size_t)b * RB * K;
     int rc = MPR_EUNSUP;
     switch (K) {
-      case 1: rc = launch_scan_mm<1>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
-      case 2: rc = launch_scan_mm<2>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
-      case 4: rc = launch_scan_mm<4>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
-      case 8: rc = launch_scan_mm<8>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
-      case 16: rc = launch_scan_mm<16>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s); break;
+#define MPR_SM(KK) \
+  case KK: rc = launch_scan_mm<KK>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s, gate); break;
+      MPR_SM(1) MPR_SM(2) MPR_SM(4) MPR_SM(8) MPR_SM(16)
+#undef MPR_SM
     }
     if (rc != MPR_OK) return rc;
     return merge_dispatch(ck, ci, b, (int64_t)RB * K, k, /*keys_are_values=*/0, metric, out_dist,
-                          out_ids, s);
+                          out_ids, s, gate);
   }
+  MPR_REQUIRE(gate == nullptr, "search: coarse path without its exact fallback");
   const int64_t nb = scan_blocks(n);
   int64_t* ci = reinterpret_cast<int64_t*>(ws);
   float* ck = reinterpret_cast<float*>(ci + (size_t)b * nb * K);

@@ -64,6 +64,14 @@ class DeviceIndex:
                   _lib.ptr(dist), _lib.stream_ptr(self.device))
         return dist, ids
 
+    def coarse_fallbacks(self) -> int:
+        """Queries of the last search (current stream) that the coarse large-batch path handed to
+        its exact fallback; -1 when that search did not take the coarse path.  Synchronises."""
+        c = _lib.c_int32()
+        _lib.call("mpr_index_coarse_fallbacks", self._h, _lib.stream_ptr(self.device),
+                  _lib.ctypes.byref(c))
+        return c.value
+
     def scores(self, q: torch.Tensor) -> torch.Tensor:
         """Full [b, n] distance (L2) or similarity (cosine) matrix (torch.cdist drop-in)."""
         q = self._q(q)

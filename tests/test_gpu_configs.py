@@ -192,3 +192,59 @@ def test_c5_scan_full_size_vs_fp64_oracle(device):
     assert torch.all(gd[:, -1] <= best_d[:, k - 1] + tol[:, k - 1])
     print(f"C5 scan: {n_exact}/{B} queries bit-exact in all {k} ids")
     assert n_exact >= B - 2
+
+
+@pytest.mark.parametrize("n,d,b,k", [(50000, 512, 128, 5), (20011, 256, 64, 8), (3000, 512, 300, 1)])
+def test_coarse_scan_matches_oracle(device, n, d, b, k):
+    """Large-batch L2 searches take the bf16 coarse scan + exact fp32 re-rank: ids equal the
+    exact ranking wherever fp64 separates neighbours by more than the fp32 bound."""
+    from multimodalpromptretrieval_amd.index import DeviceIndex
+    X = syn.index_rows(1000 + n, n, d)
+    q = syn.index_rows(2000 + n, b, d)
+    q[:4] = X[[5, 17, n - 1, n // 2]]                      # exact self matches included
+    dist, ids = DeviceIndex(X, device).search(q, k)
+    ids = ids.cpu()
+    best_d, best_i = _fp64_topk(X, q, k)
+    scale = (q.double() ** 2).sum(1, keepdim=True) + (X.double() ** 2).sum(1)[best_i]
+    gap = (best_d[:, 1:] - best_d[:, :-1]) > 4e-6 * scale[:, 1:]
+    for r in range(b):
+        for c in range(k):
+            if (c == 0 or bool(gap[r, c - 1])) and bool(gap[r, c]):
+                assert int(ids[r, c]) == int(best_i[r, c]), (r, c)
+    # squared distances within the cdist mm-path cancellation bound (exact self matches are
+    # rounding noise, ~sqrt(ulp(|x|^2)), in the reference too)
+    got2 = dist.cpu().double() ** 2
+    assert torch.all((got2 - best_d[:, :k]).abs() <= 2e-6 * scale[:, :k] + 1e-9)
+
+
+def test_coarse_scan_falls_back_on_a_dense_neighbourhood(device):
+    """Forty rows within the coarse error bound of query 0 overflow its coarse candidates: the
+    query's device flag runs the exact scan for it, and its ids are still the exact ones (lowest
+    id on the exact tie the duplicated row creates)."""
+    from multimodalpromptretrieval_amd.index import DeviceIndex
+    n, d, b, k = 20000, 512, 64, 5
+    X = syn.index_rows(31, n, d)
+    q = syn.index_rows(32, b, d)
+    base = q[0] + 0.05
+    noise = syn.index_rows(33, 40, d) * 1e-4
+    X[1000:1040] = base + noise
+    X[7000] = X[1003]                   # an exact duplicate: tie -> lowest id first
+    ix = DeviceIndex(X, device)
+    dist, ids = ix.search(q, k)
+    assert ix.coarse_fallbacks() >= 1
+    ids = ids.cpu()
+    best_d, best_i = _fp64_topk(X, q, k)
+    scale = (q.double() ** 2).sum(1, keepdim=True) + (X.double() ** 2).sum(1)[best_i]
+    gap = (best_d[:, 1:] - best_d[:, :-1]) > 4e-6 * scale[:, 1:]
+    for r in range(b):
+        for c in range(k):
+            if (c == 0 or bool(gap[r, c - 1])) and bool(gap[r, c]):
+                assert int(ids[r, c]) == int(best_i[r, c]), (r, c)
+    row0 = ids[0].tolist()
+    assert all(1000 <= j < 1040 or j == 7000 for j in row0)
+    if 7000 in row0:
+        assert 1003 in row0 and row0.index(1003) < row0.index(7000)
+    # a batch with no dense neighbourhood takes (almost) no fallback
+    ix2 = DeviceIndex(syn.index_rows(34, n, d), device)
+    ix2.search(q, k)
+    assert 0 <= ix2.coarse_fallbacks() <= 1

@@ -33,7 +33,7 @@ if [ -z "$SKIP_PROF" ]; then
   ok_or_stop $? rocprof 0
   python tools/prof_summary.py --replay "$OUT/prof/run_kernel_trace.csv" "$OUT/replay_window.json" >> "$OUT/prof.log" 2>&1
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_f32_kernel|probe_marker_kernel" \
+    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_x3_kernel|gemm_f32_kernel|probe_marker_kernel" \
       -d "$OUT/pmc_$c" -o run --output-format csv \
       -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1
     ok_or_stop $? pmc_$c 0

@@ -18,19 +18,19 @@ def _rows(path):
     return rows
 
 
-def replay_window(rows, name="gemm_f32_kernel", marker="probe_marker_kernel"):
+def replay_window(rows, names=("gemm_x3_kernel", "gemm_f32_kernel"), marker="probe_marker_kernel"):
     marks = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
     if len(marks) < 2:
         raise SystemExit("no replay markers in the trace (bench.py run without --no-probe?)")
     lo, hi = marks[-2], marks[-1]
-    return [r for r in rows[lo + 1:hi] if name in r["Kernel_Name"]]
+    return [r for r in rows[lo + 1:hi] if any(n in r["Kernel_Name"] for n in names)]
 
 
 def main():
     if sys.argv[1] == "--replay":
         rows = replay_window(_rows(sys.argv[2]))
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-        out = {"kernel": "gemm_f32_kernel", "window": "bench.py roofline replay (markers)",
+        out = {"kernel": "gemm_x3_kernel|gemm_f32_kernel", "window": "bench.py roofline replay (markers)",
                "launches": len(durs), "avg_launch_us": round(sum(durs) / len(durs) / 1e3, 3),
                "total_ms": round(sum(durs) / 1e6, 4)}
         print(json.dumps(out))
