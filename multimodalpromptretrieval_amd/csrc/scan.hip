@@ -433,7 +433,7 @@ constexpr int CB_RT = 128;             // index rows per block tile (4 x 32-row 
 constexpr int CB_QT = 128;             // queries per block: 4 waves x 32
 constexpr int CB_BK = 32;              // k per LDS stage (two 16-deep MFMA steps)
 constexpr int CB_LDK = CB_BK + 8;      // LDS row stride in bf16 (16-byte pad: conflict-free)
-constexpr int CB_D = 4;                // stages of global loads in flight (1 wave per SIMD)
+constexpr int CB_D = 8;                // stages of global loads in flight (1 wave per SIMD)
 constexpr int CB_L = 8;                // coarse candidates kept per lane list
 constexpr int CB_C = 64;               // coarse candidates re-ranked per query
 constexpr int CB_STAGE = CB_RT * CB_LDK;
@@ -486,6 +486,7 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
                                                          const float* __restrict__ xnorm,
                                                          int64_t n, int64_t row_offset,
                                                          const __bf16* __restrict__ Qb, int b,
+                                                         const float* __restrict__ qnorm,
                                                          int nqt, int RB, float* cand_key,
                                                          int64_t* cand_id, float* lane_bound) {
   constexpr int d = KS * 16, KQ = CB_BK / 8;  // 16-byte loads per staged row
@@ -512,6 +513,7 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
   constexpr int LDQ = d + 8;
   const int q = qt * CB_QT + wave * 32 + li;
   const bool qok = q < b;
+  const float qn_l = qok ? qnorm[q] : 0.f;
   for (int idx = tid; idx < CB_QT * (d / 8); idx += 256) {
     const int r = idx / (d / 8), c = (idx % (d / 8)) * 8, qq = qt * CB_QT + r;
     bf16x8 v = bf16x8{};
@@ -521,31 +523,31 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
   // B[k = 16 s + 8 lh + j][col li] = Q~[wave's query li][16 s + 8 lh + j]
   const __bf16* qrow = qs + (wave * 32 + li) * LDQ + 8 * lh;
 
+  // rows past n (and stages past the block's last tile) load row n-1: their keys are masked in the
+  // epilogue, and no select on the loaded data lets the compiler wait for a load early
   bf16x8 rx[CB_D][2];
-  bool okx[CB_D][2];
-  float rn[CB_D];
-  auto gload = [&](int j, int step) {
-    const int tt = step / SPT, ks = step - tt * SPT;
+  float rn0 = 0.f;  // a tile's first stage always lands in slot 0 (SPT % CB_D == 0)
+  // stage ks of the block's row tile tt (ks is a constant once the stage loop is unrolled)
+  auto gload = [&](int j, int tt, int ks) {
     const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB_RT;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + i * 256, r = idx / KQ, c = ks * CB_BK + (idx % KQ) * 8;
       const int64_t row = row0 + r;
-      okx[j][i] = row < n && tt < ntb;
       rx[j][i] = *reinterpret_cast<const bf16x8*>(Xb + (row < n ? row : n - 1) * (int64_t)d + c);
     }
-    // the tile's row norms ride with its first stage
-    const int64_t nrow = row0 + (tid & (CB_RT - 1));
-    rn[j] = xnorm[nrow < n ? nrow : n - 1];
+    if (ks == 0) {  // the tile's row norms ride with its first stage
+      const int64_t nrow = row0 + (tid & (CB_RT - 1));
+      rn0 = nrow < n ? xnorm[nrow] : INFINITY;  // rows past n: infinite keys
+    }
   };
-  auto swrite = [&](int st, int j, int step) {
+  auto swrite = [&](int st, int j, int tt, int ks) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + i * 256, r = idx / KQ, c = (idx % KQ) * 8;
-      *reinterpret_cast<bf16x8*>(&xs[st][r * CB_LDK + c]) = okx[j][i] ? rx[j][i] : bf16x8{};
+      *reinterpret_cast<bf16x8*>(&xs[st][r * CB_LDK + c]) = rx[j][i];
     }
-    const int tt = step / SPT;
-    if (step - tt * SPT == 0 && tid < CB_RT) xn_s[tt & 1][tid] = rn[j];
+    if (ks == 0 && tid < CB_RT) xn_s[tt & 1][tid] = rn0;
   };
   bf16x8 fa[4][2], na[4][2], fb[2], nb[2];
   // fragments of stage `ks` of a row tile: the 4 row tiles' A from the staged rows, the wave's
@@ -579,12 +581,12 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
   }
   float drop = INFINITY;
 
-  gload(0, 0);
-  swrite(0, 0, 0);
-  gload(0, 1);
-  swrite(1, 0, 1);
+  gload(0, 0, 0);
+  swrite(0, 0, 0, 0);
+  gload(0, 0, 1);
+  swrite(1, 0, 0, 1);
 #pragma unroll
-  for (int j = 0; j < CB_D; ++j) gload(j, 2 + j);
+  for (int j = 0; j < CB_D; ++j) gload(j, (2 + j) / SPT, (2 + j) % SPT);
   __syncthreads();
   sread(0, 0, fa, fb);
   __syncthreads();
@@ -594,7 +596,6 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
   for (int tt = 0; tt < ntb; ++tt) {
 #pragma clang loop unroll(full)
     for (int ks = 0; ks < SPT; ++ks) {
-      const int step = tt * SPT + ks;
       const int st = ks & 1, j = ks % CB_D;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
@@ -602,8 +603,8 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
         for (int mi = 0; mi < 4; ++mi)
           acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][u], fb[u], acc[mi], 0, 0, 0);
       sread(st ^ 1, (ks + 1) % SPT, na, nb);
-      swrite(st, j, step + 2);
-      gload(j, step + 2 + CB_D);
+      swrite(st, j, tt + (ks + 2) / SPT, (ks + 2) % SPT);
+      gload(j, tt + (ks + 2 + CB_D) / SPT, (ks + 2 + CB_D) % SPT);
       __syncthreads();
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
@@ -613,27 +614,24 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
       fb[0] = nb[0];
       fb[1] = nb[1];
     }
-    {  // coarse keys of this row tile: best two -> the lane's list, third best -> drop
-      const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB_RT;
-      float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
-      int i1 = INT_MAX, i2 = INT_MAX;
+    {  // coarse values of this row tile: v = max(|x|^2 - 2 q~.x~ + |q|^2, 0) with its 7 low
+       // mantissa bits replaced by the tile row (a nonnegative float orders as its bits; the
+       // quantisation, < 2^-16 relative, is in the re-rank's bound), so the best three are kept by
+       // integer min/median steps with no compare masks; best two -> the lane's list, third -> drop
+      uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {  // rows in increasing order: ties keep the lower id
+        for (int r = 0; r < 16; ++r) {
           const int rr = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const int row = (int)(row0 + rr);
-          float key = xn_s[tt & 1][rr] - 2.0f * acc[mi][r];
+          const float key = fmaxf(fmaf(-2.0f, acc[mi][r], xn_s[tt & 1][rr]) + qn_l, 0.0f);
           acc[mi][r] = 0.f;
-          key = row0 + rr < n ? key : INFINITY;
-          const bool l1 = key < b1, l2 = key < b2;
-          b3 = l2 ? b2 : fminf(b3, key);
-          b2 = l1 ? b1 : (l2 ? key : b2);
-          i2 = l1 ? i1 : (l2 ? row : i2);
-          b1 = l1 ? key : b1;
-          i1 = l1 ? row : i1;
+          const uint32_t v = (__float_as_uint(key) & ~127u) | (uint32_t)rr;
+          v3 = min(v3, max(v2, v));
+          v2 = min(v2, max(v1, v));
+          v1 = min(v1, v);
         }
-      drop = fminf(drop, b3);
+      drop = fminf(drop, __uint_as_float(v3 & ~127u));
       auto insert = [&](float ck, int ci) {
 #pragma unroll
         for (int t = 0; t < CB_L; ++t) {
@@ -646,8 +644,10 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
           ci = ti;
         }
       };
-      if (b1 < bk[CB_L - 1]) insert(b1, i1);
-      if (b2 < bk[CB_L - 1]) insert(b2, i2);
+      const int row0 = (rb + tt * RB) * CB_RT;  // n < 2^31 (checked by the launcher)
+      const float k1 = __uint_as_float(v1 & ~127u), k2 = __uint_as_float(v2 & ~127u);
+      if (k1 < bk[CB_L - 1]) insert(k1, row0 + (int)(v1 & 127u));
+      if (k2 < bk[CB_L - 1]) insert(k2, row0 + (int)(v2 & 127u));
     }
   }
   if (!qok) return;
@@ -823,8 +823,9 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
     const float X = sqrtf(xmax[0]), R = sqrtf(xmax[1]);
     const float E = 2.0f * (ea * X + qa * R + ea * R + 2.0f * d * 5.9604645e-8f * (qa + ea) *
                                                       (X + R)) * 1.01f +
-                    4.0f * 5.9604645e-8f * (X * X + 2.0f * qa * X);
-    const float T = sk[k - 1] + 2.0f * E;
+                    4.0f * 5.9604645e-8f * (X * X + 2.0f * qa * X + qa * qa);
+    // coarse values are quantised down by < 2^-16 relative (scan_bf_kernel's low-bit row tag)
+    const float T = sk[k - 1] * (1.0f + 3.0517578e-5f) + 2.0f * E;
     const float lists_last = fminf(fminf(lmin[0], lmin[1]), fminf(lmin[2], lmin[3]));
     const bool enough = (nvalid < CB_C || sk[CB_C - 1] > T) && lists_last > T;
     gate[qi] = enough ? 0 : 1;
@@ -1141,16 +1142,19 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     CoarseWs w = coarse_ws(ws, n, d, b);
     ws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + (w.bytes + 255) / 256 * 256);
     const int nqt = (int)cdiv(b, CB_QT), RB = coarse_rowblocks(n, b);
+    MPR_REQUIRE(n < (int64_t)1 << 31, "search: coarse scan rows %lld >= 2^31", (long long)n);
     MPR_TRY(index_to_bf16(Q, (int64_t)b * d, w.qb, s));
+    hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d, w.qn);
+    MPR_LAUNCHED();
     const size_t qlds = (size_t)CB_QT * (d + 8) * 2;
     if (d == 512)
       hipLaunchKernelGGL(scan_bf_kernel<32>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s,
-                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b, nqt,
-                         RB, w.ck, w.ci, w.lb);
+                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b,
+                         w.qn, nqt, RB, w.ck, w.ci, w.lb);
     else
       hipLaunchKernelGGL(scan_bf_kernel<16>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s,
-                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b, nqt,
-                         RB, w.ck, w.ci, w.lb);
+                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b,
+                         w.qn, nqt, RB, w.ck, w.ci, w.lb);
     MPR_LAUNCHED();
     const int n_cand = RB * 2 * CB_L;
     if (n_cand <= 256 * 16)
