@@ -184,11 +184,31 @@ def index_build(cfg, weights, device, n_batches: int = 48):
         finally:
             shutil.rmtree(d, ignore_errors=True)
         out[phase] = el
+    # the towers' GEMM flops of one build (algorithmic, from the launch probe) against the build's
+    # wall time and the fp32 MFMA peak: the roofline the index build sits under
+    d = tempfile.mkdtemp(prefix="mpr_ib_")
+    try:
+        _lib.probe_clear()
+        _lib.probe_enable(1)
+        r.create_retrieval_dataset(loader, is_training_phase=False, retrieval_k=cfg["k"],
+                                   cache_dir=d)
+        torch.cuda.synchronize()
+        _lib.probe_enable(0)
+        gms, gl, gflops, _ = _lib.probe_read()
+        _lib.probe_clear()
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
     rows = n_batches * cfg["B"]
     el = out["timed"]
+    tf = gflops / el / 1e12
     return {"workload": f"create_retrieval_dataset over {n_batches} batches x {cfg['B']} QA "
                         f"pairs (ViT-B/32 CLS + CLIP text per row, cache write, index upload)",
-            "rows": rows, "ms": round(el * 1e3, 2), "rows_per_s": round(rows / el, 1)}
+            "rows": rows, "ms": round(el * 1e3, 2), "rows_per_s": round(rows / el, 1),
+            "roofline": {"bound": "mfma", "gemm_gflop_per_row": round(gflops / rows / 1e9, 3),
+                         "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "gemm_kernel_ms": round(gms, 2), "gemm_launches": gl,
+                         "note": "GEMM algorithmic flops of the build / its wall time"}}
 
 
 def host_cpu():

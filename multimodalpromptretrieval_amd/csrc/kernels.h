@@ -159,6 +159,12 @@ int scale_inplace(float* p, int64_t n, float scale, hipStream_t s);
 // Xb / xmax (optional): the index as bf16 rows and {max_i |x_i|^2, max_i |bf16(x_i) - x_i|^2} —
 // enable the coarse bf16 scan +
 // exact re-rank for large batches (scan_coarse_eligible).
+// select.hip: per query the best k of n_cand (key, id) candidates ((key, id) ascending; ids < 0
+// are empty slots); keys_are_values && metric 1: the keys are similarities (negated inside);
+// gate (optional, per query): 0 skips the query.
+int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
+                int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
+                const int* gate);
 int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
               int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
               float* out_dist, int64_t* out_ids, hipStream_t s, const void* Xb = nullptr,

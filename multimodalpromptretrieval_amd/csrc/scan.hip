@@ -196,6 +196,131 @@ __global__ __launch_bounds__(256) void scan_kernel(const float* __restrict__ X,
   }
 }
 
+__device__ __forceinline__ uint32_t order_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+constexpr int SS_TT = 1;  // 16-row tiles per small-scan block (2 and 4 measured slower at C2)
+// ---- small-index scan (the C2 regime: n of a few thousand rows, <= 16 queries per group) -------
+// scan_kernel gives each wave whole 16-row tiles, so at n = 6,500 it launches ~100 blocks and each
+// wave walks its 4 KiB rows in d/128 dependent load rounds.  Here a block is ONE 16-row tile x 16
+// queries and its 4 waves split d: every load of the block (rows and query fragments, both read
+// straight from global memory, the queries L2-resident) is in flight at once, the 4 partial dot
+// tiles and query norms are summed through LDS, and the block emits its best min(K, 16) rows per
+// query (K-list padded with empty slots).
+template <int K, int CH, int TT>  // CH = d / 64 chunks of 16 columns per wave; TT tiles a block
+__global__ __launch_bounds__(256) void scan_small_kernel(const float* __restrict__ X,
+                                                         const float* __restrict__ xnorm,
+                                                         int64_t n, int64_t row_offset,
+                                                         int metric, const float* __restrict__ Q,
+                                                         int b, float* cand_key,
+                                                         int64_t* cand_id) {
+  constexpr int d = 64 * CH, R = 16 * TT;  // R = rows per block
+  __shared__ f32x4 red[TT][4][64];
+  __shared__ float qss[4][QG];
+  __shared__ float lk[QG][R];
+  __shared__ int li[QG][R];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, h = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int qbase = blockIdx.y * QG;
+  const int c0 = wave * CH;
+  const bool qok_i = qbase + i < b;
+  const float* qp = Q + (int64_t)(qok_i ? qbase + i : 0) * d + c0 * 16 + h * 4;
+  f32x4 xv[TT][CH], qv[CH];
+#pragma unroll
+  for (int u = 0; u < CH; ++u) qv[u] = *reinterpret_cast<const f32x4*>(qp + u * 16);
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    const int64_t row = row0 + t * 16 + i;
+    const float* xp = X + (row < n ? row : n - 1) * (int64_t)d + c0 * 16 + h * 4;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) xv[t][u] = *reinterpret_cast<const f32x4*>(xp + u * 16);
+  }
+  // the epilogue's row norms (wave 0: rows t*16 + h*4 .. +3), fetched with the rest
+  float xnr[TT][4];
+#pragma unroll
+  for (int t = 0; t < TT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row2 = row0 + t * 16 + h * 4 + r;
+      xnr[t][r] = xnorm[row2 < n ? row2 : n - 1];
+    }
+  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first wait
+  float ss = 0.f;
+  const float qscale = qok_i ? 1.f : 0.f;  // rows past b: zero query (no select on the loads)
+#pragma unroll
+  for (int u = 0; u < CH; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      qv[u][e] *= qscale;
+      ss += qv[u][e] * qv[u][e];
+    }
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    // four independent accumulation chains (one per k of the 4-deep MFMA step)
+    f32x4 acc4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc4[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc4[e] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[t][u][e], qv[u][e], acc4[e], 0, 0, 0);
+    red[t][wave][lane] = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+  }
+  ss += __shfl_xor(ss, 16, 64);
+  ss += __shfl_xor(ss, 32, 64);
+  if (h == 0) qss[wave][i] = ss;
+  __syncthreads();
+  if (wave == 0) {
+    const int j = lane & 15;  // this lane's query (D column); rows h*4 .. h*4+3 of each tile
+    const float qn = ((qss[0][j] + qss[1][j]) + qss[2][j]) + qss[3][j];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      const f32x4 a = ((red[t][0][lane] + red[t][1][lane]) + red[t][2][lane]) + red[t][3][lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row2 = row0 + t * 16 + h * 4 + r;
+        const bool ok = row2 < n && qbase + j < b;
+        lk[j][t * 16 + h * 4 + r] = ok ? score_key(metric, a[r], qn, xnr[t][r]) : INFINITY;
+        li[j][t * 16 + h * 4 + r] = ok ? (int)row2 : INT_MAX;
+      }
+    }
+  }
+  __syncthreads();
+  // thread (query q, slots t): rank of row t among the block's R by (key, row, slot); best
+  // min(K, R)
+  const int q = tid >> 4;
+  if (qbase + q < b) {
+    float* ok = cand_key + ((int64_t)(qbase + q) * gridDim.x + blockIdx.x) * K;
+    int64_t* oi = cand_id + ((int64_t)(qbase + q) * gridDim.x + blockIdx.x) * K;
+    for (int t = tid & 15; t < R; t += 16) {
+      const float kk = lk[q][t];
+      const int ii = li[q][t];
+      // (key, row, slot) order as one 64-bit word per slot (empty slots rank by slot, so every
+      // rank is written); branch-free count
+      const uint64_t ct = ((uint64_t)order_bits(kk) << 32) | (uint32_t)ii;
+      int rank = 0;
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const uint64_t cu = ((uint64_t)order_bits(lk[q][u]) << 32) | (uint32_t)li[q][u];
+        rank += (int)((cu < ct) | ((cu == ct) & (u < t)));
+      }
+      if (rank < K) {
+        ok[rank] = kk;
+        oi[rank] = ii == INT_MAX ? -1 : (int64_t)ii + row_offset;
+      }
+    }
+    for (int e = R + (tid & 15); e < K; e += 16) {  // K > R: the list's empty tail
+      ok[e] = INFINITY;
+      oi[e] = -1;
+    }
+  }
+}
+
 // ---- large-batch scan (b >= 64): the similarity GEMM with a top-k epilogue ------------------
 // At b = 256 the scan is MFMA-bound in fp32 (2 FLOP per index byte per query),
 // and the 16-query kernel above would stream the index once per query group.  Here a block owns
@@ -664,10 +789,6 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
 // Coarse selection: block per query, the CB_C smallest of its n_cand lane-list keys (ids
 // alongside), sorted by (key, id).  The CB_C-th key is found by a bisection over the keys' order
 // bits (counts by a block reduction), then the <= CB_C keys at or below it are ranked.
-__device__ __forceinline__ uint32_t order_bits(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
 
 template <int PER>
 __global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restrict__ cand_key,
@@ -843,87 +964,6 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
   }
 }
 
-// Final selection: per query, best k of n_cand (key, id) candidates.  Thread-local sorted lists
-// over a strided slice, then a pairwise tree merge through LDS.
-template <int K, int NT>
-__global__ __launch_bounds__(NT) void merge_kernel(const float* cand_key, const int64_t* cand_id,
-                                                   int64_t n_cand, int k, int keys_are_values,
-                                                   int metric, float* out_val, int64_t* out_id,
-                                                   const int* gate) {
-  if (gate && gate[blockIdx.x] == 0) return;  // coarse path fallback: flagged queries only
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* Sk = lds;                                            // [NT][K]
-  int64_t* Si = reinterpret_cast<int64_t*>(lds + NT * K);     // [NT][K]
-  const int q = blockIdx.x, tid = threadIdx.x;
-  const float* ck = cand_key + (int64_t)q * n_cand;
-  const int64_t* ci = cand_id + (int64_t)q * n_cand;
-  // keys_are_values && cosine: candidate values are similarities (descending) -> negate.
-  const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
-  float bk[K];
-  int64_t bi[K];
-#pragma unroll
-  for (int t = 0; t < K; ++t) {
-    bk[t] = INFINITY;
-    bi[t] = INT64_MAX;
-  }
-  for (int64_t c = tid; c < n_cand; c += NT) {
-    const int64_t id = ci[c];
-    if (id < 0) continue;
-    float kk = sign * ck[c];
-    int64_t ii = id;
-    if (!key_less(kk, ii, bk[K - 1], bi[K - 1])) continue;
-#pragma unroll
-    for (int t = 0; t < K; ++t) {
-      const bool sw = key_less(kk, ii, bk[t], bi[t]);
-      const float tk = sw ? bk[t] : kk;
-      const int64_t ti = sw ? bi[t] : ii;
-      bk[t] = sw ? kk : bk[t];
-      bi[t] = sw ? ii : bi[t];
-      kk = tk;
-      ii = ti;
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < K; ++t) {
-    Sk[tid * K + t] = bk[t];
-    Si[tid * K + t] = bi[t];
-  }
-  __syncthreads();
-  for (int half = NT / 2; half >= 1; half >>= 1) {
-    if (tid < half) {
-      const int a = tid, bb = tid + half;
-      int pa = 0, pb = 0;
-      float mk[K];
-      int64_t mi[K];
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const float ka = Sk[a * K + min(pa, K - 1)], kb = Sk[bb * K + min(pb, K - 1)];
-        const int64_t ia = pa < K ? Si[a * K + pa] : INT64_MAX;
-        const int64_t ib = pb < K ? Si[bb * K + pb] : INT64_MAX;
-        const float kav = pa < K ? ka : INFINITY, kbv = pb < K ? kb : INFINITY;
-        const bool takea = key_less(kav, ia, kbv, ib);
-        mk[t] = takea ? kav : kbv;
-        mi[t] = takea ? ia : ib;
-        pa += takea ? 1 : 0;
-        pb += takea ? 0 : 1;
-      }
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        Sk[a * K + t] = mk[t];
-        Si[a * K + t] = mi[t];
-      }
-    }
-    __syncthreads();
-  }
-  if (tid < k) {
-    const float kk = Sk[tid];
-    const int64_t ii = Si[tid];
-    const float val = (metric == 1) ? -kk : kk;
-    out_val[(int64_t)q * k + tid] = ii == INT64_MAX ? NAN : val;
-    out_id[(int64_t)q * k + tid] = ii == INT64_MAX ? -1 : ii;
-  }
-}
-
 __global__ void sqnorm_kernel(const float* X, int64_t n, int d, float* out) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -988,29 +1028,11 @@ int launch_scan(const float* X, const float* xnorm, int64_t n, int d, int64_t ro
   return MPR_OK;
 }
 
-template <int K>
-int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
-                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
-                 const int* gate) {
-  constexpr int NT = K >= 64 ? 128 : 256;
-  const size_t lds = (size_t)NT * K * (sizeof(float) + sizeof(int64_t));
-  hipLaunchKernelGGL((merge_kernel<K, NT>), dim3(b), dim3(NT), lds, s, ck, ci, n_cand, k,
-                     keys_are_values, metric, od, oi, gate);
-  MPR_LAUNCHED();
-  return MPR_OK;
-}
 
 int merge_dispatch(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                    int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
                    const int* gate = nullptr) {
-#define MPR_MG(K) \
-  case K: return launch_merge<K>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate);
-  switch (list_cap(k)) {
-    MPR_MG(1) MPR_MG(2) MPR_MG(4) MPR_MG(8) MPR_MG(16) MPR_MG(32) MPR_MG(64)
-  }
-#undef MPR_MG
-  set_error("top-k: k=%d unsupported (1..64)", k);
-  return MPR_EUNSUP;
+  return merge_lists(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate);
 }
 
 }  // namespace
@@ -1116,11 +1138,30 @@ int coarse_flag_count(const void* ws, int64_t n, int d, int b, int* count) {
   return MPR_OK;
 }
 
+// Slices per query of the two-level merge: enough blocks to spread over the chip (b * P <= 256)
+// with >= 512 candidates per slice; 1 = a single merge.
+int merge_split(int b, int64_t n_cand) {
+  int P = 1;
+  while (b * P * 2 <= 256 && n_cand % (P * 2) == 0 && n_cand / (P * 2) >= 512) P *= 2;
+  return P;
+}
+
+// scan_small_kernel when the tile-per-wave scan would launch fewer than ~2 blocks per CU
+bool small_regime(int64_t n, int b) {
+  return cdiv(n, 16) <= 16384 && scan_blocks(n) * cdiv(b, QG) < 512;
+}
+bool use_scan_small(int64_t n, int d, int b) {
+  return (d == 256 || d == 512 || d == 1024) && small_regime(n, b) &&
+         !getenv("MPR_SCAN_SMALL_OFF");
+}
+
 size_t scan_topk_workspace(int64_t n, int b, int k) {
   const int K = list_cap(k);
-  const int64_t per_q = std::max<int64_t>(scan_blocks(n), scan_mm_rowblocks(n, b));
+  const int64_t per_q = std::max<int64_t>(
+      std::max<int64_t>(scan_blocks(n), small_regime(n, b) ? cdiv(n, 16) : 0),
+      scan_mm_rowblocks(n, b));
   const size_t exact = (size_t)b * per_q * K * (sizeof(float) + sizeof(int64_t)) + (size_t)b * 4 +
-                       512;
+                       (size_t)256 * K * (sizeof(float) + sizeof(int64_t)) + 512;
   // the coarse path's buffers (d <= 512) ahead of the exact path's (its gated fallback)
   return exact + coarse_ws(nullptr, n, 512, b).bytes + 256;
 }
@@ -1187,11 +1228,32 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
                           out_ids, s, gate);
   }
   MPR_REQUIRE(gate == nullptr, "search: coarse path without its exact fallback");
-  const int64_t nb = scan_blocks(n);
+  const bool small = use_scan_small(n, d, b);
+  const int64_t nb = small ? cdiv(n, 16 * SS_TT) : scan_blocks(n);
   int64_t* ci = reinterpret_cast<int64_t*>(ws);
   float* ck = reinterpret_cast<float*>(ci + (size_t)b * nb * K);
   int rc = MPR_EUNSUP;
-  switch (K) {
+  if (small) {
+    const dim3 grid((unsigned)nb, (unsigned)cdiv(b, QG));
+    switch (K) {
+#define MPR_SS(KK)                                                                        \
+  case KK:                                                                                \
+    if (d == 256)                                                                         \
+      hipLaunchKernelGGL((scan_small_kernel<KK, 4, SS_TT>), grid, dim3(256), 0, s, X, xnorm, n,  \
+                         row_offset, metric, Q, b, ck, ci);                               \
+    else if (d == 512)                                                                    \
+      hipLaunchKernelGGL((scan_small_kernel<KK, 8, SS_TT>), grid, dim3(256), 0, s, X, xnorm, n,  \
+                         row_offset, metric, Q, b, ck, ci);                               \
+    else                                                                                  \
+      hipLaunchKernelGGL((scan_small_kernel<KK, 16, SS_TT>), grid, dim3(256), 0, s, X, xnorm, n, \
+                         row_offset, metric, Q, b, ck, ci);                               \
+    rc = MPR_OK;                                                                          \
+    break;
+      MPR_SS(1) MPR_SS(2) MPR_SS(4) MPR_SS(8) MPR_SS(16) MPR_SS(32) MPR_SS(64)
+#undef MPR_SS
+    }
+    MPR_LAUNCHED();
+  } else switch (K) {
     case 1: rc = launch_scan<1>(X, xnorm, n, d, row_offset, metric, Q, b, ck, ci, s); break;
     case 2: rc = launch_scan<2>(X, xnorm, n, d, row_offset, metric, Q, b, ck, ci, s); break;
     case 4: rc = launch_scan<4>(X, xnorm, n, d, row_offset, metric, Q, b, ck, ci, s); break;
@@ -1201,7 +1263,19 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     case 64: rc = launch_scan<64>(X, xnorm, n, d, row_offset, metric, Q, b, ck, ci, s); break;
   }
   if (rc != MPR_OK) return rc;
-  return merge_dispatch(ck, ci, b, nb * K, k, /*keys_are_values=*/0, metric, out_dist, out_ids, s);
+  const int64_t n_cand = nb * K;
+  const int P = merge_split(b, n_cand);
+  if (P > 1) {
+    // few queries, many candidates: P blocks per query each keep the best K of one slice, then one
+    // block per query merges the P lists (the (key, id) order makes the result the same list)
+    int64_t* ci2 = reinterpret_cast<int64_t*>(ck + (size_t)b * n_cand);
+    float* ck2 = reinterpret_cast<float*>(ci2 + (size_t)b * P * K);
+    MPR_TRY(merge_dispatch(ck, ci, b * P, n_cand / P, K, /*keys_are_values=*/0, metric, ck2, ci2,
+                           s));
+    return merge_dispatch(ck2, ci2, b, (int64_t)P * K, k, /*keys_are_values=*/1, metric,
+                          out_dist, out_ids, s);
+  }
+  return merge_dispatch(ck, ci, b, n_cand, k, /*keys_are_values=*/0, metric, out_dist, out_ids, s);
 }
 
 int scan_scores(const float* X, const float* xnorm, int64_t n, int d, int metric, const float* Q,

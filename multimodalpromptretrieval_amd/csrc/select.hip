@@ -1,0 +1,131 @@
+// select.hip — the final top-k of a scan: per query, the best k of n_cand (key, id) candidate
+// lists (scan_kernel / scan_small_kernel / scan_mm_kernel block lists, the coarse scan's lane
+// lists, a sharded search's per-shard lists).  Its own translation unit: inside scan.hip the
+// k-round kernel below did not finish compiling under hipcc 7.2; alone it compiles in seconds for
+// every list length but 16, which takes the 32 kernel).
+#include <climits>
+#include <cmath>
+
+#include "kernels.h"
+
+namespace mpr {
+namespace {
+
+__device__ __forceinline__ bool key_less(float ka, int64_t ia, float kb, int64_t ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+__device__ __forceinline__ uint32_t order_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Final selection: per query, best k of n_cand (key, id) candidates.  Thread-local sorted lists
+// over a strided slice, then k rounds of a block-wide minimum over the lists' heads, each head one
+// 64-bit word (key order bits, row id): the winner's list shifts.  (Replaces a pairwise tree
+// merge through LDS: log2(NT) levels of K dependent steps.)  Row ids are < 2^31 (every scan
+// keeps them in 32 bits); -0.0 keys count as +0.0, as the float compare of key_less does.
+__device__ __forceinline__ uint64_t head_word(float key, int64_t id) {
+  return id < 0 ? ~0ull : ((uint64_t)order_bits(key + 0.0f) << 32) | (uint32_t)id;
+}
+__device__ __forceinline__ float word_key(uint64_t w) {
+  const uint32_t o = (uint32_t)(w >> 32);
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
+template <int K, int NT>
+__global__ __launch_bounds__(NT) void merge_kernel(const float* cand_key, const int64_t* cand_id,
+                                                   int64_t n_cand, int k, int keys_are_values,
+                                                   int metric, float* out_val, int64_t* out_id,
+                                                   const int* gate) {
+  if (gate && gate[blockIdx.x] == 0) return;  // coarse path fallback: flagged queries only
+  constexpr int NW = NT / 64;
+  __shared__ uint64_t wmin[2][NW];
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* ck = cand_key + (int64_t)q * n_cand;
+  const int64_t* ci = cand_id + (int64_t)q * n_cand;
+  // keys_are_values && cosine: candidate values are similarities (descending) -> negate.
+  const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
+  float bk[K];
+  int64_t bi[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    bk[t] = INFINITY;
+    bi[t] = INT64_MAX;
+  }
+  for (int64_t c = tid; c < n_cand; c += NT) {
+    const int64_t id = ci[c];
+    if (id < 0) continue;
+    float kk = sign * ck[c];
+    int64_t ii = id;
+    if (!key_less(kk, ii, bk[K - 1], bi[K - 1])) continue;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const bool sw = key_less(kk, ii, bk[t], bi[t]);
+      const float tk = sw ? bk[t] : kk;
+      const int64_t ti = sw ? bi[t] : ii;
+      bk[t] = sw ? kk : bk[t];
+      bi[t] = sw ? ii : bi[t];
+      kk = tk;
+      ii = ti;
+    }
+  }
+  uint64_t w[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) w[t] = head_word(bk[t], bi[t] == INT64_MAX ? -1 : bi[t]);
+  for (int r = 0; r < k; ++r) {
+    uint64_t m = w[0];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint64_t o = __shfl_xor(m, off, 64);
+      m = o < m ? o : m;
+    }
+    if (lane == 0) wmin[r & 1][wave] = m;
+    __syncthreads();
+    uint64_t g = wmin[r & 1][0];
+#pragma unroll
+    for (int v = 1; v < NW; ++v) g = wmin[r & 1][v] < g ? wmin[r & 1][v] : g;
+    if (g != ~0ull && w[0] == g) {  // (key, id) words are unique: one winner
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) w[t] = w[t + 1];
+      w[K - 1] = ~0ull;
+    }
+    if (tid == 0) {
+      const bool none = g == ~0ull;
+      const float kk = word_key(g);
+      out_val[(int64_t)q * k + r] = none ? NAN : (metric == 1 ? -kk : kk);
+      out_id[(int64_t)q * k + r] = none ? -1 : (int64_t)(uint32_t)g;
+    }
+  }
+}
+
+
+template <int K>
+int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
+                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
+                 const int* gate) {
+  constexpr int NT = K >= 32 ? 128 : 256;
+  hipLaunchKernelGGL((merge_kernel<K, NT>), dim3(b), dim3(NT), 0, s, ck, ci, n_cand, k,
+                     keys_are_values, metric, od, oi, gate);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+}  // namespace
+
+int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
+                int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
+                const int* gate) {
+  int c = 1;
+  while (c < k) c <<= 1;
+  if (c == 16) c = 32;  // merge_kernel<16, *> hangs hipcc 7.2's backend (every other K compiles)
+#define MPR_MG(K) \
+  case K: return launch_merge<K>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate);
+  switch (c) {
+    MPR_MG(1) MPR_MG(2) MPR_MG(4) MPR_MG(8) MPR_MG(32) MPR_MG(64)
+  }
+#undef MPR_MG
+  set_error("top-k: k=%d unsupported (1..64)", k);
+  return MPR_EUNSUP;
+}
+
+}  // namespace mpr

@@ -251,6 +251,27 @@ class VQARetrieval:
         cur.wait_stream(s_img)
         return q
 
+    def _encode_two(self, b0, b1) -> torch.Tensor:
+        """encode_queries of two equal-sized batches in one tower pass: rows [b0 ; b1]."""
+        cur = torch.cuda.current_stream(self.device)
+        s_img = self._streams()
+        img = torch.cat([b["image"].to(self.device, torch.float32, non_blocking=True)
+                         for b in (b0, b1)])
+        toks = [self.clip_tokenize(b["question"]) for b in (b0, b1)]
+        n = b0["image"].shape[0]
+        q = torch.empty((2 * n, self.embed_dim), device=self.device, dtype=torch.float32)
+        di = self.image_encoder.out_dim
+        s_img.wait_stream(cur)
+        q.record_stream(s_img)
+        img.record_stream(s_img)
+        with torch.cuda.stream(s_img):
+            encode_towers_multi(self.image_encoder, img, CLS, out_a=q,
+                                out_a_bstride=self.embed_dim, text=self.text_encoder,
+                                tokens=toks, out_t=[q[:n, di:], q[n:, di:]],
+                                out_t_bstride=[self.embed_dim] * 2)
+        cur.wait_stream(s_img)
+        return q
+
     # ---- index -------------------------------------------------------------------------------
     def set_index(self, embeddings: torch.Tensor, answers: list, question_info: dict,
                   retrieval_k: int = 15, is_training_phase: bool = False):
@@ -285,13 +306,24 @@ class VQARetrieval:
         embs, answers = [], []
         info = {"question_type": [], "question_id": [], "question": []}
         # query rows stay on the device until the end: the host never waits on a batch, so
-        # the tower passes of consecutive batches queue back to back on the GPU
+        # the tower passes of consecutive batches queue back to back on the GPU; two equal-sized
+        # batches share one pass (twice the GEMM rows, every row bit-identical)
+        pend = None
         for batch in data_loader:
-            embs.append(self.encode_queries(batch))
             answers.extend(batch["answer"])
             info["question_type"].extend(batch["question_type"])
             info["question_id"].extend(batch["question_id"])
             info["question"].extend(batch["question"])
+            if pend is None:
+                pend = batch
+            elif pend["image"].shape[0] == batch["image"].shape[0]:
+                embs.append(self._encode_two(pend, batch))
+                pend = None
+            else:
+                embs.append(self.encode_queries(pend))
+                pend = batch
+        if pend is not None:
+            embs.append(self.encode_queries(pend))
         emb = (torch.cat(embs, 0) if embs else
                torch.empty((0, self.embed_dim), device=self.device)).cpu()
         return emb, answers, info

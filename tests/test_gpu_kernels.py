@@ -218,7 +218,9 @@ def test_encode_towers_slots_run_concurrently(device, clip_sd):
 
 def test_create_retrieval_dataset_builds_and_caches(device, clip_sd, tmp_path):
     """Index build (dataset/VQAFeatureDataset.py:118-185): the rows are
-    each batch's encode_queries rows bit for bit, the lists follow the loader, the second call
+    each batch's encode_queries rows bit for bit and the oracle towers' rows within FP_TOL at full
+    ViT-B/32 + CLIP-text size (the reference's own rows at G2 size: test_gpu_dropin.py), the lists
+    follow the loader, the second call
     loads the cache (safe formats) instead of encoding, and a query finds its own row."""
     from multimodalpromptretrieval_amd.dataset import VQARetrieval
     r = VQARetrieval(device, clip_state_dict=clip_sd, clip_tokenizer=syn.hash_clip_tokenize)
@@ -233,6 +235,12 @@ def test_create_retrieval_dataset_builds_and_caches(device, clip_sd, tmp_path):
     r.create_retrieval_dataset(loader, is_training_phase=False, retrieval_k=1,
                                cache_dir=str(tmp_path))
     assert torch.equal(r.retrieval_embeddings.cpu(), want)
+    # against the oracle's CLIP towers over the same loader (:145-148: [image CLS ‖ text EOT])
+    oracle_rows = torch.cat([torch.cat([oclip.encode_image(clip_sd, bt["image"].cpu()),
+                                        oclip.encode_text(clip_sd,
+                                                          syn.hash_clip_tokenize(bt["question"]))],
+                                       1) for bt in loader])
+    assert _rel_err(r.retrieval_embeddings.cpu(), oracle_rows) < FP_TOL
     assert r.retrieval_answers == [a for bt in loader for a in bt["answer"]]
     assert r.retrieval_question_info["question_id"] == [q for bt in loader
                                                           for q in bt["question_id"]]
@@ -243,6 +251,16 @@ def test_create_retrieval_dataset_builds_and_caches(device, clip_sd, tmp_path):
     assert torch.equal(r2.retrieval_embeddings.cpu(), want)
     got = r.retrieve_closest_qa_pairs(loader[1], return_ans=True)
     assert got == [[a] for a in loader[1]["answer"]]
+    # equal-sized batches share one tower pass: still each batch's rows bit for bit
+    loader2 = [dict(bt, image=syn.images(60 + i, 4).to(device),
+                    question=[f"which plane {i} {j}" for j in range(4)],
+                    answer=[f"p{i}{j}" for j in range(4)], question_type=["plane"] * 4,
+                    question_id=[f"p{i}-{j}" for j in range(4)]) for i, bt in enumerate(loader)]
+    want2 = torch.cat([r.encode_queries(bt).cpu() for bt in loader2])
+    r.create_retrieval_dataset(loader2, is_training_phase=False, retrieval_k=1,
+                               cache_dir=str(tmp_path / "two"))
+    assert torch.equal(r.retrieval_embeddings.cpu(), want2)
+    assert r.retrieval_answers == [a for bt in loader2 for a in bt["answer"]]
 
 
 def test_clip_text(device, clip_sd):
