@@ -212,6 +212,62 @@ int mpr_cross_entropy(const float* logits_dev, const int32_t* labels_dev, int64_
 
 int mpr_model_destroy(mpr_model* m);
 
+/* ---- training step (replaces the autograd backward of T5ForConditionalGeneration's loss that
+ * main.py:186 calls through architectures/T5VisionModel.py:219-234) ----
+ * Building blocks of the teacher-forced T5 forward + backward (multimodalpromptretrieval_amd/
+ * train.py orchestrates them).  All pointers are device pointers, row-major fp32 unless noted;
+ * every gradient is computed in a fixed order (deterministic).
+ *   mpr_gemm_f32: C[M,N] = act(A[M,K] W[N,K]^T) + R (R optional, may alias C; act 0 none, 2 relu)
+ *   on the fp32-accurate tiled GEMM of the encoders.
+ *   mpr_transpose: out[cols, ld_out] = in[rows, cols] (row stride ld_in; columns rows..ld_out of
+ *   out are zero: a GEMM's K padded to a multiple of 4).
+ *   mpr_rmsnorm_fwd/bwd: T5LayerNorm y = x * rsqrt(mean(x^2) + eps) * w * scale; rstd[M] saved;
+ *   bwd writes (accumulate = 0) or adds to dx, writes dw[D].
+ *   mpr_attn_train_fwd/bwd: head dim 64, q/k/v/o rows at base + b*bs + i*rs + h*64; optional
+ *   key mask [B, Lk] (0 = padded), causal, per-offset bias rel[(j - i + R) * H + h]; P [B,H,Lq,Lk]
+ *   saved; bwd uses a dS scratch [B,H,Lq,Lk] and adds the bias gradient by offset to drel.
+ *   mpr_rel_gather / mpr_rel_scatter: per-offset bias from / gradient onto the [buckets, H] table
+ *   through lut[2R + 1] (bucket of offset off - R).
+ *   mpr_ce_train: per-row loss of logits [n, V] against labels [n] (-100 ignored) into row_loss,
+ *   loss = sum * loss_scale; dlogits (optional, row stride ld_dlogits >= V, zero padded) =
+ *   (softmax - onehot) * grad_scale.
+ *   mpr_gather_rows / mpr_embed_bwd: embedding rows and the gradient of the gather (positions
+ *   grouped per unique id: pos[offs[u] .. offs[u+1]) hold uniq[u]), added into dW. */
+int mpr_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, float* C, int64_t ldc,
+                 int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr, int32_t act,
+                 void* stream);
+int mpr_transpose(const float* in, int64_t rows, int64_t cols, int64_t ld_in, float* out,
+                  int64_t ld_out, void* stream);
+int mpr_rmsnorm_fwd(const float* x, int32_t M, int32_t D, const float* w, float eps, float scale,
+                    float* y, float* rstd, void* stream);
+int mpr_rmsnorm_bwd(const float* x, int32_t M, int32_t D, const float* w, const float* rstd,
+                    const float* dy, float scale, float* dx, int32_t accumulate, float* dw,
+                    void* stream);
+int mpr_attn_train_fwd(const float* q, int64_t q_bs, int64_t q_rs, const float* k, int64_t k_bs,
+                       int64_t k_rs, const float* v, int64_t v_bs, int64_t v_rs, int32_t B,
+                       int32_t H, int32_t Lq, int32_t Lk, int32_t causal, const float* key_mask,
+                       const float* rel, int32_t R, float* o, int64_t o_bs, int64_t o_rs, float* P,
+                       void* stream);
+int mpr_attn_train_bwd(const float* q, int64_t q_bs, int64_t q_rs, const float* k, int64_t k_bs,
+                       int64_t k_rs, const float* v, int64_t v_bs, int64_t v_rs, int32_t B,
+                       int32_t H, int32_t Lq, int32_t Lk, const float* P, const float* dO,
+                       int64_t do_bs, int64_t do_rs, float* dS, float* dq, int64_t dq_bs,
+                       int64_t dq_rs, float* dk, int64_t dk_bs, int64_t dk_rs, float* dv,
+                       int64_t dv_bs, int64_t dv_rs, float* drel, int32_t R, void* stream);
+int mpr_rel_gather(const float* table, const int32_t* lut, int32_t R, int32_t H, float* rel,
+                   void* stream);
+int mpr_rel_scatter(const float* drel, const int32_t* lut, int32_t R, int32_t num_buckets,
+                    int32_t H, float* dtable, void* stream);
+int mpr_relu_bwd(const float* y, const float* dy, int64_t n, float* dx, void* stream);
+int mpr_add(const float* a, const float* b, int64_t n, float* out, void* stream);
+int mpr_ce_train(const float* logits, int64_t n, int32_t V, const int32_t* labels,
+                 float loss_scale, float grad_scale, float* row_loss, float* loss,
+                 float* dlogits, int64_t ld_dlogits, void* stream);
+int mpr_gather_rows(const float* table, const int32_t* ids, int64_t n, int32_t d, float* out,
+                    void* stream);
+int mpr_embed_bwd(const float* dY, int32_t d, const int32_t* uniq, const int32_t* offs,
+                  const int32_t* pos, int32_t n_uniq, float* dW, void* stream);
+
 /* ---- measurement (bench.py roofline; no reference counterpart) --------------------------------
  * kind 1 = tiled f32-MFMA GEMM, 2 = skinny (decode) GEMM, 0 = off.  While enabled, every launch
  * of that kernel (outside graph capture) is bracketed by hipEvents on its own stream.

@@ -81,6 +81,33 @@ SIGNATURES = [
     ("mpr_probe_replay", c_int32, [c_int32, c_void_p, POINTER(ctypes.c_double), I64P,
                                    POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
     ("mpr_probe_clear", c_int32, []),
+    ("mpr_gemm_f32", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32,
+                               c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p]),
+    ("mpr_transpose", c_int32, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64,
+                                c_void_p]),
+    ("mpr_rmsnorm_fwd", c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_float, c_float,
+                                  c_void_p, c_void_p, c_void_p]),
+    ("mpr_rmsnorm_bwd", c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                  c_float, c_void_p, c_int32, c_void_p, c_void_p]),
+    ("mpr_attn_train_fwd", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
+                                     c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32,
+                                     c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
+                                     c_int64, c_int64, c_void_p, c_void_p]),
+    ("mpr_attn_train_bwd", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
+                                     c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32,
+                                     c_int32, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                     c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
+                                     c_void_p, c_int64, c_int64, c_void_p, c_int32, c_void_p]),
+    ("mpr_rel_gather", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    ("mpr_rel_scatter", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
+                                  c_void_p]),
+    ("mpr_relu_bwd", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    ("mpr_add", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    ("mpr_ce_train", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_float, c_float, c_void_p,
+                               c_void_p, c_void_p, c_int64, c_void_p]),
+    ("mpr_gather_rows", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    ("mpr_embed_bwd", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                                c_void_p, c_void_p]),
 ]
 
 

@@ -33,7 +33,7 @@ class ParamTree(nn.Module):
         for k, v in (flat or {}).items():
             self.put(k, v)
 
-    def put(self, key: str, value):
+    def put(self, key: str, value, requires_grad: bool = False):
         parts = key.split(".")
         mod = self
         for p in parts[:-1]:
@@ -44,7 +44,7 @@ class ParamTree(nn.Module):
             mod.register_parameter(parts[-1], value)
         else:
             mod.register_parameter(parts[-1], nn.Parameter(value.detach().clone(),
-                                                           requires_grad=False))
+                                                           requires_grad=requires_grad))
 
 
 class _VisualTower(ParamTree):
@@ -73,14 +73,16 @@ class T5Shell(ParamTree):
 
     def __init__(self, sd: dict, owner):
         super().__init__()
-        shared = nn.Parameter(sd["shared.weight"].detach().clone(), requires_grad=False)
+        # trainable like the reference's T5ForConditionalGeneration (its vision tower is frozen,
+        # architectures/T5VisionModel.py:29-30); loss.backward() reaches them through train.py
+        shared = nn.Parameter(sd["shared.weight"].detach().clone(), requires_grad=True)
         self.shared = nn.Embedding(shared.shape[0], shared.shape[1])
         self.shared.weight = shared
         for k, v in sd.items():
             if k in ("shared.weight", "lm_head.weight", "encoder.embed_tokens.weight",
                      "decoder.embed_tokens.weight"):
                 continue
-            self.put(k, v)
+            self.put(k, v, requires_grad=True)
         # tied weights share one Parameter (T5ForConditionalGeneration tie_word_embeddings)
         self.put("encoder.embed_tokens.weight", shared)
         self.put("decoder.embed_tokens.weight", shared)
@@ -106,6 +108,13 @@ class T5Shell(ParamTree):
             decoder_input_ids = labels.new_zeros(labels.shape)
             decoder_input_ids[:, 1:] = labels[:, :-1]
             decoder_input_ids.masked_fill_(decoder_input_ids == -100, 0)
+        if (labels is not None and torch.is_grad_enabled()
+                and any(p.requires_grad for p in self.parameters())):
+            # differentiable loss (train.py): one autograd node over the whole T5
+            from .train import t5_loss
+            loss = t5_loss(dict(self.named_parameters()), inputs_embeds, attention_mask, labels,
+                           num_heads=dev.num_heads, scale_out=dev.scale_out)
+            return _GenerationOutput(loss, None)
         logits = dev.logits(inputs_embeds, attention_mask, decoder_input_ids)
         loss = dev.loss(logits, labels) if labels is not None else None
         return _GenerationOutput(loss, logits)
@@ -307,7 +316,15 @@ class T5VisionModel(nn.Module):
                 cur.wait_stream(tok_stream)
             img_tok.record_stream(cur)
             combined[:, :T].copy_(img_tok)
-        t5.embed(ids, combined, row0=T)
+        shared = self.T5_model.shared.weight
+        if torch.is_grad_enabled() and shared.requires_grad:
+            # training: the question-token gather is an autograd node (its gradient reaches the
+            # tied embedding, as T5_model.shared(ids) does at :169)
+            from .train import embed_rows
+            q = embed_rows(shared, ids)
+            combined = torch.cat([combined[:, :T], q], 1) if T else q
+        else:
+            t5.embed(ids, combined, row0=T)
         if self.use_image_info:
             mask = torch.ones((B, T + L), dtype=torch.float32)
             mask[:, T:] = encoding["attention_mask"].float()
@@ -324,7 +341,7 @@ class T5VisionModel(nn.Module):
         if not hasattr(self, "_s_main"):
             self._s_main = torch.cuda.Stream(self.device)
         self._s_main.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self._s_main):
+        with torch.cuda.stream(self._s_main), torch.no_grad():
             combined, mask, _ = self.prepare_input(batch)
             seqs = self.T5_model.generate(inputs_embeds=combined, attention_mask=mask,
                                           do_sample=False, max_new_tokens=self.max_new_tokens)
@@ -360,7 +377,8 @@ class T5VisionModel(nn.Module):
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     def forward(self, batch):
-        """architectures/T5VisionModel.py:219-234 (loss value; no autograd)."""
+        """architectures/T5VisionModel.py:219-234: the teacher-forced loss; differentiable when
+        grad mode is on and T5 parameters require grad (train.py), else the value only."""
         combined, mask, _ = self.prepare_input(batch)
         target = self.tokenizer(batch["answer"], padding="longest",
                                 max_length=self.max_target_length, truncation=True)

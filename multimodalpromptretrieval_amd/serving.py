@@ -156,7 +156,8 @@ class ServingLoop:
             self._refill()
             m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
             with torch.cuda.stream(m._s_prep):
-                combined, mask, _ = m.prepare_input(batch, _pre=pre)
+                with torch.no_grad():
+                    combined, mask, _ = m.prepare_input(batch, _pre=pre)
             if not self._add((combined, mask)):
                 continue
             # Answers are handed out as their calls complete; the host blocks on the oldest

@@ -50,6 +50,7 @@ class DeviceT5:
                  max_distance: int = 128):
         _lib.ensure_device(device)
         self.device = torch.device(device)
+        self.scale_out = scale_decoder_outputs
         self._h = None
         shared = sd["shared.weight"]
         self.vocab, self.d_model = shared.shape

@@ -1,0 +1,471 @@
+"""Teacher-forced T5 training step on the device.
+
+main.py:177-188 trains with ``loss = model(batch); loss.backward(); optimizer.step()``, and the
+loss is ``T5_model(inputs_embeds=..., attention_mask=..., labels=...).loss``
+(architectures/T5VisionModel.py:219-234): transformers' T5ForConditionalGeneration, whose
+backward the reference leaves to torch autograd.  Here the whole T5 — encoder, decoder with
+cross-attention, tied lm_head, token cross-entropy — is ONE autograd node (``T5LossFn``) whose
+forward keeps the activations the backward needs and whose backward is written out layer by
+layer on libmpr kernels (csrc/train.hip + the tiled fp32-accurate GEMM): every parameter
+gradient and the gradient of ``inputs_embeds`` in a fixed summation order.  The question-token
+embedding gather of prepare_input (:169) is a second node (``EmbedFn``) so its gradient reaches
+``shared`` as in the reference (tied with the decoder input embedding and the lm_head).
+
+Semantics follow T5ForConditionalGeneration with dropout off (``dropout_rate`` = 0, i.e. the
+reference's numbers in eval mode): torch's dropout RNG stream cannot be reproduced bit for bit,
+so a training-mode reference run is not a parity target.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .t5 import relative_position_bucket
+
+EPS = 1e-6
+RELU = 2  # csrc ACT_RELU
+
+
+def t5_param_names(n_enc: int, n_dec: int) -> list:
+    """transformers names of the T5 parameters, in the order T5LossFn takes them (the tied
+    embedding once, as shared.weight)."""
+    names = ["shared.weight", "encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight",
+             "decoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight",
+             "encoder.final_layer_norm.weight", "decoder.final_layer_norm.weight"]
+    for i in range(n_enc):
+        p = f"encoder.block.{i}.layer"
+        names += [p + ".0.layer_norm.weight", p + ".0.SelfAttention.q.weight",
+                  p + ".0.SelfAttention.k.weight", p + ".0.SelfAttention.v.weight",
+                  p + ".0.SelfAttention.o.weight", p + ".1.layer_norm.weight",
+                  p + ".1.DenseReluDense.wi.weight", p + ".1.DenseReluDense.wo.weight"]
+    for i in range(n_dec):
+        p = f"decoder.block.{i}.layer"
+        names += [p + ".0.layer_norm.weight", p + ".0.SelfAttention.q.weight",
+                  p + ".0.SelfAttention.k.weight", p + ".0.SelfAttention.v.weight",
+                  p + ".0.SelfAttention.o.weight", p + ".1.layer_norm.weight",
+                  p + ".1.EncDecAttention.q.weight", p + ".1.EncDecAttention.k.weight",
+                  p + ".1.EncDecAttention.v.weight", p + ".1.EncDecAttention.o.weight",
+                  p + ".2.layer_norm.weight", p + ".2.DenseReluDense.wi.weight",
+                  p + ".2.DenseReluDense.wo.weight"]
+    return names
+
+
+def _layers(names_or_sd, stack: str) -> int:
+    n = 0
+    while f"{stack}.block.{n}.layer.0.layer_norm.weight" in names_or_sd:
+        n += 1
+    return n
+
+
+# ---- thin wrappers over the ABI (current stream; fresh outputs) ---------------------------------
+def _s():
+    return _lib.stream_ptr()
+
+
+def _empty(*shape, like):
+    return torch.empty(shape, device=like.device, dtype=torch.float32)
+
+
+def gemm(A, W, R=None, act=0):
+    """A [M, K] @ W[N, K]^T (+ R), fp32-accurate tiled GEMM."""
+    M, K = A.shape
+    N = W.shape[0]
+    C = _empty(M, N, like=A)
+    _lib.call("mpr_gemm_f32", _lib.ptr(A), K, _lib.ptr(W), W.shape[1], _lib.ptr(C), N, M, N, K,
+              _lib.ptr(R), N if R is not None else 0, act, _s())
+    return C
+
+
+def _r4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+def transpose(x):
+    """x [r, c] -> [c, r4] (r4 = r rounded up to 4, zero columns: the GEMM K-alignment)."""
+    r, c = x.shape
+    out = _empty(c, _r4(r), like=x)
+    _lib.call("mpr_transpose", _lib.ptr(x), r, c, c, _lib.ptr(out), _r4(r), _s())
+    return out
+
+
+def linear_bwd(x, W, Wt, dy, dx_acc=None, need_dw=True, need_dx=True):
+    """y = x W^T: (dx (+ dx_acc), dW).  Wt = transpose(W) [K, N4], staged once per backward;
+    dy's row stride must be N4 (N4 = N for every projection but the vocabulary)."""
+    N, K = W.shape
+    dW = gemm(transpose(dy[:, :N].contiguous() if dy.shape[1] != N else dy),
+              transpose(x)) if need_dw else None
+    dx = gemm(dy, Wt, R=dx_acc) if need_dx else None
+    return dx, dW
+
+
+def rms_fwd(x, w, scale=1.0):
+    M, D = x.shape
+    y, r = _empty(M, D, like=x), _empty(M, like=x)
+    _lib.call("mpr_rmsnorm_fwd", _lib.ptr(x), M, D, _lib.ptr(w), EPS, float(scale), _lib.ptr(y),
+              _lib.ptr(r), _s())
+    return y, r
+
+
+def rms_bwd(x, w, rstd, dy, dx_acc=None, scale=1.0):
+    """(dx (+ dx_acc, in place), dw)"""
+    M, D = x.shape
+    dx = dx_acc if dx_acc is not None else _empty(M, D, like=x)
+    dw = _empty(D, like=x)
+    _lib.call("mpr_rmsnorm_bwd", _lib.ptr(x), M, D, _lib.ptr(w), _lib.ptr(rstd), _lib.ptr(dy),
+              float(scale), _lib.ptr(dx), 1 if dx_acc is not None else 0, _lib.ptr(dw), _s())
+    return dx, dw
+
+
+def attn_fwd(q, k, v, B, H, Lq, Lk, causal, mask, rel, R):
+    inner = q.shape[1]
+    o = _empty(B * Lq, inner, like=q)
+    P = _empty(B, H, Lq, Lk, like=q)
+    _lib.call("mpr_attn_train_fwd", _lib.ptr(q), Lq * inner, inner, _lib.ptr(k), Lk * inner,
+              inner, _lib.ptr(v), Lk * inner, inner, B, H, Lq, Lk, int(causal), _lib.ptr(mask),
+              _lib.ptr(rel), R, _lib.ptr(o), Lq * inner, inner, _lib.ptr(P), _s())
+    return o, P
+
+
+def attn_bwd(q, k, v, P, do, B, H, Lq, Lk, drel, R):
+    inner = q.shape[1]
+    dS = torch.empty_like(P)
+    dq, dk, dv = _empty(B * Lq, inner, like=q), _empty(B * Lk, inner, like=q), \
+        _empty(B * Lk, inner, like=q)
+    _lib.call("mpr_attn_train_bwd", _lib.ptr(q), Lq * inner, inner, _lib.ptr(k), Lk * inner,
+              inner, _lib.ptr(v), Lk * inner, inner, B, H, Lq, Lk, _lib.ptr(P), _lib.ptr(do),
+              Lq * inner, inner, _lib.ptr(dS), _lib.ptr(dq), Lq * inner, inner, _lib.ptr(dk),
+              Lk * inner, inner, _lib.ptr(dv), Lk * inner, inner, _lib.ptr(drel), R, _s())
+    return dq, dk, dv
+
+
+def _grouped(ids: np.ndarray):
+    """Positions of each distinct id (stable order): (uniq, offs, pos) int32 for mpr_embed_bwd."""
+    ids = ids.reshape(-1).astype(np.int64)
+    order = np.argsort(ids, kind="stable")
+    uniq, counts = np.unique(ids[order], return_counts=True)
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    return uniq.astype(np.int32), offs.astype(np.int32), order.astype(np.int32)
+
+
+def embed_bwd_into(dW, ids_host: np.ndarray, dY):
+    uniq, offs, pos = _grouped(ids_host)
+    dev = dY.device
+    u, o, p = (torch.from_numpy(a).to(dev) for a in (uniq, offs, pos))
+    _lib.call("mpr_embed_bwd", _lib.ptr(dY), dY.shape[-1], _lib.ptr(u), _lib.ptr(o), _lib.ptr(p),
+              len(uniq), _lib.ptr(dW), _s())
+
+
+def gather_rows(table, ids_dev):
+    n = ids_dev.numel()
+    d = table.shape[1]
+    out = _empty(n, d, like=table)
+    _lib.call("mpr_gather_rows", _lib.ptr(table), _lib.ptr(ids_dev), n, d, _lib.ptr(out), _s())
+    return out
+
+
+class EmbedFn(torch.autograd.Function):
+    """``T5_model.shared(input_ids)`` (architectures/T5VisionModel.py:169) with its gradient."""
+
+    @staticmethod
+    def forward(ctx, weight, ids):
+        ids_dev = ids.to(weight.device, torch.int32).contiguous()
+        ctx.ids_host = ids.detach().cpu().numpy()
+        ctx.wshape = weight.shape
+        return gather_rows(weight.detach(), ids_dev.view(-1)).view(*ids.shape, weight.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        dW = torch.zeros(ctx.wshape, device=dy.device, dtype=torch.float32)
+        embed_bwd_into(dW, ctx.ids_host, dy.contiguous().view(-1, ctx.wshape[1]))
+        return dW, None
+
+
+def embed_rows(weight, ids):
+    return EmbedFn.apply(weight, ids)
+
+
+class T5LossFn(torch.autograd.Function):
+    """T5ForConditionalGeneration(inputs_embeds, attention_mask, labels).loss and its backward.
+    ``params`` in ``t5_param_names`` order."""
+
+    @staticmethod
+    def forward(ctx, cfg, inputs_embeds, mask, labels, *params):
+        runner = _Runner(cfg, params)
+        loss, tape = runner.forward(inputs_embeds.detach(), mask, labels)
+        ctx.runner, ctx.tape = runner, tape
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        needs = ctx.needs_input_grad
+        d_emb, grads = ctx.runner.backward(ctx.tape, float(dloss), needs[4:], needs[1])
+        ctx.tape = None
+        return (None, d_emb, None, None, *grads)
+
+
+class T5Config:
+    def __init__(self, names, shapes, num_heads, max_distance=128, scale_out=True):
+        self.n_enc = _layers(names, "encoder")
+        self.n_dec = _layers(names, "decoder")
+        self.vocab, self.d = shapes["shared.weight"]
+        self.num_buckets, self.H = shapes[
+            "encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"]
+        assert self.H == num_heads
+        self.inner = shapes["encoder.block.0.layer.0.SelfAttention.q.weight"][0]
+        self.max_distance = max_distance
+        self.scale_out = scale_out
+        self._luts = {}
+
+    def lut(self, R, bidirectional, device):
+        key = (R, bidirectional, str(device))
+        if key not in self._luts:
+            rel = torch.arange(-R, R + 1, dtype=torch.long)
+            self._luts[key] = relative_position_bucket(rel, bidirectional, self.num_buckets,
+                                                       self.max_distance).to(
+                device, torch.int32).contiguous()
+        return self._luts[key]
+
+
+class _Runner:
+    def __init__(self, cfg: T5Config, params):
+        self.c = cfg
+        self.names = t5_param_names(cfg.n_enc, cfg.n_dec)
+        self.p = {n: t.detach().contiguous() for n, t in zip(self.names, params)}
+
+    # ---- forward --------------------------------------------------------------------------------
+    def forward(self, emb, mask, labels):
+        c, p = self.c, self.p
+        B, L, d = emb.shape
+        H, inner = c.H, c.inner
+        dev = emb.device
+        lab_host = labels.detach().cpu().numpy().astype(np.int64)
+        T = lab_host.shape[1]
+        dec_ids = np.zeros_like(lab_host)
+        dec_ids[:, 1:] = lab_host[:, :-1]
+        dec_ids[dec_ids == -100] = 0  # shift_right (decoder_start_token_id 0, pad 0)
+        Re, Rd = max(L, 1), max(T, 1)
+        lut_e, lut_d = c.lut(Re, True, dev), c.lut(Rd, False, dev)
+        rel_e = _empty(2 * Re + 1, H, like=emb)
+        _lib.call("mpr_rel_gather", _lib.ptr(p[self.names[1]]), _lib.ptr(lut_e), Re, H,
+                  _lib.ptr(rel_e), _s())
+        rel_d = _empty(2 * Rd + 1, H, like=emb)
+        _lib.call("mpr_rel_gather", _lib.ptr(p[self.names[2]]), _lib.ptr(lut_d), Rd, H,
+                  _lib.ptr(rel_d), _s())
+        maskf = mask.to(dev, torch.float32).contiguous()
+        tape = {"B": B, "L": L, "T": T, "Re": Re, "Rd": Rd, "lut_e": lut_e, "lut_d": lut_d,
+                "mask": maskf, "dec_ids": dec_ids, "enc": [], "dec": []}
+        # encoder
+        x = emb.contiguous().view(B * L, d)
+        for i in range(c.n_enc):
+            pre = f"encoder.block.{i}.layer"
+            t = {"x0": x}
+            t["n1"], t["r1"] = rms_fwd(x, p[pre + ".0.layer_norm.weight"])
+            t["q"] = gemm(t["n1"], p[pre + ".0.SelfAttention.q.weight"])
+            t["k"] = gemm(t["n1"], p[pre + ".0.SelfAttention.k.weight"])
+            t["v"] = gemm(t["n1"], p[pre + ".0.SelfAttention.v.weight"])
+            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, L, L, False, maskf, rel_e, Re)
+            t["x1"] = gemm(t["a"], p[pre + ".0.SelfAttention.o.weight"], R=x)
+            t["n2"], t["r2"] = rms_fwd(t["x1"], p[pre + ".1.layer_norm.weight"])
+            t["f"] = gemm(t["n2"], p[pre + ".1.DenseReluDense.wi.weight"], act=RELU)
+            x = gemm(t["f"], p[pre + ".1.DenseReluDense.wo.weight"], R=t["x1"])
+            tape["enc"].append(t)
+        tape["enc_in"] = x
+        enc, tape["enc_r"] = rms_fwd(x, p["encoder.final_layer_norm.weight"])
+        tape["enc_out"] = enc
+        # decoder
+        ids_dev = torch.from_numpy(dec_ids.astype(np.int32)).to(dev).view(-1)
+        g = gather_rows(p["shared.weight"], ids_dev)
+        for i in range(c.n_dec):
+            pre = f"decoder.block.{i}.layer"
+            t = {"g0": g}
+            t["n1"], t["r1"] = rms_fwd(g, p[pre + ".0.layer_norm.weight"])
+            t["q"] = gemm(t["n1"], p[pre + ".0.SelfAttention.q.weight"])
+            t["k"] = gemm(t["n1"], p[pre + ".0.SelfAttention.k.weight"])
+            t["v"] = gemm(t["n1"], p[pre + ".0.SelfAttention.v.weight"])
+            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, T, T, True, None, rel_d, Rd)
+            t["g1"] = gemm(t["a"], p[pre + ".0.SelfAttention.o.weight"], R=g)
+            t["n2"], t["r2"] = rms_fwd(t["g1"], p[pre + ".1.layer_norm.weight"])
+            t["cq"] = gemm(t["n2"], p[pre + ".1.EncDecAttention.q.weight"])
+            t["ck"] = gemm(enc, p[pre + ".1.EncDecAttention.k.weight"])
+            t["cv"] = gemm(enc, p[pre + ".1.EncDecAttention.v.weight"])
+            t["ca"], t["cP"] = attn_fwd(t["cq"], t["ck"], t["cv"], B, H, T, L, False, maskf, None,
+                                        0)
+            t["g2"] = gemm(t["ca"], p[pre + ".1.EncDecAttention.o.weight"], R=t["g1"])
+            t["n3"], t["r3"] = rms_fwd(t["g2"], p[pre + ".2.layer_norm.weight"])
+            t["f"] = gemm(t["n3"], p[pre + ".2.DenseReluDense.wi.weight"], act=RELU)
+            g = gemm(t["f"], p[pre + ".2.DenseReluDense.wo.weight"], R=t["g2"])
+            tape["dec"].append(t)
+        tape["dec_in"] = g
+        s = c.d ** -0.5 if c.scale_out else 1.0
+        tape["s"] = s
+        hs, tape["dec_r"] = rms_fwd(g, p["decoder.final_layer_norm.weight"], scale=s)
+        tape["hs"] = hs
+        logits = gemm(hs, p["shared.weight"])
+        tape["logits"] = logits
+        lab32 = torch.from_numpy(lab_host.astype(np.int32)).to(dev).view(-1)
+        n_valid = int((lab_host != -100).sum())
+        tape["lab"], tape["n_valid"] = lab32, n_valid
+        row_loss = _empty(B * T, like=emb)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        _lib.call("mpr_ce_train", _lib.ptr(logits), B * T, c.vocab, _lib.ptr(lab32),
+                  1.0 / max(n_valid, 1) if n_valid else float("nan"), 0.0, _lib.ptr(row_loss),
+                  _lib.ptr(loss), None, 0, _s())
+        return loss, tape
+
+    # ---- backward -------------------------------------------------------------------------------
+    def backward(self, tape, dloss: float, need_params, need_emb):
+        c, p = self.c, self.p
+        B, L, T, H = tape["B"], tape["L"], tape["T"], c.H
+        nm = self.names
+        idx = {n: i for i, n in enumerate(nm)}
+        grads = [None] * len(nm)
+
+        def want(name):
+            return bool(need_params[idx[name]])
+
+        def put(name, g):
+            if want(name):
+                grads[idx[name]] = g
+
+        dev = tape["logits"].device
+        wt = {}
+
+        def Wt(name):  # W^T once per backward
+            if name not in wt:
+                wt[name] = transpose(p[name])
+            return wt[name]
+
+        # loss -> logits
+        logits = tape["logits"]
+        V4 = _r4(c.vocab)  # dlogits rows padded with zeros: the lm_head dx GEMM's K
+        dlogits = _empty(B * T, V4, like=logits)
+        row_loss = _empty(B * T, like=logits)
+        scratch = torch.empty((), device=dev, dtype=torch.float32)
+        nv = max(tape["n_valid"], 1)
+        _lib.call("mpr_ce_train", _lib.ptr(logits), B * T, c.vocab, _lib.ptr(tape["lab"]),
+                  1.0 / nv, dloss / nv, _lib.ptr(row_loss), _lib.ptr(scratch),
+                  _lib.ptr(dlogits), V4, _s())
+        tape["logits"] = None
+        # lm_head (tied): logits = hs shared^T
+        d_shared = torch.zeros_like(p["shared.weight"])
+        dhs, dW = linear_bwd(tape["hs"], p["shared.weight"], Wt("shared.weight"), dlogits)
+        _lib.call("mpr_add", _lib.ptr(d_shared), _lib.ptr(dW), d_shared.numel(),
+                  _lib.ptr(d_shared), _s())
+        del dlogits, dW
+        dg, dw = rms_bwd(tape["dec_in"], p["decoder.final_layer_norm.weight"], tape["dec_r"], dhs,
+                         scale=tape["s"])
+        put("decoder.final_layer_norm.weight", dw)
+        drel_d = torch.zeros((2 * tape["Rd"] + 1, H), device=dev, dtype=torch.float32)
+        d_enc = None
+        for i in reversed(range(c.n_dec)):
+            pre = f"decoder.block.{i}.layer"
+            t = tape["dec"][i]
+            # FFN: g = g2 + relu(n3 Wi^T) Wo^T
+            wo, wi = pre + ".2.DenseReluDense.wo.weight", pre + ".2.DenseReluDense.wi.weight"
+            df, dW = linear_bwd(t["f"], p[wo], Wt(wo), dg, need_dw=want(wo))
+            put(wo, dW)
+            _lib.call("mpr_relu_bwd", _lib.ptr(t["f"]), _lib.ptr(df), df.numel(), _lib.ptr(df),
+                      _s())
+            dn3, dW = linear_bwd(t["n3"], p[wi], Wt(wi), df, need_dw=want(wi))
+            put(wi, dW)
+            ln = pre + ".2.layer_norm.weight"
+            dg2, dw = rms_bwd(t["g2"], p[ln], t["r3"], dn3, dx_acc=dg)
+            put(ln, dw)
+            # cross-attention: g2 = g1 + attn(n2 Wq^T, enc Wk^T, enc Wv^T) Wo^T
+            co = pre + ".1.EncDecAttention.o.weight"
+            dca, dW = linear_bwd(t["ca"], p[co], Wt(co), dg2, need_dw=want(co))
+            put(co, dW)
+            dcq, dck, dcv = attn_bwd(t["cq"], t["ck"], t["cv"], t["cP"], dca, B, H, T, L, None,
+                                     0)
+            cq, ck, cv = (pre + f".1.EncDecAttention.{x}.weight" for x in "qkv")
+            dn2, dW = linear_bwd(t["n2"], p[cq], Wt(cq), dcq, need_dw=want(cq))
+            put(cq, dW)
+            d_enc, dW = linear_bwd(tape["enc_out"], p[ck], Wt(ck), dck, dx_acc=d_enc,
+                                   need_dw=want(ck))
+            put(ck, dW)
+            d_enc, dW = linear_bwd(tape["enc_out"], p[cv], Wt(cv), dcv, dx_acc=d_enc,
+                                   need_dw=want(cv))
+            put(cv, dW)
+            ln = pre + ".1.layer_norm.weight"
+            dg1, dw = rms_bwd(t["g1"], p[ln], t["r2"], dn2, dx_acc=dg2)
+            put(ln, dw)
+            # self-attention: g1 = g0 + attn(n1 Wq^T, n1 Wk^T, n1 Wv^T; causal, bias) Wo^T
+            so = pre + ".0.SelfAttention.o.weight"
+            da, dW = linear_bwd(t["a"], p[so], Wt(so), dg1, need_dw=want(so))
+            put(so, dW)
+            dq, dk, dv = attn_bwd(t["q"], t["k"], t["v"], t["P"], da, B, H, T, T, drel_d,
+                                  tape["Rd"])
+            sq, sk, sv = (pre + f".0.SelfAttention.{x}.weight" for x in "qkv")
+            dn1, dW = linear_bwd(t["n1"], p[sq], Wt(sq), dq, need_dw=want(sq))
+            put(sq, dW)
+            dn1, dW = linear_bwd(t["n1"], p[sk], Wt(sk), dk, dx_acc=dn1, need_dw=want(sk))
+            put(sk, dW)
+            dn1, dW = linear_bwd(t["n1"], p[sv], Wt(sv), dv, dx_acc=dn1, need_dw=want(sv))
+            put(sv, dW)
+            ln = pre + ".0.layer_norm.weight"
+            dg, dw = rms_bwd(t["g0"], p[ln], t["r1"], dn1, dx_acc=dg1)
+            put(ln, dw)
+            tape["dec"][i] = None
+        # decoder input embedding (tied)
+        embed_bwd_into(d_shared, tape["dec_ids"], dg)
+        put("shared.weight", d_shared)
+        dtab = torch.zeros_like(p[nm[2]])
+        _lib.call("mpr_rel_scatter", _lib.ptr(drel_d), _lib.ptr(tape["lut_d"]), tape["Rd"],
+                  c.num_buckets, H, _lib.ptr(dtab), _s())
+        put(nm[2], dtab)
+        # encoder
+        dx, dw = rms_bwd(tape["enc_in"], p["encoder.final_layer_norm.weight"], tape["enc_r"],
+                         d_enc)
+        put("encoder.final_layer_norm.weight", dw)
+        drel_e = torch.zeros((2 * tape["Re"] + 1, H), device=dev, dtype=torch.float32)
+        for i in reversed(range(c.n_enc)):
+            pre = f"encoder.block.{i}.layer"
+            t = tape["enc"][i]
+            wo, wi = pre + ".1.DenseReluDense.wo.weight", pre + ".1.DenseReluDense.wi.weight"
+            df, dW = linear_bwd(t["f"], p[wo], Wt(wo), dx, need_dw=want(wo))
+            put(wo, dW)
+            _lib.call("mpr_relu_bwd", _lib.ptr(t["f"]), _lib.ptr(df), df.numel(), _lib.ptr(df),
+                      _s())
+            dn2, dW = linear_bwd(t["n2"], p[wi], Wt(wi), df, need_dw=want(wi))
+            put(wi, dW)
+            ln = pre + ".1.layer_norm.weight"
+            dx1, dw = rms_bwd(t["x1"], p[ln], t["r2"], dn2, dx_acc=dx)
+            put(ln, dw)
+            so = pre + ".0.SelfAttention.o.weight"
+            da, dW = linear_bwd(t["a"], p[so], Wt(so), dx1, need_dw=want(so))
+            put(so, dW)
+            dq, dk, dv = attn_bwd(t["q"], t["k"], t["v"], t["P"], da, B, H, L, L, drel_e,
+                                  tape["Re"])
+            sq, sk, sv = (pre + f".0.SelfAttention.{x}.weight" for x in "qkv")
+            dn1, dW = linear_bwd(t["n1"], p[sq], Wt(sq), dq, need_dw=want(sq))
+            put(sq, dW)
+            dn1, dW = linear_bwd(t["n1"], p[sk], Wt(sk), dk, dx_acc=dn1, need_dw=want(sk))
+            put(sk, dW)
+            dn1, dW = linear_bwd(t["n1"], p[sv], Wt(sv), dv, dx_acc=dn1, need_dw=want(sv))
+            put(sv, dW)
+            ln = pre + ".0.layer_norm.weight"
+            dx, dw = rms_bwd(t["x0"], p[ln], t["r1"], dn1, dx_acc=dx1)
+            put(ln, dw)
+            tape["enc"][i] = None
+        dtab = torch.zeros_like(p[nm[1]])
+        _lib.call("mpr_rel_scatter", _lib.ptr(drel_e), _lib.ptr(tape["lut_e"]), tape["Re"],
+                  c.num_buckets, H, _lib.ptr(dtab), _s())
+        put(nm[1], dtab)
+        d_emb = dx.view(B, L, c.d) if need_emb else None
+        return d_emb, grads
+
+
+def t5_loss(named_params: dict, inputs_embeds, attention_mask, labels, num_heads: int,
+            scale_out: bool = True):
+    """Differentiable T5ForConditionalGeneration(...).loss over ``named_params`` (transformers
+    names -> Parameters; the tied embedding as shared.weight)."""
+    names = list(named_params)
+    n_enc, n_dec = _layers(names, "encoder"), _layers(names, "decoder")
+    order = t5_param_names(n_enc, n_dec)
+    shapes = {n: tuple(named_params[n].shape) for n in order}
+    cfg = T5Config(order, shapes, num_heads, scale_out=scale_out)
+    return T5LossFn.apply(cfg, inputs_embeds, attention_mask, labels,
+                          *[named_params[n] for n in order])

@@ -178,3 +178,31 @@ def g9_retrieval_loader():
 def g9_test_batches():
     return [_g9_batch(G9["seed"] + 100 + i, G9["B"], 5000 + i * G9["B"])
             for i in range(G9["test_batches"])]
+
+
+# ---- G10 / G11: training gradients (SURVEY.md §8(f) rank 3; main.py:177-188) -----------------
+# G10: the reference's own T5VisionModel.forward(batch).backward() at G2 size (all T5 gradients;
+# the [32101, 128] shared gradient as its norm plus a row sample).  G11: transformers
+# T5ForConditionalGeneration at full t5-small size on the G3 inputs with labels below (per
+# parameter: gradient norm + its first 256 values; shared: norm + row sample).
+G10 = {"rows_seed": 1001, "n_rows": 192}
+G11 = {"t5_seed": 1101, "lab_seed": 1102, "T": 7, "rows_seed": 1103, "n_rows": 96}
+
+
+def g11_labels(B: int):
+    """[B, T] label ids (1..999, eos 1 at each row's end, -100 after it)."""
+    rng = np.random.Generator(np.random.PCG64(G11["lab_seed"]))
+    T = G11["T"]
+    lab = torch.tensor(rng.integers(2, 1000, size=(B, T)), dtype=torch.long)
+    for b in range(B):
+        n = 2 + b % (T - 1)
+        lab[b, n - 1] = 1
+        lab[b, n:] = -100
+    return lab
+
+
+def shared_rows(seed: int, n: int, vocab: int, must):
+    """sorted(rows the batch touches ∪ n random rows) of the shared gradient to compare."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rows = set(int(x) for x in must) | set(int(x) for x in rng.choice(vocab, n, replace=False))
+    return np.array(sorted(r for r in rows if 0 <= r < vocab), dtype=np.int64)

@@ -531,9 +531,71 @@ def make_g4():
     print("G4:", cls.shape, tokens.shape, txt.shape)
 
 
+# ------------------------------------------------------------------ G10 / G11: training gradients
+def _grad_record(named, rows, full=True):
+    out = {}
+    for n, g in named.items():
+        g = g.detach()
+        out["norm::" + n] = np.float64(g.double().norm().item())
+        if n == "shared.weight":
+            out["rows::" + n] = rows
+            out["sel::" + n] = g[torch.from_numpy(rows)].numpy()
+        elif full:
+            out["grad::" + n] = g.numpy()
+        else:
+            out["head::" + n] = g.reshape(-1)[:256].numpy()
+    return out
+
+
+def make_g10():
+    """The reference's T5VisionModel.forward (architectures/T5VisionModel.py:219-234) and
+    loss.backward() (main.py:186) at G2 size: every T5 parameter gradient."""
+    vm_t, t5_sd, t5cfg, retrieval_function = _g2_retrieval()
+    for prm in vm_t.parameters():
+        prm.requires_grad_(False)
+    model = ref_model(vm_t, t5_sd, t5cfg, retrieval_function)
+    batch = gi.g2_batch()
+    with torch.no_grad():
+        _, _, enc = model.prepare_input(batch)
+        lab = model.tokenizer(batch["answer"], padding="longest", max_length=128,
+                              truncation=True).input_ids
+    m = model.T5_model
+    m.zero_grad()
+    loss = model.forward(batch)
+    loss.backward()
+    named = {n: p.grad for n, p in m.named_parameters() if p.grad is not None}
+    rows = gi.shared_rows(gi.G10["rows_seed"], gi.G10["n_rows"], t5cfg.vocab_size,
+                          list(enc["input_ids"].reshape(-1)) + [x for r in lab for x in r])
+    rec = _grad_record(named, rows, full=True)
+    np.savez_compressed(os.path.join(HERE, "g10_train_grads.npz"), loss=np.float32(loss.item()),
+                        **rec)
+    print("G10 loss:", loss.item(), "params:", len(named))
+
+
+def make_g11():
+    """transformers T5ForConditionalGeneration at full t5-small size: loss.backward() on the G3
+    inputs (image-token rows + shared(ids), as prepare_input builds them) with G11 labels."""
+    cfg = syn.T5Config()
+    sd = syn.t5_state_dict(gi.G11["t5_seed"], cfg)
+    m = hf_t5(sd, cfg)
+    ids, img_tok, mask = gi.g3_inputs(cfg.d_model)
+    labels = gi.g11_labels(ids.shape[0])
+    m.zero_grad()
+    emb = torch.cat([img_tok, m.shared(ids)], 1)
+    loss = m(inputs_embeds=emb, attention_mask=mask, labels=labels).loss
+    loss.backward()
+    named = {n: p.grad for n, p in m.named_parameters() if p.grad is not None}
+    rows = gi.shared_rows(gi.G11["rows_seed"], gi.G11["n_rows"], cfg.vocab_size,
+                          list(ids.reshape(-1)) + [int(x) for x in labels.reshape(-1) if x >= 0])
+    rec = _grad_record(named, rows, full=False)
+    np.savez_compressed(os.path.join(HERE, "g11_t5_small_grads.npz"),
+                        loss=np.float32(loss.item()), labels=labels.numpy(), **rec)
+    print("G11 loss:", loss.item(), "params:", len(named))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8", "g9"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11"]
     for w in which:
         globals()["make_" + w]()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
