@@ -277,7 +277,12 @@ constexpr int x3_lds_floats() {
   return 2 * 3 * (BM + BN) * (BK + 8) / 2;
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+// KT: some K is not a multiple of BK (the loads past K are zeroed; otherwise no select touches a
+// loaded value, so no load is waited for early).  Rows past M / N read a clamped in-range row;
+// their results are not stored.  (Measured and dropped: W pre-split into three bf16 planes once
+// per model, copied into LDS without conversion: +8% on 64x128 tiles, -11% on 128x128 — the
+// planes' 32-byte row segments per k-tile coalesce worse than the 64-byte fp32 ones.)
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT>
 __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
@@ -305,14 +310,14 @@ __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, 
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = m0 + r;
-      oka[j][i] = row < M && c < K;
+      if constexpr (KT) oka[j][i] = c < K;
       ra[j][i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
                                                  min(c, K - 4));
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = n0 + r;
-      okb[j][i] = row < N && c < K;
+      if constexpr (KT) okb[j][i] = c < K;
       rb[j][i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
                                                  min(c, K - 4));
     }
@@ -331,12 +336,14 @@ __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, 
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT;
-      put(base, idx / KQ, (idx % KQ) * 4, oka[j][i] ? ra[j][i] : zero);
+      if constexpr (KT) put(base, idx / KQ, (idx % KQ) * 4, oka[j][i] ? ra[j][i] : zero);
+      else put(base, idx / KQ, (idx % KQ) * 4, ra[j][i]);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT;
-      put(base, BM + idx / KQ, (idx % KQ) * 4, okb[j][i] ? rb[j][i] : zero);
+      if constexpr (KT) put(base, BM + idx / KQ, (idx % KQ) * 4, okb[j][i] ? rb[j][i] : zero);
+      else put(base, BM + idx / KQ, (idx % KQ) * 4, rb[j][i]);
     }
   };
 
@@ -545,7 +552,7 @@ int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
 // by the largest problem instead (blockIdx.z per problem) leaves the small problems' slices
 // mostly empty, and the remap then gives whole XCDs nothing to do (the tower launches' text
 // problems: fc2 231 -> see DESIGN §3).
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT>
 __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_x3_kernel(
     const GemmGroup grp) {
   __shared__ __attribute__((aligned(16))) float smem[x3_lds_floats<BM, BN, BK>()];
@@ -572,17 +579,26 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
   }
   const GemmArgs a = select_problem(grp, z);
   const int bx = t / gy, by = t - bx * gy;
-  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW>(a, bx, by, smem);
+  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT>(a, bx, by, smem);
 }
 
+// KT when some K % BK != 0
 template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
 int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW;
   int64_t tiles = 0;
-  for (int i = 0; i < g.n; ++i) tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM);
+  bool kt = false;
+  for (int i = 0; i < g.n; ++i) {
+    tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM);
+    kt = kt || g.g[i].K % BK != 0;
+  }
   if (tiles == 0) return MPR_OK;
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW>), dim3((unsigned)tiles), dim3(NT),
-                     0, s, g);
+  if (kt)
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, true>), dim3((unsigned)tiles),
+                       dim3(NT), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, false>), dim3((unsigned)tiles),
+                       dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
 }

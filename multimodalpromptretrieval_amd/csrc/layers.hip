@@ -798,6 +798,8 @@ int attention(const AttnArgs& a, hipStream_t s) {
                 "attention: bias table radius %d too small (Lq %d, Lk %d)", a.lut_radius, a.Lq,
                 a.Lk);
   if (a.Lq == 1) {
+    // (A wave-per-(b, h) form without block barriers measured slower: 4.4 / 5.3 us self / cross
+    // against 3.8 / 4.1 — a quarter of the loads in flight per (b, h).)
     hipLaunchKernelGGL(attention_decode_kernel, dim3((unsigned)((int64_t)a.B * a.H)), dim3(256),
                        0, s, a);
     MPR_LAUNCHED();

@@ -1,7 +1,8 @@
 // x3bench.hip — the split-bf16 ("x3") fp32 GEMM against the f32-MFMA GEMM on the tower shapes:
 // device time per launch (graph of 100 launches) and max error against an fp64 host product,
 // relative to sum_k |a_k b_k| of the element (development aid).
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/x3bench.hip -o tools/x3bench
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/x3bench.hip -o tools/x3bench \
+//          -Lmultimodalpromptretrieval_amd -lmpr -Wl,-rpath,'$ORIGIN/../multimodalpromptretrieval_amd'
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -9,12 +10,7 @@
 #include <functional>
 #include <vector>
 
-#include "../multimodalpromptretrieval_amd/csrc/api.hip"
-#include "../multimodalpromptretrieval_amd/csrc/encoders.hip"
-#include "../multimodalpromptretrieval_amd/csrc/gemm.hip"
-#include "../multimodalpromptretrieval_amd/csrc/layers.hip"
-#include "../multimodalpromptretrieval_amd/csrc/scan.hip"
-#include "../multimodalpromptretrieval_amd/csrc/t5.hip"
+#include "../multimodalpromptretrieval_amd/csrc/gemm.hip"  // the rest links from libmpr.so
 
 using namespace mpr;
 
