@@ -17,6 +17,8 @@ untrained 512->1024 projection raise NotImplementedError; ``predict(output_atten
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -336,16 +338,29 @@ class T5VisionModel(nn.Module):
         """architectures/T5VisionModel.py:196-216 (greedy, max_new_tokens=20)."""
         if output_attentions:
             raise NotImplementedError("output_attentions is the eval-only plotting path")
-        # Whole predict() on a private (non-default) stream: eager launches on the legacy
-        # default stream cost more per kernel; the result is host strings, so no stream handoff.
-        if not hasattr(self, "_s_main"):
-            self._s_main = torch.cuda.Stream(self.device)
-        self._s_main.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self._s_main), torch.no_grad():
+        # Whole predict() on one non-default stream: eager launches on the legacy default
+        # stream cost more per kernel; the result is host strings, so no stream handoff.  With a
+        # VQARetrieval on this device that stream is the retrieval's own tower stream, so the
+        # towers -> scan -> T5 chain has no cross-stream waits (a private stream measured
+        # 10.8-13.4 ms per predict() depending on how the process's earlier streams happened to
+        # map onto the 4 hardware queues; MPR_PREDICT_STREAM=private restores it).
+        s_main = self._predict_stream()
+        s_main.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s_main), torch.no_grad():
             combined, mask, _ = self.prepare_input(batch)
             seqs = self.T5_model.generate(inputs_embeds=combined, attention_mask=mask,
                                           do_sample=False, max_new_tokens=self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
+
+    def _predict_stream(self):
+        retr = self._retrieval_obj()
+        streams = getattr(retr, "_streams", None)
+        if (streams is not None and getattr(retr, "device", None) == self.device
+                and os.environ.get("MPR_PREDICT_STREAM", "") != "private"):
+            return streams()
+        if not hasattr(self, "_s_main"):
+            self._s_main = torch.cuda.Stream(self.device)
+        return self._s_main
 
     def predict_many(self, batches, decodes_in_flight: int = 2, pair_decodes=None,
                      lookahead=None, tower_slots=None, decode_group=None, tower_batches=None):

@@ -85,6 +85,9 @@ int main(int argc, char** argv) {
       {"x3 128x64 1x1 8w k32 D2", launch_gemm_x3_group<128, 64, 1, 1, 32, 2, 1>},
       {"x3 64x128 1x1 8w k32 D2", launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>},
       {"x3 128x64 2x1 4w k16 D2", launch_gemm_x3_group<128, 64, 2, 1, 16, 2, 1>},
+      {"x3 128x128 2x1 8w k32 D2", launch_gemm_x3_group<128, 128, 2, 1, 32, 2, 1>},
+      {"x3 128x128 2x2 4w k32 D2", launch_gemm_x3_group<128, 128, 2, 2, 32, 2, 1>},
+      {"x3 128x256 2x2 8w k16 D2", launch_gemm_x3_group<128, 256, 2, 2, 16, 2, 1>},
   };
   int si = -1;
   for (const Shape& sh : shapes) {
