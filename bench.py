@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 from multimodalpromptretrieval_amd import _lib  # noqa: E402
 from multimodalpromptretrieval_amd import synthetic as syn  # noqa: E402
+from multimodalpromptretrieval_amd.serving import lookahead  # noqa: E402
 
 CONFIGS = {
     # name: (batch per GPU, index rows, index dim, k, t5 config)
@@ -336,21 +337,26 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def run(steps, pipelined=True):
+    def run(steps, pipelined=True, ahead=False):
         # A step = one batch through encode -> retrieve -> prompt -> T5 generate.  The serving
         # loop keeps two batches in flight (T5VisionModel.predict_many): batch i+1's encoders
         # and scan run beside batch i's decode; each batch's work and answers are predict()'s.
+        # Not pipelined: predict() one batch at a time (main.py:262-263), with `ahead` the
+        # batches come through serving.lookahead (the dropin launcher's evaluation loop: the
+        # next batch's towers and scan are enqueued before this batch's predict()).
         with torch.no_grad():
             if pipelined:
                 for _ in model.predict_many((batches[s % len(batches)] for s in range(steps)),
                                             args.inflight):
                     pass
             else:
-                for s in range(steps):
-                    model.predict(batches[s % len(batches)])
+                seq = (batches[s % len(batches)] for s in range(steps))
+                for b in (lookahead(seq, model) if ahead else seq):
+                    model.predict(b)
 
     run(args.warmup)
     run(args.warmup, pipelined=False)
+    run(args.warmup, pipelined=False, ahead=True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -371,6 +377,10 @@ def main():
     run(args.steps, pipelined=False)
     torch.cuda.synchronize()
     sync_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    t1 = time.perf_counter()
+    run(args.steps, pipelined=False, ahead=True)
+    torch.cuda.synchronize()
+    ahead_ms = (time.perf_counter() - t1) / args.steps * 1e3
 
     roofline = None
     if not args.no_probe:
@@ -448,6 +458,10 @@ def main():
                           f"loop, {args.inflight} generate calls in flight; ramp-up and drain "
                           f"inside the timed steps",
             "sync_ms_per_step": round(sync_ms, 3),
+            "lookahead_ms_per_step": round(ahead_ms, 3),
+            "sync_note": "sync: predict() one batch at a time, nothing enqueued ahead; "
+                         "lookahead: the same predict() calls with the batches iterated through "
+                         "serving.lookahead (main.py's test loop under the dropin launcher)",
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded random weights of ViT-B/32 x2, CLIP text, t5-small; "
                     "random 224x224 images + random-word questions)",

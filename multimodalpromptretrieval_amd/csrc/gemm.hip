@@ -307,12 +307,16 @@ constexpr int x3_lds_floats() {
   return 2 * 3 * (BM + BN) * (BK + 8) / 2;
 }
 
+// V (variants, tools/x3bench.hip): bit 0 interleaves the accumulators' MFMAs (term-major; the
+// order of each accumulator's own terms is unchanged, results bit-identical) — neutral, unused;
+// bit 1 raises the wave's issue priority over its MFMA run (s_setprio 1 .. 0): +0-4% on the
+// 128x128 tiles (fc2 1600x768x3072 x4: 131.2 -> 126.9 us), neutral to slightly negative on 64x128.
 // KT: some K is not a multiple of BK (the loads past K are zeroed; otherwise no select touches a
 // loaded value, so no load is waited for early).  Rows past M / N read a clamped in-range row;
 // their results are not stored.  (Measured and dropped: W pre-split into three bf16 planes once
 // per model, copied into LDS without conversion: +8% on 64x128 tiles, -11% on 128x128 — the
 // planes' 32-byte row segments per k-tile coalesce worse than the 64-byte fp32 ones.)
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0>
 __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
@@ -411,7 +415,16 @@ __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, 
   auto mfmas = [&](int u_lo, int u_hi) {
 #pragma unroll
     for (int u = u_lo; u < u_hi; ++u) {
-      const int term = u % 6, t = u / 6, ni = t % WN, mi = (t / WN) % WM, s4 = t / (WN * WM);
+      int term, t;
+      if constexpr (V & 1) {  // accumulators interleaved: term-major inside each 16-deep step
+        constexpr int A = WM * WN;
+        term = (u % (6 * A)) / A;
+        t = (u / (6 * A)) * A + u % A;
+      } else {
+        term = u % 6;
+        t = u / 6;
+      }
+      const int ni = t % WN, mi = (t / WN) % WM, s4 = t / (WN * WM);
       constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
       acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][s4][PA[term]],
                                                             fb[ni][s4][PB[term]], acc[mi][ni],
@@ -450,12 +463,14 @@ __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, 
     for (int j = 0; j < D; ++j) {
       const int st = (kt + j) & 1;
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((V & 2) != 0) __builtin_amdgcn_s_setprio(1);
       mfmas(0, U1);
       __builtin_amdgcn_sched_barrier(0);
       sread(st ^ 1, na, nb);
       __builtin_amdgcn_sched_barrier(0);
       mfmas(U1, NMF);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((V & 2) != 0) __builtin_amdgcn_s_setprio(0);
       swrite(st, j);
       gload(j, (kt + j + 2 + D) * BK);
       __syncthreads();
@@ -582,7 +597,7 @@ int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
 // by the largest problem instead (blockIdx.z per problem) leaves the small problems' slices
 // mostly empty, and the remap then gives whole XCDs nothing to do (the tower launches' text
 // problems: fc2 231 -> see DESIGN §3).
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0>
 __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_x3_kernel(
     const GemmGroup grp) {
   __shared__ __attribute__((aligned(16))) float smem[x3_lds_floats<BM, BN, BK>()];
@@ -609,11 +624,11 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
   }
   const GemmArgs a = select_problem(grp, z);
   const int bx = t / gy, by = t - bx * gy;
-  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT>(a, bx, by, smem);
+  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT, V>(a, bx, by, smem);
 }
 
 // KT when some K % BK != 0
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, int V = 0>
 int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW;
   int64_t tiles = 0;
@@ -624,10 +639,10 @@ int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   }
   if (tiles == 0) return MPR_OK;
   if (kt)
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, true>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, true, V>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   else
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, false>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, false, V>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -1036,7 +1051,7 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
         if (blocks32 >= 2048 && !g_ksplit32_only)
           return launch_gemm_group<64, 32, 1, 1, 64, 2, 4>(g, s);
         return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
-      case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1>(g, s);
+      case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>(g, s);
       default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);
     }
   });

@@ -17,6 +17,10 @@ The launcher installs two bindings, then executes ``main.py`` as ``__main__`` (r
   nothing (``weights_only=True``, a pickle reader that admits no globals), so caches the reference
   built are served and caches built here are the reference's.
 
+Evaluation loaders over a patched dataset are iterated one batch ahead (``serving.lookahead``):
+while the model is in eval mode (main.py:234), each next batch's towers and index scan are
+enqueued before the current batch is handed to ``predict()``, so they overlap its T5 decode.
+
 The prediction-head variants (``main.py:132-139``; SURVEY.md §2 "OUT") keep the reference's own
 class: their modules are imported (binding the original base class) before the swap.
 ``main.py --gpu_id cpu`` (or no ``--gpu_id``) selects the reference's CPU path (main.py:58-61):
@@ -91,6 +95,38 @@ def patch_model_module(mod: types.ModuleType) -> None:
         mod.T5VisionModel = T5VisionModel
 
 
+def _eval_model():
+    """The newest live device T5VisionModel in eval mode, or None."""
+    from .model import LIVE_MODELS
+    for m in reversed(list(LIVE_MODELS.values())):
+        if not m.training:
+            return m
+    return None
+
+
+def patch_dataloader() -> None:
+    """Iterate DataLoaders over a patched reference dataset one batch ahead
+    (``serving.lookahead``) while a device model is in eval mode (main.py:234 then the test loop
+    at :262-263): each batch's towers and index scan are enqueued while the previous batch's
+    T5 decode runs.  The batches, their order and every result are unchanged."""
+    from torch.utils.data import DataLoader
+    if getattr(DataLoader, "_mpr_orig_iter", None) is not None:
+        return
+    orig = DataLoader.__iter__
+
+    def __iter__(self):
+        it = orig(self)
+        if getattr(type(self.dataset), "_mpr_patched", False):
+            m = _eval_model()
+            if m is not None:
+                from .serving import lookahead
+                return lookahead(it, m)
+        return it
+
+    DataLoader._mpr_orig_iter = orig
+    DataLoader.__iter__ = __iter__
+
+
 def install(root: str = ".") -> None:
     """Import the reference modules from ``root`` and apply both bindings (before main.py runs)."""
     if _INSTALLED:
@@ -112,6 +148,7 @@ def install(root: str = ".") -> None:
     importlib.import_module("architectures.T5VisionModelFrozen")  # subclasses the device model
     ds = importlib.import_module("dataset.VQAFeatureDataset")
     patch_dataset_class(ds.VQADataset)
+    patch_dataloader()
     _INSTALLED.update(model=arch, dataset=ds)
 
 

@@ -18,6 +18,7 @@ untrained 512->1024 projection raise NotImplementedError; ``predict(output_atten
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 from torch import nn
@@ -132,6 +133,11 @@ def _load_t5(version: str, tokenizer):
         raise RuntimeError(f"cannot load {version} weights ({e}); pass t5_state_dict=") from e
 
 
+# live device models, newest last (dropin hands main.py's evaluation batches to the newest one in
+# eval mode as lookahead hints)
+LIVE_MODELS: "weakref.WeakValueDictionary[int, T5VisionModel]" = weakref.WeakValueDictionary()
+
+
 class T5VisionModel(nn.Module):
     def __init__(self, device, vision_encoder="ViT-B/32", T5_version="t5-small",
                  max_source_length=512, max_target_length=128, use_image_info=True,
@@ -177,6 +183,7 @@ class T5VisionModel(nn.Module):
         self._dev = {}
         self._slots = {}
         self.to(self.device)
+        LIVE_MODELS[id(self)] = self
 
     # ---- device handles, rebuilt when parameters change ------------------------------------------
     def _params_key(self, prefix):
@@ -335,22 +342,75 @@ class T5VisionModel(nn.Module):
         return combined, _lib.to_device_async(mask, self.device), encoding
 
     def predict(self, batch, output_attentions=False):
-        """architectures/T5VisionModel.py:196-216 (greedy, max_new_tokens=20)."""
+        """architectures/T5VisionModel.py:196-216 (greedy, max_new_tokens=20).  A batch
+        announced by ``hint_next`` picks up its already-enqueued retrieval work."""
         if output_attentions:
             raise NotImplementedError("output_attentions is the eval-only plotting path")
-        # Whole predict() on one non-default stream: eager launches on the legacy default
-        # stream cost more per kernel; the result is host strings, so no stream handoff.  With a
-        # VQARetrieval on this device that stream is the retrieval's own tower stream, so the
-        # towers -> scan -> T5 chain has no cross-stream waits (a private stream measured
-        # 10.8-13.4 ms per predict() depending on how the process's earlier streams happened to
-        # map onto the 4 hardware queues; MPR_PREDICT_STREAM=private restores it).
-        s_main = self._predict_stream()
+        pre = self._take_hint(batch)
+        if pre is not None:
+            # the retrieval stream may already hold the NEXT hinted batch's towers: the T5 part
+            # runs on a stream of its own (the serving loop's first generate stream)
+            which = os.environ.get("MPR_AHEAD_T5_STREAM", "gen:0")
+            if which == "private":
+                if not hasattr(self, "_s_main"):
+                    self._s_main = torch.cuda.Stream(self.device)
+                s_main = self._s_main
+            elif which == "current":
+                s_main = torch.cuda.current_stream(self.device)
+            else:
+                s_main = _lib.role_stream(self.device, which)
+        else:
+            # Whole predict() on one non-default stream: eager launches on the legacy default
+            # stream cost more per kernel; the result is host strings, so no stream handoff.
+            # With a VQARetrieval on this device that stream is the retrieval's own tower stream,
+            # so the towers -> scan -> T5 chain has no cross-stream waits (a private stream
+            # measured 10.8-13.4 ms per predict() depending on how the process's earlier streams
+            # happened to map onto the 4 hardware queues; MPR_PREDICT_STREAM=private restores it).
+            s_main = self._predict_stream()
         s_main.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s_main), torch.no_grad():
-            combined, mask, _ = self.prepare_input(batch)
+            combined, mask, _ = self.prepare_input(batch, _pre=pre)
             seqs = self.T5_model.generate(inputs_embeds=combined, attention_mask=mask,
                                           do_sample=False, max_new_tokens=self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
+
+    # ---- lookahead for batch-after-batch callers (main.py:262-263) ---------------------------
+    MAX_HINTS = 4
+
+    def hint_next(self, batch) -> bool:
+        """Announce a batch the caller will ``predict()`` soon (``serving.lookahead`` does this
+        one batch ahead; ``dropin`` wraps main.py's evaluation loaders with it).  The batch's
+        device-side retrieval work — the query towers paired with the token-feature ViT, the
+        index scan and the top-k copy to host (``_prefetch``) — is enqueued now on the retrieval
+        stream, so it runs on the GPU beside the current ``predict()``'s T5 encoder and greedy
+        decode, which leave most of the chip idle; the hinted ``predict()`` then only waits for
+        it.  Same launches, same results as an unhinted call.  Returns whether anything was
+        enqueued: nothing in training mode, without a ``VQARetrieval`` with an index on this
+        device, or for a batch already hinted."""
+        if self.training:
+            return False
+        if not hasattr(self, "_hints"):
+            self._hints = {}
+        key = id(batch["image"])
+        if key in self._hints:
+            return False
+        pre = self._prefetch([batch], int(os.environ.get("MPR_AHEAD_SLOT", "0")))[0]
+        if pre is None:
+            return False
+        while len(self._hints) >= self.MAX_HINTS:  # announced but never predicted: drop oldest
+            self._hints.pop(next(iter(self._hints)))
+        # the entry holds the batch's image tensor, so its id() is not reused while it lives
+        self._hints[key] = (batch["image"], tuple(batch["question"]), pre)
+        return True
+
+    def _take_hint(self, batch):
+        hints = getattr(self, "_hints", None)
+        if not hints:
+            return None
+        ent = hints.pop(id(batch["image"]), None)
+        if ent is None or ent[0] is not batch["image"] or ent[1] != tuple(batch["question"]):
+            return None
+        return ent[2]
 
     def _predict_stream(self):
         retr = self._retrieval_obj()
@@ -394,7 +454,7 @@ class T5VisionModel(nn.Module):
     def forward(self, batch):
         """architectures/T5VisionModel.py:219-234: the teacher-forced loss; differentiable when
         grad mode is on and T5 parameters require grad (train.py), else the value only."""
-        combined, mask, _ = self.prepare_input(batch)
+        combined, mask, _ = self.prepare_input(batch, _pre=self._take_hint(batch))
         target = self.tokenizer(batch["answer"], padding="longest",
                                 max_length=self.max_target_length, truncation=True)
         labels = torch.tensor(target["input_ids"])

@@ -174,3 +174,22 @@ class ServingLoop:
         while self.pending:
             for item in self.pending.popleft():
                 yield m._finish(*item)
+
+
+def lookahead(batches, model):
+    """Iterate ``batches`` one ahead for a caller that runs ``model.predict(batch)`` on each in
+    turn (main.py:262-263): before a batch is handed out, the NEXT one is announced with
+    ``model.hint_next``, so its towers and index scan run on the GPU beside this batch's T5
+    decode.  Batches come out unchanged and in order; ``predict()`` returns exactly what it
+    would without the hints."""
+    it = iter(batches)
+    cur = next(it, None)
+    if cur is None:
+        return
+    model.hint_next(cur)
+    for nxt in it:
+        model.hint_next(nxt)
+        yield cur
+        cur = nxt
+    yield cur
+

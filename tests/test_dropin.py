@@ -94,3 +94,63 @@ def test_launcher_leaves_cpu_runs_to_the_reference(tmp_path, capsys):
     out = capsys.readouterr()
     assert "ran ['--test', '--gpu_id', 'cpu']" in out.out
     assert not dropin._INSTALLED
+
+
+def test_lookahead_hints_one_batch_ahead_in_order():
+    from multimodalpromptretrieval_amd.serving import lookahead
+    log = []
+
+    class FakeModel:
+        training = False
+
+        def hint_next(self, b):
+            log.append(("hint", b))
+            return True
+
+    for b in lookahead(iter([1, 2, 3]), FakeModel()):
+        log.append(("use", b))
+    assert log == [("hint", 1), ("hint", 2), ("use", 1), ("hint", 3), ("use", 2), ("use", 3)]
+    assert list(lookahead([], FakeModel())) == []
+
+
+def test_dataloader_patch_wraps_only_patched_datasets_in_eval_mode():
+    from torch.utils.data import DataLoader
+
+    from multimodalpromptretrieval_amd.model import LIVE_MODELS
+    saved = DataLoader.__iter__
+    hints = []
+
+    class FakeModel:
+        training = False
+
+        def hint_next(self, b):
+            hints.append(int(b))
+            return True
+
+    class VQADataset(torch.utils.data.Dataset):
+        _mpr_patched = True
+
+        def __len__(self):
+            return 3
+
+        def __getitem__(self, i):
+            return i
+
+    class Other(VQADataset):
+        _mpr_patched = False
+
+    fake = FakeModel()
+    try:
+        dropin.patch_dataloader()
+        dropin.patch_dataloader()  # idempotent
+        LIVE_MODELS[id(fake)] = fake
+        assert [int(b) for b in DataLoader(VQADataset(), batch_size=1)] == [0, 1, 2]
+        assert hints == [0, 1, 2]
+        assert [int(b) for b in DataLoader(Other(), batch_size=1)] == [0, 1, 2]
+        fake.training = True  # a training loop is never hinted
+        assert [int(b) for b in DataLoader(VQADataset(), batch_size=1)] == [0, 1, 2]
+        assert hints == [0, 1, 2]
+    finally:
+        LIVE_MODELS.pop(id(fake), None)
+        DataLoader.__iter__ = saved
+        del DataLoader._mpr_orig_iter

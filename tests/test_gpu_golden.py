@@ -146,6 +146,7 @@ def test_g2_predict_many_matches_predict(device):
         b["question"] = [q + " which" * (i * k % 5) for k, q in enumerate(b0["question"])]
         batches.append(b)
     want = [model.predict(b) for b in batches]
+    want_ans = [retr.retrieve_closest_qa_pairs(b, return_ans=True) for b in batches]
     assert want[0] == j["predictions"]
     assert list(model.predict_many(batches)) == want
     for depth in (1, 3):  # decodes in flight on separate workspace slots
@@ -159,6 +160,22 @@ def test_g2_predict_many_matches_predict(device):
         assert list(model.predict_many(batches, decode_group=group)) == want
     assert list(model.predict_many(iter(batches[:1]))) == want[:1]
     assert list(model.predict_many([])) == []
+    # main.py-shaped loop with lookahead hints (serving.lookahead): the next batch's towers and
+    # scan run beside this batch's decode; every answer and the four analytics calls unchanged
+    from multimodalpromptretrieval_amd.serving import lookahead
+    for _ in range(2):
+        got = []
+        for b in lookahead(batches, model):
+            assert b is batches[len(got)]
+            got.append(model.predict(b))
+            assert retr.retrieve_closest_qa_pairs(b, return_ans=True) == want_ans[len(got) - 1]
+        assert got == want
+    assert not model._hints  # every hint consumed
+    model.hint_next(batches[2])  # a hinted batch predicted out of order, another never
+    assert model.predict(batches[1]) == want[1] and model.predict(batches[2]) == want[2]
+    model.train()
+    assert model.hint_next(batches[0]) is False  # no hints in training mode
+    model.eval()
 
 
 def test_g2_state_dict_roundtrip_refreshes_device_weights(device):

@@ -82,6 +82,12 @@ int main(int argc, char** argv) {
       {"x3 128x128 2x2 k16", launch_gemm_x3_group<128, 128, 2, 2, 16, 2, 1>},
       {"x3 128x128 2x1 8w k16 D2", launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1>},
       {"x3 128x128 2x1 8w k16 D3", launch_gemm_x3_group<128, 128, 2, 1, 16, 3, 1>},
+      {"x3 128x128 2x1 k16 ilv", launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 1>},
+      {"x3 128x128 2x1 k16 prio", launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>},
+      {"x3 128x128 2x1 k16 ilv+prio", launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 3>},
+      {"x3 64x128 k32 ilv", launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1, 1>},
+      {"x3 64x128 k32 prio", launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1, 2>},
+      {"x3 64x64 k16 prio", launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1, 2>},
       {"x3 128x64 1x1 8w k32 D2", launch_gemm_x3_group<128, 64, 1, 1, 32, 2, 1>},
       {"x3 64x128 1x1 8w k32 D2", launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>},
       {"x3 128x64 2x1 4w k16 D2", launch_gemm_x3_group<128, 64, 2, 1, 16, 2, 1>},
