@@ -623,7 +623,28 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
     }
   }
   const GemmArgs a = select_problem(grp, z);
-  const int bx = t / gy, by = t - bx * gy;
+  // Inside a problem the tiles go in bands of G row tiles, column-major inside a band, so the
+  // contiguous run of ~total/8 tiles an XCD gets is about sqrt(run) rows x sqrt(run) columns:
+  // its L2 then fetches ~2 sqrt(run) operand panels instead of all gy row panels plus run/gy
+  // column panels (plain column-major order).  The order changes which XCD computes a tile,
+  // never how: results are bit-identical.
+  const int gx = (int)cdiv(z == 0 ? grp.g[0].N : z == 1 ? grp.g[1].N : z == 2 ? grp.g[2].N
+                                                                       : grp.g[3].N, BN);
+  const int run = (total + 7) >> 3;
+  int G = 1;
+  while ((G + 1) * (G + 1) <= run) ++G;
+  G = G < gy ? G : gy;
+  const int full = gy / G * G, band = G * gx;
+  int bx, by;
+  if (t < (full / G) * band) {
+    const int gb = t / band, tt = t - gb * band;
+    bx = tt / G;
+    by = gb * G + (tt - bx * G);
+  } else {  // the last, shorter band
+    const int rem = gy - full, tt = t - (full / G) * band;
+    bx = tt / rem;
+    by = full + (tt - bx * rem);
+  }
   gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT, V>(a, bx, by, smem);
 }
 
