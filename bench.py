@@ -81,10 +81,11 @@ C5 = dict(N=1 << 20, D=512, B=256, k=5)
 def c5_scan(world, rank, device, group, rdev, iters=20):
     """Config C5's retrieval core: a 1,048,576 x 512 fp32 index row-sharded
     over the ranks (rows/W each, built on device from chunk-seeded streams, so the global index
-    is the same at every W), 256 queries in total (256/W per rank), k = 5.  One search = the
-    ShardedIndex exchange: all_gather of the query blocks, the local large-batch scan
-    (scan_mm_kernel), all_to_all of the per-shard top-k, merge.  Strong scaling (fixed index and
-    query set); the ids checksum is identical at every W."""
+    is the same at every W), one batch of 256 queries held by every rank, k = 5.  One search =
+    ShardedIndex.search_all: the local large-batch scan of the rank's shard (coarse bf16 scan +
+    exact re-rank), ONE all_gather of the per-shard top-k (north_star: RCCL all-gather over
+    xGMI), merge.  Strong scaling (fixed index and query batch); the ids checksum is identical at
+    every W."""
     from multimodalpromptretrieval_amd.distributed import ShardedIndex, shard_bounds
     from multimodalpromptretrieval_amd.index import DeviceIndex
     n, d, B, k = C5["N"], C5["D"], C5["B"], C5["k"]
@@ -92,21 +93,23 @@ def c5_scan(world, rank, device, group, rdev, iters=20):
     rows = syn.index_rows_device(7, lo, hi, d, device)
     gq = torch.Generator(device=device).manual_seed(8)
     q_all = torch.randn((B, d), device=device, generator=gq) * 0.3
-    bq = B // world
-    q = q_all[rank * bq:(rank + 1) * bq].contiguous()
+    q = q_all
+    six = ix = None
     if world > 1:
-        ix = ShardedIndex(rows, device, group=group, rows_are_local=True, row_offset=lo)
+        six = ShardedIndex(rows, device, group=group, rows_are_local=True, row_offset=lo)
+        search = six.search_all
     else:
         ix = DeviceIndex(rows, device)
+        search = ix.search
     del rows
     for _ in range(3):
-        ix.search(q, k)
+        search(q, k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
-        dist_k, ids = ix.search(q, k)
+        dist_k, ids = search(q, k)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     chk = torch.tensor([float(ids.sum())], device=rdev, dtype=torch.float64)
@@ -114,12 +117,13 @@ def c5_scan(world, rank, device, group, rdev, iters=20):
         t = torch.tensor([el], device=rdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        dist.all_reduce(chk)
+        dist.all_reduce(chk, op=dist.ReduceOp.MAX)  # every rank holds the whole result
     ms = el / iters * 1e3
     tf = 2.0 * n * d * B / (ms * 1e-3) / 1e12
-    del ix
+    search = six = ix = None
     torch.cuda.empty_cache()
-    return {"workload": "C5: 1,048,576 x 512 fp32 index, 256 queries, k=5, rows/W per rank",
+    return {"workload": "C5: 1,048,576 x 512 fp32 index, rows/W per rank; 256 queries on every "
+                        "rank, k=5, one all_gather of per-shard top-k",
             "ms_per_search": round(ms, 3), "queries_per_s": round(B / (ms * 1e-3), 1),
             "scan_tflops_aggregate": round(tf, 2), "scaling": "strong",
             "ids_checksum": int(chk.item())}

@@ -902,13 +902,35 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
   const float qn = (part[0] + part[1]) + (part[2] + part[3]);
   const float* sk = sel_key + (int64_t)qi * CB_C;
   const int64_t* si = sel_id + (int64_t)qi * CB_C;
+  // The bound (below): a candidate whose coarse key exceeds T = s~(k) + 2E has an exact key above
+  // the exact k-th best, so only the prefix of the sorted list with keys <= T is re-scored (a
+  // margin of 2^-16 relative keeps the excluded keys distinct from the k-th after the sqrt); the
+  // rest rank last with key +inf.  Typically k + a few of the CB_C rows are read.
+  const float qa = sqrtf(qn), ea = sqrtf((epart[0] + epart[1]) + (epart[2] + epart[3]));
+  const float Xm = sqrtf(xmax[0]), Rm = sqrtf(xmax[1]);
+  const float E = 2.0f * (ea * Xm + qa * Rm + ea * Rm + 2.0f * d * 5.9604645e-8f * (qa + ea) *
+                                                       (Xm + Rm)) * 1.01f +
+                  4.0f * 5.9604645e-8f * (Xm * Xm + 2.0f * qa * Xm + qa * qa);
+  // coarse values are quantised down by < 2^-16 relative (scan_bf_kernel's low-bit row tag)
+  const float T = sk[k - 1] * (1.0f + 3.0517578e-5f) + 2.0f * E;
+  const float Tcut = T * (1.0f + 1.5258789e-5f);
+  int need = 0;  // sorted keys: the count of keys <= Tcut is a prefix length
+  for (int c = lane; c < CB_C; c += 64) need += sk[c] <= Tcut ? 1 : 0;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) need += __shfl_xor(need, off, 64);
+  need = max(need, min(k, CB_C));
+  for (int c = need + tid; c < CB_C; c += 256) {
+    keys[c] = INFINITY;
+    ids[c] = INT64_MAX;
+  }
   // candidates round-robin over the 4 waves, 4 at a time with every load of the group in flight
   // (d <= 512: 8 components per lane), 64 lanes over the row
   constexpr int G = 4;
-  for (int c0 = wave * G; c0 < CB_C; c0 += 4 * G) {
+  for (int c0 = wave * G; c0 < need; c0 += 4 * G) {
     float xv[G][8];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+      if (c0 + g >= need) break;  // wave-uniform
       const int64_t id = si[c0 + g];
       const float* xp = X + (id >= 0 ? id - row_offset : 0) * (int64_t)d;
 #pragma unroll
@@ -920,6 +942,7 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int c = c0 + g;
+      if (c >= need) break;  // wave-uniform
       const int64_t id = si[c];
       float dot = 0.f;
 #pragma unroll
@@ -940,13 +963,6 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
   if (tid == 0) {
     int nvalid = 0;
     for (int c = 0; c < CB_C; ++c) nvalid += si[c] >= 0 ? 1 : 0;
-    const float qa = sqrtf(qn), ea = sqrtf((epart[0] + epart[1]) + (epart[2] + epart[3]));
-    const float X = sqrtf(xmax[0]), R = sqrtf(xmax[1]);
-    const float E = 2.0f * (ea * X + qa * R + ea * R + 2.0f * d * 5.9604645e-8f * (qa + ea) *
-                                                      (X + R)) * 1.01f +
-                    4.0f * 5.9604645e-8f * (X * X + 2.0f * qa * X + qa * qa);
-    // coarse values are quantised down by < 2^-16 relative (scan_bf_kernel's low-bit row tag)
-    const float T = sk[k - 1] * (1.0f + 3.0517578e-5f) + 2.0f * E;
     const float lists_last = fminf(fminf(lmin[0], lmin[1]), fminf(lmin[2], lmin[3]));
     const bool enough = (nvalid < CB_C || sk[CB_C - 1] > T) && lists_last > T;
     gate[qi] = enough ? 0 : 1;

@@ -8,7 +8,13 @@ retrieval step per batch:
                                                   its own b queries: [W, b, k];
   4. merge (libmpr topk_merge)                 -> [b, k], ties by lowest global id, so the result
                                                   is identical to the single-GPU scan.
-Messages are KB-scale (latency-bound over xGMI).  The collectives go through
+Messages are KB-scale (latency-bound over xGMI), so the candidates travel as ONE packed float64
+tensor (ids < 2^53 and fp32 distances are exact in float64), not a collective per field.
+
+``search_all`` is the replicated-query form (every rank holds the same query batch, as in
+config C5's 256-query batch): local scan of the whole batch, ONE all_gather of the per-shard
+top-k (the north_star's RCCL all-gather over xGMI), and every rank merges — one collective per
+search and no host synchronisation.  The collectives go through
 torch.distributed (backend "nccl" = RCCL on ROCm; "gloo" in the CPU tests, which inject a CPU
 searcher/merger so the sharding logic is exercised without a GPU).
 """
@@ -71,7 +77,6 @@ class ShardedIndex:
         equal sizes."""
         b = q.shape[0]
         bmax = self._max_batch(b)
-        kk = min(k, self.n_local)
         q = q.to(self.device, torch.float32).contiguous()
         if b < bmax:
             q = torch.cat([q, q.new_zeros((bmax - b, self.d))], 0)
@@ -80,22 +85,53 @@ class ShardedIndex:
         q_all = torch.empty((self.world * bmax, self.d), device=qx.device, dtype=qx.dtype)
         dist.all_gather_into_tensor(q_all, qx, group=self.group)
         q_all = q_all.to(self.device)
-        d_loc, i_loc = self._search(q_all, kk)                  # [W*bmax, kk]
-        if kk < k:                                              # tiny shard: pad with sentinels
+        d_loc, i_loc = self._padded_search(q_all, k)            # [W*bmax, k]
+        packed = self._pack(d_loc, i_loc)                       # [W*bmax, k, 2] float64
+        if stage:
+            packed = packed.cpu()
+        recv = torch.empty_like(packed)
+        dist.all_to_all_single(recv, packed, group=self.group)
+        d_recv, i_recv = self._unpack(recv.to(self.device))
+        # [W(src shard), bmax, k] -> this rank's b real queries: [b, W*k]
+        cd = d_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
+        ci = i_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
+        return self._merge(cd.contiguous(), ci.contiguous(), k)
+
+    def search_all(self, q: torch.Tensor, k: int):
+        """q: the SAME [B, d] query batch on every rank (replicated).  Returns (dist, ids)
+        [B, k] for the whole batch on every rank, identical to a single-GPU search: the local
+        scan of all B queries, one all_gather of the per-shard top-k, the merge."""
+        B = q.shape[0]
+        q = q.to(self.device, torch.float32).contiguous()
+        d_loc, i_loc = self._padded_search(q, k)                # [B, k]
+        packed = self._pack(d_loc, i_loc)                        # [B, k, 2]
+        stage = self._host_staged()
+        if stage:
+            packed = packed.cpu()
+        recv = torch.empty((self.world * B,) + tuple(packed.shape[1:]), dtype=packed.dtype,
+                           device=packed.device)
+        dist.all_gather_into_tensor(recv, packed, group=self.group)
+        d_all, i_all = self._unpack(recv.to(self.device).view(self.world, B, k, 2))  # [W, B, k]
+        cd = d_all.permute(1, 0, 2).reshape(B, self.world * k)
+        ci = i_all.permute(1, 0, 2).reshape(B, self.world * k)
+        return self._merge(cd.contiguous(), ci.contiguous(), k)
+
+    def _padded_search(self, q, k):
+        kk = min(k, self.n_local)
+        d_loc, i_loc = self._search(q, kk)
+        if kk < k:  # tiny shard: pad with sentinels
             pad = k - kk
             fill = float("inf") if self.metric == L2 else float("-inf")
             d_loc = torch.cat([d_loc, torch.full((d_loc.shape[0], pad), fill,
                                                  device=d_loc.device)], 1)
             i_loc = torch.cat([i_loc, torch.full((i_loc.shape[0], pad), -1, dtype=torch.int64,
                                                  device=i_loc.device)], 1)
-        if stage:
-            d_loc, i_loc = d_loc.cpu(), i_loc.cpu()
-        d_recv = torch.empty_like(d_loc)
-        i_recv = torch.empty_like(i_loc)
-        dist.all_to_all_single(d_recv, d_loc.contiguous(), group=self.group)
-        dist.all_to_all_single(i_recv, i_loc.contiguous(), group=self.group)
-        d_recv, i_recv = d_recv.to(self.device), i_recv.to(self.device)
-        # [W(src shard), bmax, k] -> this rank's b real queries: [b, W*k]
-        cd = d_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
-        ci = i_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
-        return self._merge(cd.contiguous(), ci.contiguous(), k)
+        return d_loc, i_loc
+
+    @staticmethod
+    def _pack(d, i):
+        return torch.stack([d.to(torch.float64), i.to(torch.float64)], -1).contiguous()
+
+    @staticmethod
+    def _unpack(p):
+        return p[..., 0].to(torch.float32), p[..., 1].to(torch.int64)

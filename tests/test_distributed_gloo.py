@@ -99,3 +99,39 @@ def test_shard_bounds_cover_rows():
         spans = [shard_bounds(n, w, r) for r in range(w)]
         assert spans[0][0] == 0 and spans[-1][1] == n
         assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def _worker_all(rank, world, port, n, d, B, k, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X = syn.index_rows(7, n, d)
+        q = syn.index_rows(9, B, d)   # the same batch on every rank (replicated queries)
+        six = ShardedIndex(X, "cpu", searcher=cpu_searcher, merger=cpu_merger)
+        out = [six.search_all(q, k)[1].tolist() for _ in range(2)]
+        result_q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,k", [(2, 1000, 5), (3, 1001, 3), (2, 9, 7)])
+def test_sharded_search_all_matches_single_index(world, n, k):
+    """Replicated queries (config C5's form): one all_gather of the per-shard top-k, merged on
+    every rank — every rank returns the single-index ids for the whole batch."""
+    d, B = 64, 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_all, args=(r, world, port, n, d, B, k, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = oret.topk_ids(oret.cdist(syn.index_rows(9, B, d), syn.index_rows(7, n, d)), k, False)
+    for r in range(world):
+        for ids in res[r]:
+            assert ids == ref.tolist()
