@@ -370,8 +370,10 @@ class T5VisionModel(nn.Module):
         s_main.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s_main), torch.no_grad():
             combined, mask, _ = self.prepare_input(batch, _pre=pre)
-            seqs = self.T5_model.generate(inputs_embeds=combined, attention_mask=mask,
-                                          do_sample=False, max_new_tokens=self.max_new_tokens)
+            # T5_model.generate (:200-205) hands back a device tensor as GenerationMixin does;
+            # the answers only need the host copy the device generate already made, so decode
+            # that one (batch_decode over a device tensor pays a D2H copy + sync per row)
+            seqs = self._device_t5().generate(combined, mask, self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     # ---- lookahead for batch-after-batch callers (main.py:262-263) ---------------------------
