@@ -16,6 +16,8 @@ affine paths are exercised.
 """
 from __future__ import annotations
 
+import functools
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -234,7 +236,10 @@ def answers(n: int, vocab: int = 50) -> list:
 # reference uses (clip.tokenize; T5Tokenizer.__call__/batch_decode/add_tokens/...).  Real
 # tokenizers are used automatically when `clip` / the hub checkpoint are available.
 
+@functools.lru_cache(maxsize=1 << 16)
 def _fnv1a(word: str) -> int:
+    # memoised: a stand-in for a compiled tokenizer should not cost Python loops per character
+    # on every call (the real T5 / CLIP tokenizers are native code)
     h = 0x811C9DC5
     for ch in word.encode("utf-8"):
         h = ((h ^ ch) * 0x01000193) & 0xFFFFFFFF
