@@ -179,6 +179,17 @@ int mpr_t5_generate_slot(mpr_model* m, int32_t slot, const float* embeds_dev,
                          const float* mask_dev, int32_t b, int32_t L, int32_t max_new,
                          int32_t decoder_start, int32_t eos, int32_t pad, int32_t* out_tokens_dev,
                          void* stream);
+/* mpr_t5_generate_slot that stops where GenerationMixin's greedy search stops: the decode loop
+ * runs as graphs of stop_chunk steps, and once every row has emitted eos no further chunk is
+ * launched (the columns of the steps not run stay pad, so out_tokens equals the full loop's).
+ * BLOCKS the host: before launching chunk c it waits for chunk c-2's flags.  *steps_run
+ * (optional) = decode steps launched (a multiple of stop_chunk, at most max_new).  Serves the
+ * one-batch predict() (architectures/T5VisionModel.py:200-205); serving loops keep the
+ * asynchronous calls. */
+int mpr_t5_generate_stop(mpr_model* m, int32_t slot, const float* embeds_dev,
+                         const float* mask_dev, int32_t b, int32_t L, int32_t max_new,
+                         int32_t decoder_start, int32_t eos, int32_t pad, int32_t stop_chunk,
+                         int32_t* out_tokens_dev, int32_t* steps_run, void* stream);
 /* Two batches (b_a, b_b <= 16 rows, own source lengths) generated with one shared decode loop of
  * b_a + b_b rows on workspace slot `slot`: each batch is encoded as mpr_t5_generate_slot would,
  * the greedy steps run once for both (every decode-step weight is read once per step for 32 rows

@@ -64,6 +64,9 @@ SIGNATURES = [
                                   c_int32, c_int32, c_int32, c_void_p, c_void_p]),
     ("mpr_t5_generate_slot", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                        c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    ("mpr_t5_generate_stop", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                       c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                                       POINTER(c_int32), c_void_p]),
     ("mpr_t5_generate_pair", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                        c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32,
                                        c_int32, c_int32, c_void_p, c_void_p, c_void_p]),

@@ -480,6 +480,21 @@ int mpr_t5_generate_slot(mpr_model* m, int32_t slot, const float* embeds, const 
   });
 }
 
+int mpr_t5_generate_stop(mpr_model* m, int32_t slot, const float* embeds, const float* mask,
+                         int32_t b, int32_t L, int32_t max_new, int32_t start, int32_t eos,
+                         int32_t pad, int32_t stop_chunk, int32_t* out_tokens,
+                         int32_t* steps_run, void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    MPR_REQUIRE(stop_chunk >= 1 && stop_chunk <= 512, "generate_stop: chunk %d", stop_chunk);
+    int steps = 0;
+    MPR_TRY(t5->generate_groups(1, &embeds, &mask, &b, &L, max_new, start, eos, pad, &out_tokens,
+                                S(stream), slot, stop_chunk, &steps));
+    if (steps_run) *steps_run = steps;
+    return MPR_OK;
+  });
+}
+
 int mpr_t5_generate_pair(mpr_model* m, int32_t slot, const float* embeds_a, const float* mask_a,
                          int32_t b_a, int32_t L_a, const float* embeds_b, const float* mask_b,
                          int32_t b_b, int32_t L_b, int32_t max_new, int32_t start, int32_t eos,

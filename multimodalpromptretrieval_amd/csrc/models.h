@@ -124,6 +124,10 @@ struct T5Work {
   std::map<GraphKey, GraphEnt> graphs;
   hipStream_t dec_stream = nullptr;  // not owned
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // early stop (generate_groups stop_chunk): per-chunk copies of the unfinished flags
+  int32_t* h_unf = nullptr;  // pinned host
+  size_t h_unf_n = 0;
+  std::vector<hipEvent_t> ev_chunk;
 };
 
 struct T5Model : mpr_model {
@@ -151,9 +155,14 @@ struct T5Model : mpr_model {
   // generate() of ng <= MAX_GROUPS independent batches (<= 16 rows each) with one shared
   // decode loop of up to 128 rows: each batch is encoded on its own (as generate() would), the
   // decode runs over all; every batch's tokens are bit-identical to its own generate() call.
+  // stop_chunk > 0: the decode runs as graphs of stop_chunk steps and no further chunk is
+  // launched once every row has emitted eos (GenerationMixin's stop; the host blocks on the
+  // chunk two behind the one it launches).  The skipped steps' columns stay pad, so the tokens
+  // equal the full loop's.  *steps_run (optional) = decode steps launched.
   int generate_groups(int ng, const float* const* embeds, const float* const* masks,
                       const int* Bs, const int* Ls, int max_new, int start, int eos, int pad,
-                      int32_t* const* outs, hipStream_t s, int slot = 0);
+                      int32_t* const* outs, hipStream_t s, int slot = 0, int stop_chunk = 0,
+                      int* steps_run = nullptr);
   int logits_tf(const float* embeds, const float* mask, int B, int L, const int32_t* dec_in,
                 int T, float* logits_out, hipStream_t s);
   int embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
@@ -168,7 +177,8 @@ struct T5Model : mpr_model {
   int cross_kv_project(int B, int L, hipStream_t s);
   int encode_body(int B, int L, int max_new, int start, hipStream_t s);
   int init_body(int B, int L, int max_new, int start, hipStream_t s);
-  int decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s);
+  int decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s, int t0 = 0,
+                  int t1 = -1);
   template <class F>
   int graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body);
 };

@@ -34,6 +34,8 @@ bool graphs_enabled() {
 
 T5Work::~T5Work() {
   for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
+  for (hipEvent_t e : ev_chunk) (void)hipEventDestroy(e);
+  if (h_unf) (void)hipHostFree(h_unf);
   if (cap_stream) (void)hipStreamDestroy(cap_stream);
   if (ev_fork) (void)hipEventDestroy(ev_fork);
   if (ev_join) (void)hipEventDestroy(ev_join);
@@ -168,7 +170,10 @@ int T5Model::init_body(int B, int L, int max_new, int start, hipStream_t s) {
   return MPR_OK;
 }
 
-int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s) {
+// Decode steps [t0, t1) of a max_new-step greedy loop (t1 < 0: to the end).
+int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s, int t0,
+                         int t1) {
+  if (t1 < 0 || t1 > max_new) t1 = max_new;
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
   const int nparts = (int)cdiv(V, 16);
@@ -183,7 +188,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
 
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
-  for (int t = 0; t < max_new; ++t) {
+  for (int t = t0; t < t1; ++t) {
     for (int l = 0; l < Ld; ++l) {
       const T5Layer& ly = *dec[l];
       float* cl = ws->cache.as<float>() + l * cache_layer;
@@ -277,8 +282,10 @@ int stage_rows(float* dst, const float* src, int B, int Lsrc, int Ldst, int64_t 
 
 int T5Model::generate_groups(int ng, const float* const* embeds, const float* const* masks,
                              const int* Bs, const int* Ls, int max_new, int start, int eos,
-                             int pad, int32_t* const* outs, hipStream_t s, int slot) {
+                             int pad, int32_t* const* outs, hipStream_t s, int slot,
+                             int stop_chunk, int* steps_run) {
   MPR_TRY(use_slot(slot));
+  if (steps_run) *steps_run = 0;
   MPR_REQUIRE(ng >= 1 && ng <= MAX_GROUPS, "t5 generate: %d batch groups (1 to %d)", ng,
               MAX_GROUPS);
   MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
@@ -400,8 +407,46 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     MPR_HIP(hipEventRecord(ws->ev_fork, s));
     MPR_HIP(hipStreamWaitEvent(ds, ws->ev_fork, 0));
   }
-  MPR_TRY(run(std::make_tuple(1, B, L, max_new, eos, pad), ds,
-              [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
+  if (stop_chunk <= 0 || max_new <= stop_chunk) {
+    MPR_TRY(run(std::make_tuple(1, B, L, max_new, eos, pad), ds,
+                [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
+    if (steps_run) *steps_run = max_new;
+  } else {
+    // Chunks of stop_chunk steps, each a graph of its own, and after each an async copy of the
+    // rows' unfinished flags.  Before launching chunk c the host waits for chunk c-2's flags
+    // (chunk c-1 keeps the GPU busy meanwhile) and stops once every row has finished.
+    const int nch = (int)cdiv(max_new, stop_chunk);
+    if (ws->h_unf_n < (size_t)nch * B) {
+      if (ws->h_unf) MPR_HIP(hipHostFree(ws->h_unf));
+      ws->h_unf = nullptr;
+      ws->h_unf_n = 0;
+      MPR_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws->h_unf), (size_t)nch * B * 4, 0));
+      ws->h_unf_n = (size_t)nch * B;
+    }
+    while ((int)ws->ev_chunk.size() < nch) {
+      hipEvent_t e;
+      MPR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ws->ev_chunk.push_back(e);
+    }
+    int launched = 0;
+    for (int c = 0; c < nch; ++c) {
+      if (c >= 2) {
+        MPR_HIP(hipEventSynchronize(ws->ev_chunk[c - 2]));
+        const int32_t* f = ws->h_unf + (size_t)(c - 2) * B;
+        bool any = false;
+        for (int r = 0; r < B && !any; ++r) any = f[r] != 0;
+        if (!any) break;
+      }
+      const int t0 = c * stop_chunk, t1 = std::min(max_new, t0 + stop_chunk);
+      MPR_TRY(run(std::make_tuple(100 + c, B, L, max_new * 1024 + stop_chunk, eos, pad), ds,
+                  [&](hipStream_t cs) { return decode_body(B, L, max_new, eos, pad, cs, t0, t1); }));
+      MPR_HIP(hipMemcpyAsync(ws->h_unf + (size_t)c * B, ws->unfinished.ptr, (size_t)B * 4,
+                             hipMemcpyDeviceToHost, ds));
+      MPR_HIP(hipEventRecord(ws->ev_chunk[c], ds));
+      launched = t1;
+    }
+    if (steps_run) *steps_run = launched;
+  }
   for (int k = 0; k < n; ++k)
     MPR_HIP(hipMemcpyAsync(gr[k].out, ws->tok_buf.as<int32_t>() + (int64_t)gr[k].row0 * T1,
                            (size_t)gr[k].B * T1 * 4, hipMemcpyDeviceToDevice, ds));

@@ -9,7 +9,9 @@ handed to the library once.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 
 import torch
 
@@ -219,10 +221,25 @@ class DeviceT5:
 
     def generate(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
                  eos_token_id=1, pad_token_id=0) -> torch.Tensor:
-        """GenerationMixin.generate(do_sample=False) result (int64, host, trimmed)."""
-        toks = self.generate_padded(embeds, mask, max_new_tokens, decoder_start_token_id,
-                                    eos_token_id, pad_token_id)
-        return self.trim(toks, eos_token_id)
+        """GenerationMixin.generate(do_sample=False) result (int64, host, trimmed).  Stops where
+        greedy search stops: the decode runs in chunks of MPR_EOS_STOP_CHUNK steps (default 2;
+        0 = one graph of all steps) and no chunk is launched once every row has emitted eos
+        (mpr_t5_generate_stop; the skipped columns are pad, as the full loop writes)."""
+        chunk = int(os.environ.get("MPR_EOS_STOP_CHUNK", "2"))
+        embeds_, mask_ = self._inputs(embeds, mask)
+        B, L, _ = embeds_.shape
+        if chunk <= 0 or B > 16 or max_new_tokens <= chunk:
+            toks = self.generate_padded(embeds, mask, max_new_tokens, decoder_start_token_id,
+                                        eos_token_id, pad_token_id)
+            self.last_steps_run = int(max_new_tokens)
+            return self.trim(toks, eos_token_id)
+        out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
+        steps = ctypes.c_int32(0)
+        _lib.call("mpr_t5_generate_stop", self._h, 0, _lib.ptr(embeds_), _lib.ptr(mask_), B, L,
+                  int(max_new_tokens), int(decoder_start_token_id), int(eos_token_id),
+                  int(pad_token_id), chunk, _lib.ptr(out), ctypes.byref(steps), self._stream())
+        self.last_steps_run = int(steps.value)
+        return self.trim(out, eos_token_id)
 
     def logits(self, embeds, mask, decoder_input_ids) -> torch.Tensor:
         embeds, mask = self._inputs(embeds, mask)
