@@ -17,9 +17,13 @@ The launcher installs two bindings, then executes ``main.py`` as ``__main__`` (r
   nothing (``weights_only=True``, a pickle reader that admits no globals), so caches the reference
   built are served and caches built here are the reference's.
 
-Evaluation loaders over a patched dataset are iterated one batch ahead (``serving.lookahead``):
-while the model is in eval mode (main.py:234), each next batch's towers and index scan are
-enqueued before the current batch is handed to ``predict()``, so they overlap its T5 decode.
+Evaluation loaders over a patched dataset are iterated with the serving loop running ahead
+(``serving.pipelined``): while the model is in eval mode (main.py:234), ``predict(batch)`` returns
+the answers a ``ServingLoop`` over the same batches computed (towers two batches per pass, decode
+groups of up to 8 batches), and the four analytics calls per batch reuse that batch's search.
+Batches, their order and every result are unchanged.  ``MPR_MAIN_PIPELINE=lookahead`` iterates
+one batch ahead instead (``serving.lookahead``: the next batch's towers and scan beside this
+batch's decode), ``=off`` not at all.
 
 The prediction-head variants (``main.py:132-139``; SURVEY.md §2 "OUT") keep the reference's own
 class: their modules are imported (binding the original base class) before the swap.
@@ -105,10 +109,10 @@ def _eval_model():
 
 
 def patch_dataloader() -> None:
-    """Iterate DataLoaders over a patched reference dataset one batch ahead
-    (``serving.lookahead``) while a device model is in eval mode (main.py:234 then the test loop
-    at :262-263): each batch's towers and index scan are enqueued while the previous batch's
-    T5 decode runs.  The batches, their order and every result are unchanged."""
+    """Iterate DataLoaders over a patched reference dataset through the serving loop
+    (``serving.pipelined``; MPR_MAIN_PIPELINE=lookahead: one batch ahead, ``serving.lookahead``;
+    =off: plain) while a device model is in eval mode (main.py:234 then the test loop at
+    :262-270).  The batches, their order and every result are unchanged."""
     from torch.utils.data import DataLoader
     if getattr(DataLoader, "_mpr_orig_iter", None) is not None:
         return
@@ -118,9 +122,10 @@ def patch_dataloader() -> None:
         it = orig(self)
         if getattr(type(self.dataset), "_mpr_patched", False):
             m = _eval_model()
-            if m is not None:
-                from .serving import lookahead
-                return lookahead(it, m)
+            mode = os.environ.get("MPR_MAIN_PIPELINE", "serving")
+            if m is not None and mode != "off":
+                from .serving import lookahead, pipelined
+                return lookahead(it, m) if mode == "lookahead" else pipelined(it, m)
         return it
 
     DataLoader._mpr_orig_iter = orig

@@ -113,8 +113,46 @@ def test_lookahead_hints_one_batch_ahead_in_order():
     assert list(lookahead([], FakeModel())) == []
 
 
-def test_dataloader_patch_wraps_only_patched_datasets_in_eval_mode():
+def test_pipelined_hands_out_batches_in_order_with_the_loops_answers(monkeypatch):
+    """serving.pipelined: the caller gets every batch in order; a batch's answers come from the
+    serving loop, pumped only as far as that batch (the loop pulls batches ahead of the caller:
+    here decode groups of 3)."""
+    from multimodalpromptretrieval_amd import serving
+    pulled = []
+
+    class FakeLoop:
+        def __init__(self, m, o):
+            pass
+
+        def run(self, batches):
+            buf = []
+            for b in batches:
+                pulled.append(b["id"])
+                buf.append(b)
+                if len(buf) == 3:
+                    yield from (f"ans{x['id']}" for x in buf)
+                    buf = []
+            yield from (f"ans{x['id']}" for x in buf)
+
+    monkeypatch.setattr(serving, "ServingLoop", FakeLoop)
+
+    class M:
+        training = False
+
+    m = M()
+    batches = [{"image": object(), "id": i} for i in range(7)]
+    out = []
+    for b in serving.pipelined(batches, m, serving.ServingOptions.resolve()):
+        pipe = m._pipes.pop(id(b["image"]))
+        out.append((b["id"], pipe.answers_for(b), len(pulled)))
+    assert [o[:2] for o in out] == [(i, f"ans{i}") for i in range(7)]
+    assert [o[2] for o in out] == [3, 3, 3, 6, 6, 6, 7]  # pumped one decode group at a time
+    assert pipe.answers_for({"image": object()}) is None  # never fed: predict() runs as usual
+
+
+def test_dataloader_patch_wraps_only_patched_datasets_in_eval_mode(monkeypatch):
     from torch.utils.data import DataLoader
+    monkeypatch.setenv("MPR_MAIN_PIPELINE", "lookahead")
 
     from multimodalpromptretrieval_amd.model import LIVE_MODELS
     saved = DataLoader.__iter__

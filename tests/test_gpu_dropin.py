@@ -41,11 +41,13 @@ class VQASLAKEFeatureDataset:
         self.device = device
 
 
-def _run_main_loop(ds, model, ahead=False):
-    from multimodalpromptretrieval_amd.serving import lookahead
+def _run_main_loop(ds, model, ahead=None):
+    from multimodalpromptretrieval_amd.serving import lookahead, pipelined
     out = []
     batches = gi.g9_test_batches()
-    for batch in (lookahead(batches, model) if ahead else batches):
+    it = {None: lambda: batches, "lookahead": lambda: lookahead(batches, model),
+          "serving": lambda: pipelined(batches, model)}[ahead]()
+    for batch in it:
         rec = {"predictions": model.predict(batch),
                "retrieved_answers": ds.retrieve_closest_qa_pairs(batch, return_ans=True),
                "retrieved_answer_types": ds.retrieve_closest_qa_pairs(
@@ -95,8 +97,10 @@ def test_main_loop_through_dropin_binding(device, tmp_path, monkeypatch):
                           retrieval_function=ds.retrieve_closest_qa_pairs).eval()
     assert model._retrieval_obj() is ds._mpr_retrieval     # the paired tower path is taken
     _check(_run_main_loop(ds, model), want)
-    # the launcher's evaluation loop: batches one ahead (dropin.patch_dataloader)
-    _check(_run_main_loop(ds, model, ahead=True), want)
+    # the launcher's evaluation loops (dropin.patch_dataloader): the serving loop running ahead
+    # (default), and one batch ahead
+    _check(_run_main_loop(ds, model, ahead="serving"), want)
+    _check(_run_main_loop(ds, model, ahead="lookahead"), want)
     assert not model._hints
 
     # a reference-built cache is served as is (no encoding)
