@@ -24,7 +24,9 @@ namespace mpr {
 
 namespace {
 constexpr float T5_EPS = 1e-6f;
-constexpr size_t MAX_GRAPHS = 64;
+// per workspace slot: an eval run meets a handful of bucketed source lengths, each with an encoder
+// graph, a decode graph and (early-stop generate) max_new / chunk decode-chunk graphs
+constexpr size_t MAX_GRAPHS = 256;
 
 bool graphs_enabled() {
   const char* e = getenv("MPR_GRAPHS");
