@@ -165,6 +165,42 @@ def build(cfg, device, group):
     return model, retr, (retr_sd, tok_sd, t5_sd, X, info)
 
 
+def decode_chain(model, batch, steps: int = 20, iters: int = 10):
+    """The greedy decode of one 16-row batch (architectures/T5VisionModel.py:200-205), timed on
+    its own with hipEvents: generate (encoder + cross K/V + 20 steps, graph replays) minus the same
+    call with 0 steps.  Its roofline: every step streams the decoder's weights and the tied
+    lm_head once (fp32), so bytes/step = 4 (Ld (6 d inner + 2 d dff) + V d)."""
+    dev = model._device_t5()
+    with torch.no_grad():
+        emb, mask, _ = model.prepare_input(batch)
+
+    def timed(n):
+        dev.generate_padded(emb, mask, n)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(iters):
+            dev.generate_padded(emb, mask, n)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters
+
+    full, enc = timed(steps), timed(0)
+    dec_ms = full - enc
+    per_step = 4.0 * (dev.n_dec * (6 * dev.d_model * dev.inner + 2 * dev.d_model * dev.d_ff)
+                      + dev.vocab * dev.d_model)
+    gbs = per_step * steps / (dec_ms * 1e-3) / 1e9
+    return {"rows": int(emb.shape[0]), "steps": steps, "ms_per_generate": round(full, 3),
+            "encoder_ms": round(enc, 3), "decode_ms": round(dec_ms, 3),
+            "us_per_step": round(dec_ms * 1e3 / steps, 1), "launches_per_step": 6 * 8 + 2,
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "algorithmic_mb_per_step": round(per_step / 1e6, 1)},
+            "note": f"a chain of 50 dependent launches per step "
+                    f"({dec_ms * 1e3 / steps / 50:.1f} us each): latency-bound, not "
+                    f"bandwidth-bound (DESIGN.md §3, the decode chain)"}
+
+
 def index_build(cfg, weights, device, n_batches: int = 48):
     """VQARetrieval.create_retrieval_dataset (dataset/VQAFeatureDataset.py
     :118-185) over a loader of synthetic batches — the retrieval ViT (CLS) + CLIP text towers per
@@ -409,6 +445,7 @@ def main():
     run(args.steps, main=True)
     torch.cuda.synchronize()
     main_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    decode = decode_chain(model, batches[0]) if rank == 0 else None
 
     roofline = None
     if not args.no_probe:
@@ -488,6 +525,7 @@ def main():
             "sync_ms_per_step": round(sync_ms, 3),
             "lookahead_ms_per_step": round(ahead_ms, 3),
             "main_loop_ms_per_step": round(main_ms, 3),
+            "decode": decode,
             "sync_note": "sync: predict() one batch at a time, nothing enqueued ahead; "
                          "lookahead: the same predict() calls with the batches iterated through "
                          "serving.lookahead (one batch ahead); main_loop: main.py's test loop "
