@@ -1042,7 +1042,7 @@ const bool g_ksplit32_only = [] {
 // X3_TALL (16-deep k steps in order, KW = 1) every output element is accumulated in the same
 // order whatever the block tile, so the tile may follow the launch (grouped or alone, one batch
 // or two concatenated: bit-identical results).
-enum GemmKind : int { F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3 };
+enum GemmKind : int { F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3, X3_SMALL = 4 };
 
 const bool g_gemm_f32 = [] {
   const char* e = getenv("MPR_GEMM");
@@ -1073,6 +1073,7 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
           return launch_gemm_group<64, 32, 1, 1, 64, 2, 4>(g, s);
         return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
       case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>(g, s);
+      case X3_SMALL: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>(g, s);
       default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);
     }
   });
@@ -1113,16 +1114,27 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // smaller tiles (ViT out 1600x768x768 x2 + text: 41.3 us against 50.6 for 64x64 blocks and 60.6
   // for the f32 kernel; qkv 106 vs 158, fc1 140 vs 196, fc2 137 vs 178) — else 64x128 blocks of 8
   // waves of 32x32 (one-batch fc2 800x768x3072 x2 + text: 93.7 vs 114 us f32).
+  // Below that, 64x64 blocks (4 waves) when the 64x128 grid would leave half the CUs idle or
+  // every K is short (tools/x3small_bench.hip, one-batch T5 encoder at M = 1440: qkv 37.2 ->
+  // 25.8 us, o 18.0 -> 14.6, wo 52.1 -> 43.5; the one-batch ViT out / fc2, K >= 768 with 156+
+  // 64x128 blocks, stay on 64x128).  Same k order in every tile: bit-identical results.
   GemmGroup fam;
   fam.n = 0;
-  int64_t b128 = 0;
+  int64_t b128 = 0, b64x128 = 0;
+  bool short_k = true;
   for (int i = 0; i < g.n; ++i) {
     const GemmArgs& a = g.g[i];
     if (a.M == 0 || a.N == 0) continue;
     fam.g[fam.n++] = a;
     b128 += cdiv(a.M, 128) * cdiv(a.N, 128);
+    b64x128 += cdiv(a.M, 64) * cdiv(a.N, 128);
+    short_k = short_k && a.K <= 512;
   }
-  if (fam.n) MPR_TRY(gemm_launch(fam, b128 >= 160 ? X3_WIDE : X3_TALL, s));
+  if (fam.n)
+    MPR_TRY(gemm_launch(fam, b128 >= 160                     ? X3_WIDE
+                             : (b64x128 < 128 || short_k) ? X3_SMALL
+                                                          : X3_TALL,
+                        s));
   return MPR_OK;
 }
 
