@@ -445,7 +445,8 @@ def main():
     run(args.steps, main=True)
     torch.cuda.synchronize()
     main_ms = (time.perf_counter() - t1) / args.steps * 1e3
-    decode = decode_chain(model, batches[0]) if rank == 0 else None
+    # every rank (its prepare_input searches a sharded index collectively); rank 0 reports
+    decode = decode_chain(model, batches[0])
 
     roofline = None
     if not args.no_probe:
