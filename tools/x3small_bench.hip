@@ -62,6 +62,9 @@ int main() {
       {"t5 crosskv 1440x6144x512", 1440, 6144, 512, 1},
       {"vit out 800x768x768 x2", 800, 768, 768, 2},  {"vit fc2 800x768x3072 x2", 800, 768, 3072, 2},
       {"vit qkv 800x2304x768 x2", 800, 2304, 768, 2}, {"vit fc1 800x3072x768 x2", 800, 3072, 768, 2},
+      {"vit qkv 1600x2304x768 x2", 1600, 2304, 768, 2},
+      {"vit fc1 1600x3072x768 x2", 1600, 3072, 768, 2},
+      {"t5 wi 5760x2048x512", 5760, 2048, 512, 1}, {"t5 qkv 5760x1536x512", 5760, 1536, 512, 1},
   };
   using L = std::function<int(const GemmGroup&, hipStream_t)>;
   struct Var { const char* name; L fn; };
@@ -72,6 +75,9 @@ int main() {
       {"64x64 k16", launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>},
       {"32x64 k32", launch_gemm_x3_group<32, 64, 1, 1, 32, 2, 1>},
       {"64x32 k32", launch_gemm_x3_group<64, 32, 1, 1, 32, 2, 1>},
+      {"128x128 2x2 4w k16", launch_gemm_x3_group<128, 128, 2, 2, 16, 2, 1>},
+      {"128x128 2x2 4w k16 prio", launch_gemm_x3_group<128, 128, 2, 2, 16, 2, 1, 2>},
+      {"128x128 2x2 4w k32 prio", launch_gemm_x3_group<128, 128, 2, 2, 32, 2, 1, 2>},
   };
   for (const Shape& sh : shapes) {
     GemmGroup G;
