@@ -222,10 +222,11 @@ class DeviceT5:
     def generate(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
                  eos_token_id=1, pad_token_id=0) -> torch.Tensor:
         """GenerationMixin.generate(do_sample=False) result (int64, host, trimmed).  Stops where
-        greedy search stops: the decode runs in chunks of MPR_EOS_STOP_CHUNK steps (default 2;
+        greedy search stops: the decode runs in chunks of MPR_EOS_STOP_CHUNK steps (default 4:
+        no cost measurable against one graph, tools/eos_chunk_ab.py, where 2 cost ~0.07 ms;
         0 = one graph of all steps) and no chunk is launched once every row has emitted eos
         (mpr_t5_generate_stop; the skipped columns are pad, as the full loop writes)."""
-        chunk = int(os.environ.get("MPR_EOS_STOP_CHUNK", "2"))
+        chunk = int(os.environ.get("MPR_EOS_STOP_CHUNK", "4"))
         embeds_, mask_ = self._inputs(embeds, mask)
         B, L, _ = embeds_.shape
         if chunk <= 0 or B > 16 or max_new_tokens <= chunk:
