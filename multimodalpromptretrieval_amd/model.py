@@ -264,7 +264,7 @@ class T5VisionModel(nn.Module):
         other = vit if self.use_image_info and self._pairable(retr, vit) else None
         return fn(batches, other, TOKENS, slot)
 
-    def prepare_input(self, batch, _pre=None):
+    def prepare_input(self, batch, _pre=None, _handles=None):
         """architectures/T5VisionModel.py:141-184.
 
         The token-feature ViT does not depend on retrieval, so it is enqueued first on a side
@@ -272,8 +272,9 @@ class T5VisionModel(nn.Module):
         builds and tokenises the prompts.  With a ``VQARetrieval`` retrieval function whose
         image tower has this tower's geometry, both ViTs run as one paired pass (their
         projections share launches; results identical to separate calls)."""
-        vit = self._device_vit()
-        t5 = self._device_t5()
+        # (_handles: the device models predict() already fetched — each fetch checks every
+        # parameter for updates, ~0.1 ms of host time on the GPU's critical path)
+        vit, t5 = _handles if _handles is not None else (self._device_vit(), self._device_t5())
         if self.use_image_info and vit.out_dim != t5.d_model:
             raise RuntimeError(f"Sizes of tensors must match: image tokens are {vit.out_dim}-d, "
                                f"{self.T5_version} d_model is {t5.d_model} (torch.cat at "
@@ -373,12 +374,13 @@ class T5VisionModel(nn.Module):
             # happened to map onto the 4 hardware queues; MPR_PREDICT_STREAM=private restores it).
             s_main = self._predict_stream()
         s_main.wait_stream(torch.cuda.current_stream(self.device))
+        handles = (self._device_vit(), self._device_t5())
         with torch.cuda.stream(s_main), torch.no_grad():
-            combined, mask, _ = self.prepare_input(batch, _pre=pre)
+            combined, mask, _ = self.prepare_input(batch, _pre=pre, _handles=handles)
             # T5_model.generate (:200-205) hands back a device tensor as GenerationMixin does;
             # the answers only need the host copy the device generate already made, so decode
             # that one (batch_decode over a device tensor pays a D2H copy + sync per row)
-            seqs = self._device_t5().generate(combined, mask, self.max_new_tokens)
+            seqs = handles[1].generate(combined, mask, self.max_new_tokens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     # ---- lookahead for batch-after-batch callers (main.py:262-263) ---------------------------
