@@ -254,13 +254,8 @@ def role_stream(device, role: str):
     words = (total + 31) // 32
     h = c_void_p()
     with torch.cuda.device(idx):
-        ahead = int(os.environ.get("MPR_AHEAD_CUS", "0")) if role == "encode:towers1" else 0
-        if ahead and not n:  # experiment: lookahead towers leave the first `ahead` CUs free
-            n, role_bits = ahead, range(ahead, total)
-        else:
-            role_bits = None
         if n:
-            bits = role_bits or (range(0, n) if role == "decode" else range(n, total))
+            bits = range(0, n) if role == "decode" else range(n, total)
             mask = (ctypes.c_uint32 * words)()
             for b in bits:
                 mask[b // 32] |= 1 << (b % 32)
