@@ -76,6 +76,7 @@ class VQARetrieval:
     """Retrieval index + CLIP query encoders on one GPU (or sharded over a process group)."""
 
     RECENT = 64  # searches kept per batch key (a serving loop ahead of main.py's analytics)
+    BUILD_SLOTS = min(2, int(os.environ.get("MPR_BUILD_SLOTS", "2")))  # index build passes in flight
 
     def __init__(self, device="cuda", clip_state_dict: dict = None, clip_tokenizer=None,
                  metric: int = L2, group=None):
@@ -254,10 +255,12 @@ class VQARetrieval:
         cur.wait_stream(s_img)
         return q
 
-    def _encode_two(self, b0, b1) -> torch.Tensor:
-        """encode_queries of two equal-sized batches in one tower pass: rows [b0 ; b1]."""
+    def _encode_two(self, b0, b1, slot: int = 0, join: bool = True) -> torch.Tensor:
+        """encode_queries of two equal-sized batches in one tower pass: rows [b0 ; b1], on
+        tower workspace ``slot`` and its stream (join=False: the caller's stream is not made to
+        wait for it; the caller joins ``self._slot_stream(slot)`` itself)."""
         cur = torch.cuda.current_stream(self.device)
-        s_img = self._streams()
+        s_img = self._slot_stream(slot)
         img = torch.cat([b["image"].to(self.device, torch.float32, non_blocking=True)
                          for b in (b0, b1)])
         toks = [self.clip_tokenize(b["question"]) for b in (b0, b1)]
@@ -271,8 +274,9 @@ class VQARetrieval:
             encode_towers_multi(self.image_encoder, img, CLS, out_a=q,
                                 out_a_bstride=self.embed_dim, text=self.text_encoder,
                                 tokens=toks, out_t=[q[:n, di:], q[n:, di:]],
-                                out_t_bstride=[self.embed_dim] * 2)
-        cur.wait_stream(s_img)
+                                out_t_bstride=[self.embed_dim] * 2, slot=slot)
+        if join:
+            cur.wait_stream(s_img)
         return q
 
     # ---- index -------------------------------------------------------------------------------
@@ -311,8 +315,12 @@ class VQARetrieval:
         info = {"question_type": [], "question_id": [], "question": []}
         # query rows stay on the device until the end: the host never waits on a batch, so
         # the tower passes of consecutive batches queue back to back on the GPU; two equal-sized
-        # batches share one pass (twice the GEMM rows, every row bit-identical)
+        # batches share one pass (twice the GEMM rows, every row bit-identical), and consecutive
+        # passes alternate between two tower workspace slots and their streams, so one pass's
+        # under-filled launches (the 768-column GEMMs, attention, norms) overlap the next's
         pend = None
+        npass = 0
+        used = set()
         for batch in data_loader:
             answers.extend(batch["answer"])
             info["question_type"].extend(batch["question_type"])
@@ -321,13 +329,20 @@ class VQARetrieval:
             if pend is None:
                 pend = batch
             elif pend["image"].shape[0] == batch["image"].shape[0]:
-                embs.append(self._encode_two(pend, batch))
+                # slots 0 and 2: a pass's two text runs use text workspaces slot and slot + 1
+                slot = 2 * (npass % self.BUILD_SLOTS)
+                embs.append(self._encode_two(pend, batch, slot=slot, join=False))
+                used.add(slot)
+                npass += 1
                 pend = None
             else:
                 embs.append(self.encode_queries(pend))
                 pend = batch
         if pend is not None:
             embs.append(self.encode_queries(pend))
+        cur = torch.cuda.current_stream(self.device)
+        for slot in used:
+            cur.wait_stream(self._slot_stream(slot))
         emb = (torch.cat(embs, 0) if embs else
                torch.empty((0, self.embed_dim), device=self.device)).cpu()
         return emb, answers, info
