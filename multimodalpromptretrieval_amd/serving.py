@@ -56,7 +56,8 @@ class ServingOptions:
                               decode_group=max(1, min(int(decode_group), 8)),
                               lookahead=bool(lookahead),
                               tower_batches=max(1, min(int(tower_batches), 2)),
-                              tower_slots=max(1, min(int(tower_slots), 4)))
+                              tower_slots=max(1, min(int(tower_slots),
+                                                     4 // max(1, min(int(tower_batches), 2)))))
 
 
 class ServingLoop:
@@ -97,7 +98,9 @@ class ServingLoop:
                 m = self.m
                 m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
                 with torch.cuda.stream(m._s_prep):
-                    pres = m._prefetch(chunk, self.passes % self.o.tower_slots)
+                    # a pass on slot s uses text workspaces s .. s + per_pass - 1: passes in
+                    # flight together must not share one, so slots step by per_pass
+                    pres = m._prefetch(chunk, (self.passes % self.o.tower_slots) * per_pass)
                 self.passes += 1
             else:
                 pres = [None] * len(chunk)

@@ -171,6 +171,17 @@ def test_g2_predict_many_matches_predict(device):
             assert retr.retrieve_closest_qa_pairs(b, return_ans=True) == want_ans[len(got) - 1]
         assert got == want
     assert not model._hints  # every hint consumed
+    # main.py-shaped loop through serving.pipelined (the dropin launcher's default): a serving
+    # loop runs ahead, predict() returns its answers, the analytics reuse each batch's search
+    from multimodalpromptretrieval_amd.serving import ServingOptions, pipelined
+    for slots in (1, 2):
+        got = []
+        opts = ServingOptions.resolve(tower_slots=slots)
+        for b in pipelined(batches, model, opts):
+            assert b is batches[len(got)]
+            got.append(model.predict(b))
+            assert retr.retrieve_closest_qa_pairs(b, return_ans=True) == want_ans[len(got) - 1]
+        assert got == want
     model.hint_next(batches[2])  # a hinted batch predicted out of order, another never
     assert model.predict(batches[1]) == want[1] and model.predict(batches[2]) == want[2]
     model.train()
