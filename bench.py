@@ -185,7 +185,10 @@ def decode_chain(model, batch, steps: int = 20, iters: int = 10):
         e1.synchronize()
         return e0.elapsed_time(e1) / iters
 
-    full, enc = timed(steps), timed(0)
+    # best of 3 for each: one stray host stall inside a 10-call window otherwise lands in one
+    # of the two numbers and skews the difference
+    full = min(timed(steps) for _ in range(3))
+    enc = min(timed(0) for _ in range(3))
     dec_ms = full - enc
     per_step = 4.0 * (dev.n_dec * (6 * dev.d_model * dev.inner + 2 * dev.d_model * dev.d_ff)
                       + dev.vocab * dev.d_model)

@@ -738,7 +738,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   float(*ssq_s)[MROWS] = reinterpret_cast<float(*)[MROWS]>(smem + XS);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
-  const int M = a.M, N = a.N, K = a.K;
+  // blockIdx.y = a block of MROWS rows (a grouped decode's rows split over blocks); rows are
+  // independent, so each row's sums keep their order whatever the split
+  const int row0 = blockIdx.y * MROWS;
+  const float* __restrict__ Ab = a.A + (int64_t)row0 * a.lda;
+  const int M = min(a.M - row0, MROWS), N = a.N, K = a.K;
   const int i = lane & 15, h = lane >> 4;
 
   const int nchunk = (K + 15) / 16;
@@ -759,7 +763,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   f32x4 rres = {0.f, 0.f, 0.f, 0.f};
   if constexpr (RES) {
     if (wave < NT * MR)
-      rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)min(er * 16 + i, M - 1) * a.ldr +
+      rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)(row0 + min(er * 16 + i, M - 1)) * a.ldr +
                                              (blockIdx.x * NT + et) * 16 + h * 4);
   }
   f32x4 acc[NT][MR][2];
@@ -787,7 +791,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     for (int u = 0; u < MR * MAXC; ++u) {
       const int q = u * 64 + lane, row = q / (4 * MAXC), col = c0 * 16 + (q % (4 * MAXC)) * 4;
       const bool ok = row < M && col < c_hi * 16 && col < K;
-      xr[u] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
+      xr[u] = *reinterpret_cast<const f32x4*>(Ab + (int64_t)min(row, M - 1) * a.lda +
                                               min(col, K - 4));
       if (!ok) xr[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -873,9 +877,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
         bi = oi;
       }
     }
-    if (lane < 16 && n0 < N) {  // row-major [rows][ntiles]: greedy_step reads rows coalesced
-      sa.amax_val[(int64_t)m * ntiles + tile] = bv;
-      sa.amax_idx[(int64_t)m * ntiles + tile] = bi;
+    if (lane < 16 && n0 < N && m < M) {  // row-major [rows][ntiles]: greedy_step reads rows
+      sa.amax_val[(int64_t)(row0 + m) * ntiles + tile] = bv;  // coalesced
+      sa.amax_idx[(int64_t)(row0 + m) * ntiles + tile] = bi;
     }
   } else {
     f32x4 v = sum * scale;
@@ -884,7 +888,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
     }
     if constexpr (RES) v = rres + v;
-    if (m < M) *reinterpret_cast<f32x4*>(a.C + (int64_t)m * a.ldc + n0 + h * 4) = v;
+    if (m < M) *reinterpret_cast<f32x4*>(a.C + (int64_t)(row0 + m) * a.ldc + n0 + h * 4) = v;
   }
 }
 
@@ -1163,10 +1167,10 @@ int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, h
 }
 
 template <int MAXC, int NT, bool LOOP, int MR = 1>
-void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s) {
+void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, unsigned gy = 1) {
 #define MPR_SK(f)                                                                          \
   case f:                                                                                  \
-    hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP, MR>), dim3(grid), dim3(512), 0, s, sa); \
+    hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP, MR>), dim3(grid, gy), dim3(512), 0, s, sa); \
     break;
   if constexpr (NT > 1) {
     switch (F) { MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS) default: break; }
@@ -1203,6 +1207,14 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
                 (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0);
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
+  // Above 32 rows (grouped decodes) the rows split over blocks of MPR_SKINNY_ROWS (16 default,
+  // or 32; 0 = one block column holds all rows, MR up to 8).  Serving loop, 20 steps: 3783-3831
+  // (0) -> 3893-3908 (32) / 3913-3932 (16) QA pairs/s; the 128-row o-proj 17.9 us at 32 blocks.
+  static const int row_blk = [] {
+    const char* e = getenv("MPR_SKINNY_ROWS");
+    const int v = e ? atoi(e) : 16;
+    return v == 16 || v == 32 ? v : 0;
+  }();
   static const bool small_lds = [] {
     const char* e = getenv("MPR_SKINNY_SMALL");
     return e && e[0] == '1';
@@ -1229,7 +1241,30 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
       MPR_LAUNCHED();
       return MPR_OK;
     }
-    if (a.M > 64) {  // eight row groups per weight load (up to 8 batches): 2-chunk passes fit
+    if (a.M > 32 && row_blk > 0) {  // rows split over blocks of row_blk rows (grouped decodes)
+      const unsigned gy = (unsigned)cdiv(a.M, row_blk);
+      if (row_blk == 16) {
+        if (amax && tiles >= 1024 && per <= 4)
+          launch_skinny<4, 2, false>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
+        else if (per <= 4)
+          launch_skinny<4, 1, false>(sa, F, (unsigned)tiles, s, gy);
+        else if (per <= 8)
+          launch_skinny<8, 1, false>(sa, F, (unsigned)tiles, s, gy);
+        else if (per <= 16)
+          launch_skinny<16, 1, false>(sa, F, (unsigned)tiles, s, gy);
+        else
+          launch_skinny<16, 1, true>(sa, F, (unsigned)tiles, s, gy);
+      } else {
+        if (amax && tiles >= 1024 && per <= 4)
+          launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
+        else if (per <= 4)
+          launch_skinny<4, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
+        else if (per <= 8)
+          launch_skinny<8, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
+        else
+          launch_skinny<8, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
+      }
+    } else if (a.M > 64) {  // eight row groups per weight load (up to 8 batches): 2-chunk passes fit
       // (one tile per block also for the lm_head: two would spill registers)
       if (per <= 2)
         launch_skinny<2, 1, false, 8>(sa, F, (unsigned)tiles, s);
