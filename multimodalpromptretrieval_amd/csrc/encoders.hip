@@ -16,6 +16,14 @@ namespace mpr {
 
 namespace {
 constexpr float CLIP_LN_EPS = 1e-5f;
+// MPR_POOL_LAST=0: the last block of pooled towers over every row (A/B; TowerRun::pool)
+bool pool_last() {
+  static const bool on = [] {
+    const char* e = getenv("MPR_POOL_LAST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 }
 
 int ClipTower::load_blocks(const float* const* t, int w, int nl) {
@@ -59,7 +67,8 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
     MPR_TRY(w.ao.ensure(M * W * 4));
     MPR_TRY(w.mlp.ensure(M * 4 * W * 4));
   }
-  for (int l = 0; l < r[0].t->layers; ++l) {
+  const int nl = r[0].t->layers;
+  for (int l = 0; l < nl; ++l) {
     GemmGroup gq, go, gf, gp;
     gq.n = go.n = gf.n = gp.n = n;
     for (int i = 0; i < n; ++i) {
@@ -85,6 +94,16 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       pj.bias = b.pj_b.as<float>(); pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M;
       pj.N = W; pj.K = 4 * W;
       g.tile_m = o.tile_m = f.tile_m = pj.tile_m = TM;
+      if (l == nl - 1 && r[i].pool != POOL_NONE) {  // the pooled rows only (TowerRun::pool)
+        const int B = r[i].B;
+        const int64_t ld = r[i].pool == POOL_CLS ? (int64_t)r[i].L * W : W;
+        float* xr = r[i].pool == POOL_CLS ? x : r[i].w->pooled.as<float>();
+        o.A = r[i].pool == POOL_CLS ? ap : hp; o.lda = ld;  // EOT: gathered attention rows in h
+        o.R = o.C = xr; o.ldr = o.ldc = ld; o.M = B;
+        f.M = B;
+        pj.R = pj.C = xr; pj.ldr = pj.ldc = ld; pj.M = B;
+        o.tile_m = f.tile_m = pj.tile_m = B / r[i].tile_div;
+      }
     }
     // the towers' LayerNorms and attentions are grouped launches too (one kernel each)
     LnGroup n1, n2;
@@ -98,6 +117,12 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
                        r[i].w->h.as<float>(), W};
       n2.p[i] = LnArgs{r[i].x, W, M, W, b.ln2_w.as<float>(), b.ln2_b.as<float>(),
                        r[i].w->h.as<float>(), W};
+      if (l == nl - 1 && r[i].pool == POOL_CLS)
+        n2.p[i] = LnArgs{r[i].x, (int64_t)L * W, r[i].B, W, b.ln2_w.as<float>(),
+                         b.ln2_b.as<float>(), r[i].w->h.as<float>(), W};
+      else if (l == nl - 1 && r[i].pool == POOL_EOT)
+        n2.p[i] = LnArgs{r[i].w->pooled.as<float>(), W, r[i].B, W, b.ln2_w.as<float>(),
+                         b.ln2_b.as<float>(), r[i].w->h.as<float>(), W};
       float* qp = r[i].w->qkv.as<float>();
       AttnArgs& at = ag.a[i];
       at.q = qp; at.q_bs = (int64_t)L * 3 * W; at.q_rs = 3 * W;
@@ -111,6 +136,14 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
     MPR_TRY(layernorm_group(n1, CLIP_LN_EPS, s));
     MPR_TRY(gemm_group(gq, s));
     MPR_TRY(attention_group(ag, s));
+    for (int i = 0; l == nl - 1 && i < n; ++i)
+      if (r[i].pool == POOL_EOT) {  // the EOT rows of the residual stream and of attention
+        const int W = r[i].t->width;
+        MPR_TRY(eot_gather(r[i].x, r[i].tok, r[i].B, r[i].L, r[i].ctx, W,
+                           r[i].w->pooled.as<float>(), s));
+        MPR_TRY(eot_gather(r[i].w->ao.as<float>(), r[i].tok, r[i].B, r[i].L, r[i].ctx, W,
+                           r[i].w->h.as<float>(), s));
+      }
     MPR_TRY(gemm_group(go, s));
     MPR_TRY(layernorm_group(n2, CLIP_LN_EPS, s));
     MPR_TRY(gemm_group(gf, s));
@@ -216,7 +249,8 @@ int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs
                            W, xp, s));
       MPR_TRY(layernorm(xp, W, B * T, W, m.lnpre_w.as<float>(), m.lnpre_b.as<float>(),
                         CLIP_LN_EPS, xp, W, s));
-      runs[nr++] = TowerRun{&m.tower, &w, xp, B, T, false, ig};
+      runs[nr++] = TowerRun{&m.tower, &w, xp, B, T, false, ig,
+                            modes[i] == 0 && pool_last() ? POOL_CLS : POOL_NONE};
     }
   }
   for (int j = 0; tm && j < ntr; ++j) {
@@ -226,7 +260,8 @@ int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs
     MPR_TRY(w.pooled.ensure((size_t)Bt * W * 4));
     MPR_TRY(embed_gather(tm->tok_emb.as<float>(), tok[j], tm->ctx, Bt, Lt, W,
                          tm->pos.as<float>(), w.x.as<float>(), (int64_t)Lt * W, 0, s));
-    runs[nr++] = TowerRun{&tm->tower, &w, w.x.as<float>(), Bt, Lt, true};
+    runs[nr++] = TowerRun{&tm->tower, &w, w.x.as<float>(), Bt, Lt, true, 1,
+                          pool_last() ? POOL_EOT : POOL_NONE, tok[j], tm->ctx};
   }
   MPR_TRY(ClipTower::run_group(runs, nr, s));
   GemmGroup pg;
@@ -254,7 +289,7 @@ int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs
     const int W = tm->width, Bt = Btv[j], Lt = Ltv[j];
     TowerWs& w = tm->ws[tslot[j]];
     float* pp = w.pooled.as<float>();
-    MPR_TRY(eot_gather(w.x.as<float>(), tok[j], Bt, Lt, tm->ctx, W, pp, s));
+    if (!pool_last()) MPR_TRY(eot_gather(w.x.as<float>(), tok[j], Bt, Lt, tm->ctx, W, pp, s));
     MPR_TRY(layernorm(pp, W, Bt, W, tm->lnf_w.as<float>(), tm->lnf_b.as<float>(), CLIP_LN_EPS,
                       pp, W, s));
     GemmArgs& pj = pg.g[pg.n++];

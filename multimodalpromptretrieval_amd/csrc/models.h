@@ -53,7 +53,16 @@ struct TowerRun {
   int B, L;
   bool causal;
   int tile_div = 1;  // the B rows are tile_div equal batches (GemmArgs::tile_m = M / tile_div)
+  // Pooled towers need one row per sequence after the last block (encode_image: the CLS row;
+  // encode_text: the EOT row; causal attention already made every other row irrelevant), so the
+  // last block's out_proj / ln_2 / MLP run on those rows only: POOL_CLS updates row 0 of every
+  // sequence of x in place, POOL_EOT gathers the EOT rows (argmax of tok, ctx ids a row) into
+  // w->pooled and updates them there.  Each pooled row is bit-identical to the full block's.
+  int pool = 0;
+  const int32_t* tok = nullptr;
+  int ctx = 0;
 };
+enum : int { POOL_NONE = 0, POOL_CLS = 1, POOL_EOT = 2 };
 
 struct ClipTower {
   int width = 0, layers = 0, heads = 0;

@@ -145,6 +145,44 @@ def test_vit_pair_matches_single(device, clip_sd):
         assert torch.equal(c_i, cls) and torch.equal(t_i, tok)
 
 
+_POOL_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from multimodalpromptretrieval_amd import synthetic as syn
+from multimodalpromptretrieval_amd.encoders import CLS, TOKENS, DeviceCLIPText, DeviceViT
+dev = torch.device("cuda:0")
+sd = syn.clip_state_dict(11)
+vit, txt = DeviceViT(sd, dev), DeviceCLIPText(sd, dev)
+img = syn.images(15, 16).to(dev)
+toks = syn.clip_tokens(17, 16)
+torch.save({{"cls": vit(img, CLS).cpu(), "tok": vit(img, TOKENS).cpu(),
+             "txt": txt(toks).cpu()}}, {out!r})
+"""
+
+
+def test_pooled_last_block_matches_full(device, clip_sd, tmp_path):
+    """The pooled towers' last block over the CLS / EOT rows only (TowerRun::pool) == the block
+    over every row (MPR_POOL_LAST=0, a fresh process), bit for bit; the CLS embedding is row 0
+    of the token features of the same weights."""
+    import os
+    import subprocess
+    import sys
+    from multimodalpromptretrieval_amd.encoders import CLS, TOKENS, DeviceCLIPText, DeviceViT
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "full.pt")
+    env = dict(os.environ, MPR_POOL_LAST="0")
+    subprocess.run([sys.executable, "-c", _POOL_SCRIPT.format(root=root, out=out)], env=env,
+                   check=True, timeout=240)
+    full = torch.load(out, weights_only=True)
+    vit, txt = DeviceViT(clip_sd, device), DeviceCLIPText(clip_sd, device)
+    img = syn.images(15, 16).to(device)
+    toks = syn.clip_tokens(17, 16)
+    cls, tok, tt = vit(img, CLS).cpu(), vit(img, TOKENS).cpu(), txt(toks).cpu()
+    assert torch.equal(cls, full["cls"]) and torch.equal(tt, full["txt"])
+    assert torch.equal(tok, full["tok"])
+    assert torch.equal(cls, tok[:, 0])
+
+
 def test_encode_towers_matches_separate(device, clip_sd):
     """ViT pair + text tower in one lockstep pass == the three separate calls, bit for bit."""
     from multimodalpromptretrieval_amd.encoders import (CLS, TOKENS, DeviceCLIPText, DeviceViT,

@@ -29,6 +29,17 @@ if len(sys.argv) > 2 and sys.argv[1] == "--report":
           f"({busy / (t1 - t0) * 100:.1f} %), idle {sum(g for g, _, _ in idle) / 1e6:.2f} ms")
     for g, at, n in sorted(idle, reverse=True)[:12]:
         print(f"  idle {g / 1e3:7.1f} us at +{at:8.1f} us before {n}")
+    # kernel time by name in the window (sums over overlapping streams: can exceed the window)
+    by = {}
+    for s, e, n in win:
+        k = n.replace("void mpr::(anonymous namespace)::", "").replace("mpr::(anonymous namespace)::", "")
+        k = k.split("(mpr::")[0]
+        c, t = by.get(k, (0, 0))
+        by[k] = (c + 1, t + e - s)
+    tot = sum(t for _, t in by.values())
+    print(f"kernel time {tot / 1e6:.2f} ms summed over streams")
+    for k, (c, t) in sorted(by.items(), key=lambda x: -x[1][1])[:18]:
+        print(f"  {t / 1e6:7.2f} ms {t / tot * 100:5.1f} % {c:6d} x {t / c / 1e3:7.2f} us  {k[:70]}")
     sys.exit(0)
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
