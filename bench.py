@@ -454,9 +454,10 @@ def main():
     roofline = None
     if not args.no_probe:
         # (1) The dominant kernel on its own: every tiled-GEMM launch of `steps` pipelined steps
-        # is recorded, then re-launched back to back on this stream with hipEvents around each
-        # launch (mpr_probe_replay; two marker kernels bracket the replay so a rocprofv3 trace
-        # of this same command can be windowed to it, tools/prof_summary.py --replay).
+        # is recorded, then re-launched back to back on this stream with one hipEvent pair
+        # around the whole replay (mpr_probe_replay; two marker kernels bracket the replay so a
+        # rocprofv3 trace of this same command can be windowed to it,
+        # tools/prof_summary.py --replay).
         _lib.probe_clear()
         _lib.probe_enable(3)
         run(args.steps)
@@ -483,8 +484,8 @@ def main():
                                    " partial products of a 3-way bf16 split; achieved/peak are fp32"
                                    " algorithmic flops against the fp32 MFMA dense peak)" if x3 else
                                    "gemm_f32_kernel (v_mfma_f32_32x32x2_f32 / 16x16x4)"),
-                        "measured": "replay of one pass's launches back to back, hipEvents "
-                                    "around each launch",
+                        "measured": "replay of the timed steps' launches back to back, one "
+                                    "hipEvent pair around the replay",
                         "launches_per_step": round(launches / args.steps, 1),
                         "avg_launch_us": round(ms * 1e3 / launches, 2),
                         "kernel_ms_per_step": round(ms / args.steps, 3),
