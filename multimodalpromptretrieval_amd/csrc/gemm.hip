@@ -1042,7 +1042,9 @@ const bool g_ksplit32_only = [] {
 // X3_TALL (16-deep k steps in order, KW = 1) every output element is accumulated in the same
 // order whatever the block tile, so the tile may follow the launch (grouped or alone, one batch
 // or two concatenated: bit-identical results).
-enum GemmKind : int { F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3, X3_SMALL = 4 };
+enum GemmKind : int {
+  F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3, X3_SMALL = 4, X3_WIDE32 = 5
+};
 
 const bool g_gemm_f32 = [] {
   const char* e = getenv("MPR_GEMM");
@@ -1073,6 +1075,7 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
           return launch_gemm_group<64, 32, 1, 1, 64, 2, 4>(g, s);
         return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
       case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>(g, s);
+      case X3_WIDE32: return launch_gemm_x3_group<128, 128, 2, 1, 32, 2, 1, 2>(g, s);
       case X3_SMALL: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>(g, s);
       default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);
     }
@@ -1130,8 +1133,20 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
     b64x128 += cdiv(a.M, 64) * cdiv(a.N, 128);
     short_k = short_k && a.K <= 512;
   }
+  // A launch of <= 256 128x128 blocks (at most one per CU) takes 32-deep K tiles: 123 KB of LDS,
+  // half the barriers per K, same k order (bit-identical).  Replayed alone equal (0.79-0.80 of
+  // 157.3 either way); in the serving loop the GEMMs run 0.64 -> 0.68 (a CU holding one leaves no
+  // LDS for decode blocks) and the loop 4157-4165 -> 4212-4309 QA pairs/s at 40 steps.  Every
+  // 128x128 launch on 32-deep tiles (MPR_X3_BK32=2) halves the blocks per CU of the > 256-block
+  // launches: 4073-4127; 0 = 16-deep only.
+  static const int bk32 = [] {
+    const char* e = getenv("MPR_X3_BK32");
+    return e ? atoi(e) : 1;
+  }();
   if (fam.n)
-    MPR_TRY(gemm_launch(fam, b128 >= 160                     ? X3_WIDE
+    MPR_TRY(gemm_launch(fam, b128 >= 160 && (bk32 == 2 || (bk32 == 1 && b128 <= 256))
+                                 ? X3_WIDE32
+                             : b128 >= 160                     ? X3_WIDE
                              : (b64x128 < 128 || short_k) ? X3_SMALL
                                                           : X3_TALL,
                         s));
