@@ -2,7 +2,8 @@
 # GPU-box round: tests -> smoke -> bench -> rocprofv3 kernel stats -> two PMC passes (GEMM HBM
 # traffic).  Each GPU step has its own time limit; anything but a clean exit (or plain test
 # failures, rc 1) ends the script.
-# usage: bash tools/gpu_round.sh <tag> [steps]
+# usage: bash tools/gpu_round.sh <tag> [steps]   (bench, trace and PMC passes all at <steps>, so
+# the trace's replay window and the PMC traffic describe the same launches as bench.json)
 TAG=${1:-r}
 STEPS=${2:-10}
 OUT=gpurun_out/$TAG
@@ -28,14 +29,14 @@ timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 4 > "$OUT/bench.json
 ok_or_stop $? bench 0
 if [ -z "$SKIP_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-    -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline \
+    -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline \
     > "$OUT/prof.log" 2>&1
   ok_or_stop $? rocprof 0
   python tools/prof_summary.py --replay "$OUT/prof/run_kernel_trace.csv" "$OUT/replay_window.json" >> "$OUT/prof.log" 2>&1
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_x3_kernel|gemm_f32_kernel|probe_marker_kernel" \
       -d "$OUT/pmc_$c" -o run --output-format csv \
-      -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1
+      -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1
     ok_or_stop $? pmc_$c 0
   done
 fi
