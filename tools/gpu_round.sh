@@ -33,11 +33,15 @@ if [ -z "$SKIP_PROF" ]; then
     > "$OUT/prof.log" 2>&1
   ok_or_stop $? rocprof 0
   python tools/prof_summary.py --replay "$OUT/prof/run_kernel_trace.csv" "$OUT/replay_window.json" >> "$OUT/prof.log" 2>&1
+  rm -f "$OUT/prof/run_kernel_trace.csv"  # summarised; the full trace of 80 steps is > 64 MiB
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_x3_kernel|gemm_f32_kernel|probe_marker_kernel" \
       -d "$OUT/pmc_$c" -o run --output-format csv \
       -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1
     ok_or_stop $? pmc_$c 0
   done
+  python tools/pmc_traffic.py "$OUT/pmc_FETCH_SIZE/run_counter_collection.csv" \
+    "$OUT/pmc_WRITE_SIZE/run_counter_collection.csv" "$OUT/pmc_gemm.json" >> "$OUT/prof.log" 2>&1
+  rm -f "$OUT"/pmc_*/run_counter_collection.csv
 fi
 echo done >> "$OUT/steps.log"

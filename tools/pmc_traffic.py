@@ -15,27 +15,36 @@ import json
 import sys
 
 
-def per_dispatch(path, counter):
+def per_dispatch(path, counter, by_class=None):
     rows = list(csv.DictReader(open(path)))
     disp = {}
     for r in rows:
         if r.get("Counter_Name") != counter:
             continue
         k = int(r["Dispatch_Id"])
-        ent = disp.setdefault(k, {"name": r["Kernel_Name"], "v": 0.0})
+        ent = disp.setdefault(k, {"name": r["Kernel_Name"], "v": 0.0,
+                                  "grid": int(r.get("Grid_Size", 0) or 0)})
         ent["v"] += float(r["Counter_Value"])
     order = sorted(disp)
     marks = [k for k in order if "probe_marker_kernel" in disp[k]["name"]]
     if len(marks) < 2:
         raise SystemExit(f"{path}: no replay markers")
     lo, hi = marks[-2], marks[-1]
-    vals = [disp[k]["v"] for k in order if lo < k < hi and ("gemm_f32_kernel" in disp[k]["name"] or "gemm_x3_kernel" in disp[k]["name"])]
-    return vals
+    sel = [k for k in order if lo < k < hi and ("gemm_f32_kernel" in disp[k]["name"] or "gemm_x3_kernel" in disp[k]["name"])]
+    if by_class is not None:  # (kernel template, grid) -> [launches, counter sum]
+        for k in sel:
+            nm = disp[k]["name"]
+            key = (nm[nm.find("gemm_"):nm.find(">") + 1], disp[k]["grid"])
+            ent = by_class.setdefault(key, [0, 0.0])
+            ent[0] += 1
+            ent[1] += disp[k]["v"]
+    return [disp[k]["v"] for k in sel]
 
 
 def main():
-    fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
-    write = per_dispatch(sys.argv[2], "WRITE_SIZE")
+    fc, wc = {}, {}
+    fetch = per_dispatch(sys.argv[1], "FETCH_SIZE", fc)
+    write = per_dispatch(sys.argv[2], "WRITE_SIZE", wc)
     n = min(len(fetch), len(write))
     fk = sum(fetch) / len(fetch)
     wk = sum(write) / len(write)
@@ -52,7 +61,13 @@ def main():
         alg = float(sys.argv[4])
         out["algorithmic_bytes_per_launch"] = round(alg)
         out["traffic_over_algorithmic"] = round(out["traffic_bytes_per_launch"] / alg, 3)
-    print(json.dumps(out))
+    # per (kernel, grid) class: launches, MB per launch (2 x FETCH + WRITE), share of the total
+    tot = sum(2 * v[1] + wc.get(k, [0, 0.0])[1] for k, v in fc.items())
+    out["classes"] = [{"kernel": k[0], "grid": k[1], "launches": v[0],
+                       "mb_per_launch": round((2 * v[1] + wc.get(k, [0, 0.0])[1]) * 1024 / v[0] / 1e6, 2),
+                       "share": round((2 * v[1] + wc.get(k, [0, 0.0])[1]) / tot, 3)}
+                      for k, v in sorted(fc.items(), key=lambda x: -(2 * x[1][1]))][:16]
+    print(json.dumps({k: v for k, v in out.items() if k != "classes"}))
     with open(sys.argv[3], "w") as f:
         json.dump(out, f, indent=1)
 
