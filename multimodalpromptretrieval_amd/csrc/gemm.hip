@@ -1218,12 +1218,15 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
                 (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0);
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
-  // Above 32 rows (grouped decodes) the rows split over blocks of MPR_SKINNY_ROWS (16 default,
-  // or 32; 0 = one block column holds all rows, MR up to 8).  Serving loop, 20 steps: 3783-3831
+  // Above 32 rows (grouped decodes) the rows split over blocks of MPR_SKINNY_ROWS (32 default,
+  // or 16; 0 = one block column holds all rows, MR up to 8).  Serving loop, 20 steps: 3783-3831
   // (0) -> 3893-3908 (32) / 3913-3932 (16) QA pairs/s; the 128-row o-proj 17.9 us at 32 blocks.
+  // At the bench's 80 steps, five alternating pairs on two boxes: 32 ahead by 0.3-1.2 % in
+  // every pair (4539-4551 vs 4493-4506; 4342-4393 vs 4292-4372), main loop 3.48-3.65 vs
+  // 3.52-3.67 ms.
   static const int row_blk = [] {
     const char* e = getenv("MPR_SKINNY_ROWS");
-    const int v = e ? atoi(e) : 16;
+    const int v = e ? atoi(e) : 32;
     return v == 16 || v == 32 ? v : 0;
   }();
   static const bool small_lds = [] {
