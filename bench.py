@@ -2,22 +2,25 @@
 
 Metric (BASELINE.json): "QA pairs/sec (encode+retrieve+T5 gen), SLAKE k=1; 1/2/4/8 GPU scaling".
 Workload (config C2): per GPU a batch of B=16 QA pairs (synthetic 224x224
-images resident in HBM + random-word questions), retrieval over a 6,500 x 1,024 fp32 index
-(k=1, test phase), prompt build + T5 tokenisation on the host, ViT-B/32 token features,
-t5-small encoder and 20 forced greedy decode steps, answers decoded on the host.  One step =
+images in pageable host memory, copied to the device inside the step as main.py's DataLoader
+batches are, + new random-word questions every step), clip.tokenize (byte-level BPE) on the
+host, retrieval over a 6,500 x 1,024 fp32 index (k=1, test phase), prompt build + SentencePiece
+T5 tokenisation on the host, ViT-B/32 token features, t5-small encoder and 20 forced greedy
+decode steps, answers decoded on the host.  One step =
 ``T5VisionModel.predict(batch)`` with ``VQARetrieval.retrieve_closest_qa_pairs`` as the
 retrieval function (the reference's main.py --test inner loop, main.py:262-263), i.e. every
 stage of the path, host included.  Weights are seeded random (no checkpoints offline).
 
 N > 1: one process per GPU (torch.distributed.run), each with its own batch of 16 (weak
-scaling); the retrieval index is row-sharded over the ranks and every batch exchanges queries
-(all_gather) and per-shard top-k candidates (all_to_all) over RCCL.
+scaling); C2's 26.6 MB index is replicated per rank (no data-path collective; --index-sharding
+shard row-shards it with one exchange per batch).  The ``c5_scan`` line is the row-sharded 1M x
+512 search (strong scaling, one all_gather of per-shard top-k).
 
-Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel (the tiled f32-MFMA
-GEMM): the launches of a pass over the same steps are recorded and replayed back to back with
-hipEvents around each launch (its ``in_serving_loop`` entry times the same launches inside the
-pipeline, sharing the chip with the decodes); ``traffic`` comes from the committed rocprofv3
-PMC summary of this command (profiles/*pmc_gemm.json).  ``cpu_baseline`` is the CPU oracle
+Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel (the split-bf16 MFMA
+GEMM, fp32-accurate): the launches of a pass over the same steps are recorded and replayed back
+to back with one hipEvent pair around the replay (its ``in_serving_loop`` entry times the same
+launches inside the pipeline, sharing the chip with the decodes); ``traffic`` comes from the
+committed rocprofv3 PMC summary of this command (profiles/*pmc_gemm.json).  ``cpu_baseline`` is the CPU oracle
 pipeline (torch-CPU fp32, KV-cached greedy decode) on a bounded sample of the same workload.
 """
 from __future__ import annotations
@@ -38,6 +41,7 @@ sys.path.insert(0, ROOT)
 from multimodalpromptretrieval_amd import _lib  # noqa: E402
 from multimodalpromptretrieval_amd import synthetic as syn  # noqa: E402
 from multimodalpromptretrieval_amd.serving import lookahead, pipelined  # noqa: E402
+from multimodalpromptretrieval_amd.tokenization import SpmT5Tokenizer, clip_tokenize  # noqa: E402
 
 CONFIGS = {
     # name: (batch per GPU, index rows, index dim, k, t5 config)
@@ -129,13 +133,26 @@ def c5_scan(world, rank, device, group, rdev, iters=20):
             "ids_checksum": int(chk.item())}
 
 
-def make_batches(n_batches: int, B: int, device, seed: int):
+N_IMAGES = 8  # distinct host image tensors cycled by the batches (every batch's questions differ)
+
+
+def make_batches(n_batches: int, B: int, seed: int, n_images: int = N_IMAGES):
+    """Batches as main.py's DataLoader yields them (main.py:94-96, no pin_memory): images fp32
+    [B, 3, 224, 224] in pageable HOST memory (copied to the device inside every step, as
+    dataset/VQAFeatureDataset.py:189 / architectures/T5VisionModel.py:156 do), and questions
+    that differ in every batch (the host tokenizers see new text every step)."""
     rng = np.random.Generator(np.random.PCG64(seed))
+    imgs = [syn.images(seed * 1000 + i, B) for i in range(min(n_images, n_batches))]
     out = []
     for i in range(n_batches):
-        qs = [" ".join(rng.choice(WORDS, size=int(rng.integers(6, 20)))) for _ in range(B)]
+        qs = []
+        for _ in range(B):
+            words = list(rng.choice(WORDS, size=int(rng.integers(6, 20))))
+            words[0] = words[0].capitalize()
+            qs.append(" ".join(words) + "?")
         out.append({
-            "image": syn.images(seed * 1000 + i, B).to(device),
+            # a view per batch: its own tensor object (batch identity), shared host storage
+            "image": imgs[i % len(imgs)].view_as(imgs[i % len(imgs)]),
             "question": qs,
             "task": [TASKS[int(t)] for t in rng.integers(0, len(TASKS), size=B)],
             "answer": ["yes"] * B,
@@ -151,7 +168,7 @@ def build(cfg, device, group):
     retr_sd = syn.clip_state_dict(1)                 # vanilla CLIP (retrieval, encode_image/text)
     tok_sd = syn.clip_state_dict(2)                  # PubMedCLIP stand-in (token features)
     t5_sd = syn.t5_state_dict(3, syn.T5Config() if cfg["t5"] == "t5-small" else syn.T5_BASE)
-    retr = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=syn.hash_clip_tokenize,
+    retr = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=clip_tokenize,
                         group=group)
     X = syn.index_rows(4, cfg["N"], cfg["D"])
     info = {"question_id": [str(j) for j in range(cfg["N"])],
@@ -159,7 +176,7 @@ def build(cfg, device, group):
     retr.set_index(X, syn.answers(cfg["N"], 50), info, cfg["k"], is_training_phase=False)
     retr.cache_enabled = False                        # every step re-encodes and re-scans
     model = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=t5_sd,
-                          tokenizer=syn.HashT5Tokenizer(),
+                          tokenizer=SpmT5Tokenizer(),
                           retrieval_function=retr.retrieve_closest_qa_pairs)
     model.eval()
     return model, retr, (retr_sd, tok_sd, t5_sd, X, info)
@@ -213,8 +230,8 @@ def index_build(cfg, weights, device, n_batches: int = 48):
     import tempfile
     from multimodalpromptretrieval_amd.dataset import VQARetrieval
     retr_sd = weights[0]
-    r = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=syn.hash_clip_tokenize)
-    loader = make_batches(n_batches, cfg["B"], device, seed=7)
+    r = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=clip_tokenize)
+    loader = make_batches(n_batches, cfg["B"], seed=7)
     out = {}
     for phase in ("warm", "timed"):
         d = tempfile.mkdtemp(prefix="mpr_ib_")
@@ -255,6 +272,59 @@ def index_build(cfg, weights, device, n_batches: int = 48):
                          "note": "GEMM algorithmic flops of the build / its wall time"}}
 
 
+def pipeline_work(model, retr, batches, cfg, n: int = 16):
+    """Host tokenizer cost and algorithmic FLOPs per QA pair over the first `n` timed batches.
+
+    Host: clip.tokenize of the questions (dataset/VQAFeatureDataset.py:190), the T5 tokenizer on
+    the prompts (architectures/T5VisionModel.py:161-167) and batch_decode of 20-token answers
+    (:207), timed on the host alone (in the serving loop they overlap the GPU).
+    FLOPs (MAC x 2, at the lengths each batch actually runs: CLIP text up to the
+    batch's last EOT, the T5 source at 50 image tokens + the longest prompt): ViT-B/32 twice
+    (CLS path 8.818, token path 8.856 GFLOP), CLIP text, the scan (2 N D), the t5-small encoder
+    and the 20-step decode (cross K/V once, lm_head every step)."""
+    dev = model._device_t5()
+    sub = batches[:n]
+    t_clip = t_t5 = t_dec = 0.0
+    flops = 0.0
+    pairs = 0
+    d, dff, H, Le, Ld, V = dev.d_model, dev.d_ff, dev.num_heads, dev.n_enc, dev.n_dec, dev.vocab
+    inner = dev.inner
+    for b in sub:
+        B = len(b["question"])
+        t0 = time.perf_counter()
+        toks = retr.clip_tokenize(b["question"])
+        t_clip += time.perf_counter() - t0
+        with torch.no_grad():
+            prompts = retr.retrieve_closest_qa_pairs(b)
+        sentences = [f"Answer the {t} question: " + q + p
+                     for t, q, p in zip(b["task"], b["question"], prompts)]
+        t0 = time.perf_counter()
+        enc = model.tokenizer(sentences, padding="longest", max_length=model.max_source_length,
+                              truncation=True, return_tensors="pt")
+        t_t5 += time.perf_counter() - t0
+        fake = torch.randint(3, 32000, (B, 21))
+        fake[:, 0] = 0
+        t0 = time.perf_counter()
+        model.tokenizer.batch_decode(fake, skip_special_tokens=True)
+        t_dec += time.perf_counter() - t0
+        lt = int(toks.argmax(dim=1).max()) + 1
+        L = 50 + enc["input_ids"].shape[1]
+        text_mac = 12 * (lt * 512 * 1536 + 2 * 8 * lt * lt * 64 + lt * 512 * 512
+                         + 2 * lt * 512 * 2048) + 512 * 512
+        enc_mac = Le * ((4 * d * inner + 2 * d * dff) * L + 2 * H * 64 * L * L)
+        dec_mac = Ld * 2 * d * inner * L + sum(
+            Ld * (6 * d * inner + 2 * d * dff + 2 * H * 64 * (t + 1 + L)) + d * V
+            for t in range(20))
+        per_pair = 2 * (text_mac + enc_mac + dec_mac) + 8.818e9 + 8.856e9 + 2.0 * cfg["N"] * cfg["D"]
+        flops += per_pair * B
+        pairs += B
+    k = 1e3 / len(sub)
+    return ({"clip_tokenize": round(t_clip * k, 3), "t5_tokenize": round(t_t5 * k, 3),
+             "batch_decode": round(t_dec * k, 3),
+             "total": round((t_clip + t_t5 + t_dec) * k, 3)},
+            flops / pairs)
+
+
 def host_cpu():
     """(CPU model, physical cores of the host, CPUs this process may run on)."""
     model, cores = None, set()
@@ -282,7 +352,7 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_answers=None):
     from oracle import pipeline
     retr_sd, tok_sd, t5_sd, X, info = weights
     answers = syn.answers(cfg["N"], 50)
-    tok = syn.HashT5Tokenizer()
+    tok = SpmT5Tokenizer()
     tok.add_tokens(["[itk]"])
     heads = 8 if cfg["t5"] == "t5-small" else 12
     cpu_batches = [{**b, "image": b["image"].cpu()} for b in batches]
@@ -294,7 +364,7 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_answers=None):
             b = cpu_batches[i]
             preds, prompts, _ = pipeline.predict(
                 b, retr_sd, tok_sd, t5_sd, heads, X, answers, info, cfg["k"], False,
-                syn.hash_clip_tokenize, tok, 20, forced_steps=True)
+                clip_tokenize, tok, 20, forced_steps=True)
             cpu_out.setdefault(i, (preds, prompts))
             n += 1
             el = time.perf_counter() - t0
@@ -374,7 +444,9 @@ def main():
     ib = None
     if rank == 0 and not args.no_index_build:
         ib = index_build(cfg, weights, device)
-    batches = make_batches(4, cfg["B"], device, seed=100 + rank)
+    # warmup batches first, then the timed steps' own: every timed step tokenizes new questions
+    pool = make_batches(args.warmup + args.steps, cfg["B"], seed=100 + rank)
+    warm, batches = pool[:args.warmup] or pool[:1], pool[args.warmup:]
 
     def barrier():
         if world > 1:
@@ -397,29 +469,30 @@ def main():
         finally:
             retr.cache_enabled = False
 
-    def run(steps, pipelined=True, ahead=False, main=False):
+    def run(steps, pipelined=True, ahead=False, main=False, src=None):
         # A step = one batch through encode -> retrieve -> prompt -> T5 generate.  The serving
         # loop keeps two batches in flight (T5VisionModel.predict_many): batch i+1's encoders
         # and scan run beside batch i's decode; each batch's work and answers are predict()'s.
         # Not pipelined: predict() one batch at a time (main.py:262-263), with `ahead` the
         # batches come through serving.lookahead (the dropin launcher's evaluation loop: the
         # next batch's towers and scan are enqueued before this batch's predict()).
+        src = batches if src is None else src
         with torch.no_grad():
             if main:
-                main_loop(batches[s % len(batches)] for s in range(steps))
+                main_loop(src[s % len(src)] for s in range(steps))
             elif pipelined:
-                for _ in model.predict_many((batches[s % len(batches)] for s in range(steps)),
+                for _ in model.predict_many((src[s % len(src)] for s in range(steps)),
                                             args.inflight):
                     pass
             else:
-                seq = (batches[s % len(batches)] for s in range(steps))
+                seq = (src[s % len(src)] for s in range(steps))
                 for b in (lookahead(seq, model) if ahead else seq):
                     model.predict(b)
 
-    run(args.warmup)
-    run(args.warmup, pipelined=False)
-    run(args.warmup, pipelined=False, ahead=True)
-    run(args.warmup, main=True)
+    run(args.warmup, src=warm)
+    run(args.warmup, pipelined=False, src=warm)
+    run(args.warmup, pipelined=False, ahead=True, src=warm)
+    run(args.warmup, main=True, src=warm)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -450,6 +523,8 @@ def main():
     main_ms = (time.perf_counter() - t1) / args.steps * 1e3
     # every rank (its prepare_input searches a sharded index collectively); rank 0 reports
     decode = decode_chain(model, batches[0])
+
+    host_ms, flop_per_pair = pipeline_work(model, retr, batches, cfg)
 
     roofline = None
     if not args.no_probe:
@@ -512,8 +587,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         with torch.no_grad():
-            gpu_answers = [(model.predict(b), retr.retrieve_closest_qa_pairs(b)) for b in batches]
-        cpu = cpu_baseline(cfg, weights, batches, args.cpu_seconds, gpu_answers)
+            gpu_answers = [(model.predict(b), retr.retrieve_closest_qa_pairs(b))
+                           for b in batches[:4]]
+        cpu = cpu_baseline(cfg, weights, batches[:4], args.cpu_seconds, gpu_answers)
 
     if rank == 0:
         pairs = world * cfg["B"] * args.steps
@@ -531,6 +607,15 @@ def main():
             "lookahead_ms_per_step": round(ahead_ms, 3),
             "main_loop_ms_per_step": round(main_ms, 3),
             "decode": decode,
+            "host_tokenize_ms_per_batch": host_ms,
+            "pipeline_roofline": {
+                "bound": "mfma", "gflop_per_pair": round(flop_per_pair / 1e9, 3),
+                "achieved": round(flop_per_pair * value / 1e12, 2),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(flop_per_pair * value / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                "note": "algorithmic fp32 FLOPs of every stage per QA pair (two ViT-B/32, CLIP "
+                        "text, scan, t5-small encoder + 20 decode steps, at each batch's run "
+                        "lengths) x QA pairs/s against the fp32 MFMA dense peak"},
             "sync_note": "sync: predict() one batch at a time, nothing enqueued ahead; "
                          "lookahead: the same predict() calls with the batches iterated through "
                          "serving.lookahead (one batch ahead); main_loop: main.py's test loop "
@@ -539,7 +624,10 @@ def main():
                          "predict() returns its answers, identical per batch)",
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded random weights of ViT-B/32 x2, CLIP text, t5-small; "
-                    "random 224x224 images + random-word questions)",
+                    "random 224x224 images in pageable host memory, copied to the device in "
+                    "every step as main.py's DataLoader batches are; new random-word questions "
+                    "every step through the real-algorithm tokenizers (CLIP byte-level BPE, "
+                    "SentencePiece T5) on same-format stand-in vocabularies)",
             "config": {"workload": cfg["desc"], "global_batch": world * cfg["B"],
                        "index_rows": cfg["N"], "index_dim": cfg["D"], "k": cfg["k"],
                        "decode_steps": 20, "index_sharding": f"rows/{world}" if shard

@@ -5,4 +5,5 @@ Python host surfaces mirror the reference (``T5VisionModel``, ``VQARetrieval`` w
 ``create_retrieval_dataset`` / ``retrieve_closest_qa_pairs``, ``utils.cosine_similarity``); the
 arithmetic runs in ``libmpr.so`` (hand-written gfx950 HIP kernels, C ABI in include/mpr.h).
 """
-__all__ = ["encoders", "index", "t5", "synthetic"]
+# (``synthetic`` — seeded weights and inputs for tests and the bench — is not part of the API)
+__all__ = ["dataset", "encoders", "index", "model", "t5", "tokenization", "utils"]

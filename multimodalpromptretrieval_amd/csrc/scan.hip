@@ -1090,8 +1090,10 @@ bool scan_coarse_eligible(int64_t n, int d, int b, int k, int metric) {
     const char* e = getenv("MPR_SCAN_COARSE");
     return e && e[0] == '0';
   }();
-  return !off && metric == 0 && b >= SM_MIN_B && k <= CB_C / 2 && (d == 256 || d == 512) &&
-         n >= CB_C;
+  static const bool mm_off = getenv("MPR_SCAN_MM_OFF") != nullptr;
+  // the coarse path's gated exact fallback is scan_mm: only where that one runs (k <= 16)
+  return !off && !mm_off && metric == 0 && b >= SM_MIN_B && k <= CB_C / 2 &&
+         (d == 256 || d == 512) && n >= CB_C && use_scan_mm(n, d, b, k);
 }
 
 int bf16_residuals(const float* X, int64_t n, int d, float* out, hipStream_t s) {

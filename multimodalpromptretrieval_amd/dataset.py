@@ -33,15 +33,27 @@ from .index import L2, DeviceIndex
 BUCKETS = ["very unlikely", "unlikely", "maybe", "likely", "very likely", "certainly"]
 
 
+def clip_package_tokenizer():
+    """``clip.tokenize`` restated (tokenization.ClipBPE) on the installed openai package's own
+    vocabulary file; None when the package is absent."""
+    try:
+        import clip
+    except ImportError:
+        return None
+    from .tokenization import ClipBPE
+    path = os.path.join(os.path.dirname(clip.__file__), "bpe_simple_vocab_16e6.txt.gz")
+    return ClipBPE(path).tokenize if os.path.exists(path) else clip.tokenize
+
+
 def _default_clip():
     try:
         import clip  # noqa: F401
     except ImportError as e:
-        raise RuntimeError("openai `clip` is not installed: pass clip_state_dict= and "
-                           "clip_tokenizer= (e.g. multimodalpromptretrieval_amd.synthetic)") from e
+        raise RuntimeError("openai `clip` is not installed: pass clip_state_dict= (and "
+                           "clip_tokenizer=, default tokenization.clip_tokenize)") from e
     import clip
     model, _ = clip.load("ViT-B/32", device="cpu")
-    return model.float().state_dict(), clip.tokenize
+    return model.float().state_dict(), clip_package_tokenizer()
 
 
 def vote_prompt(row: list, use_quantifier: bool = True) -> str:
@@ -86,7 +98,10 @@ class VQARetrieval:
             clip_state_dict, default_tok = _default_clip()
             clip_tokenizer = clip_tokenizer or default_tok
         if clip_tokenizer is None:
-            raise RuntimeError("VQARetrieval needs a clip tokenizer (clip.tokenize)")
+            # clip.tokenize's algorithm (tokenization.ClipBPE) on the openai vocabulary when the
+            # package is installed, else on the same-format stand-in vocabulary
+            from .tokenization import clip_tokenize
+            clip_tokenizer = clip_package_tokenizer() or clip_tokenize
         self.clip_tokenize = clip_tokenizer
         self.image_encoder = DeviceViT(clip_state_dict, self.device)
         self.text_encoder = DeviceCLIPText(clip_state_dict, self.device)

@@ -47,9 +47,11 @@ def _retrieval_for(ds):
     if r is None:
         import clip
 
-        from .dataset import VQARetrieval
+        from .dataset import VQARetrieval, clip_package_tokenizer
         sd = {k: v.detach().float() for k, v in ds.clip_model.state_dict().items()}
-        r = VQARetrieval(ds.device, clip_state_dict=sd, clip_tokenizer=clip.tokenize)
+        # clip.tokenize restated (tokenization.ClipBPE) on the package's own vocabulary
+        r = VQARetrieval(ds.device, clip_state_dict=sd,
+                         clip_tokenizer=clip_package_tokenizer() or clip.tokenize)
         ds.__dict__["_mpr_retrieval"] = r
     return r
 

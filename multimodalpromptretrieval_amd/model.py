@@ -9,8 +9,8 @@ unchanged.  The arithmetic runs in libmpr: the token-feature ViT (get_image_toke
 teacher-forced loss (:233).  Parameters stay the PyTorch source of truth; the device handles are
 rebuilt from them whenever they change (load_state_dict, optimizer steps, .to()).
 
-Scope notes: inference path.  ``forward`` returns the loss value without autograd (training /
-backward is SURVEY.md §8(f) "next"); RN vision encoders, the mapping checkpoint and t5-large's
+Scope notes: ``forward`` is differentiable in grad mode (train.py: the whole T5 as one autograd
+node with a written-out backward, dropout at transformers' sites in train mode); RN vision encoders, the mapping checkpoint and t5-large's
 untrained 512->1024 projection raise NotImplementedError; ``predict(output_attentions=True)``
 (attention plots) is out of scope.  As in the reference, image tokens (512-d) only fit a
 512-d T5 (t5-small); other widths raise like the reference's torch.cat.
@@ -170,8 +170,10 @@ class T5VisionModel(nn.Module):
             ck = torch.load(vision_checkpoint, map_location="cpu", weights_only=True)
             clip_state_dict = {k: v.float() for k, v in ck["state_dict"].items()}
         if tokenizer is None:
-            from transformers import T5Tokenizer
-            tokenizer = T5Tokenizer.from_pretrained(T5_version)
+            # the reference's T5Tokenizer (transformers 4.26.1, SentencePiece) restated on the
+            # checkpoint's spiece.model from the local Hugging Face cache (tokenization.py)
+            from .tokenization import SpmT5Tokenizer
+            tokenizer = SpmT5Tokenizer.from_pretrained(T5_version)
         self.tokenizer = tokenizer
         self.tokenizer.add_tokens(["[itk]"])
         if t5_state_dict is None:

@@ -207,12 +207,21 @@ class Pipelined:
     batch's latency.  Batches come out unchanged and in order; every batch gets exactly the
     answers ``predict()`` gives it (the serving loop's contract, tests/test_gpu_golden.py), and
     the retrieval keeps each batch's search for the analytics calls (VQARetrieval._topk).  A
-    ``predict()`` on a batch this iterator did not hand out runs as usual."""
+    ``predict()`` on a batch this iterator did not hand out runs as usual.
+
+    A caller that iterates without calling ``predict()`` (``get_validation_loss``, reference
+    utils.py:78-87: ``model.eval()`` then only ``model(batch)``) never pumps the loop: once it is
+    more than ``MAX_AHEAD`` batches ahead of the loop, the batches in between are dropped from the
+    loop's queue (their ``predict()``, if it ever comes, runs unpipelined), so the iterator holds
+    at most ``MAX_AHEAD`` batches whatever the loader's length.  The serving loop itself (its
+    streams) is only created by the first ``predict()``."""
 
     MAX_PENDING = 64
+    MAX_AHEAD = 16
 
     def __init__(self, batches, model, opts: ServingOptions = None):
         self.m = model
+        self.opts = opts
         self.src = iter(batches)
         self.items = deque()   # pulled from src, not yet passed by both consumers
         self.base = 0          # index of items[0]
@@ -220,7 +229,13 @@ class Pipelined:
         self.li = 0            # serving loop's next index
         self.fed = deque()     # images of the batches fed to the loop, awaiting their answers
         self.answers = {}      # id(image) -> (image, answers)
-        self.gen = ServingLoop(model, opts or ServingOptions.resolve()).run(self._feed())
+        self.gen = None        # the ServingLoop's generator, created by the first predict()
+        self.skipped = 0       # batches the caller passed without the loop ever seeing them
+
+    def _loop(self):
+        if self.gen is None:
+            self.gen = ServingLoop(self.m, self.opts or ServingOptions.resolve()).run(self._feed())
+        return self.gen
 
     def _get(self, idx):
         while idx - self.base >= len(self.items):
@@ -251,6 +266,14 @@ class Pipelined:
             except StopIteration:
                 return
             self.ci += 1
+            if self.ci - 1 - self.li > self.MAX_AHEAD:
+                # the loop is not being pumped: it will never see the batches before this one
+                for idx in range(self.li, self.ci - 1):
+                    img = self.items[idx - self.base]["image"]
+                    if pipes.get(id(img)) is self:
+                        del pipes[id(img)]
+                self.skipped += self.ci - 1 - self.li
+                self.li = self.ci - 1
             self._trim()
             while len(pipes) >= self.MAX_PENDING:  # handed out but never predicted
                 pipes.pop(next(iter(pipes)))
@@ -260,12 +283,13 @@ class Pipelined:
     def answers_for(self, batch):
         """The loop's answers for a batch this iterator handed out (None if it never fed it)."""
         img = batch["image"]
+        gen = self._loop()
         while True:
             ent = self.answers.pop(id(img), None)
             if ent is not None and ent[0] is img:
                 return ent[1]
             try:
-                ans = next(self.gen)
+                ans = next(gen)
             except StopIteration:
                 return None
             done = self.fed.popleft()

@@ -1,0 +1,502 @@
+"""Host tokenizers of the hot path, real algorithms.
+
+* ``ClipBPE`` / ``clip_tokenize`` — openai CLIP's ``clip.tokenize`` (called on every batch's
+  questions, dataset/VQAFeatureDataset.py:190): text clean-up (ftfy subset + double HTML
+  unescape + whitespace collapse), lower-casing, CLIP's regex pre-split, byte-level symbols,
+  greedy lowest-rank BPE merges with ``</w>`` word ends, ``[SOT] ids [EOT]`` zero-padded to 77,
+  RuntimeError on overflow unless ``truncate`` (then the last kept id is EOT).  Output int32
+  [B, 77] as the current openai package returns (``torch.int``).
+* ``SpmT5Tokenizer`` — the reference's ``T5Tokenizer`` (transformers 4.26.1, the slow
+  SentencePiece tokenizer, requirements.txt:9) used at architectures/T5VisionModel.py:57-61,
+  161-167, 207, 223-230: pad 0 / eos 1 / unk 2, 100 ``<extra_id_*>`` sentinels at the top of the
+  vocabulary, ``add_tokens(["[itk]"])`` -> 32100, special and added tokens split out of the text
+  before SentencePiece (whitespace around them stripped), EOS appended, truncation to
+  ``max_length`` (EOS kept), ``padding="longest"``, ``batch_decode`` with
+  ``skip_special_tokens`` and the clean-up of tokenization spaces.  SentencePiece itself is the
+  ``sentencepiece`` library (the same C++ the reference's tokenizer calls).
+
+Vocabularies: the real files are used when given (``bpe_path`` = openai's
+``bpe_simple_vocab_16e6.txt.gz``; ``vocab_file`` = t5's ``spiece.model``, also found in a local
+Hugging Face cache by ``SpmT5Tokenizer.from_pretrained``).  Neither exists offline, so the
+defaults are the same-format stand-ins generated in this container (``vocab/make_vocab.py``).
+Parity (tests/test_tokenization.py): both tokenizers against transformers' CLIPTokenizer /
+T5Tokenizer built on the same files, over >= 1,000 varied strings; against openai CLIP and the
+t5-small vocabulary themselves: parity unpinned (not available offline).
+"""
+from __future__ import annotations
+
+import gzip
+import html
+import os
+import re
+import unicodedata
+from functools import lru_cache
+
+import numpy as np
+import regex
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CLIP_BPE_DEFAULT = os.path.join(HERE, "vocab", "clip_bpe_synthetic.txt.gz")
+T5_SPM_DEFAULT = os.path.join(HERE, "vocab", "t5_spiece_synthetic.model")
+
+
+# ---- CLIP byte-level BPE -----------------------------------------------------------------------
+@lru_cache()
+def bytes_to_unicode() -> dict:
+    """Byte -> printable unicode symbol, CLIP/GPT-2's table: printable Latin-1 bytes map to
+    themselves, the other 68 bytes to U+0100 onwards in byte order.  Insertion order (the
+    vocabulary's first 256 ids) is the printable bytes first, then the others."""
+    keep = (list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1))
+            + list(range(ord("®"), ord("ÿ") + 1)))
+    table = {b: chr(b) for b in keep}
+    extra = 0
+    for b in range(256):
+        if b not in table:
+            table[b] = chr(256 + extra)
+            extra += 1
+    return table
+
+
+_LIGATURES = {"Ĳ": "IJ", "ĳ": "ij", "ŉ": "ʼn", "Ǳ": "DZ", "ǲ": "Dz", "ǳ": "dz", "Ǆ": "DŽ",
+              "ǅ": "Dž", "ǆ": "dž", "Ǉ": "LJ", "ǈ": "Lj", "ǉ": "lj", "Ǌ": "NJ", "ǋ": "Nj",
+              "ǌ": "nj", "ﬀ": "ff", "ﬁ": "fi", "ﬂ": "fl", "ﬃ": "ffi", "ﬄ": "ffl", "ﬅ": "ſt",
+              "ﬆ": "st"}
+_QUOTES = {"\u2018": "'", "\u2019": "'", "\u201a": "'", "\u201b": "'", "\u201c": '"',
+           "\u201d": '"', "\u201e": '"', "\u201f": '"'}
+_TERMINAL_ESCAPE = re.compile(r"\033\[((?:\d|;)*)([a-zA-Z])")
+_LINE_BREAK = re.compile("\r\n|\r|\u2028|\u2029|\u0085")
+_CONTROL = re.compile("[\x00-\x08\x0b\x0e-\x1f\x7f\ufeff\ufff9-\ufffc]")
+_WIDTH = re.compile("[\u3000\uff01-\uff60\uffe0-\uffee]")
+_TRANS = str.maketrans({**_LIGATURES, **_QUOTES})
+
+
+def fix_text(text: str) -> str:
+    """The subset of ``ftfy.fix_text``'s default steps that applies to text that is already
+    valid Unicode (ftfy is not installed here; its mojibake repair — re-decoding text that was
+    decoded with the wrong codec — is not restated): terminal escapes removed, line breaks
+    unified, control characters removed, Latin ligatures split, full-width characters narrowed,
+    curly quotes straightened, NFC."""
+    if text.isascii():
+        if "\033" in text:
+            text = _TERMINAL_ESCAPE.sub("", text)
+        if "\r" in text:
+            text = _LINE_BREAK.sub("\n", text)
+        return _CONTROL.sub("", text)
+    text = _TERMINAL_ESCAPE.sub("", text)
+    text = _LINE_BREAK.sub("\n", text)
+    text = _CONTROL.sub("", text)
+    text = text.translate(_TRANS)
+    text = _WIDTH.sub(lambda m: unicodedata.normalize("NFKC", m.group(0)), text)
+    return unicodedata.normalize("NFC", text)
+
+
+_WS = re.compile(r"\s+")
+
+
+def clean(text: str) -> str:
+    """openai CLIP ``basic_clean`` + ``whitespace_clean`` + ``lower()``."""
+    text = fix_text(text)
+    if "&" in text:
+        text = html.unescape(html.unescape(text))
+    return _WS.sub(" ", text.strip()).strip().lower()
+
+
+CLIP_PATTERN = (r"""<\|startoftext\|>|<\|endoftext\|>|'s|'t|'re|'ve|'m|'ll|'d|[\p{L}]+|[\p{N}]|"""
+                r"""[^\s\p{L}\p{N}]+""")
+
+
+class ClipBPE:
+    """openai CLIP's SimpleTokenizer, restated: vocabulary = 256 byte symbols, the same with
+    ``</w>``, one entry per merge, then ``<|startoftext|>`` and ``<|endoftext|>``; ``encode``
+    splits the cleaned text with CLIP's pattern and BPE-encodes each piece's byte symbols.
+    Pieces are memoised (as openai's ``self.cache``) as finished id lists."""
+
+    def __init__(self, bpe_path: str = None):
+        bpe_path = bpe_path or CLIP_BPE_DEFAULT
+        with gzip.open(bpe_path, "rt", encoding="utf-8") as f:
+            lines = f.read().split("\n")
+        merges = [tuple(m.split()) for m in lines[1:49152 - 256 - 2 + 1] if m]
+        syms = list(bytes_to_unicode().values())
+        vocab = syms + [s + "</w>" for s in syms] + ["".join(m) for m in merges]
+        vocab += ["<|startoftext|>", "<|endoftext|>"]
+        self.encoder = {v: i for i, v in enumerate(vocab)}
+        self.decoder = {i: v for v, i in self.encoder.items()}
+        self.ranks = {m: i for i, m in enumerate(merges)}
+        self.byte_sym = bytes_to_unicode()
+        self.sym_byte = {v: k for k, v in self.byte_sym.items()}
+        self.sot = self.encoder["<|startoftext|>"]
+        self.eot = self.encoder["<|endoftext|>"]
+        self.vocab_size = len(vocab)
+        self.pat = regex.compile(CLIP_PATTERN, regex.IGNORECASE)
+        self._ids = {"<|startoftext|>": [self.sot], "<|endoftext|>": [self.eot]}
+        self._words: dict = {}
+        self._byte_str = [self.byte_sym[b] for b in range(256)]
+
+    def bpe(self, piece: str) -> list:
+        """Symbols of one byte-encoded piece after the merges: repeatedly merge every occurrence
+        of the adjacent pair of lowest rank, left to right, until no pair has a rank."""
+        word = list(piece[:-1]) + [piece[-1] + "</w>"]
+        ranks = self.ranks
+        while len(word) > 1:
+            best, best_rank = None, None
+            for pair in zip(word, word[1:]):
+                r = ranks.get(pair)
+                if r is not None and (best_rank is None or r < best_rank):
+                    best, best_rank = pair, r
+            if best is None:
+                break
+            a, b = best
+            out, i, n = [], 0, len(word)
+            while i < n:
+                if i < n - 1 and word[i] == a and word[i + 1] == b:
+                    out.append(a + b)
+                    i += 2
+                else:
+                    out.append(word[i])
+                    i += 1
+            word = out
+        return word
+
+    def _piece_ids(self, piece: str) -> list:
+        ids = self._ids.get(piece)
+        if ids is None:
+            sym = "".join(self._byte_str[b] for b in piece.encode("utf-8"))
+            ids = [self.encoder[s] for s in self.bpe(sym)]
+            if len(self._ids) < (1 << 18):
+                self._ids[piece] = ids
+        return ids
+
+    def _word_ids(self, word: str) -> list:
+        """ids of one whitespace-free run of cleaned text.  No alternative of CLIP's pattern
+        matches whitespace, so the pattern's pieces of a text are the pieces of its runs, and a
+        run's ids can be memoised as a whole."""
+        ids = self._words.get(word)
+        if ids is None:
+            ids = []
+            for piece in self.pat.findall(word):
+                ids.extend(self._piece_ids(piece))
+            if len(self._words) < (1 << 18):
+                self._words[word] = ids
+        return ids
+
+    def encode(self, text: str) -> list:
+        if text.isascii() and text.isprintable() and "&" not in text:
+            words = text.lower().split()  # == clean(text).split() for such text
+        else:
+            words = clean(text).split(" ")
+        out = []
+        for w in words:
+            if w:
+                out.extend(self._word_ids(w))
+        return out
+
+    def encode_cleaned(self, text: str) -> list:
+        """``encode`` of text that is already clean (lower-cased, whitespace collapsed)."""
+        out = []
+        for piece in self.pat.findall(text):
+            out.extend(self._piece_ids(piece))
+        return out
+
+    def decode(self, ids) -> str:
+        text = "".join(self.decoder[int(i)] for i in ids)
+        data = bytearray(self.sym_byte[c] for c in text)
+        return data.decode("utf-8", errors="replace").replace("</w>", " ")
+
+    def tokenize(self, texts, context_length: int = 77, truncate: bool = False) -> torch.Tensor:
+        """``clip.tokenize``: int32 [B, context_length]."""
+        if isinstance(texts, str):
+            texts = [texts]
+        out = torch.zeros((len(texts), context_length), dtype=torch.int32)
+        buf = out.numpy()
+        for i, t in enumerate(texts):
+            ids = [self.sot] + self.encode(t) + [self.eot]
+            if len(ids) > context_length:
+                if not truncate:
+                    raise RuntimeError(f"Input {t} is too long for context length "
+                                       f"{context_length}")
+                ids = ids[:context_length]
+                ids[-1] = self.eot
+            buf[i, :len(ids)] = ids
+        return out
+
+    __call__ = tokenize
+
+
+@lru_cache(maxsize=4)
+def _clip_bpe(path: str) -> ClipBPE:
+    return ClipBPE(path)
+
+
+def clip_tokenize(texts, context_length: int = 77, truncate: bool = False,
+                  bpe_path: str = None) -> torch.Tensor:
+    """``clip.tokenize(texts, context_length=77, truncate=False)`` on the default (or given)
+    vocabulary."""
+    return _clip_bpe(bpe_path or CLIP_BPE_DEFAULT).tokenize(texts, context_length, truncate)
+
+
+# ---- T5 SentencePiece --------------------------------------------------------------------------
+class _Encoding(dict):
+    """``BatchEncoding``-like result (a dict with attribute access)."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+
+class SpmT5Tokenizer:
+    """transformers 4.26.1 ``T5Tokenizer`` (the reference's pinned version) on SentencePiece."""
+
+    model_input_names = ["input_ids", "attention_mask"]
+    padding_side = "right"
+
+    def __init__(self, vocab_file: str = None, extra_ids: int = 100, model_max_length=512):
+        import sentencepiece as spm
+        self.vocab_file = vocab_file or T5_SPM_DEFAULT
+        self.sp = spm.SentencePieceProcessor()
+        self.sp.Load(self.vocab_file)
+        self._pieces = self.sp.GetPieceSize()
+        self._extra_ids = extra_ids
+        self.model_max_length = model_max_length
+        self.pad_token, self.eos_token, self.unk_token = "<pad>", "</s>", "<unk>"
+        self.pad_token_id = self.sp.PieceToId("<pad>")
+        self.eos_token_id = self.sp.PieceToId("</s>")
+        self.unk_token_id = self.sp.PieceToId("<unk>")
+        self.additional_special_tokens = [f"<extra_id_{i}>" for i in range(extra_ids)]
+        self.added_tokens_encoder: dict = {}
+        self.added_tokens_decoder: dict = {}
+        self._rebuild()
+
+    @classmethod
+    def from_pretrained(cls, name_or_path: str, **kw):
+        """A directory holding ``spiece.model``, a path to the model file, or a hub name whose
+        ``spiece.model`` is already in the local Hugging Face cache (no download)."""
+        if os.path.isdir(name_or_path):
+            return cls(os.path.join(name_or_path, "spiece.model"), **kw)
+        if os.path.isfile(name_or_path):
+            return cls(name_or_path, **kw)
+        try:
+            from huggingface_hub import try_to_load_from_cache
+            p = try_to_load_from_cache(name_or_path, "spiece.model")
+        except Exception:  # noqa: BLE001 - no hub library / malformed name
+            p = None
+        if isinstance(p, str) and os.path.isfile(p):
+            return cls(p, **kw)
+        raise OSError(f"{name_or_path}: no spiece.model locally (offline; pass vocab_file=)")
+
+    # ---- vocabulary ---------------------------------------------------------------------------
+    @property
+    def vocab_size(self) -> int:
+        return self._pieces + self._extra_ids
+
+    def __len__(self) -> int:
+        return self.vocab_size + len(self.added_tokens_encoder)
+
+    @property
+    def all_special_tokens(self) -> list:
+        return [self.eos_token, self.unk_token, self.pad_token] + self.additional_special_tokens
+
+    @property
+    def all_special_ids(self) -> list:
+        return [self.convert_tokens_to_ids(t) for t in self.all_special_tokens]
+
+    def _rebuild(self):
+        # the no-split tokens (special + added): leftmost-longest split as the tokens trie
+        nosplit = set(self.all_special_tokens) | set(self.added_tokens_encoder)
+        alts = sorted(nosplit, key=len, reverse=True)
+        self._nosplit = nosplit
+        self._first = "".join(sorted({t[0] for t in nosplit}))
+        self._split = re.compile("(" + "|".join(re.escape(t) for t in alts) + ")")
+        self._special_ids = set(self.all_special_ids)
+        self._special_tokens = set(self.all_special_tokens)
+        self._words: dict = {}
+
+    def add_tokens(self, tokens) -> int:
+        if isinstance(tokens, str):
+            tokens = [tokens]
+        n = 0
+        for t in tokens:
+            t = str(t)
+            if (not t or t in self.added_tokens_encoder
+                    or self._token_id(t) != self.unk_token_id or t == self.unk_token):
+                continue
+            i = len(self)
+            self.added_tokens_encoder[t] = i
+            self.added_tokens_decoder[i] = t
+            n += 1
+        self._rebuild()
+        return n
+
+    def _token_id(self, tok: str) -> int:
+        if tok.startswith("<extra_id_"):
+            m = re.match(r"<extra_id_(\d+)>", tok)
+            if m:
+                return self.vocab_size - int(m.group(1)) - 1
+        return self.sp.PieceToId(tok)
+
+    def convert_tokens_to_ids(self, tokens):
+        if isinstance(tokens, str):
+            i = self.added_tokens_encoder.get(tokens)
+            return i if i is not None else self._token_id(tokens)
+        return [self.convert_tokens_to_ids(t) for t in tokens]
+
+    def _id_token(self, i: int) -> str:
+        if i in self.added_tokens_decoder:
+            return self.added_tokens_decoder[i]
+        if i < self._pieces:
+            return self.sp.IdToPiece(i)
+        return f"<extra_id_{self.vocab_size - 1 - i}>"
+
+    def convert_ids_to_tokens(self, ids, skip_special_tokens: bool = False):
+        if isinstance(ids, int):
+            return self._id_token(ids)
+        out = []
+        for i in ids:
+            i = int(i)
+            if skip_special_tokens and i in self._special_ids:
+                continue
+            out.append(self._id_token(i))
+        return out
+
+    # ---- encoding -----------------------------------------------------------------------------
+    def _has_nosplit(self, text: str) -> bool:
+        return any(c in text for c in self._first) and self._split.search(text) is not None
+
+    def _sp_encode(self, text: str) -> list:
+        """SentencePiece ids of a chunk.  Printable ASCII goes word by word through a memo:
+        with the model's whitespace pre-split (split_by_whitespace, remove_extra_whitespaces,
+        the dummy prefix) no piece spans a space, so a chunk's pieces are its words' pieces
+        (each word as "\u2581word"), and nmt_nfkc leaves printable ASCII unchanged.  Anything
+        else is encoded whole."""
+        if not (text.isascii() and text.isprintable()):
+            return self.sp.EncodeAsIds(text) if text else []
+        out = []
+        words = self._words
+        for w in text.split(" "):
+            if not w:
+                continue
+            ids = words.get(w)
+            if ids is None:
+                ids = self.sp.EncodeAsIds(w)
+                if len(words) < (1 << 18):
+                    words[w] = ids
+            out.extend(ids)
+        return out
+
+    def _encode_text(self, text: str) -> list:
+        """``tokenize`` + ``convert_tokens_to_ids``: no-split tokens cut out (whitespace around
+        each stripped), every other chunk through SentencePiece."""
+        if not self._has_nosplit(text):
+            return self._sp_encode(text)
+        parts = self._split.split(text)  # [chunk, tok, chunk, tok, ..., chunk]
+        for j in range(1, len(parts), 2):
+            parts[j - 1] = parts[j - 1].rstrip()
+            parts[j + 1] = parts[j + 1].lstrip()
+        ids = []
+        for j, p in enumerate(parts):
+            if not p:
+                continue
+            if j % 2:
+                ids.append(self.convert_tokens_to_ids(p))
+            else:
+                ids.extend(self._sp_encode(p))
+        return ids
+
+    def _finish(self, ids: list, max_length, truncation) -> list:
+        if truncation and max_length is not None and len(ids) + 1 > max_length:
+            ids = ids[:max(max_length - 1, 0)]
+        if not ids or ids[-1] != self.eos_token_id:
+            ids = ids + [self.eos_token_id]
+        return ids
+
+    def encode(self, text: str, max_length=None, truncation=False, add_special_tokens=True):
+        ids = self._encode_text(text)
+        return self._finish(ids, max_length, truncation) if add_special_tokens else ids
+
+    def __call__(self, text, padding=False, max_length=None, truncation=False,
+                 return_tensors=None, add_special_tokens=True, **kw):
+        single = isinstance(text, str)
+        texts = [text] if single else list(text)
+        rows = []
+        for t in texts:
+            ids = self._encode_text(t)
+            rows.append(self._finish(ids, max_length, truncation) if add_special_tokens else ids)
+        if padding in (True, "longest") or (padding == "max_length" and max_length):
+            L = max((len(r) for r in rows), default=0) if padding != "max_length" else max_length
+            ids = [r + [self.pad_token_id] * (L - len(r)) for r in rows]
+            mask = [[1] * len(r) + [0] * (L - len(r)) for r in rows]
+        else:
+            ids = rows
+            mask = [[1] * len(r) for r in rows]
+        if return_tensors == "pt":
+            if ids and all(len(r) == len(ids[0]) for r in ids):
+                a = np.zeros((len(ids), len(ids[0])), dtype=np.int64)
+                m = np.zeros_like(a)
+                for i, r in enumerate(rows):
+                    a[i, :len(r)] = r
+                    m[i, :len(r)] = 1
+                return _Encoding(input_ids=torch.from_numpy(a), attention_mask=torch.from_numpy(m))
+            return _Encoding(input_ids=torch.tensor(ids, dtype=torch.long),
+                             attention_mask=torch.tensor(mask, dtype=torch.long))
+        if single:
+            return _Encoding(input_ids=ids[0], attention_mask=mask[0])
+        return _Encoding(input_ids=ids, attention_mask=mask)
+
+    # ---- decoding -----------------------------------------------------------------------------
+    @staticmethod
+    def clean_up_tokenization(s: str) -> str:
+        return (s.replace(" .", ".").replace(" ?", "?").replace(" !", "!").replace(" ,", ",")
+                .replace(" ' ", "'").replace(" n't", "n't").replace(" 'm", "'m")
+                .replace(" 's", "'s").replace(" 've", "'ve").replace(" 're", "'re"))
+
+    def _pieces_to_string(self, pieces: list) -> str:
+        """T5Tokenizer.convert_tokens_to_string (4.26.1): special tokens are not decoded by
+        SentencePiece."""
+        out, cur, prev_special = "", [], False
+        special = self._special_tokens
+        for p in pieces:
+            if p in special:
+                if not prev_special:
+                    out += " "
+                out += self.sp.DecodePieces(cur) + p
+                prev_special, cur = True, []
+            else:
+                cur.append(p)
+                prev_special = False
+        out += self.sp.DecodePieces(cur)
+        return out.strip()
+
+    def decode(self, ids, skip_special_tokens: bool = False,
+               clean_up_tokenization_spaces: bool = True, **kw) -> str:
+        if hasattr(ids, "tolist"):
+            ids = ids.tolist()
+        ids = [int(i) for i in ids]
+        if skip_special_tokens and not self.added_tokens_decoder.keys() & set(ids):
+            # only SentencePiece pieces remain: their decode, stripped (4.26.1
+            # convert_tokens_to_string), then the clean-up
+            keep = [i for i in ids if i not in self._special_ids]
+            text = self.sp.DecodeIds(keep).strip()
+            return self.clean_up_tokenization(text) if clean_up_tokenization_spaces else text
+        toks = self.convert_ids_to_tokens(ids, skip_special_tokens)
+        subs, cur = [], []
+        for t in toks:
+            if t in self.added_tokens_encoder:
+                if cur:
+                    subs.append(self._pieces_to_string(cur))
+                    cur = []
+                subs.append(t)
+            else:
+                cur.append(t)
+        if cur:
+            subs.append(self._pieces_to_string(cur))
+        text = " ".join(subs)
+        return self.clean_up_tokenization(text) if clean_up_tokenization_spaces else text
+
+    def batch_decode(self, sequences, skip_special_tokens: bool = False,
+                     clean_up_tokenization_spaces: bool = True, **kw) -> list:
+        if hasattr(sequences, "tolist"):
+            sequences = sequences.tolist()
+        return [self.decode(s, skip_special_tokens, clean_up_tokenization_spaces)
+                for s in sequences]

@@ -35,7 +35,10 @@ def index_mod():
                                      (512, 512, 33, 64), (7, 16, 3, 7), (65536, 1024, 16, 5),
                                      # large batches: the GEMM-shaped scan (b >= 64, k <= 16)
                                      (20000, 512, 256, 5), (5003, 1024, 64, 16),
-                                     (999, 64, 100, 1), (70, 512, 300, 3)])
+                                     (999, 64, 100, 1), (70, 512, 300, 3),
+                                     # b >= 64, d = 512, k 17..32: not coarse-eligible (its
+                                     # gated exact fallback handles k <= 16 only)
+                                     (20000, 512, 256, 20), (20000, 512, 128, 32)])
 def test_scan_topk_l2(device, index_mod, n, d, b, k):
     X = syn.index_rows(1, n, d)
     q = syn.index_rows(2, b, d)
