@@ -221,6 +221,36 @@ def decode_chain(model, batch, steps: int = 20, iters: int = 10):
                     f"bandwidth-bound (DESIGN.md §3, the decode chain)"}
 
 
+def eos_leg(cfg, weights, retr, device, batches, steps: int):
+    """The serving loop with greedy search's stop (architectures/T5VisionModel.py:200-205,
+    GenerationMixin ends once every row emitted eos) on a T5 that answers in one token
+    (synthetic.eos_early_t5; SLAKE's answers are 1-3 tokens): QA pairs/s with the stop polled
+    asynchronously (mpr_t5_generate_begin / _poll) against the same model forced to 20 steps, and
+    the decode steps each generate call launched."""
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    _, tok_sd, t5_sd, _, _ = weights
+    m = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=syn.eos_early_t5(t5_sd),
+                      tokenizer=SpmT5Tokenizer(),
+                      retrieval_function=retr.retrieve_closest_qa_pairs).eval()
+    out = {"model": "t5-small weights with an eos-early decoder (synthetic.eos_early_t5)"}
+    with torch.no_grad():
+        for stop in (False, True, False, True):  # warm, then timed
+            loops = []
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in m.predict_many((batches[s % len(batches)] for s in range(steps)),
+                                    eos_stop=stop, _loop_out=loops):
+                pass
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            key = "eos_stop" if stop else "forced_20"
+            out[key] = {"qa_pairs_per_s": round(steps * cfg["B"] / el, 1),
+                        "steps_run_per_call": loops[0].steps_run}
+    m = None
+    torch.cuda.empty_cache()
+    return out
+
+
 def index_build(cfg, weights, device, n_batches: int = 48):
     """VQARetrieval.create_retrieval_dataset (dataset/VQAFeatureDataset.py
     :118-185) over a loader of synthetic batches — the retrieval ViT (CLS) + CLIP text towers per
@@ -408,6 +438,8 @@ def main():
                     help="N>1: row-shard the serving index over the ranks (an RCCL exchange per "
                          "batch) or keep a replica per rank; auto shards past 64 MiB (SURVEY "
                          "§8(e): C2/C3 replicas, C4's 268 MB sharded; C5's scan always sharded)")
+    ap.add_argument("--no-eos-leg", action="store_true",
+                    help="skip the eos-stop serving line (an eos-early T5)")
     ap.add_argument("--no-index-build", action="store_true",
                     help="skip the index-build line (create_retrieval_dataset throughput)")
     ap.add_argument("--inflight", type=int, default=2,
@@ -481,8 +513,9 @@ def main():
             if main:
                 main_loop(src[s % len(src)] for s in range(steps))
             elif pipelined:
+                # forced 20 decode steps (deterministic work per pair)
                 for _ in model.predict_many((src[s % len(src)] for s in range(steps)),
-                                            args.inflight):
+                                            args.inflight, eos_stop=False):
                     pass
             else:
                 seq = (src[s % len(src)] for s in range(steps))
@@ -525,6 +558,7 @@ def main():
     decode = decode_chain(model, batches[0])
 
     host_ms, flop_per_pair = pipeline_work(model, retr, batches, cfg)
+    eos = eos_leg(cfg, weights, retr, device, batches, args.steps) if not args.no_eos_leg else None
 
     roofline = None
     if not args.no_probe:
@@ -607,6 +641,7 @@ def main():
             "lookahead_ms_per_step": round(ahead_ms, 3),
             "main_loop_ms_per_step": round(main_ms, 3),
             "decode": decode,
+            "eos_stop_leg": eos,
             "host_tokenize_ms_per_batch": host_ms,
             "pipeline_roofline": {
                 "bound": "mfma", "gflop_per_pair": round(flop_per_pair / 1e9, 3),

@@ -15,8 +15,10 @@
  *     the library owns its copies until *_destroy.  The caller owns every I/O buffer.
  *   - `stream` is a hipStream_t (NULL = the legacy default stream).  Work is enqueued on it; the
  *     functions do not synchronise the host unless stated.
- *   - All floating-point arithmetic is IEEE fp32 (f32-input MFMA / VALU), like the reference's
- *     CPU path.
+ *   - Floating-point arithmetic is fp32-accurate, like the reference's CPU path, but not
+ *     IEEE-fp32 bitwise: the tiled GEMMs form each fp32 product from six bf16 MFMA partial
+ *     products of a 3-way bf16 split (max error ~1.6e-7 of sum |a*b|, the f32 MFMA's ~2e-7;
+ *     MPR_GEMM=f32 selects the f32-input MFMA kernel); everything else is fp32 VALU / f32 MFMA.
  */
 #ifndef MPR_H_
 #define MPR_H_
@@ -209,6 +211,25 @@ int mpr_t5_generate_batches(mpr_model* m, int32_t slot, int32_t n,
                             const int32_t* b, const int32_t* L, int32_t max_new,
                             int32_t decoder_start, int32_t eos, int32_t pad,
                             int32_t* const* out_dev, void* stream);
+/* mpr_t5_generate_batches for a host that must not block (a serving loop; GenerationMixin's
+ * stop of greedy search, architectures/T5VisionModel.py:200-205): enqueues the n batches'
+ * encoders and, with stop_chunk > 0, the first `ahead` decode chunks of stop_chunk steps (each
+ * followed by an async copy of the rows' unfinished flags), and returns without waiting.
+ * stop_chunk = 0: the whole max_new-step loop as one graph (nothing to poll but the finish).
+ * mpr_t5_generate_poll then advances the call: it reads the flags of every chunk that has
+ * completed (oldest first; wait = 0 never blocks), launches the next chunk while fewer than
+ * `ahead` are unread, and once every row has emitted eos — or every chunk is launched — enqueues
+ * the token copies into out[i] ordered before later work on `stream` and sets *done = 1,
+ * *steps_run = decode steps launched.  Columns of steps not run stay pad, so out[i] equals
+ * mpr_t5_generate_batches's.  wait = 1 blocks until done.  One call per slot in flight: a
+ * begin on a slot whose call is not done fails. */
+int mpr_t5_generate_begin(mpr_model* m, int32_t slot, int32_t n,
+                          const float* const* embeds_dev, const float* const* masks_dev,
+                          const int32_t* b, const int32_t* L, int32_t max_new,
+                          int32_t decoder_start, int32_t eos, int32_t pad, int32_t stop_chunk,
+                          int32_t ahead, int32_t* const* out_dev, void* stream);
+int mpr_t5_generate_poll(mpr_model* m, int32_t slot, int32_t wait, int32_t* done,
+                         int32_t* steps_run, void* stream);
 /* Run the greedy decode loop of later generate calls on a slot on decode_stream (null = the
  * call's own stream).  The call's stream still orders everything: the loop starts after the
  * encoder enqueued on it and the call's stream waits for the tokens. */

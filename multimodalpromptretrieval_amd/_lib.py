@@ -73,6 +73,12 @@ SIGNATURES = [
     ("mpr_t5_generate_batches", c_int32, [c_void_p, c_int32, c_int32, POINTER(c_void_p),
                                           POINTER(c_void_p), I32P, I32P, c_int32, c_int32,
                                           c_int32, c_int32, POINTER(c_void_p), c_void_p]),
+    ("mpr_t5_generate_begin", c_int32, [c_void_p, c_int32, c_int32, POINTER(c_void_p),
+                                        POINTER(c_void_p), I32P, I32P, c_int32, c_int32,
+                                        c_int32, c_int32, c_int32, c_int32, POINTER(c_void_p),
+                                        c_void_p]),
+    ("mpr_t5_generate_poll", c_int32, [c_void_p, c_int32, c_int32, POINTER(c_int32),
+                                       POINTER(c_int32), c_void_p]),
     ("mpr_t5_set_decode_stream", c_int32, [c_void_p, c_int32, c_void_p]),
     ("mpr_t5_logits", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                                 c_int32, c_void_p, c_void_p]),

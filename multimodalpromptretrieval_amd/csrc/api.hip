@@ -527,6 +527,39 @@ int mpr_t5_generate_batches(mpr_model* m, int32_t slot, int32_t n,
   });
 }
 
+int mpr_t5_generate_begin(mpr_model* m, int32_t slot, int32_t n, const float* const* embeds,
+                          const float* const* masks, const int32_t* b, const int32_t* L,
+                          int32_t max_new, int32_t start, int32_t eos, int32_t pad,
+                          int32_t stop_chunk, int32_t ahead, int32_t* const* outs,
+                          void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    MPR_REQUIRE(n >= 1 && n <= T5Model::MAX_GROUPS && embeds && masks && b && L && outs,
+                "t5 generate_begin: n=%d (1 to %d) and every array", n, T5Model::MAX_GROUPS);
+    MPR_REQUIRE(stop_chunk >= 0 && stop_chunk <= 512, "generate_begin: chunk %d", stop_chunk);
+    int bs[T5Model::MAX_GROUPS], ls[T5Model::MAX_GROUPS];
+    for (int i = 0; i < n; ++i) {
+      bs[i] = b[i];
+      ls[i] = L[i];
+    }
+    return t5->gen_begin(n, embeds, masks, bs, ls, max_new, start, eos, pad, outs, S(stream),
+                         slot, stop_chunk, ahead);
+  });
+}
+
+int mpr_t5_generate_poll(mpr_model* m, int32_t slot, int32_t wait, int32_t* done,
+                         int32_t* steps_run, void* stream) {
+  return guarded([&]() -> int {
+    T5_HANDLE(m);
+    MPR_REQUIRE(done != nullptr, "generate_poll: done is required");
+    int d = 0, st = 0;
+    MPR_TRY(t5->gen_poll(slot, wait != 0, &d, &st, S(stream)));
+    *done = d;
+    if (steps_run) *steps_run = st;
+    return MPR_OK;
+  });
+}
+
 int mpr_t5_set_decode_stream(mpr_model* m, int32_t slot, void* decode_stream) {
   return guarded([&]() -> int {
     T5_HANDLE(m);

@@ -137,6 +137,19 @@ struct T5Work {
   int32_t* h_unf = nullptr;  // pinned host
   size_t h_unf_n = 0;
   std::vector<hipEvent_t> ev_chunk;
+  // the generate call in flight on this slot (gen_begin .. gen_poll finalising it)
+  struct Pending {
+    bool active = false;
+    int B = 0, L = 0, max_new = 0, eos = 0, pad = 0, chunk = 0, nch = 0;
+    int launched = 0, checked = 0;  // decode chunks enqueued / whose flags were read
+    bool stop = false;              // every row had emitted eos after chunk `checked - 1`
+    int ahead = 2;                  // chunks kept launched but unread
+    int steps = 0;                  // decode steps launched by the last finished call
+    int n = 0;
+    int32_t* outs[8] = {};
+    int row0[8] = {}, rows[8] = {};
+    hipStream_t ds = nullptr;
+  } pend;
 };
 
 struct T5Model : mpr_model {
@@ -172,6 +185,16 @@ struct T5Model : mpr_model {
                       const int* Bs, const int* Ls, int max_new, int start, int eos, int pad,
                       int32_t* const* outs, hipStream_t s, int slot = 0, int stop_chunk = 0,
                       int* steps_run = nullptr);
+  // generate_groups split for a host that must not block: gen_begin enqueues the encoders and,
+  // with stop_chunk > 0, the first decode chunks (their unfinished flags copied to pinned host
+  // memory after each), then returns; gen_poll(wait = false) reads the flags of every chunk that
+  // has completed, launches the next chunk while fewer than `ahead` are unread, and once every row
+  // has emitted eos (or every chunk is launched) enqueues the token copies on `s` and reports
+  // *done = 1.  wait = true blocks until then.  One call per slot in flight.
+  int gen_begin(int ng, const float* const* embeds, const float* const* masks, const int* Bs,
+                const int* Ls, int max_new, int start, int eos, int pad, int32_t* const* outs,
+                hipStream_t s, int slot, int stop_chunk, int ahead);
+  int gen_poll(int slot, bool wait, int* done, int* steps_run, hipStream_t s);
   int logits_tf(const float* embeds, const float* mask, int B, int L, const int32_t* dec_in,
                 int T, float* logits_out, hipStream_t s);
   int embed(const int32_t* ids, int B, int len, float* out, int64_t out_bs, int row0,
@@ -188,8 +211,12 @@ struct T5Model : mpr_model {
   int init_body(int B, int L, int max_new, int start, hipStream_t s);
   int decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s, int t0 = 0,
                   int t1 = -1);
+  int launch_chunk(int c);          // decode chunk c of the pending call + its flag copy
+  int finish_pending(hipStream_t s);  // token copies, join onto s, slot free
   template <class F>
   int graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body);
+  template <class F>
+  int run_graph(const GraphKey& key, hipStream_t st, F&& body);
 };
 
 }  // namespace mpr

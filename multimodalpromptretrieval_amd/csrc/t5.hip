@@ -288,8 +288,22 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
                              const int* Bs, const int* Ls, int max_new, int start, int eos,
                              int pad, int32_t* const* outs, hipStream_t s, int slot,
                              int stop_chunk, int* steps_run) {
-  MPR_TRY(use_slot(slot));
   if (steps_run) *steps_run = 0;
+  MPR_TRY(gen_begin(ng, embeds, masks, Bs, Ls, max_new, start, eos, pad, outs, s, slot,
+                    stop_chunk, 2));
+  int done = 0;
+  return gen_poll(slot, true, &done, steps_run, s);
+}
+
+int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* masks,
+                       const int* Bs, const int* Ls, int max_new, int start, int eos, int pad,
+                       int32_t* const* outs, hipStream_t s, int slot, int stop_chunk,
+                       int ahead) {
+  MPR_TRY(use_slot(slot));
+  MPR_REQUIRE(!ws->pend.active,
+              "t5 generate: slot %d still has a decode in flight (poll it to the end first)",
+              slot);
+  MPR_REQUIRE(ahead >= 1 && ahead <= 16, "t5 generate: ahead=%d", ahead);
   MPR_REQUIRE(ng >= 1 && ng <= MAX_GROUPS, "t5 generate: %d batch groups (1 to %d)", ng,
               MAX_GROUPS);
   MPR_REQUIRE(max_new >= 0 && max_new <= 512, "t5 generate: max_new=%d", max_new);
@@ -320,7 +334,10 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     Lp = std::max(Lp, Lb);
     Mg += (int64_t)Bs[g] * Lb;  // the batches' encoder rows, stacked
   }
-  if (n == 0) return MPR_OK;
+  if (n == 0) {
+    ws->pend = T5Work::Pending();  // nothing to decode: polls report done
+    return MPR_OK;
+  }
   const int L = Lp, B = Btot;
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t M = (int64_t)B * L, Mx = std::max(M, Mg);
@@ -347,13 +364,8 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     MPR_TRY(grow(ws->mask_enc, (size_t)Mg * 4));
     MPR_TRY(grow(ws->enc_tmp, (size_t)Mg * d * 4));
   }
-  const bool graphs = graphs_enabled();
   auto run = [&](const GraphKey& key, hipStream_t st, auto&& body) -> int {
-    if (!graphs) return body(st);
-    hipGraphExec_t exec = nullptr;
-    MPR_TRY(graph_for(key, &exec, body));
-    MPR_HIP(hipGraphLaunch(exec, st));
-    return MPR_OK;
+    return run_graph(key, st, body);
   };
   if (n == 1) {
     const Grp& g = gr[0];
@@ -411,54 +423,113 @@ int T5Model::generate_groups(int ng, const float* const* embeds, const float* co
     MPR_HIP(hipEventRecord(ws->ev_fork, s));
     MPR_HIP(hipStreamWaitEvent(ds, ws->ev_fork, 0));
   }
-  if (stop_chunk <= 0 || max_new <= stop_chunk) {
-    MPR_TRY(run(std::make_tuple(1, B, L, max_new, eos, pad), ds,
-                [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
-    if (steps_run) *steps_run = max_new;
-  } else {
-    // Chunks of stop_chunk steps, each a graph of its own, and after each an async copy of the
-    // rows' unfinished flags.  Before launching chunk c the host waits for chunk c-2's flags
-    // (chunk c-1 keeps the GPU busy meanwhile) and stops once every row has finished.
-    const int nch = (int)cdiv(max_new, stop_chunk);
-    if (ws->h_unf_n < (size_t)nch * B) {
-      if (ws->h_unf) MPR_HIP(hipHostFree(ws->h_unf));
-      ws->h_unf = nullptr;
-      ws->h_unf_n = 0;
-      MPR_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws->h_unf), (size_t)nch * B * 4, 0));
-      ws->h_unf_n = (size_t)nch * B;
-    }
-    while ((int)ws->ev_chunk.size() < nch) {
-      hipEvent_t e;
-      MPR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      ws->ev_chunk.push_back(e);
-    }
-    int launched = 0;
-    for (int c = 0; c < nch; ++c) {
-      if (c >= 2) {
-        MPR_HIP(hipEventSynchronize(ws->ev_chunk[c - 2]));
-        const int32_t* f = ws->h_unf + (size_t)(c - 2) * B;
-        bool any = false;
-        for (int r = 0; r < B && !any; ++r) any = f[r] != 0;
-        if (!any) break;
-      }
-      const int t0 = c * stop_chunk, t1 = std::min(max_new, t0 + stop_chunk);
-      MPR_TRY(run(std::make_tuple(100 + c, B, L, max_new * 1024 + stop_chunk, eos, pad), ds,
-                  [&](hipStream_t cs) { return decode_body(B, L, max_new, eos, pad, cs, t0, t1); }));
-      MPR_HIP(hipMemcpyAsync(ws->h_unf + (size_t)c * B, ws->unfinished.ptr, (size_t)B * 4,
-                             hipMemcpyDeviceToHost, ds));
-      MPR_HIP(hipEventRecord(ws->ev_chunk[c], ds));
-      launched = t1;
-    }
-    if (steps_run) *steps_run = launched;
+  T5Work::Pending& P = ws->pend;
+  P = T5Work::Pending();
+  P.B = B; P.L = L; P.max_new = max_new; P.eos = eos; P.pad = pad; P.ds = ds; P.n = n;
+  P.ahead = ahead;
+  for (int k = 0; k < n; ++k) {
+    P.outs[k] = gr[k].out;
+    P.row0[k] = gr[k].row0;
+    P.rows[k] = gr[k].B;
   }
-  for (int k = 0; k < n; ++k)
-    MPR_HIP(hipMemcpyAsync(gr[k].out, ws->tok_buf.as<int32_t>() + (int64_t)gr[k].row0 * T1,
-                           (size_t)gr[k].B * T1 * 4, hipMemcpyDeviceToDevice, ds));
-  if (ds != s) {  // the caller's stream sees the tokens (and may reuse the buffers) after this
-    MPR_HIP(hipEventRecord(ws->ev_join, ds));
+  if (stop_chunk <= 0 || max_new <= stop_chunk) {
+    // one graph of all max_new steps: nothing to poll
+    MPR_TRY(run_graph(std::make_tuple(1, B, L, max_new, eos, pad), ds,
+                      [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
+    P.chunk = 0;
+    P.nch = P.launched = 1;
+    P.active = true;
+    return MPR_OK;
+  }
+  // Chunks of stop_chunk steps, each a graph of its own, and after each an async copy of the
+  // rows' unfinished flags; gen_poll reads them in order and keeps `ahead` chunks unread.
+  P.chunk = stop_chunk;
+  P.nch = (int)cdiv(max_new, stop_chunk);
+  if (ws->h_unf_n < (size_t)P.nch * B) {
+    if (ws->h_unf) MPR_HIP(hipHostFree(ws->h_unf));
+    ws->h_unf = nullptr;
+    ws->h_unf_n = 0;
+    MPR_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws->h_unf), (size_t)P.nch * B * 4, 0));
+    ws->h_unf_n = (size_t)P.nch * B;
+  }
+  while ((int)ws->ev_chunk.size() < P.nch) {
+    hipEvent_t e;
+    MPR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ws->ev_chunk.push_back(e);
+  }
+  P.active = true;
+  for (int c = 0; c < std::min(ahead, P.nch); ++c) MPR_TRY(launch_chunk(c));
+  return MPR_OK;
+}
+
+int T5Model::launch_chunk(int c) {
+  T5Work::Pending& P = ws->pend;
+  const int t0 = c * P.chunk, t1 = std::min(P.max_new, t0 + P.chunk);
+  const int B = P.B, L = P.L, max_new = P.max_new, eos = P.eos, pad = P.pad;
+  MPR_TRY(run_graph(std::make_tuple(100 + c, B, L, max_new * 1024 + P.chunk, eos, pad), P.ds,
+                    [&](hipStream_t cs) {
+                      return decode_body(B, L, max_new, eos, pad, cs, t0, t1);
+                    }));
+  MPR_HIP(hipMemcpyAsync(ws->h_unf + (size_t)c * B, ws->unfinished.ptr, (size_t)B * 4,
+                         hipMemcpyDeviceToHost, P.ds));
+  MPR_HIP(hipEventRecord(ws->ev_chunk[c], P.ds));
+  P.launched = c + 1;
+  return MPR_OK;
+}
+
+int T5Model::finish_pending(hipStream_t s) {
+  T5Work::Pending& P = ws->pend;
+  const int T1 = P.max_new + 1;
+  for (int k = 0; k < P.n; ++k)
+    MPR_HIP(hipMemcpyAsync(P.outs[k], ws->tok_buf.as<int32_t>() + (int64_t)P.row0[k] * T1,
+                           (size_t)P.rows[k] * T1 * 4, hipMemcpyDeviceToDevice, P.ds));
+  if (P.ds != s) {  // the caller's stream sees the tokens (and may reuse the buffers) after this
+    MPR_HIP(hipEventRecord(ws->ev_join, P.ds));
     MPR_HIP(hipStreamWaitEvent(s, ws->ev_join, 0));
   }
+  P.steps = P.chunk == 0 ? P.max_new : std::min(P.max_new, P.launched * P.chunk);
+  P.active = false;
   return MPR_OK;
+}
+
+int T5Model::gen_poll(int slot, bool wait, int* done, int* steps_run, hipStream_t s) {
+  MPR_TRY(use_slot(slot));
+  T5Work::Pending& P = ws->pend;
+  *done = 0;
+  if (!P.active) {
+    *done = 1;
+    if (steps_run) *steps_run = P.steps;
+    return MPR_OK;
+  }
+  for (;;) {
+    // read the flags of every completed chunk, oldest first
+    while (P.chunk > 0 && !P.stop && P.checked < P.launched) {
+      hipEvent_t e = ws->ev_chunk[P.checked];
+      if (wait) {
+        MPR_HIP(hipEventSynchronize(e));
+      } else {
+        const hipError_t r = hipEventQuery(e);
+        if (r == hipErrorNotReady) break;
+        MPR_HIP(r);
+      }
+      const int32_t* f = ws->h_unf + (size_t)P.checked * P.B;
+      bool any = false;
+      for (int r = 0; r < P.B && !any; ++r) any = f[r] != 0;
+      ++P.checked;
+      if (!any) P.stop = true;  // greedy search is over for every row
+    }
+    if (P.stop || P.launched == P.nch) {
+      MPR_TRY(finish_pending(s));
+      *done = 1;
+      if (steps_run) *steps_run = P.steps;
+      return MPR_OK;
+    }
+    if (P.launched - P.checked < P.ahead) {
+      MPR_TRY(launch_chunk(P.launched));
+      continue;
+    }
+    if (!wait) return MPR_OK;
+  }
 }
 
 int T5Model::set_decode_stream(int slot, hipStream_t ds) {
@@ -503,6 +574,15 @@ int T5Model::graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body) {
     it = graphs.emplace(key, T5Work::GraphEnt{exec, ws->gen}).first;
   }
   *out = it->second.exec;
+  return MPR_OK;
+}
+
+template <class F>
+int T5Model::run_graph(const GraphKey& key, hipStream_t st, F&& body) {
+  if (!graphs_enabled()) return body(st);
+  hipGraphExec_t exec = nullptr;
+  MPR_TRY(graph_for(key, &exec, body));
+  MPR_HIP(hipGraphLaunch(exec, st));
   return MPR_OK;
 }
 

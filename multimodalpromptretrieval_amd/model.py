@@ -434,7 +434,8 @@ class T5VisionModel(nn.Module):
         return self._s_main
 
     def predict_many(self, batches, decodes_in_flight: int = 2, pair_decodes=None,
-                     lookahead=None, tower_slots=None, decode_group=None, tower_batches=None):
+                     lookahead=None, tower_slots=None, decode_group=None, tower_batches=None,
+                     eos_stop=None, _loop_out=None):
         """predict() over an iterable of batches as a serving pipeline.  A greedy decode is a
         chain of small latency-bound launches that leaves most of the chip idle, so
         (1) ``decode_group`` (1-8, default MPR_DECODE_GROUP or 8; ``pair_decodes`` = False / True
@@ -450,12 +451,19 @@ class T5VisionModel(nn.Module):
         2) batches share one tower pass (the ViTs over their images concatenated: fewer, fuller
         launches); ``tower_slots`` > 1 (MPR_TOWER_SLOTS, default 1) overlaps consecutive passes
         on workspace slots of their own (measured slower beside the decodes).
+        (4) ``eos_stop`` (default on, MPR_SERVING_EOS_STOP=0 turns it off) ends each call's
+        decode at the first chunk of MPR_EOS_STOP_CHUNK steps after which every row has emitted
+        eos, as greedy search stops (architectures/T5VisionModel.py:200-205), polled without
+        blocking the host; off, every call runs max_new_tokens steps.
         Yields each batch's answers in order; every batch gets exactly the result predict()
-        gives it (serving.ServingLoop)."""
+        gives it (serving.ServingLoop).  ``_loop_out`` (a list) receives the ServingLoop."""
         from .serving import ServingLoop, ServingOptions
         opts = ServingOptions.resolve(decodes_in_flight, pair_decodes, lookahead, tower_slots,
-                                      decode_group, tower_batches)
-        return ServingLoop(self, opts).run(batches)
+                                      decode_group, tower_batches, eos_stop)
+        loop = ServingLoop(self, opts)
+        if _loop_out is not None:
+            _loop_out.append(loop)
+        return loop.run(batches)
 
     def _finish(self, host_tokens, done):
         done.synchronize()  # this batch's tokens only; the next batch keeps running

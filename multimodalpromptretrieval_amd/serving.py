@@ -8,8 +8,15 @@ overlapped across batches on their own streams:
   batch the host is preparing (lookahead);
 * prompts: ``T5VisionModel.prepare_input(batch, _pre=...)`` waits for that batch's retrieval
   copy only, builds and tokenises the prompts, gathers the T5 embeddings;
-* generate: ``decode_group`` consecutive batches share one ``mpr_t5_generate_batches`` call;
-  up to ``depth`` calls are in flight, each on a stream and T5 workspace slot of its own;
+* generate: ``decode_group`` consecutive batches share one grouped generate call; up to
+  ``depth`` calls are in flight, each on a stream and T5 workspace slot of its own.  With
+  ``eos_stop`` (the default: GenerationMixin stops greedy search once every row has emitted
+  eos, architectures/T5VisionModel.py:200-205) a call decodes in chunks of ``stop_chunk`` steps
+  (``mpr_t5_generate_begin``); the loop polls every call once per batch it prepares (never
+  blocking: ``mpr_t5_generate_poll``), which reads the rows' finished flags of completed chunks,
+  keeps ``stop_ahead`` chunks queued, and ends the call at the first chunk after which every row
+  is done.  ``eos_stop=False`` runs every call's max_new steps as one graph (the bench's forced
+  20-step headline);
 * answers are handed out in order as their calls complete (``_finish``).
 
 Every batch gets exactly the answers ``predict()`` gives it (the grouped launches keep each
@@ -33,12 +40,17 @@ class ServingOptions:
     lookahead: bool     # enqueue the next tower pass before blocking on a retrieval result
     tower_batches: int  # batches per tower pass
     tower_slots: int    # tower workspace slots used round robin
+    eos_stop: bool = True   # stop a call's decode once every row emitted eos
+    stop_chunk: int = 4     # decode steps per chunk (eos_stop)
+    stop_ahead: int = 3     # chunks kept queued ahead of the flags read (eos_stop)
 
     @staticmethod
     def resolve(decodes_in_flight=2, pair_decodes=None, lookahead=None, tower_slots=None,
-                decode_group=None, tower_batches=None) -> "ServingOptions":
+                decode_group=None, tower_batches=None, eos_stop=None) -> "ServingOptions":
         """Explicit arguments first, then the MPR_* environment, then the measured defaults."""
         env = os.environ.get
+        if eos_stop is None:
+            eos_stop = env("MPR_SERVING_EOS_STOP", "1") != "0"
         if decode_group is None:
             if pair_decodes is not None:
                 decode_group = 2 if pair_decodes else 1
@@ -57,7 +69,21 @@ class ServingOptions:
                               lookahead=bool(lookahead),
                               tower_batches=max(1, min(int(tower_batches), 2)),
                               tower_slots=max(1, min(int(tower_slots),
-                                                     4 // max(1, min(int(tower_batches), 2)))))
+                                                     4 // max(1, min(int(tower_batches), 2)))),
+                              eos_stop=bool(eos_stop),
+                              stop_chunk=max(1, int(env("MPR_EOS_STOP_CHUNK", "4"))),
+                              stop_ahead=max(1, min(16, int(env("MPR_EOS_AHEAD", "3")))))
+
+
+class _Call:
+    """One generate call of the loop: its slot and stream, device token tensors and, once the
+    call is over, the pinned host copies + their event."""
+    __slots__ = ("slot", "stream", "toks", "items", "steps")
+
+    def __init__(self, slot, stream, toks):
+        self.slot, self.stream, self.toks = slot, stream, toks
+        self.items = None   # [(pinned host tokens, done event), ...] when finished
+        self.steps = None   # decode steps launched
 
 
 class ServingLoop:
@@ -72,13 +98,14 @@ class ServingLoop:
             model._s_gen = []
         while len(model._s_gen) < opts.depth:
             model._s_gen.append(_lib.role_stream(model.device, f"gen:{len(model._s_gen)}"))
-        self.pending = deque()  # one entry per generate call: [(host tokens, done event), ...]
+        self.pending = deque()  # one _Call per generate call, in launch order
         self.held = []          # prepared batches waiting for the rest of their decode group
         self.ready = deque()    # (batch, prefetched handles) in order
         self.calls = 0
         self.passes = 0
         self.it = None
         self.exhausted = False
+        self.steps_run = []     # decode steps launched per generate call
 
     # ---- towers (one pass ahead) -----------------------------------------------------------
     def _refill(self):
@@ -107,10 +134,41 @@ class ServingLoop:
             self.ready.extend(zip(chunk, pres))
 
     # ---- generate ----------------------------------------------------------------------------
+    def _copy_out(self, call):
+        """Pinned host copies of a finished call's tokens on its stream (the current one)."""
+        hosts = []
+        for t in call.toks:
+            host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            host.copy_(t, non_blocking=True)
+            hosts.append(host)
+        done = torch.cuda.Event()
+        done.record(call.stream)
+        call.items = [(h, done) for h in hosts]
+
+    def _advance(self, call, wait=False) -> bool:
+        """Poll an eos-stop call (never blocks unless ``wait``); True once it is over."""
+        if call.items is not None:
+            return True
+        with torch.cuda.stream(call.stream):
+            done, steps = self.m._device_t5().generate_poll(call.slot, wait)
+            if done:
+                call.steps = steps
+                self.steps_run.append(steps)
+                self._copy_out(call)
+        return call.items is not None
+
+    def _pump(self):
+        for call in self.pending:
+            if call.items is None:
+                self._advance(call)
+
     def _launch(self, inputs):
         m = self.m
         slot = self.calls % self.o.depth
         self.calls += 1
+        for call in self.pending:  # the slot's workspace is reused: its last call must be over
+            if call.slot == slot and call.items is None:
+                self._advance(call, wait=True)
         sg = m._s_gen[slot]
         sg.wait_stream(m._s_prep)
         with torch.cuda.stream(sg):
@@ -118,18 +176,20 @@ class ServingLoop:
                 combined.record_stream(sg)
                 mask.record_stream(sg)
             t5 = m._device_t5()
-            if len(inputs) > 1:
-                toks = t5.generate_batches_padded(inputs, m.max_new_tokens, slot=slot)
+            if self.o.eos_stop:
+                toks = t5.generate_begin(inputs, m.max_new_tokens, slot=slot,
+                                         stop_chunk=self.o.stop_chunk, ahead=self.o.stop_ahead)
+                call = _Call(slot, sg, toks)
             else:
-                toks = (t5.generate_padded(*inputs[0], m.max_new_tokens, slot=slot),)
-            hosts = []
-            for t in toks:
-                host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-                host.copy_(t, non_blocking=True)
-                hosts.append(host)
-            done = torch.cuda.Event()
-            done.record(sg)
-        self.pending.append([(h, done) for h in hosts])
+                if len(inputs) > 1:
+                    toks = t5.generate_batches_padded(inputs, m.max_new_tokens, slot=slot)
+                else:
+                    toks = (t5.generate_padded(*inputs[0], m.max_new_tokens, slot=slot),)
+                call = _Call(slot, sg, toks)
+                call.steps = m.max_new_tokens
+                self.steps_run.append(call.steps)
+                self._copy_out(call)
+        self.pending.append(call)
 
     def _add(self, prepared) -> bool:
         """Queue a prepared batch: grouped with its neighbours (<= 16 rows) or alone.  Returns
@@ -147,10 +207,27 @@ class ServingLoop:
         self._launch([prepared])
         return True
 
+    def _hand_out(self, drain=False):
+        """Answers of the oldest calls whose host copies are complete, in order (the host
+        blocks on the oldest only when more than depth + 2 calls are outstanding, or at the end:
+        a slot's next call is ordered behind its previous one, and a blocked host would leave
+        the tower stream without its next pass)."""
+        m = self.m
+        while self.pending:
+            call = self.pending[0]
+            if not (drain or len(self.pending) > self.o.depth + 2):
+                if call.items is None or not call.items[-1][1].query():
+                    return
+            self._advance(call, wait=True)
+            self.pending.popleft()
+            for item in call.items:
+                yield m._finish(*item)
+
     def run(self, batches):
         m = self.m
         self.it = iter(batches)
         while True:
+            self._pump()
             if not self.ready:
                 self._refill()
             if not self.ready:
@@ -161,22 +238,14 @@ class ServingLoop:
             with torch.cuda.stream(m._s_prep):
                 with torch.no_grad():
                     combined, mask, _ = m.prepare_input(batch, _pre=pre)
+            self._pump()
             if not self._add((combined, mask)):
                 continue
-            # Answers are handed out as their calls complete; the host blocks on the oldest
-            # only when more than depth + 2 calls are outstanding (a slot's next call is ordered
-            # behind its previous one by the slot's stream, so reuse needs no host wait, and a
-            # blocked host would leave the tower stream without its next pass).
-            while self.pending and (len(self.pending) > self.o.depth + 2
-                                    or self.pending[0][-1][1].query()):
-                for item in self.pending.popleft():
-                    yield m._finish(*item)
+            yield from self._hand_out()
         if self.held:
             self._launch(self.held)
             self.held = []
-        while self.pending:
-            for item in self.pending.popleft():
-                yield m._finish(*item)
+        yield from self._hand_out(drain=True)
 
 
 def lookahead(batches, model):

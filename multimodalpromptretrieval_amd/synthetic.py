@@ -172,6 +172,24 @@ def t5_state_dict(seed: int, cfg: T5Config = T5Config()) -> dict:
     return sd
 
 
+def eos_early_t5(sd: dict) -> dict:
+    """A T5 whose greedy search ends at step 1 in every row, as a trained SLAKE model's short
+    answers end after a few tokens: decoder layers that add nothing (self-attention o, cross o and
+    FFN wo zero) and a tied embedding whose eos row is 100 x the start token's, so the first step's
+    argmax is eos everywhere."""
+    sd = {k: v.clone() for k, v in sd.items()}
+    for k in list(sd):
+        if k.startswith("decoder.block.") and (k.endswith("SelfAttention.o.weight")
+                                              or k.endswith("EncDecAttention.o.weight")
+                                              or k.endswith("DenseReluDense.wo.weight")):
+            sd[k].zero_()
+    sd["shared.weight"][1] = 100.0 * sd["shared.weight"][0]
+    for k in ("lm_head.weight", "encoder.embed_tokens.weight", "decoder.embed_tokens.weight"):
+        if k in sd:
+            sd[k] = sd["shared.weight"]
+    return sd
+
+
 def images(seed: int, b: int, size: int = 224) -> torch.Tensor:
     """CLIP-normalised-range images fp32 [b, 3, size, size]."""
     x = _rng(seed).standard_normal((b, 3, size, size), dtype=np.float32)

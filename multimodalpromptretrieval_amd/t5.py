@@ -190,6 +190,38 @@ class DeviceT5:
                   _lib.tensor_array(outs), self._stream())
         return outs
 
+    def generate_begin(self, batches, max_new_tokens=20, slot: int = 0, stop_chunk: int = 4,
+                       ahead: int = 2, decoder_start_token_id=0, eos_token_id=1,
+                       pad_token_id=0):
+        """Non-blocking grouped generate with greedy search's stop (mpr_t5_generate_begin): the
+        encoders and the first ``ahead`` decode chunks of ``stop_chunk`` steps are enqueued on
+        the current stream; ``generate_poll(slot)`` advances the call.  Returns the [B_i,
+        1+max_new] int32 output tensors, valid on the current stream once a poll reports done
+        (each equal to generate_batches_padded's)."""
+        if not 1 <= len(batches) <= 8:
+            raise ValueError(f"generate_begin: {len(batches)} batches (1 to 8)")
+        ins = [self._inputs(e, m) for e, m in batches]
+        for e, _ in ins:
+            if e.shape[0] > 16:
+                raise ValueError(f"generate_begin: a batch of {e.shape[0]} rows (at most 16)")
+        outs = [torch.empty((e.shape[0], max_new_tokens + 1), device=self.device,
+                            dtype=torch.int32) for e, _ in ins]
+        _lib.call("mpr_t5_generate_begin", self._h, int(slot), len(ins),
+                  _lib.tensor_array([e for e, _ in ins]), _lib.tensor_array([m for _, m in ins]),
+                  _lib.int_array([e.shape[0] for e, _ in ins]),
+                  _lib.int_array([e.shape[1] for e, _ in ins]), int(max_new_tokens),
+                  int(decoder_start_token_id), int(eos_token_id), int(pad_token_id),
+                  int(stop_chunk), int(ahead), _lib.tensor_array(outs), self._stream())
+        return outs
+
+    def generate_poll(self, slot: int = 0, wait: bool = False):
+        """(done, decode steps launched) of the slot's generate_begin call; never blocks unless
+        ``wait``.  When done, the tokens are ordered before later work on the current stream."""
+        done, steps = ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.call("mpr_t5_generate_poll", self._h, int(slot), int(bool(wait)),
+                  ctypes.byref(done), ctypes.byref(steps), self._stream())
+        return bool(done.value), int(steps.value)
+
     def generate_pair_padded(self, embeds_a, mask_a, embeds_b, mask_b, max_new_tokens=20,
                              decoder_start_token_id=0, eos_token_id=1, pad_token_id=0,
                              slot: int = 0):
