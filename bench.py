@@ -251,6 +251,77 @@ def eos_leg(cfg, weights, retr, device, batches, steps: int):
     return out
 
 
+def train_leg(cfg, weights, retr, device, batches, steps: int = 10):
+    """main.py:177-188 — per step ``loss = model(batch)`` (train mode,
+    dropout 0.1 at transformers' sites, training-phase retrieval that skips the self match),
+    ``model.predict(batch)`` (:179), ``loss.backward()``, AdamW ``step()`` (the device handles
+    predict() uses are rebuilt from the updated parameters).  ms per step, and the tiled GEMM's
+    share: its algorithmic FLOPs over its own kernel time and over the step's wall time."""
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    _, tok_sd, t5_sd, _, _ = weights
+    m = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=t5_sd,
+                      tokenizer=SpmT5Tokenizer(), retrieval_function=retr.retrieve_closest_qa_pairs,
+                      t5_dropout_rate=0.1)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-5)  # main.py:149 (AdamW over parameters())
+    phase = retr.is_training_phase
+    retr.is_training_phase = True   # main.py:119-122: --train builds a training-phase index
+    m.train()
+    timings = {"forward": 0.0, "predict": 0.0, "backward_step": 0.0}
+
+    def step(b, timed):
+        t0 = time.perf_counter()
+        loss = m(b)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        m.predict(b)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        if timed:
+            timings["forward"] += t1 - t0
+            timings["predict"] += t2 - t1
+            timings["backward_step"] += t3 - t2
+        return float(loss.detach())
+
+    try:
+        for i in range(2):
+            step(batches[i % len(batches)], False)
+        _lib.probe_clear()
+        _lib.probe_enable(1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        losses = [step(batches[i % len(batches)], True) for i in range(steps)]
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        _lib.probe_enable(0)
+        gms, gl, gflops, _ = _lib.probe_read()
+        _lib.probe_clear()
+    finally:
+        retr.is_training_phase = phase
+    m = opt = None
+    torch.cuda.empty_cache()
+    ms = el / steps * 1e3
+    return {"workload": f"main.py:177-188 train step: t5-small + ViT-B/32 token features, batch "
+                        f"{cfg['B']}, dropout 0.1, forward + predict + backward + AdamW",
+            "ms_per_step": round(ms, 2),
+            "ms_per_step_parts": {k: round(v / steps * 1e3, 2) for k, v in timings.items()},
+            "qa_pairs_per_s": round(cfg["B"] / (ms * 1e-3), 1),
+            "loss_first_last": [round(losses[0], 4), round(losses[-1], 4)],
+            "roofline": {"bound": "mfma", "kernel": "gemm_x3_kernel (tiled split-bf16 GEMM)",
+                         "gemm_launches_per_step": round(gl / steps, 1),
+                         "achieved": round(gflops / (gms * 1e-3) / 1e12, 2) if gms else None,
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(gflops / (gms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)
+                         if gms else None,
+                         "gemm_share_of_wall": round(gms / (el * 1e3), 4),
+                         "note": "GEMM algorithmic flops / the GEMM launches' own time (hipEvents "
+                                 "per launch); gemm_share_of_wall = GEMM time / step wall time"}}
+
+
 def index_build(cfg, weights, device, n_batches: int = 48):
     """VQARetrieval.create_retrieval_dataset (dataset/VQAFeatureDataset.py
     :118-185) over a loader of synthetic batches — the retrieval ViT (CLS) + CLIP text towers per
@@ -438,6 +509,8 @@ def main():
                     help="N>1: row-shard the serving index over the ranks (an RCCL exchange per "
                          "batch) or keep a replica per rank; auto shards past 64 MiB (SURVEY "
                          "§8(e): C2/C3 replicas, C4's 268 MB sharded; C5's scan always sharded)")
+    ap.add_argument("--no-train-leg", action="store_true",
+                    help="skip the training-step line (main.py:177-188)")
     ap.add_argument("--no-eos-leg", action="store_true",
                     help="skip the eos-stop serving line (an eos-early T5)")
     ap.add_argument("--no-index-build", action="store_true",
@@ -559,6 +632,8 @@ def main():
 
     host_ms, flop_per_pair = pipeline_work(model, retr, batches, cfg)
     eos = eos_leg(cfg, weights, retr, device, batches, args.steps) if not args.no_eos_leg else None
+    train = (train_leg(cfg, weights, retr, device, batches)
+             if rank == 0 and world == 1 and not args.no_train_leg else None)
 
     roofline = None
     if not args.no_probe:
@@ -642,6 +717,7 @@ def main():
             "main_loop_ms_per_step": round(main_ms, 3),
             "decode": decode,
             "eos_stop_leg": eos,
+            "train_step": train,
             "host_tokenize_ms_per_batch": host_ms,
             "pipeline_roofline": {
                 "bound": "mfma", "gflop_per_pair": round(flop_per_pair / 1e9, 3),

@@ -257,7 +257,14 @@ int mpr_model_destroy(mpr_model* m);
  *   bwd writes (accumulate = 0) or adds to dx, writes dw[D].
  *   mpr_attn_train_fwd/bwd: head dim 64, q/k/v/o rows at base + b*bs + i*rs + h*64; optional
  *   key mask [B, Lk] (0 = padded), causal, per-offset bias rel[(j - i + R) * H + h]; P [B,H,Lq,Lk]
- *   saved; bwd uses a dS scratch [B,H,Lq,Lk] and adds the bias gradient by offset to drel.
+ *   saved (before dropout); bwd uses a dS scratch [B,H,Lq,Lk] and adds the bias gradient by
+ *   offset to drel.  drop_*: dropout of the probabilities in train mode (T5Attention's
+ *   functional dropout; drop_thresh 0 = off), the mask regenerated in the backward.
+ *   mpr_dropout: y = residual + x * mask (residual optional; y may alias x or residual), mask
+ *   element e of (seed, site) kept iff the top 24 bits of splitmix64(seed ^ site * 0x9E37..,
+ *   + e * 0xD1B5..) are >= thresh (thresh = p * 2^24), kept elements * scale (1 / (1 - p)):
+ *   T5's nn.Dropout sites in train mode (main.py:170 model.train()), counter-based so the
+ *   backward applies the same mask without storing it.
  *   mpr_rel_gather / mpr_rel_scatter: per-offset bias from / gradient onto the [buckets, H] table
  *   through lut[2R + 1] (bucket of offset off - R).
  *   mpr_ce_train: per-row loss of logits [n, V] against labels [n] (-100 ignored) into row_loss,
@@ -279,13 +286,17 @@ int mpr_attn_train_fwd(const float* q, int64_t q_bs, int64_t q_rs, const float* 
                        int64_t k_rs, const float* v, int64_t v_bs, int64_t v_rs, int32_t B,
                        int32_t H, int32_t Lq, int32_t Lk, int32_t causal, const float* key_mask,
                        const float* rel, int32_t R, float* o, int64_t o_bs, int64_t o_rs, float* P,
-                       void* stream);
+                       uint64_t drop_seed, uint32_t drop_site, uint32_t drop_thresh,
+                       float drop_scale, void* stream);
 int mpr_attn_train_bwd(const float* q, int64_t q_bs, int64_t q_rs, const float* k, int64_t k_bs,
                        int64_t k_rs, const float* v, int64_t v_bs, int64_t v_rs, int32_t B,
                        int32_t H, int32_t Lq, int32_t Lk, const float* P, const float* dO,
                        int64_t do_bs, int64_t do_rs, float* dS, float* dq, int64_t dq_bs,
                        int64_t dq_rs, float* dk, int64_t dk_bs, int64_t dk_rs, float* dv,
-                       int64_t dv_bs, int64_t dv_rs, float* drel, int32_t R, void* stream);
+                       int64_t dv_bs, int64_t dv_rs, float* drel, int32_t R, uint64_t drop_seed,
+                       uint32_t drop_site, uint32_t drop_thresh, float drop_scale, void* stream);
+int mpr_dropout(const float* x, int64_t n, uint64_t seed, uint32_t site, uint32_t thresh,
+                float scale, const float* residual, float* y, void* stream);
 int mpr_rel_gather(const float* table, const int32_t* lut, int32_t R, int32_t H, float* rel,
                    void* stream);
 int mpr_rel_scatter(const float* drel, const int32_t* lut, int32_t R, int32_t num_buckets,

@@ -101,12 +101,17 @@ SIGNATURES = [
     ("mpr_attn_train_fwd", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
                                      c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32,
                                      c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
-                                     c_int64, c_int64, c_void_p, c_void_p]),
+                                     c_int64, c_int64, c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_uint32, c_float, c_void_p]),
     ("mpr_attn_train_bwd", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
                                      c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32,
                                      c_int32, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                      c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
-                                     c_void_p, c_int64, c_int64, c_void_p, c_int32, c_void_p]),
+                                     c_void_p, c_int64, c_int64, c_void_p, c_int32,
+                                     ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, c_float,
+                                     c_void_p]),
+    ("mpr_dropout", c_int32, [c_void_p, c_int64, ctypes.c_uint64, ctypes.c_uint32,
+                              ctypes.c_uint32, c_float, c_void_p, c_void_p, c_void_p]),
     ("mpr_rel_gather", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     ("mpr_rel_scatter", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
                                   c_void_p]),

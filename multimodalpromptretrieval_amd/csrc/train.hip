@@ -118,6 +118,35 @@ __global__ __launch_bounds__(256) void rms_bwd_dw_kernel(const float* __restrict
                                (part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
+// Counter-based dropout mask (train mode: T5's nn.Dropout / functional dropout sites): element
+// idx of site `site` under a forward's seed is kept iff the top 24 bits of a splitmix64 mix of
+// (seed, site, idx) are >= thresh (= p * 2^24), kept elements scaled by 1 / (1 - p).  Nothing is
+// stored: the backward regenerates the same mask.  thresh == 0: identity.
+struct Drop {
+  uint64_t seed;
+  uint32_t site, thresh;
+  float scale;
+};
+__device__ __forceinline__ float drop_factor(const Drop& d, uint64_t idx) {
+  if (d.thresh == 0) return 1.f;
+  uint64_t x = d.seed ^ ((uint64_t)d.site * 0x9E3779B97F4A7C15ull);
+  x += idx * 0xD1B54A32D192ED03ull;
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 40) >= d.thresh ? d.scale : 0.f;
+}
+
+// y[e] = (r ? r[e] : 0) + x[e] * mask[e]   (y may alias x or r)
+__global__ void dropout_kernel(const float* x, int64_t n, Drop d, const float* r, float* y) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const float v = x[e] * drop_factor(d, (uint64_t)e);
+  y[e] = r ? r[e] + v : v;
+}
+
 struct TrainAttn {
   const float *q, *k, *v;  // row (b, i) of head h at base + b*bs + i*rs + h*64
   int64_t q_bs, q_rs, k_bs, k_rs, v_bs, v_rs;
@@ -126,6 +155,7 @@ struct TrainAttn {
   const float* key_mask;  // [B, Lk] 1/0, optional
   const float* rel;       // per offset [(j - i + R) * H + h], optional
   int R;
+  Drop drop;              // on the probabilities (index (b, h, i, j) of P), applied in P V only
 };
 
 // Wave per (b, h, query row i): lane per key for the scores and the softmax (P row kept in the
@@ -171,7 +201,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(TrainAttn a, float* __res
   float* Pr = P + item * a.Lk;
   for (int j = lane; j < a.Lk; j += 64) {
     const float p = prow[wave][j] * inv;
-    prow[wave][j] = p;
+    prow[wave][j] = p * drop_factor(a.drop, (uint64_t)item * a.Lk + j);  // dropout(P) V
     Pr[j] = p;
   }
   wave_lds_sync();
@@ -180,8 +210,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(TrainAttn a, float* __res
   o[b * o_bs + i * o_rs + h * 64 + lane] = acc;
 }
 
-// Pass 1, wave per (b, h, i): dP_ij = dO_i . V_j (lane per key), D_i = sum_j P_ij dP_ij,
-// dS_ij = P_ij (dP_ij - D_i) (kept in dS), dQ_i = sum_j dS_ij K_j (lane per column).
+// Pass 1, wave per (b, h, i): dP_ij = (dO_i . V_j) m_ij (lane per key; m the dropout factor of
+// P_ij), D_i = sum_j P_ij dP_ij, dS_ij = P_ij (dP_ij - D_i) (kept in dS), dQ_i = sum_j dS_ij K_j
+// (lane per column).
 __global__ __launch_bounds__(256) void attn_bwd_q_kernel(TrainAttn a, const float* __restrict__ P,
                                                          const float* __restrict__ dO,
                                                          int64_t do_bs, int64_t do_rs,
@@ -205,6 +236,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(TrainAttn a, const floa
       const float* vr = a.v + b * a.v_bs + j * a.v_rs + h * 64;
 #pragma unroll 16
       for (int c = 0; c < 64; ++c) dp += gs[wave][c] * vr[c];
+      dp *= drop_factor(a.drop, (uint64_t)item * a.Lk + j);
     }
     srow[wave][j] = dp;
     dsum += p * dp;
@@ -222,7 +254,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(TrainAttn a, const floa
   dq[b * dq_bs + i * dq_rs + h * 64 + lane] = acc;
 }
 
-// Pass 2, wave per (b, h, key row j), lane per column: dV_j = sum_i P_ij dO_i,
+// Pass 2, wave per (b, h, key row j), lane per column: dV_j = sum_i P_ij m_ij dO_i,
 // dK_j = sum_i dS_ij Q_i.
 __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(TrainAttn a, const float* __restrict__ P,
                                                           const float* __restrict__ dS,
@@ -238,7 +270,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(TrainAttn a, const flo
   const int64_t base = ((int64_t)b * a.H + h) * a.Lq;  // (b, h, i = 0) row of P / dS
   float gv = 0.f, gk = 0.f;
   for (int i = 0; i < a.Lq; ++i) {
-    const float p = P[(base + i) * a.Lk + j];
+    const float p = P[(base + i) * a.Lk + j] * drop_factor(a.drop, (uint64_t)(base + i) * a.Lk + j);
     const float ds = dS[(base + i) * a.Lk + j];
     gv += p * dO[b * do_bs + i * do_rs + h * 64 + lane];
     gk += ds * a.q[b * a.q_bs + i * a.q_rs + h * 64 + lane];
@@ -398,6 +430,7 @@ TrainAttn make_attn(const float* q, int64_t q_bs, int64_t q_rs, const float* k, 
   a.v = v; a.v_bs = v_bs; a.v_rs = v_rs;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.causal = causal;
   a.key_mask = mask; a.rel = rel; a.R = R;
+  a.drop = Drop{0, 0, 0, 1.f};
   return a;
 }
 
@@ -457,13 +490,15 @@ int mpr_attn_train_fwd(const float* q, int64_t q_bs, int64_t q_rs, const float* 
                        int64_t k_rs, const float* v, int64_t v_bs, int64_t v_rs, int32_t B,
                        int32_t H, int32_t Lq, int32_t Lk, int32_t causal, const float* key_mask,
                        const float* rel, int32_t R, float* o, int64_t o_bs, int64_t o_rs, float* P,
-                       void* stream) {
+                       uint64_t drop_seed, uint32_t drop_site, uint32_t drop_thresh,
+                       float drop_scale, void* stream) {
   MPR_REQUIRE(Lk >= 1 && Lk <= TA_MAXK, "train attention: Lk=%d (1..%d)", Lk, TA_MAXK);
   MPR_REQUIRE(!rel || (Lq - 1 <= R && Lk - 1 <= R), "train attention: L exceeds the bias radius");
   const int64_t items = (int64_t)B * H * Lq;
   if (items == 0) return MPR_OK;
   TrainAttn a = make_attn(q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs, B, H, Lq, Lk, causal,
                           key_mask, rel, R);
+  a.drop = Drop{drop_seed, drop_site, drop_thresh, drop_scale};
   hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)cdiv(items, 4)), dim3(256), 0, S(stream), a,
                      o, o_bs, o_rs, P);
   MPR_LAUNCHED();
@@ -475,12 +510,14 @@ int mpr_attn_train_bwd(const float* q, int64_t q_bs, int64_t q_rs, const float* 
                        int32_t H, int32_t Lq, int32_t Lk, const float* P, const float* dO,
                        int64_t do_bs, int64_t do_rs, float* dS, float* dq, int64_t dq_bs,
                        int64_t dq_rs, float* dk, int64_t dk_bs, int64_t dk_rs, float* dv,
-                       int64_t dv_bs, int64_t dv_rs, float* drel, int32_t R, void* stream) {
+                       int64_t dv_bs, int64_t dv_rs, float* drel, int32_t R, uint64_t drop_seed,
+                       uint32_t drop_site, uint32_t drop_thresh, float drop_scale, void* stream) {
   MPR_REQUIRE(Lk >= 1 && Lk <= TA_MAXK, "train attention: Lk=%d (1..%d)", Lk, TA_MAXK);
   MPR_REQUIRE(!drel || (Lq - 1 <= R && Lk - 1 <= R), "train attention: L exceeds the bias radius");
   if ((int64_t)B * H * Lq == 0) return MPR_OK;
   TrainAttn a = make_attn(q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs, B, H, Lq, Lk, 0, nullptr,
                           nullptr, R);
+  a.drop = Drop{drop_seed, drop_site, drop_thresh, drop_scale};
   hipLaunchKernelGGL(attn_bwd_q_kernel, dim3((unsigned)cdiv((int64_t)B * H * Lq, 4)), dim3(256), 0,
                      S(stream), a, P, dO, do_bs, do_rs, dS, dq, dq_bs, dq_rs);
   MPR_LAUNCHED();
@@ -509,6 +546,15 @@ int mpr_rel_scatter(const float* drel, const int32_t* lut, int32_t R, int32_t nu
   MPR_REQUIRE(H <= 1024, "rel scatter: H=%d", H);
   hipLaunchKernelGGL(rel_scatter_kernel, dim3((unsigned)num_buckets), dim3(64 * (int)cdiv(H, 64)),
                      0, S(stream), drel, lut, R, num_buckets, H, dtable);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int mpr_dropout(const float* x, int64_t n, uint64_t seed, uint32_t site, uint32_t thresh,
+                float scale, const float* residual, float* y, void* stream) {
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(dropout_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(stream), x, n,
+                     Drop{seed, site, thresh, scale}, residual, y);
   MPR_LAUNCHED();
   return MPR_OK;
 }

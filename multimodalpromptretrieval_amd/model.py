@@ -10,9 +10,12 @@ teacher-forced loss (:233).  Parameters stay the PyTorch source of truth; the de
 rebuilt from them whenever they change (load_state_dict, optimizer steps, .to()).
 
 Scope notes: ``forward`` is differentiable in grad mode (train.py: the whole T5 as one autograd
-node with a written-out backward, dropout at transformers' sites in train mode); RN vision encoders, the mapping checkpoint and t5-large's
-untrained 512->1024 projection raise NotImplementedError; ``predict(output_attentions=True)``
-(attention plots) is out of scope.  As in the reference, image tokens (512-d) only fit a
+node with a written-out backward; in train mode with T5's dropout at transformers' sites, rate
+``t5_dropout_rate``).  ``predict()`` decodes deterministically in either mode (the reference's
+train-mode predict at main.py:179 runs generate with dropout active, but its result is unused
+for the generative model).  RN vision encoders, the mapping checkpoint and t5-large's untrained
+512->1024 projection raise NotImplementedError; ``predict(output_attentions=True)`` (attention
+plots) is out of scope.  As in the reference, image tokens (512-d) only fit a
 512-d T5 (t5-small); other widths raise like the reference's torch.cat.
 """
 from __future__ import annotations
@@ -74,8 +77,11 @@ class _GenerationOutput:
 class T5Shell(ParamTree):
     """``T5_model``: parameters under transformers names + generate / __call__ on the device."""
 
-    def __init__(self, sd: dict, owner):
+    def __init__(self, sd: dict, owner, dropout_rate: float = 0.1):
         super().__init__()
+        # T5Config.dropout_rate (0.1 for t5-small / t5-base): applied in train mode
+        self.dropout_rate = float(dropout_rate)
+        self.next_dropout_seed = None  # tests: the seed of the next train-mode forward
         # trainable like the reference's T5ForConditionalGeneration (its vision tower is frozen,
         # architectures/T5VisionModel.py:29-30); loss.backward() reaches them through train.py
         shared = nn.Parameter(sd["shared.weight"].detach().clone(), requires_grad=True)
@@ -111,12 +117,16 @@ class T5Shell(ParamTree):
             decoder_input_ids = labels.new_zeros(labels.shape)
             decoder_input_ids[:, 1:] = labels[:, :-1]
             decoder_input_ids.masked_fill_(decoder_input_ids == -100, 0)
-        if (labels is not None and torch.is_grad_enabled()
-                and any(p.requires_grad for p in self.parameters())):
-            # differentiable loss (train.py): one autograd node over the whole T5
+        drop = self.dropout_rate if self.training else 0.0
+        if labels is not None and (drop > 0.0 or (torch.is_grad_enabled() and any(
+                p.requires_grad for p in self.parameters()))):
+            # differentiable loss (train.py): one autograd node over the whole T5; in train mode
+            # with transformers' dropout sites (even without grad, as T5 in train mode does)
             from .train import t5_loss
+            seed, self.next_dropout_seed = self.next_dropout_seed, None
             loss = t5_loss(dict(self.named_parameters()), inputs_embeds, attention_mask, labels,
-                           num_heads=dev.num_heads, scale_out=dev.scale_out)
+                           num_heads=dev.num_heads, scale_out=dev.scale_out,
+                           dropout_rate=drop, dropout_seed=seed)
             return _GenerationOutput(loss, None)
         logits = dev.logits(inputs_embeds, attention_mask, decoder_input_ids)
         loss = dev.loss(logits, labels) if labels is not None else None
@@ -143,7 +153,7 @@ class T5VisionModel(nn.Module):
                  max_source_length=512, max_target_length=128, use_image_info=True,
                  vision_checkpoint=None, mapping_checkpoint=None, retrieval_function=None,
                  use_quantifier=True, *, clip_state_dict=None, t5_state_dict=None,
-                 tokenizer=None, max_new_tokens=20):
+                 tokenizer=None, max_new_tokens=20, t5_dropout_rate=0.1):
         super().__init__()
         self.device = torch.device(device)
         _lib.ensure_device(self.device)
@@ -180,7 +190,7 @@ class T5VisionModel(nn.Module):
             t5_state_dict = _load_t5(T5_version, self.tokenizer)
         self.vision_model = _CLIPParams({k: v.float() for k, v in clip_state_dict.items()})
         object.__setattr__(self.vision_model.visual, "_owner_fn", self.get_image_token_features)
-        self.T5_model = T5Shell(t5_state_dict, self)
+        self.T5_model = T5Shell(t5_state_dict, self, dropout_rate=t5_dropout_rate)
         self.image_token_id = self.tokenizer.convert_tokens_to_ids("[itk]")
         self._dev = {}
         self._slots = {}

@@ -11,9 +11,15 @@ gradient and the gradient of ``inputs_embeds`` in a fixed summation order.  The 
 embedding gather of prepare_input (:169) is a second node (``EmbedFn``) so its gradient reaches
 ``shared`` as in the reference (tied with the decoder input embedding and the lm_head).
 
-Semantics follow T5ForConditionalGeneration with dropout off (``dropout_rate`` = 0, i.e. the
-reference's numbers in eval mode): torch's dropout RNG stream cannot be reproduced bit for bit,
-so a training-mode reference run is not a parity target.
+Train mode (main.py:170 ``model.train()``): dropout at every site transformers' T5 applies it
+(modeling_t5.py: T5Stack's dropout of the input embeddings and of the final-norm output,
+T5Attention's dropout of the attention probabilities, T5LayerSelfAttention /
+T5LayerCrossAttention / T5LayerFF's dropout of each sublayer's output before the residual add,
+T5DenseActDense's dropout after the ReLU), rate ``dropout_rate`` (0.1 in the t5-small / t5-base
+configs).  torch's RNG stream cannot be reproduced, so the masks are counter-based
+(``mpr_dropout``: a hash of (seed, site, element index), one seed per forward) and the backward
+regenerates them instead of storing them; parity is against the reference's forward/backward
+with the same masks injected at transformers' sites (G12, tests/golden/make_goldens.py).
 """
 from __future__ import annotations
 
@@ -27,6 +33,43 @@ from .t5 import relative_position_bucket
 
 EPS = 1e-6
 RELU = 2  # csrc ACT_RELU
+
+# dropout sites: ((stack * 256 + layer) * 8 + kind), stack 0 = encoder / 1 = decoder, layer 255
+# for the stack-level sites (input embeddings, final-norm output)
+D_IN, D_FINAL, D_SELF_P, D_SELF_OUT, D_CROSS_P, D_CROSS_OUT, D_FFN_ACT, D_FFN_OUT = range(8)
+
+
+def dropout_site(stack: int, layer: int, kind: int) -> int:
+    return (stack * 256 + layer) * 8 + kind
+
+
+class Dropout:
+    """One forward's dropout: rate p, seed; ``args(site)`` = the mpr_dropout / attention
+    (seed, site, thresh, scale) of a site (keep iff hash >= thresh = p * 2^24, kept * 1/(1-p))."""
+
+    def __init__(self, p: float, seed: int):
+        if not 0.0 < p < 1.0:
+            raise ValueError(f"dropout rate {p}")
+        self.p = float(p)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.thresh = int(self.p * (1 << 24))
+        self.scale = float(np.float32(1.0 / (1.0 - self.p)))
+
+    def args(self, site: int):
+        return (self.seed, int(site), self.thresh, self.scale)
+
+
+NO_DROP = (0, 0, 0, 1.0)
+
+
+def dropout(x, dr, site, residual=None):
+    """residual + x * mask (a fresh tensor); dr None: x (+ residual)."""
+    if dr is None:
+        return x if residual is None else x + residual
+    y = torch.empty_like(x)
+    _lib.call("mpr_dropout", _lib.ptr(x), x.numel(), *dr.args(site), _lib.ptr(residual),
+              _lib.ptr(y), _s())
+    return y
 
 
 def t5_param_names(n_enc: int, n_dec: int) -> list:
@@ -119,17 +162,18 @@ def rms_bwd(x, w, rstd, dy, dx_acc=None, scale=1.0):
     return dx, dw
 
 
-def attn_fwd(q, k, v, B, H, Lq, Lk, causal, mask, rel, R):
+def attn_fwd(q, k, v, B, H, Lq, Lk, causal, mask, rel, R, drop=NO_DROP):
+    """(dropout(P) V, P): P [B, H, Lq, Lk] kept before dropout (drop = Dropout.args(site))."""
     inner = q.shape[1]
     o = _empty(B * Lq, inner, like=q)
     P = _empty(B, H, Lq, Lk, like=q)
     _lib.call("mpr_attn_train_fwd", _lib.ptr(q), Lq * inner, inner, _lib.ptr(k), Lk * inner,
               inner, _lib.ptr(v), Lk * inner, inner, B, H, Lq, Lk, int(causal), _lib.ptr(mask),
-              _lib.ptr(rel), R, _lib.ptr(o), Lq * inner, inner, _lib.ptr(P), _s())
+              _lib.ptr(rel), R, _lib.ptr(o), Lq * inner, inner, _lib.ptr(P), *drop, _s())
     return o, P
 
 
-def attn_bwd(q, k, v, P, do, B, H, Lq, Lk, drel, R):
+def attn_bwd(q, k, v, P, do, B, H, Lq, Lk, drel, R, drop=NO_DROP):
     inner = q.shape[1]
     dS = torch.empty_like(P)
     dq, dk, dv = _empty(B * Lq, inner, like=q), _empty(B * Lk, inner, like=q), \
@@ -137,7 +181,7 @@ def attn_bwd(q, k, v, P, do, B, H, Lq, Lk, drel, R):
     _lib.call("mpr_attn_train_bwd", _lib.ptr(q), Lq * inner, inner, _lib.ptr(k), Lk * inner,
               inner, _lib.ptr(v), Lk * inner, inner, B, H, Lq, Lk, _lib.ptr(P), _lib.ptr(do),
               Lq * inner, inner, _lib.ptr(dS), _lib.ptr(dq), Lq * inner, inner, _lib.ptr(dk),
-              Lk * inner, inner, _lib.ptr(dv), Lk * inner, inner, _lib.ptr(drel), R, _s())
+              Lk * inner, inner, _lib.ptr(dv), Lk * inner, inner, _lib.ptr(drel), R, *drop, _s())
     return dq, dk, dv
 
 
@@ -217,6 +261,7 @@ class T5Config:
         self.inner = shapes["encoder.block.0.layer.0.SelfAttention.q.weight"][0]
         self.max_distance = max_distance
         self.scale_out = scale_out
+        self.dropout = None  # Dropout in train mode
         self._luts = {}
 
     def lut(self, R, bidirectional, device):
@@ -238,6 +283,7 @@ class _Runner:
     # ---- forward --------------------------------------------------------------------------------
     def forward(self, emb, mask, labels):
         c, p = self.c, self.p
+        dr = c.dropout  # a Dropout in train mode, else None
         B, L, d = emb.shape
         H, inner = c.H, c.inner
         dev = emb.device
@@ -257,8 +303,17 @@ class _Runner:
         maskf = mask.to(dev, torch.float32).contiguous()
         tape = {"B": B, "L": L, "T": T, "Re": Re, "Rd": Rd, "lut_e": lut_e, "lut_d": lut_d,
                 "mask": maskf, "dec_ids": dec_ids, "enc": [], "dec": []}
+
+        def pdrop(stack, layer, kind):  # attention-probability dropout arguments
+            return dr.args(dropout_site(stack, layer, kind)) if dr else NO_DROP
+
+        def proj_res(a, W, R, site):  # R + dropout(a W^T)  (the sublayer output's dropout)
+            if dr is None:
+                return gemm(a, W, R=R)
+            return dropout(gemm(a, W), dr, site, residual=R)
+
         # encoder
-        x = emb.contiguous().view(B * L, d)
+        x = dropout(emb.contiguous().view(B * L, d), dr, dropout_site(0, 255, D_IN))
         for i in range(c.n_enc):
             pre = f"encoder.block.{i}.layer"
             t = {"x0": x}
@@ -266,18 +321,23 @@ class _Runner:
             t["q"] = gemm(t["n1"], p[pre + ".0.SelfAttention.q.weight"])
             t["k"] = gemm(t["n1"], p[pre + ".0.SelfAttention.k.weight"])
             t["v"] = gemm(t["n1"], p[pre + ".0.SelfAttention.v.weight"])
-            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, L, L, False, maskf, rel_e, Re)
-            t["x1"] = gemm(t["a"], p[pre + ".0.SelfAttention.o.weight"], R=x)
+            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, L, L, False, maskf, rel_e, Re,
+                                      pdrop(0, i, D_SELF_P))
+            t["x1"] = proj_res(t["a"], p[pre + ".0.SelfAttention.o.weight"], x,
+                               dropout_site(0, i, D_SELF_OUT))
             t["n2"], t["r2"] = rms_fwd(t["x1"], p[pre + ".1.layer_norm.weight"])
             t["f"] = gemm(t["n2"], p[pre + ".1.DenseReluDense.wi.weight"], act=RELU)
-            x = gemm(t["f"], p[pre + ".1.DenseReluDense.wo.weight"], R=t["x1"])
+            fd = dropout(t["f"], dr, dropout_site(0, i, D_FFN_ACT))
+            x = proj_res(fd, p[pre + ".1.DenseReluDense.wo.weight"], t["x1"],
+                         dropout_site(0, i, D_FFN_OUT))
             tape["enc"].append(t)
         tape["enc_in"] = x
         enc, tape["enc_r"] = rms_fwd(x, p["encoder.final_layer_norm.weight"])
+        enc = dropout(enc, dr, dropout_site(0, 255, D_FINAL))
         tape["enc_out"] = enc
         # decoder
         ids_dev = torch.from_numpy(dec_ids.astype(np.int32)).to(dev).view(-1)
-        g = gather_rows(p["shared.weight"], ids_dev)
+        g = dropout(gather_rows(p["shared.weight"], ids_dev), dr, dropout_site(1, 255, D_IN))
         for i in range(c.n_dec):
             pre = f"decoder.block.{i}.layer"
             t = {"g0": g}
@@ -285,23 +345,29 @@ class _Runner:
             t["q"] = gemm(t["n1"], p[pre + ".0.SelfAttention.q.weight"])
             t["k"] = gemm(t["n1"], p[pre + ".0.SelfAttention.k.weight"])
             t["v"] = gemm(t["n1"], p[pre + ".0.SelfAttention.v.weight"])
-            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, T, T, True, None, rel_d, Rd)
-            t["g1"] = gemm(t["a"], p[pre + ".0.SelfAttention.o.weight"], R=g)
+            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, T, T, True, None, rel_d, Rd,
+                                      pdrop(1, i, D_SELF_P))
+            t["g1"] = proj_res(t["a"], p[pre + ".0.SelfAttention.o.weight"], g,
+                               dropout_site(1, i, D_SELF_OUT))
             t["n2"], t["r2"] = rms_fwd(t["g1"], p[pre + ".1.layer_norm.weight"])
             t["cq"] = gemm(t["n2"], p[pre + ".1.EncDecAttention.q.weight"])
             t["ck"] = gemm(enc, p[pre + ".1.EncDecAttention.k.weight"])
             t["cv"] = gemm(enc, p[pre + ".1.EncDecAttention.v.weight"])
             t["ca"], t["cP"] = attn_fwd(t["cq"], t["ck"], t["cv"], B, H, T, L, False, maskf, None,
-                                        0)
-            t["g2"] = gemm(t["ca"], p[pre + ".1.EncDecAttention.o.weight"], R=t["g1"])
+                                        0, pdrop(1, i, D_CROSS_P))
+            t["g2"] = proj_res(t["ca"], p[pre + ".1.EncDecAttention.o.weight"], t["g1"],
+                               dropout_site(1, i, D_CROSS_OUT))
             t["n3"], t["r3"] = rms_fwd(t["g2"], p[pre + ".2.layer_norm.weight"])
             t["f"] = gemm(t["n3"], p[pre + ".2.DenseReluDense.wi.weight"], act=RELU)
-            g = gemm(t["f"], p[pre + ".2.DenseReluDense.wo.weight"], R=t["g2"])
+            fd = dropout(t["f"], dr, dropout_site(1, i, D_FFN_ACT))
+            g = proj_res(fd, p[pre + ".2.DenseReluDense.wo.weight"], t["g2"],
+                         dropout_site(1, i, D_FFN_OUT))
             tape["dec"].append(t)
         tape["dec_in"] = g
         s = c.d ** -0.5 if c.scale_out else 1.0
         tape["s"] = s
         hs, tape["dec_r"] = rms_fwd(g, p["decoder.final_layer_norm.weight"], scale=s)
+        hs = dropout(hs, dr, dropout_site(1, 255, D_FINAL))
         tape["hs"] = hs
         logits = gemm(hs, p["shared.weight"])
         tape["logits"] = logits
@@ -318,6 +384,7 @@ class _Runner:
     # ---- backward -------------------------------------------------------------------------------
     def backward(self, tape, dloss: float, need_params, need_emb):
         c, p = self.c, self.p
+        dr = c.dropout
         B, L, T, H = tape["B"], tape["L"], tape["T"], c.H
         nm = self.names
         idx = {n: i for i, n in enumerate(nm)}
@@ -329,6 +396,12 @@ class _Runner:
         def put(name, g):
             if want(name):
                 grads[idx[name]] = g
+
+        def pdrop(stack, layer, kind):
+            return dr.args(dropout_site(stack, layer, kind)) if dr else NO_DROP
+
+        def dmask(g, stack, layer, kind):  # gradient through a dropout site: g * mask
+            return dropout(g, dr, dropout_site(stack, layer, kind))
 
         dev = tape["logits"].device
         wt = {}
@@ -355,18 +428,21 @@ class _Runner:
         _lib.call("mpr_add", _lib.ptr(d_shared), _lib.ptr(dW), d_shared.numel(),
                   _lib.ptr(d_shared), _s())
         del dlogits, dW
-        dg, dw = rms_bwd(tape["dec_in"], p["decoder.final_layer_norm.weight"], tape["dec_r"], dhs,
-                         scale=tape["s"])
+        dg, dw = rms_bwd(tape["dec_in"], p["decoder.final_layer_norm.weight"], tape["dec_r"],
+                         dmask(dhs, 1, 255, D_FINAL), scale=tape["s"])
         put("decoder.final_layer_norm.weight", dw)
         drel_d = torch.zeros((2 * tape["Rd"] + 1, H), device=dev, dtype=torch.float32)
         d_enc = None
         for i in reversed(range(c.n_dec)):
             pre = f"decoder.block.{i}.layer"
             t = tape["dec"][i]
-            # FFN: g = g2 + relu(n3 Wi^T) Wo^T
+            # FFN: g = g2 + drop(drop(relu(n3 Wi^T)) Wo^T)
             wo, wi = pre + ".2.DenseReluDense.wo.weight", pre + ".2.DenseReluDense.wi.weight"
-            df, dW = linear_bwd(t["f"], p[wo], Wt(wo), dg, need_dw=want(wo))
+            fd = dropout(t["f"], dr, dropout_site(1, i, D_FFN_ACT))
+            df, dW = linear_bwd(fd, p[wo], Wt(wo), dmask(dg, 1, i, D_FFN_OUT), need_dw=want(wo))
             put(wo, dW)
+            del fd
+            df = dmask(df, 1, i, D_FFN_ACT)
             _lib.call("mpr_relu_bwd", _lib.ptr(t["f"]), _lib.ptr(df), df.numel(), _lib.ptr(df),
                       _s())
             dn3, dW = linear_bwd(t["n3"], p[wi], Wt(wi), df, need_dw=want(wi))
@@ -374,12 +450,13 @@ class _Runner:
             ln = pre + ".2.layer_norm.weight"
             dg2, dw = rms_bwd(t["g2"], p[ln], t["r3"], dn3, dx_acc=dg)
             put(ln, dw)
-            # cross-attention: g2 = g1 + attn(n2 Wq^T, enc Wk^T, enc Wv^T) Wo^T
+            # cross-attention: g2 = g1 + drop(attn(n2 Wq^T, enc Wk^T, enc Wv^T) Wo^T)
             co = pre + ".1.EncDecAttention.o.weight"
-            dca, dW = linear_bwd(t["ca"], p[co], Wt(co), dg2, need_dw=want(co))
+            dca, dW = linear_bwd(t["ca"], p[co], Wt(co), dmask(dg2, 1, i, D_CROSS_OUT),
+                                 need_dw=want(co))
             put(co, dW)
             dcq, dck, dcv = attn_bwd(t["cq"], t["ck"], t["cv"], t["cP"], dca, B, H, T, L, None,
-                                     0)
+                                     0, pdrop(1, i, D_CROSS_P))
             cq, ck, cv = (pre + f".1.EncDecAttention.{x}.weight" for x in "qkv")
             dn2, dW = linear_bwd(t["n2"], p[cq], Wt(cq), dcq, need_dw=want(cq))
             put(cq, dW)
@@ -392,12 +469,13 @@ class _Runner:
             ln = pre + ".1.layer_norm.weight"
             dg1, dw = rms_bwd(t["g1"], p[ln], t["r2"], dn2, dx_acc=dg2)
             put(ln, dw)
-            # self-attention: g1 = g0 + attn(n1 Wq^T, n1 Wk^T, n1 Wv^T; causal, bias) Wo^T
+            # self-attention: g1 = g0 + drop(attn(n1 Wq^T, n1 Wk^T, n1 Wv^T; causal, bias) Wo^T)
             so = pre + ".0.SelfAttention.o.weight"
-            da, dW = linear_bwd(t["a"], p[so], Wt(so), dg1, need_dw=want(so))
+            da, dW = linear_bwd(t["a"], p[so], Wt(so), dmask(dg1, 1, i, D_SELF_OUT),
+                                need_dw=want(so))
             put(so, dW)
             dq, dk, dv = attn_bwd(t["q"], t["k"], t["v"], t["P"], da, B, H, T, T, drel_d,
-                                  tape["Rd"])
+                                  tape["Rd"], pdrop(1, i, D_SELF_P))
             sq, sk, sv = (pre + f".0.SelfAttention.{x}.weight" for x in "qkv")
             dn1, dW = linear_bwd(t["n1"], p[sq], Wt(sq), dq, need_dw=want(sq))
             put(sq, dW)
@@ -409,8 +487,8 @@ class _Runner:
             dg, dw = rms_bwd(t["g0"], p[ln], t["r1"], dn1, dx_acc=dg1)
             put(ln, dw)
             tape["dec"][i] = None
-        # decoder input embedding (tied)
-        embed_bwd_into(d_shared, tape["dec_ids"], dg)
+        # decoder input embedding (tied), through its dropout
+        embed_bwd_into(d_shared, tape["dec_ids"], dmask(dg, 1, 255, D_IN))
         put("shared.weight", d_shared)
         dtab = torch.zeros_like(p[nm[2]])
         _lib.call("mpr_rel_scatter", _lib.ptr(drel_d), _lib.ptr(tape["lut_d"]), tape["Rd"],
@@ -418,15 +496,18 @@ class _Runner:
         put(nm[2], dtab)
         # encoder
         dx, dw = rms_bwd(tape["enc_in"], p["encoder.final_layer_norm.weight"], tape["enc_r"],
-                         d_enc)
+                         dmask(d_enc, 0, 255, D_FINAL))
         put("encoder.final_layer_norm.weight", dw)
         drel_e = torch.zeros((2 * tape["Re"] + 1, H), device=dev, dtype=torch.float32)
         for i in reversed(range(c.n_enc)):
             pre = f"encoder.block.{i}.layer"
             t = tape["enc"][i]
             wo, wi = pre + ".1.DenseReluDense.wo.weight", pre + ".1.DenseReluDense.wi.weight"
-            df, dW = linear_bwd(t["f"], p[wo], Wt(wo), dx, need_dw=want(wo))
+            fd = dropout(t["f"], dr, dropout_site(0, i, D_FFN_ACT))
+            df, dW = linear_bwd(fd, p[wo], Wt(wo), dmask(dx, 0, i, D_FFN_OUT), need_dw=want(wo))
             put(wo, dW)
+            del fd
+            df = dmask(df, 0, i, D_FFN_ACT)
             _lib.call("mpr_relu_bwd", _lib.ptr(t["f"]), _lib.ptr(df), df.numel(), _lib.ptr(df),
                       _s())
             dn2, dW = linear_bwd(t["n2"], p[wi], Wt(wi), df, need_dw=want(wi))
@@ -435,10 +516,11 @@ class _Runner:
             dx1, dw = rms_bwd(t["x1"], p[ln], t["r2"], dn2, dx_acc=dx)
             put(ln, dw)
             so = pre + ".0.SelfAttention.o.weight"
-            da, dW = linear_bwd(t["a"], p[so], Wt(so), dx1, need_dw=want(so))
+            da, dW = linear_bwd(t["a"], p[so], Wt(so), dmask(dx1, 0, i, D_SELF_OUT),
+                                need_dw=want(so))
             put(so, dW)
             dq, dk, dv = attn_bwd(t["q"], t["k"], t["v"], t["P"], da, B, H, L, L, drel_e,
-                                  tape["Re"])
+                                  tape["Re"], pdrop(0, i, D_SELF_P))
             sq, sk, sv = (pre + f".0.SelfAttention.{x}.weight" for x in "qkv")
             dn1, dW = linear_bwd(t["n1"], p[sq], Wt(sq), dq, need_dw=want(sq))
             put(sq, dW)
@@ -454,18 +536,24 @@ class _Runner:
         _lib.call("mpr_rel_scatter", _lib.ptr(drel_e), _lib.ptr(tape["lut_e"]), tape["Re"],
                   c.num_buckets, H, _lib.ptr(dtab), _s())
         put(nm[1], dtab)
-        d_emb = dx.view(B, L, c.d) if need_emb else None
+        d_emb = dmask(dx, 0, 255, D_IN).view(B, L, c.d) if need_emb else None
         return d_emb, grads
 
 
 def t5_loss(named_params: dict, inputs_embeds, attention_mask, labels, num_heads: int,
-            scale_out: bool = True):
+            scale_out: bool = True, dropout_rate: float = 0.0, dropout_seed: int = None):
     """Differentiable T5ForConditionalGeneration(...).loss over ``named_params`` (transformers
-    names -> Parameters; the tied embedding as shared.weight)."""
+    names -> Parameters; the tied embedding as shared.weight).  ``dropout_rate`` > 0: train
+    mode's dropout at transformers' sites, masks from ``dropout_seed`` (default: drawn from
+    torch's global generator, so torch.manual_seed fixes them)."""
     names = list(named_params)
     n_enc, n_dec = _layers(names, "encoder"), _layers(names, "decoder")
     order = t5_param_names(n_enc, n_dec)
     shapes = {n: tuple(named_params[n].shape) for n in order}
     cfg = T5Config(order, shapes, num_heads, scale_out=scale_out)
+    if dropout_rate > 0.0:
+        if dropout_seed is None:
+            dropout_seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64))
+        cfg.dropout = Dropout(dropout_rate, dropout_seed)
     return T5LossFn.apply(cfg, inputs_embeds, attention_mask, labels,
                           *[named_params[n] for n in order])

@@ -187,6 +187,7 @@ def g9_test_batches():
 # parameter: gradient norm + its first 256 values; shared: norm + row sample).
 G10 = {"rows_seed": 1001, "n_rows": 192}
 G11 = {"t5_seed": 1101, "lab_seed": 1102, "T": 7, "rows_seed": 1103, "n_rows": 96}
+G12 = {"p": 0.1, "seed": 1201}  # train-mode dropout (make_g12)
 
 
 def g11_labels(B: int):

@@ -211,13 +211,14 @@ class HFVisual(nn.Module):
 
 
 # ------------------------------------------------------------------ HF T5 second source
-def hf_t5(sd: dict, cfg: syn.T5Config):
+def hf_t5(sd: dict, cfg: syn.T5Config, dropout_rate: float = 0.0):
     tc = transformers.T5Config(d_model=cfg.d_model, d_kv=cfg.d_kv, num_heads=cfg.num_heads,
                                d_ff=cfg.d_ff, num_layers=cfg.num_layers,
                                num_decoder_layers=cfg.num_decoder_layers,
                                vocab_size=cfg.vocab_size, feed_forward_proj="relu",
-                               dropout_rate=0.0, decoder_start_token_id=0, eos_token_id=1,
-                               pad_token_id=0, tie_word_embeddings=True)
+                               dropout_rate=dropout_rate, decoder_start_token_id=0,
+                               eos_token_id=1, pad_token_id=0, tie_word_embeddings=True)
+    tc._attn_implementation = "eager"
     m = transformers.T5ForConditionalGeneration(tc).eval()
     missing, unexpected = m.load_state_dict(sd, strict=False)
     assert not unexpected and not [k for k in missing if "embed_tokens" not in k
@@ -593,9 +594,103 @@ def make_g11():
     print("G11 loss:", loss.item(), "params:", len(named))
 
 
+class _SiteDropout(nn.Module):
+    """Stands in for one of T5's nn.Dropout modules: multiplies by the counter-based mask of the
+    site(s) it occupies (a T5Stack's dropout runs twice per forward: input embeddings, then the
+    final-norm output)."""
+
+    def __init__(self, seed, p, sites):
+        super().__init__()
+        self.seed, self.p, self.sites, self.calls = seed, p, list(sites), 0
+
+    def forward(self, x):
+        from oracle import dropout as od
+        site = self.sites[self.calls]
+        self.calls += 1
+        return x * od.factors(self.seed, site, x.shape, self.p)
+
+
+def install_site_dropout(t5, seed: int, p: float):
+    """Replace every dropout of a train-mode transformers T5 by the device step's masks
+    (multimodalpromptretrieval_amd/train.py dropout_site numbering).  Returns (modules, attention
+    sites, a patched torch.nn.functional.dropout that takes the probability sites in call order:
+    the encoder's self-attentions, then per decoder layer self then cross)."""
+    from multimodalpromptretrieval_amd import train as tr
+    mods = []
+
+    def put(owner, name, sites):
+        m = _SiteDropout(seed, p, sites)
+        setattr(owner, name, m)
+        mods.append(m)
+
+    for stack, st in ((0, t5.encoder), (1, t5.decoder)):
+        put(st, "dropout", [tr.dropout_site(stack, 255, tr.D_IN),
+                            tr.dropout_site(stack, 255, tr.D_FINAL)])
+        for i, blk in enumerate(st.block):
+            put(blk.layer[0], "dropout", [tr.dropout_site(stack, i, tr.D_SELF_OUT)])
+            if stack == 1:
+                put(blk.layer[1], "dropout", [tr.dropout_site(stack, i, tr.D_CROSS_OUT)])
+            ff = blk.layer[-1]
+            put(ff, "dropout", [tr.dropout_site(stack, i, tr.D_FFN_OUT)])
+            put(ff.DenseReluDense, "dropout", [tr.dropout_site(stack, i, tr.D_FFN_ACT)])
+    asites = [tr.dropout_site(0, i, tr.D_SELF_P) for i in range(len(t5.encoder.block))]
+    for i in range(len(t5.decoder.block)):
+        asites += [tr.dropout_site(1, i, tr.D_SELF_P), tr.dropout_site(1, i, tr.D_CROSS_P)]
+    state = {"n": 0}
+
+    def fdropout(x, p=0.5, training=True, inplace=False, _rate=p):
+        from oracle import dropout as od
+        if not training or p == 0.0:
+            return x
+        assert abs(p - _rate) < 1e-12, p
+        site = asites[state["n"]]
+        state["n"] += 1
+        return x * od.factors(seed, site, x.shape, _rate)
+    return mods, asites, state, fdropout
+
+
+def make_g12():
+    """Train mode (main.py:170 model.train()): the reference's T5VisionModel.forward
+    (architectures/T5VisionModel.py:219-234) + loss.backward() at G2 size with transformers' T5
+    in train mode (dropout_rate 0.1) whose every dropout site is given the counter-based mask of
+    the device training step (oracle/dropout.py, seed G12["seed"]): loss and every gradient."""
+    vm_t, t5_sd, t5cfg, retrieval_function = _g2_retrieval()
+    for prm in vm_t.parameters():
+        prm.requires_grad_(False)
+    model = ref_model(vm_t, t5_sd, t5cfg, retrieval_function)
+    p, seed = gi.G12["p"], gi.G12["seed"]
+    model.T5_model = hf_t5(t5_sd, t5cfg, dropout_rate=p)
+    model.T5_model.train()
+    mods, asites, state, fdropout = install_site_dropout(model.T5_model, seed, p)
+    batch = gi.g2_batch()
+    with torch.no_grad():
+        _, _, enc = model.prepare_input(batch)
+        lab = model.tokenizer(batch["answer"], padding="longest", max_length=128,
+                              truncation=True).input_ids
+    m = model.T5_model
+    m.zero_grad()
+    orig = torch.nn.functional.dropout
+    torch.nn.functional.dropout = fdropout
+    try:
+        loss = model.forward(batch)
+    finally:
+        torch.nn.functional.dropout = orig
+    assert state["n"] == len(asites), (state["n"], len(asites))
+    assert all(md.calls == len(md.sites) for md in mods)
+    loss.backward()
+    named = {n: prm.grad for n, prm in m.named_parameters() if prm.grad is not None}
+    rows = gi.shared_rows(gi.G10["rows_seed"], gi.G10["n_rows"], t5cfg.vocab_size,
+                          list(enc["input_ids"].reshape(-1)) + [x for r in lab for x in r])
+    rec = _grad_record(named, rows, full=True)
+    np.savez_compressed(os.path.join(HERE, "g12_train_dropout.npz"),
+                        loss=np.float32(loss.item()), p=np.float64(p), seed=np.int64(seed), **rec)
+    print("G12 loss:", loss.item(), "params:", len(named))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11",
+                             "g12"]
     for w in which:
         globals()["make_" + w]()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:

@@ -41,7 +41,9 @@ def _rel(a, b) -> float:
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
-def _g2_model(device):
+def _g2_model(device, dropout=0.0):
+    # G10 / G11 were made with dropout_rate 0 (the reference's numbers without dropout); train
+    # mode's dropout is checked against G12
     from multimodalpromptretrieval_amd.dataset import VQARetrieval
     from multimodalpromptretrieval_amd.model import T5VisionModel
     ccfg, clip_sd, tcfg, tok_sd, t5cfg, t5_sd = gi.g2_models()
@@ -50,7 +52,8 @@ def _g2_model(device):
     retr.set_index(X, answers, info, gi.G2["k"], False)
     model = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=t5_sd,
                           tokenizer=syn.HashT5Tokenizer(),
-                          retrieval_function=retr.retrieve_closest_qa_pairs)
+                          retrieval_function=retr.retrieve_closest_qa_pairs,
+                          t5_dropout_rate=dropout)
     return model
 
 
@@ -136,3 +139,48 @@ def test_adamw_steps_lower_the_loss_and_refresh_predict(device):
         assert abs(float(model(batch)) - losses[-1]) < losses[0]  # the updated weights serve
     after = model.predict(batch)
     assert isinstance(after, list) and len(after) == len(before)
+
+
+def test_g12_train_mode_dropout_gradients(device):
+    """Train mode with dropout 0.1 (main.py:170): loss and every gradient against the reference's
+    forward/backward run by transformers' T5 in train mode with the same counter-based masks
+    injected at its dropout sites (G12, make_goldens.make_g12)."""
+    z = np.load(os.path.join(GOLD, "g12_train_dropout.npz"))
+    model = _g2_model(device, dropout=float(z["p"]))
+    model.train()
+    batch = gi.g2_batch()
+    model.zero_grad()
+    model.T5_model.next_dropout_seed = int(z["seed"])
+    loss = model(batch)
+    assert abs(float(loss.detach()) - float(z["loss"])) <= 1e-5 * abs(float(z["loss"]))
+    loss.backward()
+    _check_grads(dict(model.T5_model.named_parameters()), z, full=True)
+    # another seed: another loss (the masks are live), same in eval mode as without dropout
+    model.zero_grad()
+    model.T5_model.next_dropout_seed = int(z["seed"]) + 1
+    other = float(model(batch).detach())
+    assert other != float(loss.detach())
+    g10 = np.load(os.path.join(GOLD, "g10_train_grads.npz"))
+    model.eval()
+    with torch.no_grad():
+        assert abs(float(model(batch)) - float(g10["loss"])) <= 1e-5 * abs(float(g10["loss"]))
+
+
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_dropout_mask_matches_oracle(device, p):
+    """mpr_dropout's mask bit for bit against oracle/dropout.py (the numpy hash the G12 golden
+    injected), its density and its scale."""
+    from multimodalpromptretrieval_amd.train import Dropout, dropout
+    from oracle import dropout as od
+    n = 1 << 20
+    x = torch.ones(n, device=device)
+    dr = Dropout(p, 0xDEADBEEF12345)
+    for site in (0, 7, 2047, 4095):
+        y = dropout(x, dr, site).cpu()
+        want = od.factors(dr.seed, site, (n,), p)
+        assert torch.equal(y, want), site
+        kept = float((y != 0).float().mean())
+        assert abs(kept - (1 - p)) < 5e-3, kept
+        assert float(y.max()) == float(np.float32(1 / (1 - p)))
+    r = torch.full((n,), 2.0, device=device)
+    assert torch.equal(dropout(x, dr, 7, residual=r).cpu(), 2.0 + od.factors(dr.seed, 7, (n,), p))

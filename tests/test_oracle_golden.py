@@ -230,3 +230,20 @@ def test_g8_long_source_oracle():
     assert _rel(enc[:, ::37], z["enc_rows"]) < FP_TOL
     assert ot5.generate_cached(sd, emb, mask, cfg.num_heads, 20).tolist() == \
         z["sequences"].tolist()
+
+
+def test_dropout_oracle_masks():
+    """oracle/dropout.py (the device step's counter-based masks): density, scale, determinism,
+    independence between sites and seeds."""
+    from oracle import dropout as od
+    n = 1 << 18
+    for p in (0.1, 0.3):
+        a = od.factors(5, 3, (n,), p)
+        assert abs(float((a != 0).float().mean()) - (1 - p)) < 5e-3
+        assert float(a.max()) == float(np.float32(1 / (1 - p))) and float(a.min()) == 0.0
+        assert torch.equal(a, od.factors(5, 3, (n,), p))
+        b, c = od.factors(5, 4, (n,), p), od.factors(6, 3, (n,), p)
+        for o in (b, c):
+            agree = float(((a != 0) == (o != 0)).float().mean())
+            assert abs(agree - ((1 - p) ** 2 + p ** 2)) < 5e-3  # independent masks
+    assert bool((od.factors(1, 1, (64,), 0.0) == 1.0).all())
