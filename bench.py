@@ -169,7 +169,7 @@ def build(cfg, device, group):
     tok_sd = syn.clip_state_dict(2)                  # PubMedCLIP stand-in (token features)
     t5_sd = syn.t5_state_dict(3, syn.T5Config() if cfg["t5"] == "t5-small" else syn.T5_BASE)
     retr = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=clip_tokenize,
-                        group=group)
+                        group=group, max_batch=cfg["B"])
     X = syn.index_rows(4, cfg["N"], cfg["D"])
     info = {"question_id": [str(j) for j in range(cfg["N"])],
             "question_type": ["open"] * cfg["N"], "question": [""] * cfg["N"]}

@@ -91,7 +91,7 @@ class VQARetrieval:
     BUILD_SLOTS = min(2, int(os.environ.get("MPR_BUILD_SLOTS", "2")))  # index build passes in flight
 
     def __init__(self, device="cuda", clip_state_dict: dict = None, clip_tokenizer=None,
-                 metric: int = L2, group=None):
+                 metric: int = L2, group=None, max_batch: int = None):
         self.device = torch.device(device)
         _lib.ensure_device(self.device)
         if clip_state_dict is None:
@@ -108,6 +108,7 @@ class VQARetrieval:
         self.embed_dim = self.image_encoder.out_dim + self.text_encoder.out_dim
         self.metric = metric
         self.group = group
+        self.max_batch = max_batch  # sharded index: fixed query-block size (no per-search sync)
         self.retrieval_k = 15
         self.is_training_phase = False
         self.index = None
@@ -304,7 +305,8 @@ class VQARetrieval:
         emb = embeddings.detach().to(torch.float32)
         if self.group is not None:
             from .distributed import ShardedIndex
-            self.index = ShardedIndex(emb, self.device, self.metric, group=self.group)
+            self.index = ShardedIndex(emb, self.device, self.metric, group=self.group,
+                                      max_batch=self.max_batch)
         else:
             self.index = DeviceIndex(emb, self.device, self.metric)
         self.retrieval_embeddings = emb

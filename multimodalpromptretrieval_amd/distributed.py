@@ -11,6 +11,14 @@ retrieval step per batch:
 Messages are KB-scale (latency-bound over xGMI), so the candidates travel as ONE packed float64
 tensor (ids < 2^53 and fp32 distances are exact in float64), not a collective per field.
 
+Data-parallel ranks may hold different numbers of batches (a DataLoader sharded over ranks): a
+rank that has run out calls ``finish()`` (or leaves a ``joined()`` block), which keeps answering
+the other ranks' searches with empty query blocks until every rank has finished, so the
+collectives stay paired and nothing deadlocks.  With ``max_batch`` set, every query block is
+padded to that size and carries a header row (its real size and an active flag) through the
+same all_gather: a search needs no all-reduce and no host synchronisation; without it, each
+search all-reduces (MAX) the ranks' [batch size, active flag] first.
+
 ``search_all`` is the replicated-query form (every rank holds the same query batch, as in
 config C5's 256-query batch): local scan of the whole batch, ONE all_gather of the per-shard
 top-k (the north_star's RCCL all-gather over xGMI), and every rank merges — one collective per
@@ -19,6 +27,8 @@ torch.distributed (backend "nccl" = RCCL on ROCm; "gloo" in the CPU tests, which
 searcher/merger so the sharding logic is exercised without a GPU).
 """
 from __future__ import annotations
+
+import contextlib
 
 import torch
 import torch.distributed as dist
@@ -35,8 +45,10 @@ def shard_bounds(n: int, world: int, rank: int):
 class ShardedIndex:
     def __init__(self, rows: torch.Tensor, device, metric: int = L2, group=None,
                  rows_are_local: bool = False, row_offset: int = None, searcher=None,
-                 merger=None):
+                 merger=None, max_batch: int = None):
         self.group = group
+        self.max_batch = int(max_batch) if max_batch else None
+        self.finished = False
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.metric = metric
@@ -62,28 +74,73 @@ class ShardedIndex:
         # gloo (CPU tests, or a one-GPU rehearsal of N ranks) moves host tensors only
         return dist.get_backend(self.group) == "gloo" and self.device.type == "cuda"
 
-    def _max_batch(self, b: int) -> int:
-        """All-reduced max of the per-rank batch sizes (a DataLoader's last partial batch gives
-        ranks different b; every collective below is sized from the common maximum)."""
+    def _reduce(self, b: int, active: int):
+        """All-reduced MAX of (batch size, active flag) over the ranks (host ints)."""
         dev = "cpu" if dist.get_backend(self.group) == "gloo" else self.device
-        t = torch.tensor([b], device=dev, dtype=torch.int64)
+        t = torch.tensor([b, active], device=dev, dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return int(t.item())
+        return int(t[0]), int(t[1])
 
     def search(self, q: torch.Tensor, k: int):
         """q: this rank's [b, d] queries (b may differ between ranks).  Returns (dist, ids)
-        [b, k].  Every rank pads its block to the group's largest b with zero rows (their
-        candidates are computed and dropped before the merge), so the collectives always see
-        equal sizes."""
-        b = q.shape[0]
-        bmax = self._max_batch(b)
-        q = q.to(self.device, torch.float32).contiguous()
-        if b < bmax:
-            q = torch.cat([q, q.new_zeros((bmax - b, self.d))], 0)
+        [b, k].  Every rank pads its block to a common size (the group's largest b, or
+        max_batch) with zero rows (their candidates are computed and dropped before the merge),
+        so the collectives always see equal sizes."""
+        if self.finished:
+            raise RuntimeError("ShardedIndex.search after finish()")
+        return self._step(q, k, active=True)[0]
+
+    def finish(self, k: int = 1) -> int:
+        """This rank has no more queries: take part in the other ranks' searches with empty
+        blocks until every rank has called finish().  Returns the number of empty searches."""
+        n = 0
+        while True:
+            _, any_active = self._step(None, k, active=False)
+            if not any_active:
+                break
+            n += 1
+        self.finished = True
+        return n
+
+    @contextlib.contextmanager
+    def joined(self, k: int = 1):
+        """``with index.joined(): for batch in my_batches: index.search(...)`` — finish() on
+        exit, so ranks with fewer batches do not leave the others waiting."""
+        try:
+            yield self
+        finally:
+            if not self.finished:
+                self.finish(k)
+
+    def _step(self, q, k: int, active: bool):
+        """One exchange round.  Returns ((dist, ids) or None, whether any rank is active)."""
+        b = 0 if q is None else q.shape[0]
+        fixed = self.max_batch is not None
+        if fixed:
+            if b > self.max_batch:
+                raise ValueError(f"batch {b} > max_batch {self.max_batch}")
+            bmax = self.max_batch
+        else:
+            bmax, any_active = self._reduce(b, int(active))
+            if not any_active:
+                return None, False
+        qb = torch.zeros((bmax + (1 if fixed else 0), self.d), device=self.device,
+                         dtype=torch.float32)
+        if b:
+            qb[:b] = q.to(self.device, torch.float32)
+        if fixed:  # header row: [b, active]
+            qb[bmax, 0] = float(b)
+            qb[bmax, 1] = 1.0 if active else 0.0
         stage = self._host_staged()
-        qx = q.cpu() if stage else q
-        q_all = torch.empty((self.world * bmax, self.d), device=qx.device, dtype=qx.dtype)
+        qx = qb.cpu() if stage else qb
+        q_all = torch.empty((self.world * qb.shape[0], self.d), device=qx.device, dtype=qx.dtype)
         dist.all_gather_into_tensor(q_all, qx, group=self.group)
+        if fixed:
+            blocks = q_all.view(self.world, bmax + 1, self.d)
+            if not active:  # only an idle rank reads the flags (a host sync it can afford)
+                if not bool((blocks[:, bmax, 1] != 0).any()):
+                    return None, False
+            q_all = blocks[:, :bmax].reshape(self.world * bmax, self.d)
         q_all = q_all.to(self.device)
         d_loc, i_loc = self._padded_search(q_all, k)            # [W*bmax, k]
         packed = self._pack(d_loc, i_loc)                       # [W*bmax, k, 2] float64
@@ -91,11 +148,16 @@ class ShardedIndex:
             packed = packed.cpu()
         recv = torch.empty_like(packed)
         dist.all_to_all_single(recv, packed, group=self.group)
+        if not b:
+            if not active:
+                return None, True
+            return (torch.empty((0, k), device=self.device, dtype=torch.float32),
+                    torch.empty((0, k), device=self.device, dtype=torch.int64)), True
         d_recv, i_recv = self._unpack(recv.to(self.device))
         # [W(src shard), bmax, k] -> this rank's b real queries: [b, W*k]
         cd = d_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
         ci = i_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
-        return self._merge(cd.contiguous(), ci.contiguous(), k)
+        return self._merge(cd.contiguous(), ci.contiguous(), k), True
 
     def search_all(self, q: torch.Tensor, k: int):
         """q: the SAME [B, d] query batch on every rank (replicated).  Returns (dist, ids)

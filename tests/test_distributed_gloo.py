@@ -135,3 +135,52 @@ def test_sharded_search_all_matches_single_index(world, n, k):
     for r in range(world):
         for ids in res[r]:
             assert ids == ref.tolist()
+
+
+def _worker_uneven(rank, world, port, n, d, counts, k, max_batch, result_q):
+    """Data-parallel ranks with different numbers of batches (counts[rank] batches of 4): each
+    searches its own, then finishes; finish() answers the others' searches until all are done."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X = syn.index_rows(7, n, d)
+        six = ShardedIndex(X, "cpu", searcher=cpu_searcher, merger=cpu_merger,
+                           max_batch=max_batch)
+        got = []
+        with six.joined(k):
+            for j in range(counts[rank]):
+                q = syn.index_rows(100 + 10 * rank + j, 4 - (j % 2), d)  # batches of 4 and 3
+                got.append(six.search(q, k)[1].tolist())
+        result_q.put((rank, got, six.finished))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,counts,max_batch", [(2, [3, 2], None), (2, [3, 2], 4),
+                                                    (3, [2, 0, 3], None), (3, [2, 0, 3], 4)])
+def test_sharded_search_uneven_batch_counts(world, counts, max_batch):
+    """Ranks holding different numbers of batches do not deadlock (ShardedIndex.finish /
+    joined), and every search still returns the single-index ids."""
+    n, d, k = 500, 32, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_uneven, args=(r, world, port, n, d, counts, k, max_batch,
+                                                      q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got, fin = q.get(timeout=120)
+        res[r] = (got, fin)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X = syn.index_rows(7, n, d)
+    for r in range(world):
+        got, fin = res[r]
+        assert fin and len(got) == counts[r]
+        for j, ids in enumerate(got):
+            qq = syn.index_rows(100 + 10 * r + j, 4 - (j % 2), d)
+            assert ids == oret.topk_ids(oret.cdist(qq, X), k, False).tolist()
