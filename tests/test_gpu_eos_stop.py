@@ -22,8 +22,10 @@ def _inputs(device, B=6, L=23, d=128, seed=11):
     g = torch.Generator().manual_seed(seed)
     emb = torch.randn((B, L, d), generator=g) * 0.5
     mask = torch.ones((B, L))
-    mask[1, 17:] = 0
-    mask[4, 9:] = 0
+    if B > 1:
+        mask[1, min(17, L - 1):] = 0
+    if B > 4:
+        mask[4, min(9, L - 1):] = 0
     return emb.to(device), mask.to(device)
 
 
