@@ -136,6 +136,63 @@ def c5_scan(world, rank, device, group, rdev, iters=20):
 N_IMAGES = 8  # distinct host image tensors cycled by the batches (every batch's questions differ)
 
 
+# RCCL all_gather over xGMI, modelled (one GPU per box here: an N-rank RCCL run is not
+# available to this build; the driver's 8-GPU runs measure it): alpha + bytes / beta
+AG_ALPHA_US = 20.0
+AG_BETA_GBS = 50.0
+
+
+def c5_projection(device, iters: int = 20):
+    """Config C5's strong scaling, projected from one GPU: the exact per-rank
+    work of W = 2, 4, 8 — the search of a 1,048,576 / W-row shard for all 256 queries (k = 5)
+    and the merge of the W x 5 gathered candidates per query — timed here, plus a modelled RCCL
+    all_gather of the W x 256 x 5 packed (dist, id) float64 pairs."""
+    from multimodalpromptretrieval_amd.index import DeviceIndex, topk_merge
+    n, d, B, k = C5["N"], C5["D"], C5["B"], C5["k"]
+    gq = torch.Generator(device=device).manual_seed(8)
+    q = torch.randn((B, d), device=device, generator=gq) * 0.3
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters * 1e3  # us
+
+    out = {}
+    t1 = None
+    for W in (1, 2, 4, 8):
+        rows = syn.index_rows_device(7, 0, n // W, d, device)
+        ix = DeviceIndex(rows, device)
+        del rows
+        t_search = timed(lambda: ix.search(q, k))
+        dl, il = ix.search(q, k)
+        ix.close()
+        torch.cuda.empty_cache()
+        if W == 1:
+            t1 = t_search
+            out["1"] = {"search_us": round(t_search, 1), "projected_us": round(t_search, 1)}
+            continue
+        cd = dl.repeat(1, W).contiguous()
+        ci = (il.repeat(1, W) + torch.arange(W, device=device).repeat_interleave(k)
+              * (n // W)).contiguous()
+        t_merge = timed(lambda: topk_merge(cd, ci, k))
+        ag_bytes = W * B * k * 16
+        t_ag = AG_ALPHA_US + ag_bytes / (AG_BETA_GBS * 1e3)
+        tot = t_search + t_merge + t_ag
+        out[str(W)] = {"search_us": round(t_search, 1), "merge_us": round(t_merge, 1),
+                       "all_gather_us_model": round(t_ag, 1), "projected_us": round(tot, 1),
+                       "speedup": round(t1 / tot, 2)}
+    out["model"] = (f"per rank: the W-shard search (timed) + merge of W x {k} candidates (timed) + "
+                    f"all_gather {AG_ALPHA_US} us + bytes / {AG_BETA_GBS} GB/s (modelled)")
+    return out
+
+
 def make_batches(n_batches: int, B: int, seed: int, n_images: int = N_IMAGES):
     """Batches as main.py's DataLoader yields them (main.py:94-96, no pin_memory): images fp32
     [B, 3, 224, 224] in pageable HOST memory (copied to the device inside every step, as
@@ -691,6 +748,8 @@ def main():
     c5 = None
     if not args.no_c5:
         c5 = c5_scan(world, rank, device, group, rdev)
+        if world == 1:
+            c5["projection_1_to_8"] = c5_projection(device)
         barrier()
 
     cpu = None

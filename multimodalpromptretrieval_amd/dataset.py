@@ -29,6 +29,7 @@ import torch
 from . import _lib
 from .encoders import CLS, DeviceCLIPText, DeviceViT, encode_towers, encode_towers_multi  # noqa: F401,E501
 from .index import L2, DeviceIndex
+from .staging import to_device, uploader
 
 BUCKETS = ["very unlikely", "unlikely", "maybe", "likely", "very likely", "certainly"]
 
@@ -82,6 +83,27 @@ def read_pickled_data(path):
     a list of answer strings / a dict of lists.  Refuses anything that needs a global."""
     with open(path, "rb") as f:
         return _DataOnlyUnpickler(f).load()
+
+
+def _staged(batches, up, ahead: int = 2):
+    """Iterate ``batches`` with the next ``ahead`` batches' images already submitted to the
+    uploader (staging.ImageUploader), so their host -> device copies overlap this batch."""
+    if up is None:
+        yield from batches
+        return
+    from collections import deque
+    q = deque()
+    it = iter(batches)
+    while True:
+        while len(q) < ahead + 1:
+            b = next(it, None)
+            if b is None:
+                break
+            up.submit(b.get("image") if isinstance(b, dict) else None)
+            q.append(b)
+        if not q:
+            return
+        yield q.popleft()
 
 
 class VQARetrieval:
@@ -151,7 +173,7 @@ class VQARetrieval:
         the stream it is produced on (the caller waits on that stream before using it)."""
         s_img = self._streams()
         cur = torch.cuda.current_stream(self.device)
-        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+        img = to_device(batch["image"], self.device)
         toks = self.clip_tokenize(batch["question"])
         B = img.shape[0]
         q = torch.empty((B, self.embed_dim), device=self.device, dtype=torch.float32)
@@ -200,7 +222,7 @@ class VQARetrieval:
             return [self.prefetch_many([b], other_vit, other_mode, slot)[0] for b in batches]
         s_img = self._slot_stream(int(slot))
         cur = torch.cuda.current_stream(self.device)
-        imgs = [b["image"].to(self.device, torch.float32, non_blocking=True) for b in batches]
+        imgs = [to_device(b["image"], self.device) for b in batches]
         img = imgs[0] if len(imgs) == 1 else torch.cat(imgs)
         toks = [self.clip_tokenize(b["question"]) for b in batches]
         sizes = [x.shape[0] for x in imgs]
@@ -257,7 +279,7 @@ class VQARetrieval:
                 and pending[2] == tuple(batch["question"])):
             cur.wait_stream(s_img)
             return pending[1]
-        img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+        img = to_device(batch["image"], self.device)
         toks = self.clip_tokenize(batch["question"])
         q = torch.empty((img.shape[0], self.embed_dim), device=self.device, dtype=torch.float32)
         di = self.image_encoder.out_dim
@@ -277,8 +299,7 @@ class VQARetrieval:
         wait for it; the caller joins ``self._slot_stream(slot)`` itself)."""
         cur = torch.cuda.current_stream(self.device)
         s_img = self._slot_stream(slot)
-        img = torch.cat([b["image"].to(self.device, torch.float32, non_blocking=True)
-                         for b in (b0, b1)])
+        img = torch.cat([to_device(b["image"], self.device) for b in (b0, b1)])
         toks = [self.clip_tokenize(b["question"]) for b in (b0, b1)]
         n = b0["image"].shape[0]
         q = torch.empty((2 * n, self.embed_dim), device=self.device, dtype=torch.float32)
@@ -338,7 +359,8 @@ class VQARetrieval:
         pend = None
         npass = 0
         used = set()
-        for batch in data_loader:
+        up = uploader(self.device)
+        for batch in _staged(data_loader, up):
             answers.extend(batch["answer"])
             info["question_type"].extend(batch["question_type"])
             info["question_id"].extend(batch["question_id"])

@@ -28,6 +28,7 @@ from torch import nn
 
 from . import _lib
 from .encoders import TOKENS, DeviceViT
+from .staging import to_device
 from .t5 import DeviceT5
 
 
@@ -305,7 +306,7 @@ class T5VisionModel(nn.Module):
                 # pass (shared launches), the retrieval picks its half up in encode_queries
                 img_tok, tok_stream = pair(batch, vit, TOKENS)
             else:
-                img = batch["image"].to(self.device, torch.float32, non_blocking=True)
+                img = to_device(batch["image"], self.device)
                 if not hasattr(self, "_s_tok"):
                     self._s_tok = torch.cuda.Stream(self.device)
                 self._s_tok.wait_stream(cur)

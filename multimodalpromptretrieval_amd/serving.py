@@ -30,7 +30,7 @@ from dataclasses import dataclass
 
 import torch
 
-from . import _lib
+from . import _lib, staging
 
 
 @dataclass(frozen=True)
@@ -89,6 +89,8 @@ class _Call:
 class ServingLoop:
     """One pass of the pipeline over an iterable of batches (see the module docstring)."""
 
+    STAGE_AHEAD = 4  # batches whose host images are being uploaded ahead of their tower pass
+
     def __init__(self, model, opts: ServingOptions):
         self.m = model
         self.o = opts
@@ -106,6 +108,22 @@ class ServingLoop:
         self.it = None
         self.exhausted = False
         self.steps_run = []     # decode steps launched per generate call
+        self.upcoming = deque()  # pulled from the source, images submitted to the uploader
+        self.src_done = False
+        self.uploader = staging.uploader(model.device)
+
+    def _pull(self):
+        """The next source batch; the STAGE_AHEAD batches after it already have their images on
+        their way to the device (staging.ImageUploader), off this thread."""
+        while len(self.upcoming) < self.STAGE_AHEAD + 1 and not self.src_done:
+            b = next(self.it, None)
+            if b is None:
+                self.src_done = True
+                break
+            if self.uploader is not None:
+                self.uploader.submit(b["image"])
+            self.upcoming.append(b)
+        return self.upcoming.popleft() if self.upcoming else None
 
     # ---- towers (one pass ahead) -----------------------------------------------------------
     def _refill(self):
@@ -114,7 +132,7 @@ class ServingLoop:
         while not self.exhausted and len(self.ready) < per_pass:
             chunk = []
             while len(chunk) < per_pass:
-                b = next(self.it, None)
+                b = self._pull()
                 if b is None:
                     self.exhausted = True
                     break
