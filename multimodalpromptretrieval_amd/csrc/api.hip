@@ -1,4 +1,5 @@
 // api.hip — the extern "C" boundary of libmpr.so (declared in include/mpr.h).
+#include <cstdlib>
 #include <cstring>
 
 #include "models.h"
@@ -435,6 +436,11 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
       MPR_TRY(pack(ly->pk_wo, ly->wo, d, dff));
     }
     MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
+    {
+      const char* e = getenv("MPR_DECODE_FOLD");
+      m->fold = !(e && e[0] == '0');
+    }
+    if (m->fold) MPR_TRY(m->build_folded());
     MPR_HIP(hipDeviceSynchronize());
     *out = m.release();
     return MPR_OK;

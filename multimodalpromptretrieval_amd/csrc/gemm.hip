@@ -711,7 +711,11 @@ __global__ __launch_bounds__(256) void pack_rows16_kernel(const float* __restric
 // Every option is a template flag: measured on MI355X, each runtime-optional part of this
 // kernel (a residual/bias branch, an argmax branch, a K loop) added 0.4-0.6 us to a ~3 us
 // launch, so each launch carries only the code its call needs, straight-line.
-enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8 };
+// SKF_RELU_IN: ReLU applied to the A operand as it is staged (relu commutes with the positive
+// per-row scale of SKF_RSCALE); SKF_RSCALE: the epilogue scales row m by rsqrt(mean(src_m^2) +
+// eps) of an external row (the decode chain's folded RMSNorm, t5.hip).
+enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8, SKF_RELU_IN = 16,
+             SKF_RSCALE = 32 };
 
 // NT 16-column tiles per block share the activation slab (NT > 1 for the 32k-column lm_head,
 // which needs more bytes in flight per wave); two accumulator chains per tile halve the
@@ -721,7 +725,9 @@ enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8 };
 template <int MAXC, int NT, int F, bool LOOP, int MR>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   constexpr bool RMS = (F & SKF_RMS) != 0, RES = (F & SKF_RES) != 0,
-                 RELU = (F & SKF_RELU) != 0, AMAX = (F & SKF_AMAX) != 0;
+                 RELU = (F & SKF_RELU) != 0, AMAX = (F & SKF_AMAX) != 0,
+                 RELU_IN = (F & SKF_RELU_IN) != 0, RSCALE = (F & SKF_RSCALE) != 0;
+  static_assert(!(RMS && RSCALE), "one row-scale source");
   constexpr int MROWS = 16 * MR;      // activation rows: MR 16-row groups share each weight load
   const GemmArgs& a = sa.g;
   constexpr int XLD = MAXC * 16 + 4;  // slab row stride (floats): conflict-free fragment reads
@@ -795,6 +801,12 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
                                               min(col, K - 4));
       if (!ok) xr[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if constexpr (RELU_IN) {
+#pragma unroll
+      for (int u = 0; u < MR * MAXC; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xr[u][e] = xr[u][e] > 0.f ? xr[u][e] : 0.f;
+    }
     // every load of the pass is in flight before the first wait (hipcc otherwise sinks the
     // weight loads next to their MFMAs, behind the activation round trip through LDS)
     __builtin_amdgcn_sched_barrier(0);
@@ -840,6 +852,20 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       if (lane < 16) ssq_s[wave][r * 16 + lane] = v;
     }
   }
+  if constexpr (RSCALE) {
+    // sum of squares of each of the block's rows of the scale source, a wave per row
+    for (int r = wave; r < MROWS; r += SK_WAVES) {
+      const float* src = sa.rs_src + (int64_t)(row0 + min(r, M - 1)) * sa.rs_ld;
+      float v = 0.f;
+      for (int c = lane * 4; c < sa.rs_n; c += 256) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(src + c);
+        v += x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0) ssq_s[0][r] = v;
+    }
+  }
   __syncthreads();
   if (wave >= NT * MR) return;
   const int tile = blockIdx.x * NT + et;
@@ -855,6 +881,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][m];
     scale = (1.0f / sqrtf(t / (float)K + sa.rms_eps)) * sa.a_scale;
   }
+  if constexpr (RSCALE) scale = (1.0f / sqrtf(ssq_s[0][m] / (float)sa.rs_n + sa.rms_eps)) * sa.a_scale;
   if constexpr (AMAX) {
     // greedy head: per (row m, block) best column, lowest index on ties (torch.argmax)
     float bv = -INFINITY;
@@ -1189,6 +1216,7 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, un
     switch (F) {
       MPR_SK(0) MPR_SK(1) MPR_SK(2) MPR_SK(3) MPR_SK(4) MPR_SK(5) MPR_SK(6) MPR_SK(7)
       MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS)
+      MPR_SK(SKF_RELU_IN | SKF_RSCALE | SKF_RES)
       default: break;
     }
   }
@@ -1214,8 +1242,16 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(amax || (a.C && a.N % 16 == 0 && a.ldc % 4 == 0 && aligned16(a.C) &&
                        (!a.R || (a.ldr % 4 == 0 && aligned16(a.R)))),
               "gemm_skinny: N must be a multiple of 16, C/R rows 16-byte aligned");
+  MPR_REQUIRE(!sa.rs_src || (!sa.rms_w && !amax && sa.rs_n % 4 == 0 && sa.rs_ld % 4 == 0 &&
+                              aligned16(sa.rs_src)),
+              "gemm_skinny: an external row scale excludes the fused RMSNorm / argmax; its rows "
+              "16-byte aligned");
   const int F = (sa.rms_w ? SKF_RMS : 0) | (a.R ? SKF_RES : 0) |
-                (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0);
+                (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0) |
+                (sa.relu_in ? SKF_RELU_IN : 0) | (sa.rs_src ? SKF_RSCALE : 0);
+  MPR_REQUIRE(!(F & (SKF_RELU_IN | SKF_RSCALE)) || F == (SKF_RELU_IN | SKF_RSCALE | SKF_RES),
+              "gemm_skinny: relu_in / row scale only as the folded FFN-out (relu_in + scale + "
+              "residual)");
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
   // Above 32 rows (grouped decodes) the rows split over blocks of MPR_SKINNY_ROWS (32 default,

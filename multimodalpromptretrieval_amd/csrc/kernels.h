@@ -61,6 +61,12 @@ struct SkinnyArgs {
   // (C must be null).
   float* amax_val = nullptr;
   int32_t* amax_idx = nullptr;
+  // Folded RMSNorm of the decode chain (t5.hip): relu_in applies ReLU to A as it is staged;
+  // rs_src: row m of the result is scaled by rsqrt(mean(rs_src[m, :rs_n]^2) + rms_eps)
+  bool relu_in = false;
+  const float* rs_src = nullptr;
+  int64_t rs_ld = 0;
+  int rs_n = 0;
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
@@ -117,6 +123,12 @@ struct AttnArgs {
   // (the layer-0 bias table gathered through the bucket LUT once at model load), optional.
   const float* rel_tab = nullptr;
   int lut_radius = 0;
+  // one-query decode only: q row b is scaled by rsqrt(mean(q_rms_src[b, :q_rms_n]^2) + eps) (the
+  // decode chain's folded RMSNorm ahead of the cross-attention query, t5.hip)
+  const float* q_rms_src = nullptr;
+  int64_t q_rms_bs = 0;
+  int q_rms_n = 0;
+  float q_rms_eps = 1e-6f;
 };
 int attention(const AttnArgs& a, hipStream_t s);
 // The attentions of up to ATTN_GROUP towers of a lockstep pass (or batches of a T5 encoder
@@ -147,9 +159,10 @@ int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hip
 // lm_head's per-tile partials part_*[b*nparts + p] (first maximal index); finished rows emit pad;
 // tokens[b*tok_ld + col] = next; unfinished[b] &= next != eos;
 // x[b, :] = table[next, :] (decoder input embedding of the next step, may be null).
+// (x: the next step's input rows, row stride x_ld)
 int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int M,
                 int32_t* unfinished, int32_t* tokens, int64_t tok_ld, int col, int eos, int pad,
-                const float* table, int D, float* x, hipStream_t s);
+                const float* table, int D, float* x, hipStream_t s, int64_t x_ld = -1);
 
 // Generic device helpers.
 int fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s);

@@ -271,6 +271,18 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
   int lk_end = a.Lk;
   if (a.causal) lk_end = min(lk_end, qpos + 1);
   const int dg = tid & 15, kg = tid >> 4;  // PV: dims 4*dg..4*dg+3, keys kg*16..kg*16+15
+  float qscale = a.scale;
+  if (a.q_rms_src) {  // the folded RMSNorm of the query's source row (t5.hip decode chain)
+    const float* src = a.q_rms_src + (int64_t)b * a.q_rms_bs;
+    float v = 0.f;
+    for (int c = tid; c < a.q_rms_n; c += 256) v += src[c] * src[c];
+    v = wave_sum(v);
+    if (lane == 0) red[0][wave] = v;
+    __syncthreads();
+    const float t = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    qscale = a.scale * (1.0f / sqrtf(t / (float)a.q_rms_n + a.q_rms_eps));
+    __syncthreads();  // red reused below
+  }
   float m = -INFINITY, l = 0.f;
   f32x4 o = {0.f, 0.f, 0.f, 0.f};
   for (int kc = 0; kc < lk_end; kc += DEC_KC) {
@@ -301,7 +313,7 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
     for (int d = 0; d < ATT_D / 4; ++d)
       s += qv[d][0] * kr[d][0] + qv[d][1] * kr[d][1] + qv[d][2] * kr[d][2] + qv[d][3] * kr[d][3];
     const bool valid = in && mk != 0.f;
-    const float sc = valid ? s * a.scale + rb : -INFINITY;  // rb is 0 without a bias table
+    const float sc = valid ? s * qscale + rb : -INFINITY;  // rb is 0 without a bias table
     float wm = wave_max(sc);
     if (lane == 0) red[0][wave] = wm;
     __syncthreads();
@@ -601,7 +613,7 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(const float* part_val,
                                                           int32_t* unfinished, int32_t* tokens,
                                                           int64_t tok_ld, int col, int eos,
                                                           int pad, const float* table, int D,
-                                                          float* x) {
+                                                          float* x, int64_t x_ld) {
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int unf = unfinished[row];  // issued with the partial loads, not after the argmax
@@ -661,7 +673,7 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(const float* part_val,
   }
   if (x) {
     const float* src = table + (int64_t)next * D;
-    for (int c = tid; c < D; c += 256) x[(int64_t)row * D + c] = src[c];
+    for (int c = tid; c < D; c += 256) x[(int64_t)row * x_ld + c] = src[c];
   }
 }
 
@@ -797,6 +809,8 @@ int attention(const AttnArgs& a, hipStream_t s) {
     MPR_REQUIRE(std::max(a.q_pos0 + a.Lq, a.Lk) - 1 <= a.lut_radius,
                 "attention: bias table radius %d too small (Lq %d, Lk %d)", a.lut_radius, a.Lq,
                 a.Lk);
+  MPR_REQUIRE(!a.q_rms_src || (a.Lq == 1 && a.q_rms_n > 0),
+              "attention: a query row scale only on the one-query decode path");
   if (a.Lq == 1) {
     // (A wave-per-(b, h) form without block barriers measured slower: 4.4 / 5.3 us self / cross
     // against 3.8 / 4.1 — a quarter of the loads in flight per (b, h).)
@@ -901,11 +915,12 @@ int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hip
 
 int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int M,
                 int32_t* unfinished, int32_t* tokens, int64_t tok_ld, int col, int eos, int pad,
-                const float* table, int D, float* x, hipStream_t s) {
+                const float* table, int D, float* x, hipStream_t s, int64_t x_ld) {
   if (M == 0) return MPR_OK;
   MPR_REQUIRE(M <= 128, "greedy_step: %d rows > 128", M);
   hipLaunchKernelGGL(greedy_step_kernel, dim3(M), dim3(256), 0, s, part_val, part_idx, nparts,
-                     unfinished, tokens, tok_ld, col, eos, pad, table, D, x);
+                     unfinished, tokens, tok_ld, col, eos, pad, table, D, x,
+                     x_ld < 0 ? (int64_t)D : x_ld);
   MPR_LAUNCHED();
   return MPR_OK;
 }

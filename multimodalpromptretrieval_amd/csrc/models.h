@@ -113,6 +113,10 @@ struct T5Layer {
   DevBuf cq, co, ln2;                      // decoder only: cross-attn q/o, ffn norm
   // decoder only: pack_rows16 images of qkv, o, cq, co, wi, wo for the decode-step GEMMs
   DevBuf pk_qkv, pk_o, pk_cq, pk_co, pk_wi, pk_wo;
+  // decoder only, folded decode chain (T5Model::fold): images of
+  //   W_ocq  = [[o | I_d], [cq diag(ln1) o | cq diag(ln1)]]     [d + inner, inner + d]
+  //   W_cowi = [[co | I_d], [wi diag(ln2) co | wi diag(ln2)]]   [d + d_ff, inner + d]
+  DevBuf pk_ocq, pk_cowi;
 };
 
 // Per-call workspace of generate(): activations, decode caches, captured graphs and the decode
@@ -123,6 +127,7 @@ struct T5Work {
   DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, unfinished, cur_tok;
   DevBuf enc_in, mask_in, part_val, part_idx, tok_buf;
   DevBuf mask_enc, enc_tmp;  // a group's encoder mask / output when several groups share a decode
+  DevBuf ax, yq, hz;  // folded decode chain rows: [a | x], [c | h | u], [h2 | z]
   uint64_t gen = 0;  // bumped by every buffer growth: invalidates captured graphs
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {
@@ -158,6 +163,10 @@ struct T5Model : mpr_model {
   T5Model() : mpr_model(T5) { use_slot(0); }
   int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
   int inner = 0, lut_radius = 0;
+  // The decode chain with its RMSNorms folded into the preceding projections (6 launches per
+  // layer instead of 8; MPR_DECODE_FOLD=0 keeps the 8-launch chain): see decode_body.
+  bool fold = false;
+  int build_folded();
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
   DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
   // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
@@ -211,6 +220,8 @@ struct T5Model : mpr_model {
   int init_body(int B, int L, int max_new, int start, hipStream_t s);
   int decode_body(int B, int L, int max_new, int eos, int pad, hipStream_t s, int t0 = 0,
                   int t1 = -1);
+  int decode_body_folded(int B, int L, int max_new, int eos, int pad, hipStream_t s, int t0,
+                         int t1);
   int launch_chunk(int c);          // decode chunk c of the pending call + its flag copy
   int finish_pending(hipStream_t s);  // token copies, join onto s, slot free
   template <class F>

@@ -32,7 +32,72 @@ bool graphs_enabled() {
   const char* e = getenv("MPR_GRAPHS");
   return !(e && e[0] == '0');
 }
+
+// One folded decode-chain weight [d + N2, inner + d] (row-major):
+//   rows n < d:       [top[n, :] | e_n]                      (top: [d, inner], the o / co weight)
+//   rows d + j < N2:  [sum_k bot[j, k] w[k] top[k, :] | bot[j, :] * w]
+// (bot: [N2, d], the cq / wi weight; w the RMSNorm weight between them).  The product is summed
+// in double and rounded once.
+__global__ void fold_weights_kernel(const float* __restrict__ top, const float* __restrict__ bot,
+                                    const float* __restrict__ w, int d, int inner, int N2,
+                                    float* __restrict__ out) {
+  const int K = inner + d;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)(d + N2) * K) return;
+  const int row = (int)(e / K), col = (int)(e % K);
+  float v;
+  if (row < d) {
+    v = col < inner ? top[(int64_t)row * inner + col] : (col - inner == row ? 1.f : 0.f);
+  } else {
+    const int j = row - d;
+    const float* br = bot + (int64_t)j * d;
+    if (col < inner) {
+      double acc = 0.0;
+      for (int k = 0; k < d; ++k)
+        acc += (double)br[k] * (double)w[k] * (double)top[(int64_t)k * inner + col];
+      v = (float)acc;
+    } else {
+      v = br[col - inner] * w[col - inner];
+    }
+  }
+  out[e] = v;
+}
 }  // namespace
+
+// The folded decode chain.  T5's decoder layer is
+//   x1 = x + a Wo^T;  q = rms(x1) ln1 Wcq^T;  x2 = x1 + c Wco^T;  f = relu(rms(x2) ln2 Wi^T);
+//   x3 = x2 + f Wwo^T
+// and rms(v) = v / sqrt(mean(v^2) + eps) is a positive per-row scale, so with
+// M1 = Wcq diag(ln1), M3 = Wi diag(ln2):
+//   [x1 | u] = [a | x] [[Wo | I], [M1 Wo | M1]]^T,  q = u / rms_scale(x1)
+//   [x2 | z] = [c | x1] [[Wco | I], [M3 Wco | M3]]^T,  f Wwo^T = (relu(z) Wwo^T) / rms_scale(x2)
+// (relu commutes with the positive scale): the two RMSNorm launches fold into the o and co
+// projections, the cross-attention applies its query's scale from the x1 row it reads, and the
+// FFN-out GEMM applies relu on load and the x2 scale in its epilogue.  8 -> 6 dependent launches
+// per layer, at a different fp32 rounding order than the reference's.
+int T5Model::build_folded() {
+  const int K = inner + d;
+  DevBuf tmp;
+  MPR_TRY(tmp.ensure((size_t)(d + std::max(inner, dff)) * K * 4));
+  auto fold = [&](DevBuf& dst, const DevBuf& top, const DevBuf& bot, const DevBuf& w,
+                  int N2) -> int {
+    const int64_t n = (int64_t)(d + N2) * K;
+    hipLaunchKernelGGL(fold_weights_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, nullptr,
+                       top.as<float>(), bot.as<float>(), w.as<float>(), d, inner, N2,
+                       tmp.as<float>());
+    MPR_LAUNCHED();
+    MPR_TRY(dst.ensure((size_t)packed_rows16_elems(d + N2, K) * 4));
+    MPR_TRY(pack_rows16(tmp.as<float>(), d + N2, K, K, dst.as<float>(), nullptr));
+    MPR_HIP(hipStreamSynchronize(nullptr));  // tmp is reused by the next fold
+    return MPR_OK;
+  };
+  for (auto& lp : dec) {
+    T5Layer& ly = *lp;
+    MPR_TRY(fold(ly.pk_ocq, ly.o, ly.cq, ly.ln1, inner));
+    MPR_TRY(fold(ly.pk_cowi, ly.co, ly.wi, ly.ln2, dff));
+  }
+  return MPR_OK;
+}
 
 T5Work::~T5Work() {
   for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
@@ -167,8 +232,12 @@ int T5Model::init_body(int B, int L, int max_new, int start, hipStream_t s) {
   MPR_TRY(fill_i32(ws->unfinished.as<int32_t>(), 1, B, s));
   MPR_TRY(fill_i32(ws->cur_tok.as<int32_t>(), start, B, s));
   MPR_TRY(fill_i32(ws->tok_buf.as<int32_t>(), start, (int64_t)B * T1, s));  // column 0 = start
-  MPR_TRY(embed_gather(shared.as<float>(), ws->cur_tok.as<int32_t>(), 1, B, 1, d, nullptr,
-                       ws->dx.as<float>(), d, 0, s));
+  if (fold)  // the residual stream lives in the x half of the [a | x] rows
+    MPR_TRY(embed_gather(shared.as<float>(), ws->cur_tok.as<int32_t>(), 1, B, 1, d, nullptr,
+                         ws->ax.as<float>() + inner, inner + d, 0, s));
+  else
+    MPR_TRY(embed_gather(shared.as<float>(), ws->cur_tok.as<int32_t>(), 1, B, 1, d, nullptr,
+                         ws->dx.as<float>(), d, 0, s));
   return MPR_OK;
 }
 
@@ -190,6 +259,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
 
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
+  if (fold) return decode_body_folded(B, L, max_new, eos, pad, s, t0, t1);
   for (int t = t0; t < t1; ++t) {
     for (int l = 0; l < Ld; ++l) {
       const T5Layer& ly = *dec[l];
@@ -257,6 +327,85 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
     MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), nparts, B, unf, toks, T1,
                         t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,
                         s));
+  }
+  return MPR_OK;
+}
+
+// decode_body with the folded chain (build_folded): per layer qkv (RMS fused), self-attention into
+// the a half of [a | x], [x1 | u] (one GEMM over [a | x]), cross-attention (query scaled by
+// x1's RMS) into the c half of [c | x1 | u], [x2 | z] (one GEMM over [c | x1]), FFN-out (relu on
+// load, x2's RMS scale, + x2) into the x half of [a | x].
+int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hipStream_t s,
+                                int t0, int t1) {
+  const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
+  const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
+  const int nparts = (int)cdiv(V, 16);
+  const float* maskp = ws->mask_in.as<float>();
+  const int64_t ldA = inner + d, ldY = 2 * inner + d, ldZ = d + dff;
+  float* ax = ws->ax.as<float>();  // [a | x]
+  float* yq = ws->yq.as<float>();  // [c | x1 | u]
+  float* hz = ws->hz.as<float>();  // [x2 | z]
+  float* xp = ax + inner;
+  int32_t* unf = ws->unfinished.as<int32_t>();
+  int32_t* toks = ws->tok_buf.as<int32_t>();
+  const float* ckv = ws->cross_kv.as<float>();
+  const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
+  const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
+  for (int t = t0; t < t1; ++t) {
+    for (int l = 0; l < Ld; ++l) {
+      const T5Layer& ly = *dec[l];
+      float* cl = ws->cache.as<float>() + l * cache_layer;
+      SkinnyArgs sq;  // q | k | v of this position = rms(x) ln0 Wqkv^T
+      sq.g.A = xp; sq.g.lda = ldA;
+      sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
+      sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
+      sq.wpk = ly.pk_qkv.as<float>();
+      MPR_TRY(gemm_skinny(sq, s));
+      AttnArgs at;
+      at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
+      at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
+      at.v = cl + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
+      at.o = ax; at.o_bs = ldA; at.o_rs = ldA;
+      at.B = B; at.H = H; at.Lq = 1; at.Lk = t + 1; at.scale = 1.f; at.causal = 1; at.q_pos0 = t;
+      at.rel_tab = dec_tab.as<float>();
+      at.lut_radius = lut_radius;
+      MPR_TRY(attention(at, s));
+      SkinnyArgs so;  // [x1 | u] = [a | x] W_ocq^T
+      so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
+      so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
+      so.wpk = ly.pk_ocq.as<float>();
+      MPR_TRY(gemm_skinny(so, s));
+      AttnArgs ca;  // c = attention(u / rms_scale(x1), K_enc, V_enc)
+      ca.q = yq + inner + d; ca.q_bs = ldY; ca.q_rs = ldY;
+      ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
+      ca.v = ckv + (int64_t)l * 2 * inner + inner; ca.v_bs = ca.k_bs; ca.v_rs = ckv_ld;
+      ca.o = yq; ca.o_bs = ldY; ca.o_rs = ldY;
+      ca.B = B; ca.H = H; ca.Lq = 1; ca.Lk = L; ca.scale = 1.f;
+      ca.key_mask = maskp; ca.mask_bs = L;
+      ca.q_rms_src = yq + inner; ca.q_rms_bs = ldY; ca.q_rms_n = d; ca.q_rms_eps = T5_EPS;
+      MPR_TRY(attention(ca, s));
+      SkinnyArgs cw;  // [x2 | z] = [c | x1] W_cowi^T
+      cw.g.A = yq; cw.g.lda = ldY; cw.g.C = hz; cw.g.ldc = ldZ;
+      cw.g.M = B; cw.g.N = d + dff; cw.g.K = inner + d;
+      cw.wpk = ly.pk_cowi.as<float>();
+      MPR_TRY(gemm_skinny(cw, s));
+      SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
+      fo.g.A = hz + d; fo.g.lda = ldZ; fo.g.R = hz; fo.g.ldr = ldZ;
+      fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
+      fo.relu_in = true; fo.rs_src = hz; fo.rs_ld = ldZ; fo.rs_n = d; fo.rms_eps = T5_EPS;
+      fo.wpk = ly.pk_wo.as<float>();
+      MPR_TRY(gemm_skinny(fo, s));
+    }
+    SkinnyArgs hd;
+    hd.g.A = xp; hd.g.lda = ldA; hd.g.C = nullptr; hd.g.M = B; hd.g.N = V; hd.g.K = d;
+    hd.rms_w = dec_final.as<float>(); hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
+    hd.amax_val = ws->part_val.as<float>();
+    hd.amax_idx = ws->part_idx.as<int32_t>();
+    hd.wpk = pk_lm_head.as<float>();
+    MPR_TRY(gemm_skinny(hd, s));
+    MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), nparts, B, unf, toks,
+                        T1, t + 1, eos, pad, shared.as<float>(), d,
+                        t + 1 < max_new ? xp : nullptr, s, ldA));
   }
   return MPR_OK;
 }
@@ -355,6 +504,11 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
   MPR_TRY(grow(ws->cache, (size_t)Ld * B * Tc * 3 * inner * 4));
   MPR_TRY(grow(ws->dx, (size_t)B * d * 4));
   MPR_TRY(grow(ws->dq, (size_t)B * inner * 4));
+  if (fold) {
+    MPR_TRY(grow(ws->ax, (size_t)B * (inner + d) * 4));
+    MPR_TRY(grow(ws->yq, (size_t)B * (2 * inner + d) * 4));
+    MPR_TRY(grow(ws->hz, (size_t)B * (d + dff) * 4));
+  }
   MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->unfinished, (size_t)16 * MAX_GROUPS * 4));
