@@ -160,6 +160,11 @@ int mpr_clip_text_forward(mpr_model* m, const int32_t* tok_dev, int32_t b, int32
 int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* tensors, int32_t n_tensors,
                   const int32_t* enc_lut, const int32_t* dec_lut, int32_t lut_radius,
                   mpr_model** out);
+/* New weights for an existing T5 handle (same configuration and tensor list as mpr_t5_create):
+ * copied into the handle's own buffers, so its captured generate graphs stay valid (an optimizer
+ * step between training-mode predict() calls, main.py:179-187).  Waits for the device first. */
+int mpr_t5_update(mpr_model* m, const float* const* tensors, int32_t n_tensors,
+                  const int32_t* enc_lut, const int32_t* dec_lut);
 /* Gather shared[ids] into out[b*out_bstride + (row0+t)*d + c] (T5VisionModel.py:169). */
 int mpr_t5_embed(mpr_model* m, const int32_t* ids_dev, int32_t b, int32_t len, float* out_dev,
                  int64_t out_bstride, int32_t row0, void* stream);

@@ -56,6 +56,7 @@ SIGNATURES = [
                                         c_void_p]),
     ("mpr_t5_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32, I32P, I32P, c_int32,
                                 POINTER(c_void_p)]),
+    ("mpr_t5_update", c_int32, [c_void_p, POINTER(c_void_p), c_int32, I32P, I32P]),
     ("mpr_t5_embed", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_int32,
                                c_void_p]),
     ("mpr_t5_encode", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,

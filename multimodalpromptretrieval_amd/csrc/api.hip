@@ -349,6 +349,83 @@ int mpr_clip_text_forward(mpr_model* m, const int32_t* tok, int32_t b, int32_t s
 }
 
 // ---- T5 -------------------------------------------------------------------------------------------
+namespace {
+// Weights of a T5 handle from the tensor list of mpr_t5_create (fresh: allocate the layers) or
+// into the same device buffers (an update: every pointer a captured graph holds stays valid).
+int t5_load(T5Model* m, const float* const* t, const int32_t* enc_lut, const int32_t* dec_lut,
+            bool fresh) {
+  const int d = m->d, inner = m->inner, dff = m->dff, Le = m->Le, Ld = m->Ld;
+  const int radius = m->lut_radius;
+  // Relative position bias by offset r = key - query: tab[(r + radius) * H + h] =
+  // rel_bias[lut[r + radius], h] (the bucket gather done once here, not per score).
+  auto bias_table = [&](DevBuf& dst, const float* rel, const int32_t* lut) -> int {
+    std::vector<float> hrel((size_t)m->nb * m->H);
+    MPR_HIP(hipMemcpy(hrel.data(), rel, hrel.size() * 4, hipMemcpyDefault));
+    const size_t nr = (size_t)2 * radius + 1;
+    std::vector<int32_t> hl(nr);
+    MPR_HIP(hipMemcpy(hl.data(), lut, nr * 4, hipMemcpyDefault));
+    std::vector<float> tab(nr * m->H);
+    for (size_t r = 0; r < nr; ++r) {
+      MPR_REQUIRE(hl[r] >= 0 && hl[r] < m->nb, "t5_create: lut bucket %d out of range", hl[r]);
+      for (int hh = 0; hh < m->H; ++hh) tab[r * m->H + hh] = hrel[(size_t)hl[r] * m->H + hh];
+    }
+    return upload(dst, tab.data(), tab.size());
+  };
+  int p = 0;
+  MPR_TRY(upload(m->shared, t[p++], (size_t)m->V * d));
+  MPR_TRY(bias_table(m->enc_tab, t[p++], enc_lut));
+  for (int l = 0; l < Le; ++l) {
+    if (fresh) m->enc.push_back(std::make_unique<T5Layer>());
+    T5Layer& ly = *m->enc[l];
+    MPR_TRY(upload(ly.ln0, t[p++], d));
+    MPR_TRY(ly.qkv.ensure((size_t)3 * inner * d * 4));
+    for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly.qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(upload(ly.o, t[p++], (size_t)d * inner));
+    MPR_TRY(upload(ly.ln1, t[p++], d));
+    MPR_TRY(upload(ly.wi, t[p++], (size_t)dff * d));
+    MPR_TRY(upload(ly.wo, t[p++], (size_t)d * dff));
+  }
+  MPR_TRY(upload(m->enc_final, t[p++], d));
+  MPR_TRY(bias_table(m->dec_tab, t[p++], dec_lut));
+  MPR_TRY(m->cross_kv_w.ensure((size_t)Ld * 2 * inner * d * 4));
+  for (int l = 0; l < Ld; ++l) {
+    if (fresh) m->dec.push_back(std::make_unique<T5Layer>());
+    T5Layer& ly = *m->dec[l];
+    MPR_TRY(upload(ly.ln0, t[p++], d));
+    MPR_TRY(ly.qkv.ensure((size_t)3 * inner * d * 4));
+    for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly.qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(upload(ly.o, t[p++], (size_t)d * inner));
+    MPR_TRY(upload(ly.ln1, t[p++], d));
+    MPR_TRY(upload(ly.cq, t[p++], (size_t)inner * d));
+    MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l) * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l + 1) * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(upload(ly.co, t[p++], (size_t)d * inner));
+    MPR_TRY(upload(ly.ln2, t[p++], d));
+    MPR_TRY(upload(ly.wi, t[p++], (size_t)dff * d));
+    MPR_TRY(upload(ly.wo, t[p++], (size_t)d * dff));
+  }
+  MPR_TRY(upload(m->dec_final, t[p++], d));
+  MPR_TRY(upload(m->lm_head, t[p++], (size_t)m->V * d));
+  // lane-order images of the decoder projections for the decode-step GEMMs
+  auto pack = [](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
+    MPR_TRY(dst.ensure((size_t)packed_rows16_elems(n, k) * 4));
+    return pack_rows16(src.as<float>(), n, k, k, dst.as<float>(), nullptr);
+  };
+  for (auto& ly : m->dec) {
+    MPR_TRY(pack(ly->pk_qkv, ly->qkv, 3 * inner, d));
+    MPR_TRY(pack(ly->pk_o, ly->o, d, inner));
+    MPR_TRY(pack(ly->pk_cq, ly->cq, inner, d));
+    MPR_TRY(pack(ly->pk_co, ly->co, d, inner));
+    MPR_TRY(pack(ly->pk_wi, ly->wi, dff, d));
+    MPR_TRY(pack(ly->pk_wo, ly->wo, d, dff));
+  }
+  MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
+  if (m->fold) MPR_TRY(m->build_folded());
+  MPR_HIP(hipDeviceSynchronize());
+  return MPR_OK;
+}
+}  // namespace
+
 int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int32_t nt,
                   const int32_t* enc_lut, const int32_t* dec_lut, int32_t radius,
                   mpr_model** out) {
@@ -366,84 +443,32 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
     m->scale_out = cfg[8];
     m->inner = m->H * m->dkv;
     m->lut_radius = radius;
-    const int d = m->d, inner = m->inner, dff = m->dff, Le = m->Le, Ld = m->Ld;
+    const int d = m->d, dff = m->dff, Le = m->Le, Ld = m->Ld;
     MPR_REQUIRE(m->dkv == 64, "t5_create: d_kv=%d (head dim 64 supported)", m->dkv);
     MPR_REQUIRE(d % 16 == 0 && d <= 1024 && dff % 16 == 0, "t5_create: d_model=%d d_ff=%d", d, dff);
     MPR_REQUIRE(radius >= 64, "t5_create: lut radius %d too small", radius);
     const int expect = 2 + 8 * Le + 1 + 1 + 13 * Ld + 2;
     MPR_REQUIRE(nt == expect, "t5_create: expected %d tensors, got %d", expect, nt);
-    // Relative position bias by offset r = key - query: tab[(r + radius) * H + h] =
-    // rel_bias[lut[r + radius], h] (the bucket gather done once here, not per score).
-    auto bias_table = [&](DevBuf& dst, const float* rel, const int32_t* lut) -> int {
-      std::vector<float> hrel((size_t)m->nb * m->H);
-      MPR_HIP(hipMemcpy(hrel.data(), rel, hrel.size() * 4, hipMemcpyDefault));
-      const size_t nr = (size_t)2 * radius + 1;
-      std::vector<int32_t> hl(nr);
-      MPR_HIP(hipMemcpy(hl.data(), lut, nr * 4, hipMemcpyDefault));
-      std::vector<float> tab(nr * m->H);
-      for (size_t r = 0; r < nr; ++r) {
-        MPR_REQUIRE(hl[r] >= 0 && hl[r] < m->nb, "t5_create: lut bucket %d out of range", hl[r]);
-        for (int hh = 0; hh < m->H; ++hh) tab[r * m->H + hh] = hrel[(size_t)hl[r] * m->H + hh];
-      }
-      return upload(dst, tab.data(), tab.size());
-    };
-    int p = 0;
-    MPR_TRY(upload(m->shared, t[p++], (size_t)m->V * d));
-    MPR_TRY(bias_table(m->enc_tab, t[p++], enc_lut));
-    for (int l = 0; l < Le; ++l) {
-      auto ly = std::make_unique<T5Layer>();
-      MPR_TRY(upload(ly->ln0, t[p++], d));
-      MPR_TRY(ly->qkv.ensure((size_t)3 * inner * d * 4));
-      for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly->qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
-      MPR_TRY(upload(ly->o, t[p++], (size_t)d * inner));
-      MPR_TRY(upload(ly->ln1, t[p++], d));
-      MPR_TRY(upload(ly->wi, t[p++], (size_t)dff * d));
-      MPR_TRY(upload(ly->wo, t[p++], (size_t)d * dff));
-      m->enc.push_back(std::move(ly));
-    }
-    MPR_TRY(upload(m->enc_final, t[p++], d));
-    MPR_TRY(bias_table(m->dec_tab, t[p++], dec_lut));
-    MPR_TRY(m->cross_kv_w.ensure((size_t)Ld * 2 * inner * d * 4));
-    for (int l = 0; l < Ld; ++l) {
-      auto ly = std::make_unique<T5Layer>();
-      MPR_TRY(upload(ly->ln0, t[p++], d));
-      MPR_TRY(ly->qkv.ensure((size_t)3 * inner * d * 4));
-      for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly->qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
-      MPR_TRY(upload(ly->o, t[p++], (size_t)d * inner));
-      MPR_TRY(upload(ly->ln1, t[p++], d));
-      MPR_TRY(upload(ly->cq, t[p++], (size_t)inner * d));
-      MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l) * inner * d, t[p++], (size_t)inner * d));
-      MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l + 1) * inner * d, t[p++], (size_t)inner * d));
-      MPR_TRY(upload(ly->co, t[p++], (size_t)d * inner));
-      MPR_TRY(upload(ly->ln2, t[p++], d));
-      MPR_TRY(upload(ly->wi, t[p++], (size_t)dff * d));
-      MPR_TRY(upload(ly->wo, t[p++], (size_t)d * dff));
-      m->dec.push_back(std::move(ly));
-    }
-    MPR_TRY(upload(m->dec_final, t[p++], d));
-    MPR_TRY(upload(m->lm_head, t[p++], (size_t)m->V * d));
-    // lane-order images of the decoder projections for the decode-step GEMMs
-    auto pack = [](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
-      MPR_TRY(dst.ensure((size_t)packed_rows16_elems(n, k) * 4));
-      return pack_rows16(src.as<float>(), n, k, k, dst.as<float>(), nullptr);
-    };
-    for (auto& ly : m->dec) {
-      MPR_TRY(pack(ly->pk_qkv, ly->qkv, 3 * inner, d));
-      MPR_TRY(pack(ly->pk_o, ly->o, d, inner));
-      MPR_TRY(pack(ly->pk_cq, ly->cq, inner, d));
-      MPR_TRY(pack(ly->pk_co, ly->co, d, inner));
-      MPR_TRY(pack(ly->pk_wi, ly->wi, dff, d));
-      MPR_TRY(pack(ly->pk_wo, ly->wo, d, dff));
-    }
-    MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
     {
       const char* e = getenv("MPR_DECODE_FOLD");
       m->fold = !(e && e[0] == '0');
     }
-    if (m->fold) MPR_TRY(m->build_folded());
-    MPR_HIP(hipDeviceSynchronize());
+    MPR_TRY(t5_load(m.get(), t, enc_lut, dec_lut, /*fresh=*/true));
     *out = m.release();
     return MPR_OK;
+  });
+}
+
+int mpr_t5_update(mpr_model* mm, const float* const* t, int32_t nt, const int32_t* enc_lut,
+                  const int32_t* dec_lut) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(mm && mm->kind == mpr_model::T5 && t && enc_lut && dec_lut,
+                "t5_update: bad arguments");
+    T5Model* m = static_cast<T5Model*>(mm);
+    const int expect = 2 + 8 * m->Le + 1 + 1 + 13 * m->Ld + 2;
+    MPR_REQUIRE(nt == expect, "t5_update: expected %d tensors, got %d", expect, nt);
+    MPR_HIP(hipDeviceSynchronize());  // no work in flight reads the weights being replaced
+    return t5_load(m, t, enc_lut, dec_lut, /*fresh=*/false);
   });
 }
 

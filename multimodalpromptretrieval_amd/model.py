@@ -219,13 +219,19 @@ class T5VisionModel(nn.Module):
                         None if p is None else p._version))
         return tuple(key)
 
-    def _handle(self, name, prefix, build):
+    def _handle(self, name, prefix, build, update=None):
         key = self._params_key(prefix)
         ent = self._dev.get(name)
         if ent is None or ent[0] != key:
             sd = {n[len(prefix):]: p.detach() for n, p in self.named_parameters()
                   if n.startswith(prefix)}
-            ent = (key, build(sd))
+            shapes = tuple((n, tuple(p.shape)) for n, p in sorted(sd.items()))
+            if (update is not None and ent is not None and ent[2] == shapes
+                    and [k[0] for k in ent[0]] == [k[0] for k in key]):
+                # same parameters, new values (an optimizer step): update in place
+                ent = (key, update(ent[1], sd), shapes)
+            else:
+                ent = (key, build(sd), shapes)
             self._dev[name] = ent
         return ent[1]
 
@@ -241,7 +247,7 @@ class T5VisionModel(nn.Module):
                                            else torch.cuda.current_device()):
                 dev.set_decode_stream(_lib.role_stream(self.device, "decode"))
             return dev
-        return self._handle("t5", "T5_model.", build)
+        return self._handle("t5", "T5_model.", build, lambda dev, sd: dev.update(sd))
 
     # ---- reference surface -----------------------------------------------------------------------
     def get_image_token_features(self, x):
@@ -287,10 +293,13 @@ class T5VisionModel(nn.Module):
         projections share launches; results identical to separate calls)."""
         # (_handles: the device models predict() already fetched — each fetch checks every
         # parameter for updates, ~0.1 ms of host time on the GPU's critical path)
-        vit, t5 = _handles if _handles is not None else (self._device_vit(), self._device_t5())
-        if self.use_image_info and vit.out_dim != t5.d_model:
+        # (the device T5 handle is only needed for the no-grad embedding gather: a training
+        # forward after an optimizer step must not refresh it just for its width)
+        vit = _handles[0] if _handles is not None else self._device_vit()
+        d_model = self.T5_model.shared.weight.shape[1]
+        if self.use_image_info and vit.out_dim != d_model:
             raise RuntimeError(f"Sizes of tensors must match: image tokens are {vit.out_dim}-d, "
-                               f"{self.T5_version} d_model is {t5.d_model} (torch.cat at "
+                               f"{self.T5_version} d_model is {d_model} (torch.cat at "
                                f"architectures/T5VisionModel.py:176)")
         cur = torch.cuda.current_stream(self.device)
         img_tok = None
@@ -331,7 +340,7 @@ class T5VisionModel(nn.Module):
         ids = encoding["input_ids"]
         L = ids.shape[1]
         T = vit.tokens if self.use_image_info else 0
-        combined = torch.empty((B, T + L, t5.d_model), device=self.device, dtype=torch.float32)
+        combined = torch.empty((B, T + L, d_model), device=self.device, dtype=torch.float32)
         if self.use_image_info:
             if tok_event is not None:
                 cur.wait_event(tok_event)
@@ -347,6 +356,7 @@ class T5VisionModel(nn.Module):
             q = embed_rows(shared, ids)
             combined = torch.cat([combined[:, :T], q], 1) if T else q
         else:
+            t5 = _handles[1] if _handles is not None else self._device_t5()
             t5.embed(ids, combined, row0=T)
         if self.use_image_info:
             mask = torch.ones((B, T + L), dtype=torch.float32)

@@ -64,6 +64,19 @@ class DeviceT5:
         self.d_ff = sd["encoder.block.0.layer.1.DenseReluDense.wi.weight"].shape[0]
         self.n_enc = _layers(sd, "encoder")
         self.n_dec = _layers(sd, "decoder")
+        self._max_distance = max_distance
+        host, enc_lut, dec_lut = self._tensors(sd)
+        cfg = [self.d_model, self.d_kv, self.num_heads, self.d_ff, self.n_enc, self.n_dec,
+               self.vocab, self.num_buckets, 1 if scale_decoder_outputs else 0]
+        h = _lib.ctypes.c_void_p()
+        _lib.call("mpr_t5_create", _lib.int_array(cfg), len(cfg), _lib.tensor_array(host),
+                  len(host), enc_lut, dec_lut, LUT_RADIUS, _lib.ctypes.byref(h))
+        self._h = h
+
+    def _tensors(self, sd: dict):
+        """The mpr_t5_create tensor list of a transformers-named state dict + the bucket LUTs."""
+        shared = sd["shared.weight"]
+        rel = sd["encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"]
         lm_head = sd.get("lm_head.weight", shared)
         t = [shared, rel]
         for i in range(self.n_enc):
@@ -85,16 +98,19 @@ class DeviceT5:
                   sd[p + ".2.DenseReluDense.wo.weight"]]
         t += [sd["decoder.final_layer_norm.weight"], lm_head]
         host = [x.detach().to(torch.float32).contiguous() for x in t]  # host or device
-        rel_pos = torch.arange(-LUT_RADIUS, LUT_RADIUS + 1, dtype=torch.long)
-        enc_lut = relative_position_bucket(rel_pos, True, self.num_buckets, max_distance)
-        dec_lut = relative_position_bucket(rel_pos, False, self.num_buckets, max_distance)
-        cfg = [self.d_model, self.d_kv, self.num_heads, self.d_ff, self.n_enc, self.n_dec,
-               self.vocab, self.num_buckets, 1 if scale_decoder_outputs else 0]
-        h = _lib.ctypes.c_void_p()
-        _lib.call("mpr_t5_create", _lib.int_array(cfg), len(cfg), _lib.tensor_array(host),
-                  len(host), _lib.int_array(enc_lut.tolist()), _lib.int_array(dec_lut.tolist()),
-                  LUT_RADIUS, _lib.ctypes.byref(h))
-        self._h = h
+        if not hasattr(self, "_luts"):
+            rel_pos = torch.arange(-LUT_RADIUS, LUT_RADIUS + 1, dtype=torch.long)
+            enc = relative_position_bucket(rel_pos, True, self.num_buckets, self._max_distance)
+            dec = relative_position_bucket(rel_pos, False, self.num_buckets, self._max_distance)
+            self._luts = (_lib.int_array(enc.tolist()), _lib.int_array(dec.tolist()))
+        return host, self._luts[0], self._luts[1]
+
+    def update(self, sd: dict) -> "DeviceT5":
+        """New parameter values (same shapes) into this handle's buffers (mpr_t5_update): its
+        captured generate graphs stay valid — an optimizer step costs a copy, not a rebuild."""
+        host, enc_lut, dec_lut = self._tensors(sd)
+        _lib.call("mpr_t5_update", self._h, _lib.tensor_array(host), len(host), enc_lut, dec_lut)
+        return self
 
     def close(self):
         if self._h is not None and _lib._lib is not None:
