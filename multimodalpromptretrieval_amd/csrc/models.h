@@ -166,6 +166,7 @@ struct T5Model : mpr_model {
   // The decode chain with its RMSNorms folded into the preceding projections (6 launches per
   // layer instead of 8; MPR_DECODE_FOLD=0 keeps the 8-launch chain): see decode_body.
   bool fold = false;
+  bool fold_rows(int B) const;  // fold and B <= MPR_DECODE_FOLD_ROWS (16)
   int build_folded();
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
   DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)

@@ -75,6 +75,17 @@ __global__ void fold_weights_kernel(const float* __restrict__ top, const float* 
 // projections, the cross-attention applies its query's scale from the x1 row it reads, and the
 // FFN-out GEMM applies relu on load and the x2 scale in its epilogue.  8 -> 6 dependent launches
 // per layer, at a different fp32 rounding order than the reference's.
+// The folded chain trades launches for MACs (its two merged GEMMs read 50 % more weight per
+// layer): it wins for the latency-bound decodes of one batch and loses for the grouped
+// 128-row decodes of a serving loop, where the launches overlap other work (measured).
+bool T5Model::fold_rows(int B) const {
+  static const int max_rows = [] {
+    const char* e = getenv("MPR_DECODE_FOLD_ROWS");
+    return e ? atoi(e) : 16;
+  }();
+  return fold && B <= max_rows;
+}
+
 int T5Model::build_folded() {
   const int K = inner + d;
   DevBuf tmp;
@@ -232,7 +243,7 @@ int T5Model::init_body(int B, int L, int max_new, int start, hipStream_t s) {
   MPR_TRY(fill_i32(ws->unfinished.as<int32_t>(), 1, B, s));
   MPR_TRY(fill_i32(ws->cur_tok.as<int32_t>(), start, B, s));
   MPR_TRY(fill_i32(ws->tok_buf.as<int32_t>(), start, (int64_t)B * T1, s));  // column 0 = start
-  if (fold)  // the residual stream lives in the x half of the [a | x] rows
+  if (fold_rows(B))  // the residual stream lives in the x half of the [a | x] rows
     MPR_TRY(embed_gather(shared.as<float>(), ws->cur_tok.as<int32_t>(), 1, B, 1, d, nullptr,
                          ws->ax.as<float>() + inner, inner + d, 0, s));
   else
@@ -259,7 +270,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
 
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
-  if (fold) return decode_body_folded(B, L, max_new, eos, pad, s, t0, t1);
+  if (fold_rows(B)) return decode_body_folded(B, L, max_new, eos, pad, s, t0, t1);
   for (int t = t0; t < t1; ++t) {
     for (int l = 0; l < Ld; ++l) {
       const T5Layer& ly = *dec[l];
@@ -504,7 +515,7 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
   MPR_TRY(grow(ws->cache, (size_t)Ld * B * Tc * 3 * inner * 4));
   MPR_TRY(grow(ws->dx, (size_t)B * d * 4));
   MPR_TRY(grow(ws->dq, (size_t)B * inner * 4));
-  if (fold) {
+  if (fold_rows(B)) {
     MPR_TRY(grow(ws->ax, (size_t)B * (inner + d) * 4));
     MPR_TRY(grow(ws->yq, (size_t)B * (2 * inner + d) * 4));
     MPR_TRY(grow(ws->hz, (size_t)B * (d + dff) * 4));
