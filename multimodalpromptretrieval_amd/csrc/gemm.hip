@@ -715,7 +715,7 @@ __global__ __launch_bounds__(256) void pack_rows16_kernel(const float* __restric
 // per-row scale of SKF_RSCALE); SKF_RSCALE: the epilogue scales row m by rsqrt(mean(src_m^2) +
 // eps) of an external row (the decode chain's folded RMSNorm, t5.hip).
 enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8, SKF_RELU_IN = 16,
-             SKF_RSCALE = 32 };
+             SKF_RSCALE = 32, SKF_SSQ = 64 };
 
 // NT 16-column tiles per block share the activation slab (NT > 1 for the 32k-column lm_head,
 // which needs more bytes in flight per wave); two accumulator chains per tile halve the
@@ -726,7 +726,8 @@ template <int MAXC, int NT, int F, bool LOOP, int MR>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   constexpr bool RMS = (F & SKF_RMS) != 0, RES = (F & SKF_RES) != 0,
                  RELU = (F & SKF_RELU) != 0, AMAX = (F & SKF_AMAX) != 0,
-                 RELU_IN = (F & SKF_RELU_IN) != 0, RSCALE = (F & SKF_RSCALE) != 0;
+                 RELU_IN = (F & SKF_RELU_IN) != 0, RSCALE = (F & SKF_RSCALE) != 0,
+                 SSQ = (F & SKF_SSQ) != 0;
   static_assert(!(RMS && RSCALE), "one row-scale source");
   constexpr int MROWS = 16 * MR;      // activation rows: MR 16-row groups share each weight load
   const GemmArgs& a = sa.g;
@@ -736,7 +737,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   // parks its NT * MR partial tiles in its own slab (wave-private until the block barrier), so
   // the partials cost no LDS of their own: more blocks stay resident per CU.
   static_assert(NT * MR * 256 <= MROWS * XLD, "partial tiles must fit the wave's slab");
-  __shared__ __attribute__((aligned(16))) float smem[XS + SK_WAVES * MROWS];
+  __shared__ __attribute__((aligned(16))) float smem[XS + SK_WAVES * MROWS +
+                                                     (RSCALE ? 4 * 512 : 0)];
   float(*xs)[MROWS][XLD] = reinterpret_cast<float(*)[MROWS][XLD]>(smem);
   auto red = [&](int slot, int w) -> f32x4* {  // partial tile `slot` of wave w, 64 lanes
     return reinterpret_cast<f32x4*>(smem + w * MROWS * XLD) + slot * 64;
@@ -771,6 +773,18 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     if (wave < NT * MR)
       rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)(row0 + min(er * 16 + i, M - 1)) * a.ldr +
                                              (blockIdx.x * NT + et) * 16 + h * 4);
+  }
+  // RSCALE: the rows' partial sums of squares (MROWS x rs_nparts <= 4 x 512 floats), issued with
+  // the first loads and parked in LDS after the main loop
+  float rsp[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RSCALE) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * 512;
+      if (e < MROWS * sa.rs_nparts)
+        rsp[u] = sa.rs_part[(int64_t)(row0 + min(e / sa.rs_nparts, M - 1)) * sa.rs_nparts +
+                            e % sa.rs_nparts];
+    }
   }
   f32x4 acc[NT][MR][2];
 #pragma unroll
@@ -852,19 +866,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       if (lane < 16) ssq_s[wave][r * 16 + lane] = v;
     }
   }
+  float* rsp_s = smem + XS + SK_WAVES * MROWS;  // RSCALE partials [MROWS][rs_nparts]
   if constexpr (RSCALE) {
-    // sum of squares of each of the block's rows of the scale source, a wave per row
-    for (int r = wave; r < MROWS; r += SK_WAVES) {
-      const float* src = sa.rs_src + (int64_t)(row0 + min(r, M - 1)) * sa.rs_ld;
-      float v = 0.f;
-      for (int c = lane * 4; c < sa.rs_n; c += 256) {
-        const f32x4 x = *reinterpret_cast<const f32x4*>(src + c);
-        v += x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
-      }
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0) ssq_s[0][r] = v;
-    }
+    for (int u = 0; u < 4; ++u)
+      if (tid + u * 512 < MROWS * sa.rs_nparts) rsp_s[tid + u * 512] = rsp[u];
   }
   __syncthreads();
   if (wave >= NT * MR) return;
@@ -881,7 +887,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     for (int w = 0; w < SK_WAVES; ++w) t += ssq_s[w][m];
     scale = (1.0f / sqrtf(t / (float)K + sa.rms_eps)) * sa.a_scale;
   }
-  if constexpr (RSCALE) scale = (1.0f / sqrtf(ssq_s[0][m] / (float)sa.rs_n + sa.rms_eps)) * sa.a_scale;
+  if constexpr (RSCALE) {
+    float t = 0.f;  // the row's partials in tile order
+    for (int p = 0; p < sa.rs_nparts; ++p) t += rsp_s[min(m, M - 1) * sa.rs_nparts + p];
+    scale = (1.0f / sqrtf(t / (float)sa.rs_n + sa.rms_eps)) * sa.a_scale;
+  }
   if constexpr (AMAX) {
     // greedy head: per (row m, block) best column, lowest index on ties (torch.argmax)
     float bv = -INFINITY;
@@ -916,6 +926,14 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     }
     if constexpr (RES) v = rres + v;
     if (m < M) *reinterpret_cast<f32x4*>(a.C + (int64_t)(row0 + m) * a.ldc + n0 + h * 4) = v;
+    if constexpr (SSQ) {
+      // the tile's 16 columns of row m: this lane's 4, then the 4 lane groups (h) of the row
+      float q = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (n0 < sa.ssq_cols && lane < 16 && m < M)
+        sa.ssq_out[(int64_t)(row0 + m) * (sa.ssq_cols / 16) + tile] = q;
+    }
   }
 }
 
@@ -1216,7 +1234,7 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, un
     switch (F) {
       MPR_SK(0) MPR_SK(1) MPR_SK(2) MPR_SK(3) MPR_SK(4) MPR_SK(5) MPR_SK(6) MPR_SK(7)
       MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS)
-      MPR_SK(SKF_RELU_IN | SKF_RSCALE | SKF_RES)
+      MPR_SK(SKF_RELU_IN | SKF_RSCALE | SKF_RES) MPR_SK(SKF_SSQ)
       default: break;
     }
   }
@@ -1242,16 +1260,20 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(amax || (a.C && a.N % 16 == 0 && a.ldc % 4 == 0 && aligned16(a.C) &&
                        (!a.R || (a.ldr % 4 == 0 && aligned16(a.R)))),
               "gemm_skinny: N must be a multiple of 16, C/R rows 16-byte aligned");
-  MPR_REQUIRE(!sa.rs_src || (!sa.rms_w && !amax && sa.rs_n % 4 == 0 && sa.rs_ld % 4 == 0 &&
-                              aligned16(sa.rs_src)),
-              "gemm_skinny: an external row scale excludes the fused RMSNorm / argmax; its rows "
-              "16-byte aligned");
+  MPR_REQUIRE(!sa.rs_part || (!sa.rms_w && !amax && sa.rs_n > 0 && sa.rs_nparts > 0 &&
+                               32 * sa.rs_nparts <= 4 * 512),
+              "gemm_skinny: an external row scale excludes the fused RMSNorm / argmax; at most "
+              "64 partials per row");
+  MPR_REQUIRE(!sa.ssq_out || (sa.ssq_cols % 16 == 0 && sa.ssq_cols <= a.N),
+              "gemm_skinny: ssq columns %d", sa.ssq_cols);
   const int F = (sa.rms_w ? SKF_RMS : 0) | (a.R ? SKF_RES : 0) |
                 (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0) |
-                (sa.relu_in ? SKF_RELU_IN : 0) | (sa.rs_src ? SKF_RSCALE : 0);
+                (sa.relu_in ? SKF_RELU_IN : 0) | (sa.rs_part ? SKF_RSCALE : 0) |
+                (sa.ssq_out ? SKF_SSQ : 0);
   MPR_REQUIRE(!(F & (SKF_RELU_IN | SKF_RSCALE)) || F == (SKF_RELU_IN | SKF_RSCALE | SKF_RES),
               "gemm_skinny: relu_in / row scale only as the folded FFN-out (relu_in + scale + "
               "residual)");
+  MPR_REQUIRE(!(F & SKF_SSQ) || F == SKF_SSQ, "gemm_skinny: ssq only on a plain projection");
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
   // Above 32 rows (grouped decodes) the rows split over blocks of MPR_SKINNY_ROWS (32 default,
@@ -1265,6 +1287,8 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
     const int v = e ? atoi(e) : 32;
     return v == 16 || v == 32 ? v : 0;
   }();
+  MPR_REQUIRE(!sa.rs_part || a.M <= 32 || row_blk > 0,
+              "gemm_skinny: an external row scale needs row blocks of <= 32 rows");
   static const bool small_lds = [] {
     const char* e = getenv("MPR_SKINNY_SMALL");
     return e && e[0] == '1';

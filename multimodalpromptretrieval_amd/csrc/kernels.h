@@ -61,11 +61,16 @@ struct SkinnyArgs {
   // (C must be null).
   float* amax_val = nullptr;
   int32_t* amax_idx = nullptr;
-  // Folded RMSNorm of the decode chain (t5.hip): relu_in applies ReLU to A as it is staged;
-  // rs_src: row m of the result is scaled by rsqrt(mean(rs_src[m, :rs_n]^2) + rms_eps)
+  // Folded RMSNorm of the decode chain (t5.hip).  ssq_out: for the output columns < ssq_cols,
+  // each 16-column tile also stores its rows' partial sums of squares,
+  // ssq_out[row * (ssq_cols / 16) + tile].  relu_in: ReLU applied to A as it is staged.
+  // rs_part: row m of the result is scaled by rsqrt(sum_t rs_part[m * rs_nparts + t] / rs_n +
+  // rms_eps) (the partials another launch's ssq_out wrote, summed in tile order).
+  float* ssq_out = nullptr;
+  int ssq_cols = 0;
   bool relu_in = false;
-  const float* rs_src = nullptr;
-  int64_t rs_ld = 0;
+  const float* rs_part = nullptr;
+  int rs_nparts = 0;
   int rs_n = 0;
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
@@ -123,10 +128,11 @@ struct AttnArgs {
   // (the layer-0 bias table gathered through the bucket LUT once at model load), optional.
   const float* rel_tab = nullptr;
   int lut_radius = 0;
-  // one-query decode only: q row b is scaled by rsqrt(mean(q_rms_src[b, :q_rms_n]^2) + eps) (the
-  // decode chain's folded RMSNorm ahead of the cross-attention query, t5.hip)
-  const float* q_rms_src = nullptr;
-  int64_t q_rms_bs = 0;
+  // one-query decode only: q row b is scaled by rsqrt(sum_t q_rms_part[b * q_rms_nparts + t] /
+  // q_rms_n + eps) — the decode chain's folded RMSNorm ahead of the cross-attention query, from
+  // the per-tile partial sums of squares the producing GEMM wrote (t5.hip)
+  const float* q_rms_part = nullptr;
+  int q_rms_nparts = 0;
   int q_rms_n = 0;
   float q_rms_eps = 1e-6f;
 };

@@ -272,16 +272,14 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
   if (a.causal) lk_end = min(lk_end, qpos + 1);
   const int dg = tid & 15, kg = tid >> 4;  // PV: dims 4*dg..4*dg+3, keys kg*16..kg*16+15
   float qscale = a.scale;
-  if (a.q_rms_src) {  // the folded RMSNorm of the query's source row (t5.hip decode chain)
-    const float* src = a.q_rms_src + (int64_t)b * a.q_rms_bs;
+  if (a.q_rms_part) {
+    // the folded RMSNorm of the query's source row (t5.hip decode chain): the producing GEMM's
+    // per-tile partial sums of squares; every wave sums them in the same fixed order
+    const float* pp = a.q_rms_part + (int64_t)b * a.q_rms_nparts;
     float v = 0.f;
-    for (int c = tid; c < a.q_rms_n; c += 256) v += src[c] * src[c];
+    for (int t = lane; t < a.q_rms_nparts; t += 64) v += pp[t];
     v = wave_sum(v);
-    if (lane == 0) red[0][wave] = v;
-    __syncthreads();
-    const float t = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    qscale = a.scale * (1.0f / sqrtf(t / (float)a.q_rms_n + a.q_rms_eps));
-    __syncthreads();  // red reused below
+    qscale = a.scale * (1.0f / sqrtf(v / (float)a.q_rms_n + a.q_rms_eps));
   }
   float m = -INFINITY, l = 0.f;
   f32x4 o = {0.f, 0.f, 0.f, 0.f};
@@ -809,7 +807,7 @@ int attention(const AttnArgs& a, hipStream_t s) {
     MPR_REQUIRE(std::max(a.q_pos0 + a.Lq, a.Lk) - 1 <= a.lut_radius,
                 "attention: bias table radius %d too small (Lq %d, Lk %d)", a.lut_radius, a.Lq,
                 a.Lk);
-  MPR_REQUIRE(!a.q_rms_src || (a.Lq == 1 && a.q_rms_n > 0),
+  MPR_REQUIRE(!a.q_rms_part || (a.Lq == 1 && a.q_rms_n > 0 && a.q_rms_nparts > 0),
               "attention: a query row scale only on the one-query decode path");
   if (a.Lq == 1) {
     // (A wave-per-(b, h) form without block barriers measured slower: 4.4 / 5.3 us self / cross

@@ -356,6 +356,8 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
   float* ax = ws->ax.as<float>();  // [a | x]
   float* yq = ws->yq.as<float>();  // [c | x1 | u]
   float* hz = ws->hz.as<float>();  // [x2 | z]
+  float* x1ss = ws->x1ss.as<float>();  // [B, d / 16] per-tile sums of squares of x1 / x2
+  float* x2ss = ws->x2ss.as<float>();
   float* xp = ax + inner;
   int32_t* unf = ws->unfinished.as<int32_t>();
   int32_t* toks = ws->tok_buf.as<int32_t>();
@@ -385,6 +387,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
       so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
       so.wpk = ly.pk_ocq.as<float>();
+      so.ssq_out = x1ss; so.ssq_cols = d;  // x1's per-tile sums of squares (its RMS)
       MPR_TRY(gemm_skinny(so, s));
       AttnArgs ca;  // c = attention(u / rms_scale(x1), K_enc, V_enc)
       ca.q = yq + inner + d; ca.q_bs = ldY; ca.q_rs = ldY;
@@ -393,17 +396,19 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       ca.o = yq; ca.o_bs = ldY; ca.o_rs = ldY;
       ca.B = B; ca.H = H; ca.Lq = 1; ca.Lk = L; ca.scale = 1.f;
       ca.key_mask = maskp; ca.mask_bs = L;
-      ca.q_rms_src = yq + inner; ca.q_rms_bs = ldY; ca.q_rms_n = d; ca.q_rms_eps = T5_EPS;
+      ca.q_rms_part = x1ss; ca.q_rms_nparts = d / 16; ca.q_rms_n = d; ca.q_rms_eps = T5_EPS;
       MPR_TRY(attention(ca, s));
       SkinnyArgs cw;  // [x2 | z] = [c | x1] W_cowi^T
       cw.g.A = yq; cw.g.lda = ldY; cw.g.C = hz; cw.g.ldc = ldZ;
       cw.g.M = B; cw.g.N = d + dff; cw.g.K = inner + d;
       cw.wpk = ly.pk_cowi.as<float>();
+      cw.ssq_out = x2ss; cw.ssq_cols = d;
       MPR_TRY(gemm_skinny(cw, s));
       SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
       fo.g.A = hz + d; fo.g.lda = ldZ; fo.g.R = hz; fo.g.ldr = ldZ;
       fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
-      fo.relu_in = true; fo.rs_src = hz; fo.rs_ld = ldZ; fo.rs_n = d; fo.rms_eps = T5_EPS;
+      fo.relu_in = true; fo.rs_part = x2ss; fo.rs_nparts = d / 16; fo.rs_n = d;
+      fo.rms_eps = T5_EPS;
       fo.wpk = ly.pk_wo.as<float>();
       MPR_TRY(gemm_skinny(fo, s));
     }
@@ -519,6 +524,8 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
     MPR_TRY(grow(ws->ax, (size_t)B * (inner + d) * 4));
     MPR_TRY(grow(ws->yq, (size_t)B * (2 * inner + d) * 4));
     MPR_TRY(grow(ws->hz, (size_t)B * (d + dff) * 4));
+    MPR_TRY(grow(ws->x1ss, (size_t)B * (d / 16) * 4));
+    MPR_TRY(grow(ws->x2ss, (size_t)B * (d / 16) * 4));
   }
   MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * MAX_GROUPS * 4));
