@@ -888,8 +888,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     scale = (1.0f / sqrtf(t / (float)K + sa.rms_eps)) * sa.a_scale;
   }
   if constexpr (RSCALE) {
-    float t = 0.f;  // the row's partials in tile order
-    for (int p = 0; p < sa.rs_nparts; ++p) t += rsp_s[min(m, M - 1) * sa.rs_nparts + p];
+    float t = 0.f;  // the row's partials in tile order (reads unrolled: in flight together)
+    const float* rp = rsp_s + min(m, M - 1) * sa.rs_nparts;
+#pragma unroll
+    for (int p = 0; p < 64; ++p)
+      if (p < sa.rs_nparts) t += rp[p];
     scale = (1.0f / sqrtf(t / (float)sa.rs_n + sa.rms_eps)) * sa.a_scale;
   }
   if constexpr (AMAX) {
@@ -1261,7 +1264,7 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
                        (!a.R || (a.ldr % 4 == 0 && aligned16(a.R)))),
               "gemm_skinny: N must be a multiple of 16, C/R rows 16-byte aligned");
   MPR_REQUIRE(!sa.rs_part || (!sa.rms_w && !amax && sa.rs_n > 0 && sa.rs_nparts > 0 &&
-                               32 * sa.rs_nparts <= 4 * 512),
+                               sa.rs_nparts <= 64),
               "gemm_skinny: an external row scale excludes the fused RMSNorm / argmax; at most "
               "64 partials per row");
   MPR_REQUIRE(!sa.ssq_out || (sa.ssq_cols % 16 == 0 && sa.ssq_cols <= a.N),

@@ -271,16 +271,10 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
   int lk_end = a.Lk;
   if (a.causal) lk_end = min(lk_end, qpos + 1);
   const int dg = tid & 15, kg = tid >> 4;  // PV: dims 4*dg..4*dg+3, keys kg*16..kg*16+15
-  float qscale = a.scale;
-  if (a.q_rms_part) {
-    // the folded RMSNorm of the query's source row (t5.hip decode chain): the producing GEMM's
-    // per-tile partial sums of squares; every wave sums them in the same fixed order
-    const float* pp = a.q_rms_part + (int64_t)b * a.q_rms_nparts;
-    float v = 0.f;
-    for (int t = lane; t < a.q_rms_nparts; t += 64) v += pp[t];
-    v = wave_sum(v);
-    qscale = a.scale * (1.0f / sqrtf(v / (float)a.q_rms_n + a.q_rms_eps));
-  }
+  // folded RMSNorm of the query's source row (t5.hip decode chain): the producing GEMM's per-tile
+  // partial sums of squares (<= 64), loaded now and reduced once the first pass's loads are out
+  float qscale = a.scale, qpart = 0.f;
+  if (a.q_rms_part && lane < a.q_rms_nparts) qpart = a.q_rms_part[(int64_t)b * a.q_rms_nparts + lane];
   float m = -INFINITY, l = 0.f;
   f32x4 o = {0.f, 0.f, 0.f, 0.f};
   for (int kc = 0; kc < lk_end; kc += DEC_KC) {
@@ -306,6 +300,8 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
     const float* bp = a.rel_tab ? a.rel_tab + (int64_t)(jc - qpos + a.lut_radius) * a.H + h : kp;
     const float mraw = *mp, braw = *bp;
     const float mk = maskb ? mraw : 1.f, rb = a.rel_tab ? braw : 0.f;
+    if (a.q_rms_part && kc == 0)  // every wave sums the partials in the same fixed order
+      qscale = a.scale * (1.0f / sqrtf(wave_sum(qpart) / (float)a.q_rms_n + a.q_rms_eps));
     float s = 0.f;
 #pragma unroll
     for (int d = 0; d < ATT_D / 4; ++d)
@@ -807,7 +803,8 @@ int attention(const AttnArgs& a, hipStream_t s) {
     MPR_REQUIRE(std::max(a.q_pos0 + a.Lq, a.Lk) - 1 <= a.lut_radius,
                 "attention: bias table radius %d too small (Lq %d, Lk %d)", a.lut_radius, a.Lq,
                 a.Lk);
-  MPR_REQUIRE(!a.q_rms_part || (a.Lq == 1 && a.q_rms_n > 0 && a.q_rms_nparts > 0),
+  MPR_REQUIRE(!a.q_rms_part || (a.Lq == 1 && a.q_rms_n > 0 && a.q_rms_nparts > 0 &&
+                                a.q_rms_nparts <= 64),
               "attention: a query row scale only on the one-query decode path");
   if (a.Lq == 1) {
     // (A wave-per-(b, h) form without block barriers measured slower: 4.4 / 5.3 us self / cross
