@@ -738,7 +738,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   // the partials cost no LDS of their own: more blocks stay resident per CU.
   static_assert(NT * MR * 256 <= MROWS * XLD, "partial tiles must fit the wave's slab");
   __shared__ __attribute__((aligned(16))) float smem[XS + SK_WAVES * MROWS +
-                                                     (RSCALE ? 4 * 512 : 0)];
+                                                     (RSCALE ? MROWS : 0)];
   float(*xs)[MROWS][XLD] = reinterpret_cast<float(*)[MROWS][XLD]>(smem);
   auto red = [&](int slot, int w) -> f32x4* {  // partial tile `slot` of wave w, 64 lanes
     return reinterpret_cast<f32x4*>(smem + w * MROWS * XLD) + slot * 64;
@@ -774,17 +774,16 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)(row0 + min(er * 16 + i, M - 1)) * a.ldr +
                                              (blockIdx.x * NT + et) * 16 + h * 4);
   }
-  // RSCALE: the rows' partial sums of squares (MROWS x rs_nparts <= 4 x 512 floats), issued with
-  // the first loads and parked in LDS after the main loop
-  float rsp[4] = {0.f, 0.f, 0.f, 0.f};
+  // RSCALE: the rows' partial sums of squares (<= 64 per row): wave w loads those of rows w,
+  // w + 8, ... (lane = partial), issued with the first loads, summed after the main loop
+  constexpr int RPW = MROWS / SK_WAVES;  // rows per wave (2 or 4)
+  float rsp[RSCALE ? RPW : 1];
   if constexpr (RSCALE) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + u * 512;
-      if (e < MROWS * sa.rs_nparts)
-        rsp[u] = sa.rs_part[(int64_t)(row0 + min(e / sa.rs_nparts, M - 1)) * sa.rs_nparts +
-                            e % sa.rs_nparts];
-    }
+    for (int u = 0; u < RPW; ++u)
+      rsp[u] = lane < sa.rs_nparts
+                   ? sa.rs_part[(int64_t)(row0 + min(wave + u * SK_WAVES, M - 1)) * sa.rs_nparts + lane]
+                   : 0.f;
   }
   f32x4 acc[NT][MR][2];
 #pragma unroll
@@ -866,11 +865,15 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       if (lane < 16) ssq_s[wave][r * 16 + lane] = v;
     }
   }
-  float* rsp_s = smem + XS + SK_WAVES * MROWS;  // RSCALE partials [MROWS][rs_nparts]
+  float* rsp_s = smem + XS + SK_WAVES * MROWS;  // RSCALE row sums of squares [MROWS]
   if constexpr (RSCALE) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (tid + u * 512 < MROWS * sa.rs_nparts) rsp_s[tid + u * 512] = rsp[u];
+    for (int u = 0; u < RPW; ++u) {
+      float v = rsp[u];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0) rsp_s[wave + u * SK_WAVES] = v;
+    }
   }
   __syncthreads();
   if (wave >= NT * MR) return;
@@ -888,12 +891,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
     scale = (1.0f / sqrtf(t / (float)K + sa.rms_eps)) * sa.a_scale;
   }
   if constexpr (RSCALE) {
-    float t = 0.f;  // the row's partials in tile order (reads unrolled: in flight together)
-    const float* rp = rsp_s + min(m, M - 1) * sa.rs_nparts;
-#pragma unroll
-    for (int p = 0; p < 64; ++p)
-      if (p < sa.rs_nparts) t += rp[p];
-    scale = (1.0f / sqrtf(t / (float)sa.rs_n + sa.rms_eps)) * sa.a_scale;
+    scale = (1.0f / sqrtf(rsp_s[m] / (float)sa.rs_n + sa.rms_eps)) * sa.a_scale;
   }
   if constexpr (AMAX) {
     // greedy head: per (row m, block) best column, lowest index on ties (torch.argmax)
