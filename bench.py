@@ -287,6 +287,158 @@ def decode_chain(model, batch, steps: int = 20, iters: int = 10):
                     f"layer's two RMSNorms folded into the o / co projections)"}
 
 
+def eos_leg(cfg, weights, retr, device, batches, steps: int):
+    """The serving loop with greedy search's stop (architectures/T5VisionModel.py:200-205,
+    GenerationMixin ends once every row emitted eos) on a T5 that answers in one token
+    (synthetic.eos_early_t5; SLAKE's answers are 1-3 tokens): QA pairs/s with the stop polled
+    asynchronously (mpr_t5_generate_begin / _poll) against the same model forced to 20 steps, and
+    the decode steps each generate call launched."""
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    _, tok_sd, t5_sd, _, _ = weights
+    m = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=syn.eos_early_t5(t5_sd),
+                      tokenizer=SpmT5Tokenizer(),
+                      retrieval_function=retr.retrieve_closest_qa_pairs).eval()
+    out = {"model": "t5-small weights with an eos-early decoder (synthetic.eos_early_t5)"}
+    with torch.no_grad():
+        for stop in (False, True, False, True):  # warm, then timed
+            loops = []
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in m.predict_many((batches[s % len(batches)] for s in range(steps)),
+                                    eos_stop=stop, _loop_out=loops):
+                pass
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            key = "eos_stop" if stop else "forced_20"
+            out[key] = {"qa_pairs_per_s": round(steps * cfg["B"] / el, 1),
+                        "steps_run_per_call": loops[0].steps_run}
+    m = None
+    torch.cuda.empty_cache()
+    return out
+
+
+def train_leg(cfg, weights, retr, device, batches, steps: int = 10):
+    """main.py:177-188 — per step ``loss = model(batch)`` (train mode,
+    dropout 0.1 at transformers' sites, training-phase retrieval that skips the self match),
+    ``model.predict(batch)`` (:179), ``loss.backward()``, AdamW ``step()`` (the device handles
+    predict() uses are rebuilt from the updated parameters).  ms per step, and the tiled GEMM's
+    share: its algorithmic FLOPs over its own kernel time and over the step's wall time."""
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    _, tok_sd, t5_sd, _, _ = weights
+    m = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=t5_sd,
+                      tokenizer=SpmT5Tokenizer(), retrieval_function=retr.retrieve_closest_qa_pairs,
+                      t5_dropout_rate=0.1)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-5)  # main.py:149 (AdamW over parameters())
+    phase = retr.is_training_phase
+    retr.is_training_phase = True   # main.py:119-122: --train builds a training-phase index
+    m.train()
+    timings = {"forward": 0.0, "predict": 0.0, "backward_step": 0.0}
+
+    def step(b, timed):
+        t0 = time.perf_counter()
+        loss = m(b)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        m.predict(b)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        if timed:
+            timings["forward"] += t1 - t0
+            timings["predict"] += t2 - t1
+            timings["backward_step"] += t3 - t2
+        return float(loss.detach())
+
+    try:
+        for i in range(2):
+            step(batches[i % len(batches)], False)
+        _lib.probe_clear()
+        _lib.probe_enable(1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        losses = [step(batches[i % len(batches)], True) for i in range(steps)]
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        _lib.probe_enable(0)
+        gms, gl, gflops, _ = _lib.probe_read()
+        _lib.probe_clear()
+    finally:
+        retr.is_training_phase = phase
+    m = opt = None
+    torch.cuda.empty_cache()
+    ms = el / steps * 1e3
+    return {"workload": f"main.py:177-188 train step: t5-small + ViT-B/32 token features, batch "
+                        f"{cfg['B']}, dropout 0.1, forward + predict + backward + AdamW",
+            "ms_per_step": round(ms, 2),
+            "ms_per_step_parts": {k: round(v / steps * 1e3, 2) for k, v in timings.items()},
+            "qa_pairs_per_s": round(cfg["B"] / (ms * 1e-3), 1),
+            "loss_first_last": [round(losses[0], 4), round(losses[-1], 4)],
+            "roofline": {"bound": "mfma", "kernel": "gemm_x3_kernel (tiled split-bf16 GEMM)",
+                         "gemm_launches_per_step": round(gl / steps, 1),
+                         "achieved": round(gflops / (gms * 1e-3) / 1e12, 2) if gms else None,
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(gflops / (gms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)
+                         if gms else None,
+                         "gemm_share_of_wall": round(gms / (el * 1e3), 4),
+                         "note": "GEMM algorithmic flops / the GEMM launches' own time (hipEvents "
+                                 "per launch); gemm_share_of_wall = GEMM time / step wall time"}}
+
+
+def index_build(cfg, weights, device, n_batches: int = 48):
+    """VQARetrieval.create_retrieval_dataset (dataset/VQAFeatureDataset.py
+    :118-185) over a loader of synthetic batches — the retrieval ViT (CLS) + CLIP text towers per
+    row, the [N, 1024] fp32 matrix written to the cache directory, the index uploaded — timed
+    end to end on rank 0 (a fresh cache directory: nothing is loaded from disk)."""
+    import shutil
+    import tempfile
+    from multimodalpromptretrieval_amd.dataset import VQARetrieval
+    retr_sd = weights[0]
+    r = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=clip_tokenize)
+    loader = make_batches(n_batches, cfg["B"], seed=7)
+    out = {}
+    for phase in ("warm", "timed"):
+        d = tempfile.mkdtemp(prefix="mpr_ib_")
+        try:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r.create_retrieval_dataset(loader, is_training_phase=False, retrieval_k=cfg["k"],
+                                       cache_dir=d)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+        out[phase] = el
+    # the towers' GEMM flops of one build (algorithmic, from the launch probe) against the build's
+    # wall time and the fp32 MFMA peak: the roofline the index build sits under
+    d = tempfile.mkdtemp(prefix="mpr_ib_")
+    try:
+        _lib.probe_clear()
+        _lib.probe_enable(1)
+        r.create_retrieval_dataset(loader, is_training_phase=False, retrieval_k=cfg["k"],
+                                   cache_dir=d)
+        torch.cuda.synchronize()
+        _lib.probe_enable(0)
+        gms, gl, gflops, _ = _lib.probe_read()
+        _lib.probe_clear()
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    rows = n_batches * cfg["B"]
+    el = out["timed"]
+    tf = gflops / el / 1e12
+    return {"workload": f"create_retrieval_dataset over {n_batches} batches x {cfg['B']} QA "
+                        f"pairs (ViT-B/32 CLS + CLIP text per row, cache write, index upload)",
+            "rows": rows, "ms": round(el * 1e3, 2), "rows_per_s": round(rows / el, 1),
+            "roofline": {"bound": "mfma", "gemm_gflop_per_row": round(gflops / rows / 1e9, 3),
+                         "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "gemm_kernel_ms": round(gms, 2), "gemm_launches": gl,
+                         "note": "GEMM algorithmic flops of the build / its wall time"}}
+
+
 def pipeline_work(model, retr, batches, cfg, n: int = 16):
     """Host tokenizer cost and algorithmic FLOPs per QA pair over the first `n` timed batches.
 
