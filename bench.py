@@ -193,6 +193,62 @@ def c5_projection(device, iters: int = 20):
     return out
 
 
+class _C5Retrieval:
+    """Config C5's retrieval for the end-to-end leg: the questions' CLIP text embeddings (512-d,
+    the index's width) searched over the 1,048,576 x 512 index (k = 5), then the reference's
+    vote / bucket prompt (dataset/VQAFeatureDataset.py:190-246 with a text-only query: the
+    reference's [img || txt] rows are 1024-d, C5's index is 512-d as stated)."""
+
+    def __init__(self, text, index, answers, k):
+        self.text, self.index, self.answers, self.k = text, index, answers, k
+
+    def __call__(self, batch, use_quantifier=True, **kw):
+        from multimodalpromptretrieval_amd.dataset import vote_prompt
+        q = self.text(clip_tokenize(batch["question"]))
+        _, ids = self.index.search(q, self.k)
+        return [vote_prompt([self.answers[int(j) % len(self.answers)] for j in row],
+                            use_quantifier) for row in ids.cpu().tolist()]
+
+
+def c5_serving(device, batches: int = 4):
+    """Config C5 end to end on one GPU: per batch of 256 questions, CLIP text
+    tower -> 1M x 512 search (k = 5) -> prompts -> t5-base encoder + 20 greedy steps with
+    use_image_info=0 (t5-base cannot take the 512-d image tokens), through
+    T5VisionModel.predict (architectures/T5VisionModel.py:196-216).  Forced 20 steps (the
+    synthetic weights rarely stop)."""
+    from multimodalpromptretrieval_amd.encoders import DeviceCLIPText
+    from multimodalpromptretrieval_amd.index import DeviceIndex
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    n, d, B, k = C5["N"], C5["D"], C5["B"], C5["k"]
+    ix = DeviceIndex(syn.index_rows_device(7, 0, n, d, device), device)
+    text = DeviceCLIPText(syn.clip_state_dict(1), device)
+    retr = _C5Retrieval(text, ix, syn.answers(n, 50), k)
+    m = T5VisionModel(device, T5_version="t5-base", use_image_info=False,
+                      clip_state_dict=syn.clip_state_dict(2),
+                      t5_state_dict=syn.t5_state_dict(5, syn.T5_BASE),
+                      tokenizer=SpmT5Tokenizer(), retrieval_function=retr).eval()
+    pool = make_batches(batches, B, seed=500, n_images=1)
+    os.environ["MPR_EOS_STOP_CHUNK"] = "0"  # forced 20 steps
+    try:
+        with torch.no_grad():
+            m.predict(pool[0])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for b in pool:
+                m.predict(b)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+    finally:
+        os.environ.pop("MPR_EOS_STOP_CHUNK", None)
+    m = ix = text = None
+    torch.cuda.empty_cache()
+    return {"workload": "C5 end to end, 1 GPU: 256 questions per batch -> CLIP text (512-d) -> "
+                        "1M x 512 search k=5 -> prompts -> t5-base (use_image_info=0) encoder + "
+                        "20 greedy steps (T5VisionModel.predict)",
+            "ms_per_batch": round(el / len(pool) * 1e3, 2),
+            "qa_pairs_per_s": round(len(pool) * B / el, 1)}
+
+
 def make_batches(n_batches: int, B: int, seed: int, n_images: int = N_IMAGES):
     """Batches as main.py's DataLoader yields them (main.py:94-96, no pin_memory): images fp32
     [B, 3, 224, 224] in pageable HOST memory (copied to the device inside every step, as
@@ -759,6 +815,7 @@ def main():
         c5 = c5_scan(world, rank, device, group, rdev)
         if world == 1:
             c5["projection_1_to_8"] = c5_projection(device)
+            c5["end_to_end_t5_base"] = c5_serving(device)
         barrier()
 
     cpu = None
