@@ -568,6 +568,23 @@ __global__ void to_bf16_kernel(const float* __restrict__ x, int64_t n4, bf16x4* 
     out[i] = __builtin_convertvector(reinterpret_cast<const f32x4*>(x)[i], bf16x4);
 }
 
+// The coarse path's query prep in one launch: Q rounded to bf16 (as to_bf16_kernel) and |q|^2
+// (qnorm_kernel's summation order, so the gated exact fallback reuses it bit for bit).
+__global__ void qprep_kernel(const float* __restrict__ Q, int b, int d, __bf16* __restrict__ qb,
+                             float* __restrict__ out) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= b) return;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    const float v = Q[(int64_t)q * d + c];
+    qb[(int64_t)q * d + c] = (__bf16)v;
+    s += v * v;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[q] = s;
+}
+
 // |bf16(x) - x|^2 per row (wave per row; runs once per index)
 __global__ void bf16_residual_kernel(const float* __restrict__ X, int64_t n, int d, float* out) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -790,39 +807,79 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
 // alongside), sorted by (key, id).  The CB_C-th key is found by a bisection over the keys' order
 // bits (counts by a block reduction), then the <= CB_C keys at or below it are ranked.
 
+// Block-wide: the best CB_C of one query's n_cand coarse candidates, sorted by (key, id), into
+// sel_key / sel_id (this query's rows; global memory or LDS), padded with (+inf, -1).
 template <int PER>
-__global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restrict__ cand_key,
-                                                            const int64_t* __restrict__ cand_id,
-                                                            int n_cand, float* sel_key,
-                                                            int64_t* sel_id) {
-  __shared__ int cnt[4];
+__device__ __forceinline__ void select_block(const float* __restrict__ ck,
+                                             const int64_t* __restrict__ ci, int n_cand,
+                                             float* sel_key, int64_t* sel_id) {
   __shared__ float sk[CB_C * 2];
   __shared__ int64_t si[CB_C * 2];
   __shared__ int nsel;
-  const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* ck = cand_key + (int64_t)qi * n_cand;
-  const int64_t* ci = cand_id + (int64_t)qi * n_cand;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t u[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int c = tid + j * 256;
     u[j] = c < n_cand && ci[c] >= 0 ? order_bits(ck[c]) : 0xFFFFFFFFu;
   }
-  // smallest v with count(u <= v) >= CB_C
-  uint32_t lo = 0, hi = 0xFFFFFFFFu;
-  while (lo < hi) {
-    const uint32_t mid = lo + ((hi - lo) >> 1);
-    int c = 0;
+  // smallest v with count(u <= v) >= CB_C: a radix select over the order bits, 8 bits per pass
+  // (4 passes of a 256-bin LDS histogram and one wave's prefix scan, instead of a 32-step
+  // bisection with a block reduction per step)
+  __shared__ int hist[256];
+  __shared__ uint32_t s_prefix;
+  __shared__ int s_below;
+  uint32_t lo;
+  if (n_cand < CB_C) {
+    lo = 0xFFFFFFFFu;  // every candidate is kept
+  } else {
+    uint32_t prefix = 0;
+    int below = 0;  // keys whose decided bits are below the prefix
+#pragma unroll 1
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+      hist[tid] = 0;
+      __syncthreads();
 #pragma unroll
-    for (int j = 0; j < PER; ++j) c += u[j] <= mid ? 1 : 0;
+      for (int j = 0; j < PER; ++j)
+        if (tid + j * 256 < n_cand && (u[j] & hmask) == prefix)
+          atomicAdd(&hist[(u[j] >> shift) & 255u], 1);  // LDS atomic
+      __syncthreads();
+      if (wave == 0) {
+        const int c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2],
+                  c3 = hist[4 * lane + 3];
+        int inc = c0 + c1 + c2 + c3;  // inclusive scan of the lanes' 4-bin sums
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
-    if (lane == 0) cnt[wave] = c;
-    __syncthreads();
-    const int tot = (cnt[0] + cnt[1]) + (cnt[2] + cnt[3]);
-    __syncthreads();
-    if (tot >= CB_C) hi = mid;
-    else lo = mid + 1;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int o = __shfl_up(inc, off, 64);
+          if (lane >= off) inc += o;
+        }
+        const int excl = below + inc - (c0 + c1 + c2 + c3);
+        const bool hit = excl < CB_C && below + inc >= CB_C;  // exactly one lane
+        if (hit) {
+          int run = excl, dgt = 4 * lane;
+          if (run + c0 < CB_C) {
+            run += c0;
+            ++dgt;
+            if (run + c1 < CB_C) {
+              run += c1;
+              ++dgt;
+              if (run + c2 < CB_C) {
+                run += c2;
+                ++dgt;
+              }
+            }
+          }
+          s_prefix = prefix | ((uint32_t)dgt << shift);
+          s_below = run;
+        }
+      }
+      __syncthreads();
+      prefix = s_prefix;
+      below = s_below;
+    }
+    lo = prefix;
   }
   if (tid == 0) nsel = 0;
   __syncthreads();
@@ -841,8 +898,8 @@ __global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restr
   __syncthreads();
   const int m = min(nsel, 2 * CB_C);
   for (int c = tid; c < CB_C; c += 256) {  // pad a short list
-    sel_key[(int64_t)qi * CB_C + c] = INFINITY;
-    sel_id[(int64_t)qi * CB_C + c] = -1;
+    sel_key[c] = INFINITY;
+    sel_id[c] = -1;
   }
   __syncthreads();
   if (tid < m) {
@@ -851,24 +908,33 @@ __global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restr
     int rank = 0;
     for (int c = 0; c < m; ++c) rank += key_less(sk[c], si[c], a, ia) ? 1 : 0;
     if (rank < CB_C) {
-      sel_key[(int64_t)qi * CB_C + rank] = a;
-      sel_id[(int64_t)qi * CB_C + rank] = ia;
+      sel_key[rank] = a;
+      sel_id[rank] = ia;
     }
   }
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restrict__ cand_key,
+                                                            const int64_t* __restrict__ cand_id,
+                                                            int n_cand, float* sel_key,
+                                                            int64_t* sel_id) {
+  const int64_t qi = blockIdx.x;
+  select_block<PER>(cand_key + qi * n_cand, cand_id + qi * n_cand, n_cand, sel_key + qi * CB_C,
+                    sel_id + qi * CB_C);
 }
 
 // Exact re-rank: block per query over its CB_C coarse candidates (sorted coarse keys, global ids):
 // the sufficiency test (against the selected list and every lane's bound), the fp32 key
 // of every candidate (the exact scan's formula), the best k by (key, id); gate[q] = 1 asks the
 // exact scan for this query.
-__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X,
-                                                     const float* __restrict__ xnorm, int d,
-                                                     int64_t row_offset,
-                                                     const float* __restrict__ Q,
-                                                     const float* sel_key, const int64_t* sel_id,
-                                                     const float* lane_bound, int n_lists, int k,
-                                                     const float* xmax, float* out_dist,
-                                                     int64_t* out_id, int* gate) {
+__device__ __forceinline__ void rerank_block(const float* __restrict__ X,
+                                             const float* __restrict__ xnorm, int d,
+                                             int64_t row_offset, const float* __restrict__ Q,
+                                             const float* sk, const int64_t* si,
+                                             const float* lane_bound, int n_lists, int k,
+                                             const float* xmax, float* out_dist,
+                                             int64_t* out_id, int* gate) {
   __shared__ float qs[512];
   __shared__ float keys[CB_C];
   __shared__ int64_t ids[CB_C];
@@ -900,8 +966,6 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
   }
   __syncthreads();
   const float qn = (part[0] + part[1]) + (part[2] + part[3]);
-  const float* sk = sel_key + (int64_t)qi * CB_C;
-  const int64_t* si = sel_id + (int64_t)qi * CB_C;
   // The bound (below): a candidate whose coarse key exceeds T = s~(k) + 2E has an exact key above
   // the exact k-th best, so only the prefix of the sorted list with keys <= T is re-scored (a
   // margin of 2^-16 relative keeps the excluded keys distinct from the k-th after the sqrt); the
@@ -978,6 +1042,35 @@ __global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X
       out_id[(int64_t)qi * k + rank] = ia == INT64_MAX ? -1 : ia;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X,
+                                                     const float* __restrict__ xnorm, int d,
+                                                     int64_t row_offset,
+                                                     const float* __restrict__ Q,
+                                                     const float* sel_key, const int64_t* sel_id,
+                                                     const float* lane_bound, int n_lists, int k,
+                                                     const float* xmax, float* out_dist,
+                                                     int64_t* out_id, int* gate) {
+  const int64_t qi = blockIdx.x;
+  rerank_block(X, xnorm, d, row_offset, Q, sel_key + qi * CB_C, sel_id + qi * CB_C, lane_bound,
+               n_lists, k, xmax, out_dist, out_id, gate);
+}
+
+// select + re-rank in one block per query (n_cand <= 256 * PER): the sorted CB_C stay in LDS
+template <int PER>
+__global__ __launch_bounds__(256) void coarse_rerank_kernel(
+    const float* __restrict__ cand_key, const int64_t* __restrict__ cand_id, int n_cand,
+    const float* __restrict__ X, const float* __restrict__ xnorm, int d, int64_t row_offset,
+    const float* __restrict__ Q, const float* lane_bound, int n_lists, int k, const float* xmax,
+    float* out_dist, int64_t* out_id, int* gate) {
+  __shared__ float sel_k[CB_C];
+  __shared__ int64_t sel_i[CB_C];
+  const int64_t qi = blockIdx.x;
+  select_block<PER>(cand_key + qi * n_cand, cand_id + qi * n_cand, n_cand, sel_k, sel_i);
+  __syncthreads();
+  rerank_block(X, xnorm, d, row_offset, Q, sel_k, sel_i, lane_bound, n_lists, k, xmax, out_dist,
+               out_id, gate);
 }
 
 __global__ void sqnorm_kernel(const float* X, int64_t n, int d, float* out) {
@@ -1068,9 +1161,12 @@ int scan_mm_rowblocks(int64_t n, int b) {
 template <int K>
 int launch_scan_mm(const float* X, int64_t n, int d, int64_t row_offset, int metric,
                    const float* Q, float* qn, int b, float* ck, int64_t* ci, hipStream_t s,
-                   const int* gate) {
+                   const int* gate, const float* qn_pre) {
   const int nqt = (int)cdiv(b, SM_B), RB = scan_mm_rowblocks(n, b);
-  hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d, qn);
+  if (qn_pre)
+    qn = const_cast<float*>(qn_pre);
+  else
+    hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d, qn);
   hipLaunchKernelGGL((scan_mm_kernel<K>), dim3((unsigned)(nqt * RB)), dim3(256), 0, s, X, n, d,
                      row_offset, metric, Q, qn, b, nqt, RB, ck, ci, gate);
   MPR_LAUNCHED();
@@ -1196,15 +1292,17 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
   MPR_REQUIRE(ws_bytes >= scan_topk_workspace(n, b, k), "search: workspace too small");
   const int K = list_cap(k);
   const int* gate = nullptr;
+  const float* qn_pre = nullptr;  // |q|^2 already computed by the coarse path
   if (Xb && xmax && scan_coarse_eligible(n, d, b, k, metric)) {
     // coarse bf16 scan -> top CB_C per query -> exact re-rank (+ the gated exact fallback below)
     CoarseWs w = coarse_ws(ws, n, d, b);
     ws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + (w.bytes + 255) / 256 * 256);
     const int nqt = (int)cdiv(b, CB_QT), RB = coarse_rowblocks(n, b);
     MPR_REQUIRE(n < (int64_t)1 << 31, "search: coarse scan rows %lld >= 2^31", (long long)n);
-    MPR_TRY(index_to_bf16(Q, (int64_t)b * d, w.qb, s));
-    hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d, w.qn);
+    hipLaunchKernelGGL(qprep_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d,
+                       reinterpret_cast<__bf16*>(w.qb), w.qn);
     MPR_LAUNCHED();
+    qn_pre = w.qn;
     const size_t qlds = (size_t)CB_QT * (d + 8) * 2;
     if (d == 512)
       hipLaunchKernelGGL(scan_bf_kernel<32>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s,
@@ -1216,17 +1314,24 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
                          w.qn, nqt, RB, w.ck, w.ci, w.lb);
     MPR_LAUNCHED();
     const int n_cand = RB * 2 * CB_L;
-    if (n_cand <= 256 * 16)
-      hipLaunchKernelGGL(coarse_select_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck, w.ci,
-                         n_cand, w.sk, w.si);
-    else
-      MPR_TRY(merge_dispatch(w.ck, w.ci, b, n_cand, CB_C, /*keys_are_values=*/0, /*metric=*/0,
-                             w.sk, w.si, s));
-    MPR_LAUNCHED();
-    hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)b), dim3(256), 0, s, X, xnorm, d,
-                       row_offset, Q, w.sk, w.si, w.lb, RB * 2, k, xmax, out_dist, out_ids,
-                       w.gate);
-    MPR_LAUNCHED();
+    if (n_cand <= 256 * 16 && !getenv("MPR_COARSE_UNFUSED")) {
+      hipLaunchKernelGGL(coarse_rerank_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck, w.ci,
+                         n_cand, X, xnorm, d, row_offset, Q, w.lb, RB * 2, k, xmax, out_dist,
+                         out_ids, w.gate);
+      MPR_LAUNCHED();
+    } else {
+      if (n_cand <= 256 * 16)
+        hipLaunchKernelGGL(coarse_select_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
+                           w.ci, n_cand, w.sk, w.si);
+      else
+        MPR_TRY(merge_dispatch(w.ck, w.ci, b, n_cand, CB_C, /*keys_are_values=*/0, /*metric=*/0,
+                               w.sk, w.si, s));
+      MPR_LAUNCHED();
+      hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)b), dim3(256), 0, s, X, xnorm, d,
+                         row_offset, Q, w.sk, w.si, w.lb, RB * 2, k, xmax, out_dist, out_ids,
+                         w.gate);
+      MPR_LAUNCHED();
+    }
     gate = w.gate;
   }
   if (use_scan_mm(n, d, b, k) && !getenv("MPR_SCAN_MM_OFF")) {
@@ -1237,7 +1342,8 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     int rc = MPR_EUNSUP;
     switch (K) {
 #define MPR_SM(KK) \
-  case KK: rc = launch_scan_mm<KK>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s, gate); break;
+  case KK: rc = launch_scan_mm<KK>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s, gate, qn_pre); \
+    break;
       MPR_SM(1) MPR_SM(2) MPR_SM(4) MPR_SM(8) MPR_SM(16)
 #undef MPR_SM
     }

@@ -11,7 +11,8 @@ from multimodalpromptretrieval_amd import synthetic as syn  # noqa: E402
 from multimodalpromptretrieval_amd.index import DeviceIndex  # noqa: E402
 
 dev = torch.device("cuda:0")
-n, d, b, k = (1 << 20) // int(sys.argv[1] if len(sys.argv) > 1 else 1), 512, 256, 5
+n, d, k = (1 << 20) // int(sys.argv[1] if len(sys.argv) > 1 else 1), 512, 5
+b = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 ix = DeviceIndex(syn.index_rows_device(7, 0, n, d, dev), dev)
 q = torch.randn((b, d), device=dev, generator=torch.Generator(device=dev).manual_seed(8)) * 0.3
 for _ in range(3):
@@ -23,5 +24,5 @@ for _ in range(10):
     ix.search(q, k)
 e1.record()
 torch.cuda.synchronize()
-print(f"C5 search ({n} rows): {e0.elapsed_time(e1) / 10:.3f} ms, exact fallbacks {ix.coarse_fallbacks()}",
+print(f"C5 search ({n} rows, {b} queries): {e0.elapsed_time(e1) / 10:.3f} ms, exact fallbacks {ix.coarse_fallbacks()}",
       flush=True)
