@@ -803,6 +803,175 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
   lane_bound[((int64_t)q * RB + rb) * 2 + lh] = fminf(bk[CB_L - 1], drop);
 }
 
+// The coarse scan with the queries in REGISTERS, so one block covers up to 256 queries and the
+// bf16 index is streamed from HBM once per search (scan_bf_kernel holds 128 queries in LDS and
+// reads the index once per 128-query tile: twice at C5).  Block = NW waves x 32 queries; wave w's
+// lane keeps its query's bf16 row as the MFMA B operand for every 16-deep k-step (KS x 16 B:
+// 128 VGPRs at d = 512), so only the index tile passes through LDS: 64-row x 64-deep stages
+// (register prefetch CB2_D stages ahead, two LDS buffers, one barrier per stage), every wave reading
+// the A fragments of all 64 rows (1 KiB of LDS per 32x32x16 MFMA: 128 B/clk/CU at the MFMA rate,
+// half the array's 256).  Two waves per SIMD at NW = 8, so one wave's key epilogue runs beside the
+// other's MFMAs.  Keys, lists and the lane bound are scan_bf_kernel's (the row tag now 6 bits, so
+// the quantisation is < 2^-17 relative, inside the re-rank's 2^-16 margin); the outputs share its
+// layout ([q][RB][2 lanes][CB_L]), so select / re-rank / fallback are unchanged.
+constexpr int CB2_RT = 64;             // index rows per tile (2 x 32-row MFMA tiles)
+constexpr int CB2_BK = 64;             // k per LDS stage (4 x 16-deep MFMA steps)
+constexpr int CB2_LDK = CB2_BK + 8;    // LDS row stride in bf16 (144 B: ds_read_b128 conflict-free)
+constexpr int CB2_STAGE = CB2_RT * CB2_LDK;
+
+template <int KS, int NW, int D>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16* __restrict__ Xb,
+                                                              const float* __restrict__ xnorm,
+                                                              int64_t n, int64_t row_offset,
+                                                              const __bf16* __restrict__ Qb, int b,
+                                                              const float* __restrict__ qnorm,
+                                                              int nqt, int RB, float* cand_key,
+                                                              int64_t* cand_id, float* lane_bound) {
+  constexpr int d = KS * 16, NT = NW * 64;
+  constexpr int SPT = d / CB2_BK;                   // stages per row tile
+  constexpr int LPS = CB2_RT * CB2_BK / 8 / NT;     // 16-byte loads per thread per stage
+  constexpr int CPR = CB2_BK / 8;                   // 16-byte chunks per staged row
+  static_assert(LPS >= 1 && SPT % D == 0, "stage slots repeat per row tile");
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][CB2_STAGE];
+  __shared__ float xn_s[2][CB2_RT];
+  int qt, rb;
+  {
+    const int total = gridDim.x, hw = blockIdx.x;
+    const int xcd = hw & 7, slot = hw >> 3, q8 = total >> 3, r8 = total & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+    qt = t % nqt;
+    rb = t / nqt;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int64_t ntile = (n + CB2_RT - 1) / CB2_RT;
+  const int ntb = (int)((ntile - rb + RB - 1) / RB);
+
+  const int q = qt * NW * 32 + wave * 32 + li;
+  const bool qok = q < b;
+  const float qn_l = qok ? qnorm[q] : 0.f;
+  // B[k = 16 j + 8 lh + e][col li] = Q~[q][16 j + 8 lh + e]; queries past b read row b-1 (their
+  // lists are never written)
+  bf16x8 qf[KS];
+  {
+    const __bf16* qp = Qb + (int64_t)(qok ? q : b - 1) * d + 8 * lh;
+#pragma unroll
+    for (int j = 0; j < KS; ++j) qf[j] = *reinterpret_cast<const bf16x8*>(qp + 16 * j);
+  }
+
+  bf16x8 rx[D][LPS];
+  float rn[D];
+  // stage ks of the block's row tile tt: rows past n load row n-1 (masked by an infinite norm)
+  auto gload = [&](int j, int tt, int ks) {
+    const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB2_RT;
+#pragma unroll
+    for (int i = 0; i < LPS; ++i) {
+      const int idx = tid + i * NT, r = idx / CPR, c = ks * CB2_BK + (idx % CPR) * 8;
+      const int64_t row = row0 + r;
+      rx[j][i] = *reinterpret_cast<const bf16x8*>(Xb + (row < n ? row : n - 1) * (int64_t)d + c);
+    }
+    if (ks == 0) {
+      const int64_t nrow = row0 + (tid & (CB2_RT - 1));
+      rn[j] = nrow < n ? xnorm[nrow] : INFINITY;
+    }
+  };
+  auto swrite = [&](int st, int j, int tt, int ks) {
+#pragma unroll
+    for (int i = 0; i < LPS; ++i) {
+      const int idx = tid + i * NT, r = idx / CPR, c = (idx % CPR) * 8;
+      *reinterpret_cast<bf16x8*>(&xs[st][r * CB2_LDK + c]) = rx[j][i];
+    }
+    if (ks == 0 && tid < CB2_RT) xn_s[tt & 1][tid] = rn[j];
+  };
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[mi][r] = 0.f;
+  float bk[CB_L];
+  int bi[CB_L];
+#pragma unroll
+  for (int t = 0; t < CB_L; ++t) {
+    bk[t] = INFINITY;
+    bi[t] = INT_MAX;
+  }
+  float drop = INFINITY;
+
+  // prologue: stage 0 in LDS buffer 0, stages 1..D in flight (stage s >= 1 in slot (s - 1) % D)
+  gload(0, 0, 0);
+  swrite(0, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < D; ++j) gload(j, (1 + j) / SPT, (1 + j) % SPT);
+  __syncthreads();
+  for (int tt = 0; tt < ntb; ++tt) {
+#pragma clang loop unroll(full)
+    for (int ks = 0; ks < SPT; ++ks) {
+      const int st = ks & 1;  // SPT is even: a tile's first stage is always in buffer 0
+#pragma unroll
+      for (int u = 0; u < CB2_BK / 16; ++u) {
+        bf16x8 fa[2];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+          fa[mi] = *reinterpret_cast<const bf16x8*>(
+              &xs[st][(mi * 32 + li) * CB2_LDK + 16 * u + 8 * lh]);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+          acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi], qf[ks * (CB2_BK / 16) + u],
+                                                            acc[mi], 0, 0, 0);
+      }
+      // stage g+1 (held in slot g % D = ks % D) into the other buffer, then re-arm that slot with
+      // stage g+1+D
+      const int j1 = ks % D;
+      swrite(st ^ 1, j1, tt + (ks + 1) / SPT, (ks + 1) % SPT);
+      gload(j1, tt + (ks + 1 + D) / SPT, (ks + 1 + D) % SPT);
+      __syncthreads();
+    }
+    {  // keys of this row tile (scan_bf_kernel's epilogue, 6-bit row tag)
+      uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const float key = fmaxf(fmaf(-2.0f, acc[mi][r], xn_s[tt & 1][rr]) + qn_l, 0.0f);
+          acc[mi][r] = 0.f;
+          const uint32_t v = (__float_as_uint(key) & ~63u) | (uint32_t)rr;
+          v3 = min(v3, max(v2, v));
+          v2 = min(v2, max(v1, v));
+          v1 = min(v1, v);
+        }
+      drop = fminf(drop, __uint_as_float(v3 & ~63u));
+      auto insert = [&](float ck, int ci) {
+#pragma unroll
+        for (int t = 0; t < CB_L; ++t) {
+          const bool sw = ck < bk[t];
+          const float tk = sw ? bk[t] : ck;
+          const int ti = sw ? bi[t] : ci;
+          bk[t] = sw ? ck : bk[t];
+          bi[t] = sw ? ci : bi[t];
+          ck = tk;
+          ci = ti;
+        }
+      };
+      const int row0 = (rb + tt * RB) * CB2_RT;  // n < 2^31 (checked by the launcher)
+      const float k1 = __uint_as_float(v1 & ~63u), k2 = __uint_as_float(v2 & ~63u);
+      if (k1 < bk[CB_L - 1]) insert(k1, row0 + (int)(v1 & 63u));
+      if (k2 < bk[CB_L - 1]) insert(k2, row0 + (int)(v2 & 63u));
+    }
+  }
+  if (!qok) return;
+  float* okp = cand_key + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
+  int64_t* oip = cand_id + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
+#pragma unroll
+  for (int t = 0; t < CB_L; ++t) {
+    okp[t] = bk[t];
+    oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
+  }
+  lane_bound[((int64_t)q * RB + rb) * 2 + lh] = fminf(bk[CB_L - 1], drop);
+}
+
 // Coarse selection: block per query, the CB_C smallest of its n_cand lane-list keys (ids
 // alongside), sorted by (key, id).  The CB_C-th key is found by a bisection over the keys' order
 // bits (counts by a block reduction), then the <= CB_C keys at or below it are ranked.
@@ -1174,7 +1343,21 @@ int launch_scan_mm(const float* X, int64_t n, int d, int64_t row_offset, int met
 }
 
 // ---- coarse path launchers --------------------------------------------------------------------
+// scan_bf2_kernel (queries in registers, the index read once per 256 queries) unless
+// MPR_COARSE_V1 asks for the LDS-resident-query kernel
+bool coarse_v2() {
+  static const bool v = getenv("MPR_COARSE_V1") == nullptr;
+  return v;
+}
+int coarse_waves(int b) { return b <= 128 ? 4 : 8; }
 int coarse_rowblocks(int64_t n, int b) {
+  if (coarse_v2()) {
+    // one 8-wave block (two at 4 waves) per CU, every lane seeing >= 8 row tiles
+    const int64_t ntile = (n + CB2_RT - 1) / CB2_RT;
+    const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
+    const int64_t per = std::max<int64_t>(1, (NW == 4 ? 512 : 256) / nqt);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(per, ntile / 8));
+  }
   // ~2 blocks per CU, but every lane sees >= 8 row tiles (its bound gets tight: few fallbacks)
   const int64_t ntile = (n + CB_RT - 1) / CB_RT;
   const int nqt = (int)cdiv(b, CB_QT);
@@ -1297,21 +1480,35 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     // coarse bf16 scan -> top CB_C per query -> exact re-rank (+ the gated exact fallback below)
     CoarseWs w = coarse_ws(ws, n, d, b);
     ws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + (w.bytes + 255) / 256 * 256);
-    const int nqt = (int)cdiv(b, CB_QT), RB = coarse_rowblocks(n, b);
+    const int RB = coarse_rowblocks(n, b);
     MPR_REQUIRE(n < (int64_t)1 << 31, "search: coarse scan rows %lld >= 2^31", (long long)n);
     hipLaunchKernelGGL(qprep_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d,
                        reinterpret_cast<__bf16*>(w.qb), w.qn);
     MPR_LAUNCHED();
     qn_pre = w.qn;
-    const size_t qlds = (size_t)CB_QT * (d + 8) * 2;
-    if (d == 512)
-      hipLaunchKernelGGL(scan_bf_kernel<32>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s,
-                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b,
-                         w.qn, nqt, RB, w.ck, w.ci, w.lb);
-    else
-      hipLaunchKernelGGL(scan_bf_kernel<16>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s,
-                         reinterpret_cast<const __bf16*>(Xb), xnorm, n, row_offset, w.qb, b,
-                         w.qn, nqt, RB, w.ck, w.ci, w.lb);
+    const __bf16* xb = reinterpret_cast<const __bf16*>(Xb);
+    if (coarse_v2()) {
+      const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
+      const dim3 grid((unsigned)(nqt * RB)), blk((unsigned)(NW * 64));
+#define MPR_BF2(KS_, NW_)                                                                       \
+  hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, 4>), grid, blk, 0, s, xb, xnorm, n, row_offset, \
+                     w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
+      if (d == 512) {
+        if (NW == 8) MPR_BF2(32, 8); else MPR_BF2(32, 4);
+      } else {
+        if (NW == 8) MPR_BF2(16, 8); else MPR_BF2(16, 4);
+      }
+#undef MPR_BF2
+    } else {
+      const int nqt = (int)cdiv(b, CB_QT);
+      const size_t qlds = (size_t)CB_QT * (d + 8) * 2;
+      if (d == 512)
+        hipLaunchKernelGGL(scan_bf_kernel<32>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s, xb,
+                           xnorm, n, row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb);
+      else
+        hipLaunchKernelGGL(scan_bf_kernel<16>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s, xb,
+                           xnorm, n, row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb);
+    }
     MPR_LAUNCHED();
     const int n_cand = RB * 2 * CB_L;
     if (n_cand <= 256 * 16 && !getenv("MPR_COARSE_UNFUSED")) {

@@ -7,7 +7,12 @@ retrieval step per batch:
   3. all_to_all of the candidates              -> each rank receives the W shard-candidates of
                                                   its own b queries: [W, b, k];
   4. merge (libmpr topk_merge)                 -> [b, k], ties by lowest global id, so the result
-                                                  is identical to the single-GPU scan.
+                                                  is the single-GPU scan's whenever the shards'
+                                                  searches take the single search's kernel path.
+A row's exact fp32 distance is summed in one order per path (the exact scans' MFMA chains, the
+coarse path's re-rank, scan.hip), so two rows within an ulp of each other can order differently
+when a shard's size or a batch's size selects another path than the single-GPU search did:
+same ids up to fp32 rounding ties (exact ties always go to the lowest id).
 Messages are KB-scale (latency-bound over xGMI), so the candidates travel as ONE packed float64
 tensor (ids < 2^53 and fp32 distances are exact in float64), not a collective per field.
 
@@ -161,7 +166,8 @@ class ShardedIndex:
 
     def search_all(self, q: torch.Tensor, k: int):
         """q: the SAME [B, d] query batch on every rank (replicated).  Returns (dist, ids)
-        [B, k] for the whole batch on every rank, identical to a single-GPU search: the local
+        [B, k] for the whole batch on every rank, a single-GPU search's (up to fp32 rounding ties,
+        above): the local
         scan of all B queries, one all_gather of the per-shard top-k, the merge."""
         B = q.shape[0]
         q = q.to(self.device, torch.float32).contiguous()

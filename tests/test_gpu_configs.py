@@ -194,7 +194,8 @@ def test_c5_scan_full_size_vs_fp64_oracle(device):
     assert n_exact >= B - 2
 
 
-@pytest.mark.parametrize("n,d,b,k", [(50000, 512, 128, 5), (20011, 256, 64, 8), (3000, 512, 300, 1)])
+@pytest.mark.parametrize("n,d,b,k", [(50000, 512, 128, 5), (20011, 256, 64, 8), (3000, 512, 300, 1),
+                                     (30001, 256, 200, 3), (131072, 512, 256, 5)])
 def test_coarse_scan_matches_oracle(device, n, d, b, k):
     """Large-batch L2 searches take the bf16 coarse scan + exact fp32 re-rank: ids equal the
     exact ranking wherever fp64 separates neighbours by more than the fp32 bound."""

@@ -86,6 +86,26 @@ def test_scan_large_batch_ties_and_cosine(device, index_mod):
     assert torch.allclose(sim.cpu(), ref_sim, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("b", [96, 256])
+def test_coarse_path_ties_lowest_id(device, index_mod, b):
+    """The coarse bf16 path (L2, d = 512, b >= 64): exact duplicates resolve to the lowest id,
+    as in the exact scans.  Small-integer rows make every dot product exact in bf16 and in any
+    fp32 summation order, so the coarse keys, the re-rank and the reference all tie exactly."""
+    g = np.random.Generator(np.random.PCG64(19))
+    n = 20000
+    X = torch.from_numpy(g.integers(-3, 4, size=(n, 512)).astype(np.float32))
+    X[[40, 9001, 19999]] = X[12345].clone()
+    q = torch.from_numpy(g.integers(-3, 4, size=(b, 512)).astype(np.float32))
+    q[0] = X[12345]
+    q[1] = X[12345] + 1.0          # all four duplicates tie at the same nonzero distance
+    ix = index_mod.DeviceIndex(X, device)
+    dist, ids = ix.search(q.to(device), 5)
+    ref_ids = oret.topk_ids(oret.cdist(q, X), 5, skip_first=False)
+    assert torch.equal(ids.cpu(), ref_ids)
+    assert ids[0, :4].tolist() == [40, 9001, 12345, 19999]
+    assert ids[1, :4].tolist() == [40, 9001, 12345, 19999]
+
+
 def test_scan_cosine(device, index_mod):
     X = syn.index_rows(3, 5000, 512)
     q = syn.index_rows(4, 16, 512)

@@ -24,5 +24,5 @@ for _ in range(10):
     ix.search(q, k)
 e1.record()
 torch.cuda.synchronize()
-print(f"C5 search ({n} rows, {b} queries): {e0.elapsed_time(e1) / 10:.3f} ms, exact fallbacks {ix.coarse_fallbacks()}",
+print(f"[{"v1" if os.environ.get("MPR_COARSE_V1") else "v2"}] C5 search ({n} rows, {b} queries): {e0.elapsed_time(e1) / 10:.3f} ms, exact fallbacks {ix.coarse_fallbacks()}",
       flush=True)
