@@ -210,43 +210,66 @@ class _C5Retrieval:
                             use_quantifier) for row in ids.cpu().tolist()]
 
 
-def c5_serving(device, batches: int = 4):
-    """Config C5 end to end on one GPU: per batch of 256 questions, CLIP text
-    tower -> 1M x 512 search (k = 5) -> prompts -> t5-base encoder + 20 greedy steps with
+def c5_serving(world, rank, device, group, rdev, batches: int = 4):
+    """Config C5 end to end: per batch of 256 questions, CLIP text tower ->
+    1M x 512 search (k = 5) -> prompts -> t5-base encoder + 20 greedy steps with
     use_image_info=0 (t5-base cannot take the 512-d image tokens), through
     T5VisionModel.predict (architectures/T5VisionModel.py:196-216).  Forced 20 steps (the
-    synthetic weights rarely stop)."""
+    synthetic weights rarely stop).  N > 1: the index is row-sharded (rows/W per rank,
+    distributed.ShardedIndex with fixed 256-query blocks: all_gather of the ranks' query blocks,
+    the local scan of all W x 256, all_to_all of the candidates, merge) and every rank serves its
+    own 256-question batches (weak scaling: the per-rank scan work stays that of the whole index
+    for 256 queries while each GPU holds 1/W of it)."""
+    from multimodalpromptretrieval_amd.distributed import ShardedIndex, shard_bounds
     from multimodalpromptretrieval_amd.encoders import DeviceCLIPText
     from multimodalpromptretrieval_amd.index import DeviceIndex
     from multimodalpromptretrieval_amd.model import T5VisionModel
     n, d, B, k = C5["N"], C5["D"], C5["B"], C5["k"]
-    ix = DeviceIndex(syn.index_rows_device(7, 0, n, d, device), device)
+    lo, hi = shard_bounds(n, world, rank)
+    rows = syn.index_rows_device(7, lo, hi, d, device)
+    if world > 1:
+        ix = ShardedIndex(rows, device, group=group, rows_are_local=True, row_offset=lo,
+                          max_batch=B)
+    else:
+        ix = DeviceIndex(rows, device)
+    del rows
     text = DeviceCLIPText(syn.clip_state_dict(1), device)
     retr = _C5Retrieval(text, ix, syn.answers(n, 50), k)
     m = T5VisionModel(device, T5_version="t5-base", use_image_info=False,
                       clip_state_dict=syn.clip_state_dict(2),
                       t5_state_dict=syn.t5_state_dict(5, syn.T5_BASE),
                       tokenizer=SpmT5Tokenizer(), retrieval_function=retr).eval()
-    pool = make_batches(batches, B, seed=500, n_images=1)
+    pool = make_batches(batches + 1, B, seed=500 + rank, n_images=1)
     os.environ["MPR_EOS_STOP_CHUNK"] = "0"  # forced 20 steps
     try:
         with torch.no_grad():
             m.predict(pool[0])
             torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
             t0 = time.perf_counter()
-            for b in pool:
+            for b in pool[1:]:
                 m.predict(b)
             torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
             el = time.perf_counter() - t0
     finally:
         os.environ.pop("MPR_EOS_STOP_CHUNK", None)
-    m = ix = text = None
+    if world > 1:
+        t = torch.tensor([el], device=rdev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    m = ix = text = retr = None
     torch.cuda.empty_cache()
-    return {"workload": "C5 end to end, 1 GPU: 256 questions per batch -> CLIP text (512-d) -> "
-                        "1M x 512 search k=5 -> prompts -> t5-base (use_image_info=0) encoder + "
-                        "20 greedy steps (T5VisionModel.predict)",
-            "ms_per_batch": round(el / len(pool) * 1e3, 2),
-            "qa_pairs_per_s": round(len(pool) * B / el, 1)}
+    nb = len(pool) - 1
+    return {"workload": f"C5 end to end, {world} GPU(s): 256 questions per batch per GPU -> CLIP "
+                        f"text (512-d) -> 1M x 512 search k=5 (index rows/{world} per GPU) -> "
+                        "prompts -> t5-base (use_image_info=0) encoder + 20 greedy steps "
+                        "(T5VisionModel.predict)",
+            "scaling": "weak" if world > 1 else None,
+            "ms_per_batch": round(el / nb * 1e3, 2),
+            "qa_pairs_per_s": round(world * nb * B / el, 1)}
 
 
 def make_batches(n_batches: int, B: int, seed: int, n_images: int = N_IMAGES):
@@ -815,7 +838,7 @@ def main():
         c5 = c5_scan(world, rank, device, group, rdev)
         if world == 1:
             c5["projection_1_to_8"] = c5_projection(device)
-            c5["end_to_end_t5_base"] = c5_serving(device)
+        c5["end_to_end_t5_base"] = c5_serving(world, rank, device, group, rdev)
         barrier()
 
     cpu = None

@@ -5,6 +5,7 @@
 // every list length but 16, which takes the 32 kernel).
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -99,10 +100,67 @@ __global__ __launch_bounds__(NT) void merge_kernel(const float* cand_key, const 
 }
 
 
+// Short candidate lists (a sharded search's W x k per query, <= MW_MAX): one WAVE per query, four
+// queries per block, so the k rounds are wave shuffles with no block barrier (the block kernel
+// above spends a barrier per round).  Same (key, id) order, same outputs.
+constexpr int MW_MAX = 512;
+template <int K>
+__global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
+                                                         const int64_t* cand_id, int64_t n_cand,
+                                                         int b, int k, int keys_are_values,
+                                                         int metric, float* out_val,
+                                                         int64_t* out_id, const int* gate) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= b || (gate && gate[q] == 0)) return;  // wave-uniform
+  const float* ck = cand_key + (int64_t)q * n_cand;
+  const int64_t* ci = cand_id + (int64_t)q * n_cand;
+  const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
+  uint64_t w[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) w[t] = ~0ull;
+  for (int64_t c = lane; c < n_cand; c += 64) {
+    const float kk = sign * ck[c];
+    uint64_t v = head_word(kk, kk == kk ? ci[c] : -1);  // NaN keys never rank (as key_less)
+#pragma unroll
+    for (int t = 0; t < K; ++t) {  // sorted insert (words are unique per valid candidate)
+      const uint64_t lo = v < w[t] ? v : w[t], hi = v < w[t] ? w[t] : v;
+      w[t] = lo;
+      v = hi;
+    }
+  }
+  for (int r = 0; r < k; ++r) {
+    uint64_t m = w[0];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const uint64_t o = __shfl_xor(m, off, 64);
+      m = o < m ? o : m;
+    }
+    if (m != ~0ull && w[0] == m) {
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) w[t] = w[t + 1];
+      w[K - 1] = ~0ull;
+    }
+    if (lane == 0) {
+      const bool none = m == ~0ull;
+      const float kk = word_key(m);
+      out_val[(int64_t)q * k + r] = none ? NAN : (metric == 1 ? -kk : kk);
+      out_id[(int64_t)q * k + r] = none ? -1 : (int64_t)(uint32_t)m;
+    }
+  }
+}
+
 template <int K>
 int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                  int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
                  const int* gate) {
+  if constexpr (K <= 8) {
+    if (n_cand <= MW_MAX && !getenv("MPR_MERGE_BLOCK")) {
+      hipLaunchKernelGGL((merge_wave_kernel<K>), dim3((unsigned)((b + 3) / 4)), dim3(256), 0, s,
+                         ck, ci, n_cand, b, k, keys_are_values, metric, od, oi, gate);
+      MPR_LAUNCHED();
+      return MPR_OK;
+    }
+  }
   constexpr int NT = K >= 32 ? 128 : 256;
   hipLaunchKernelGGL((merge_kernel<K, NT>), dim3(b), dim3(NT), 0, s, ck, ci, n_cand, k,
                      keys_are_values, metric, od, oi, gate);

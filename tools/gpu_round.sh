@@ -9,6 +9,9 @@ STEPS=${2:-10}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# the profiled passes skip the side legs (C5, training, eos, index build): their kernels are not
+# in the replay window or the GEMM counters
+LEAN="--no-c5 --no-train-leg --no-eos-leg --no-index-build"
 
 ok_or_stop() {  # $1 = rc, $2 = step name, $3 = allow-rc-1
   local rc=$1
@@ -29,7 +32,7 @@ timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 4 > "$OUT/bench.json
 ok_or_stop $? bench 0
 if [ -z "$SKIP_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-    -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline \
+    -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline $LEAN \
     > "$OUT/prof.log" 2>&1
   ok_or_stop $? rocprof 0
   python tools/prof_summary.py --replay "$OUT/prof/run_kernel_trace.csv" "$OUT/replay_window.json" >> "$OUT/prof.log" 2>&1
@@ -37,7 +40,7 @@ if [ -z "$SKIP_PROF" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_x3_kernel|gemm_f32_kernel|probe_marker_kernel" \
       -d "$OUT/pmc_$c" -o run --output-format csv \
-      -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1
+      -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline $LEAN > "$OUT/pmc_$c.log" 2>&1
     ok_or_stop $? pmc_$c 0
   done
   python tools/pmc_traffic.py "$OUT/pmc_FETCH_SIZE/run_counter_collection.csv" \
