@@ -126,10 +126,20 @@ def c5_scan(world, rank, device, group, rdev, iters=20):
     tf = 2.0 * n * d * B / (ms * 1e-3) / 1e12
     search = six = ix = None
     torch.cuda.empty_cache()
+    # the coarse path's algorithmic bytes: the bf16 index copy read once per search (2 B per
+    # element), against the whole search's time at this rank count (every rank's shard in
+    # parallel): a lower bound on the coarse kernel's own fraction
+    gbs = n * d * 2 / (ms * 1e-3) / 1e9
     return {"workload": "C5: 1,048,576 x 512 fp32 index, rows/W per rank; 256 queries on every "
                         "rank, k=5, one all_gather of per-shard top-k",
             "ms_per_search": round(ms, 3), "queries_per_s": round(B / (ms * 1e-3), 1),
             "scan_tflops_aggregate": round(tf, 2), "scaling": "strong",
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS * world,
+                         "unit": "GB/s", "frac": round(gbs / (HBM_PEAK_GBS * world), 4),
+                         "note": "bf16 index bytes (N x D x 2, read once per search by the "
+                                 "register-query coarse kernel) / the whole search time (coarse "
+                                 "scan, select + exact re-rank, gated fallback launches, merge, "
+                                 "all_gather at W > 1) against W x 8 TB/s"},
             "ids_checksum": int(chk.item())}
 
 

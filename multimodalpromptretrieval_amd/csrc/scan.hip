@@ -813,7 +813,8 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
 // half the array's 256).  Two waves per SIMD at NW = 8, so one wave's key epilogue runs beside the
 // other's MFMAs.  Keys, lists and the lane bound are scan_bf_kernel's (the row tag now 6 bits, so
 // the quantisation is < 2^-17 relative, inside the re-rank's 2^-16 margin); the outputs share its
-// layout ([q][RB][2 lanes][CB_L]), so select / re-rank / fallback are unchanged.
+// layout with one list per (query, block) ([q][RB][CB_L]: the two lane halves merged in-kernel),
+// so select / re-rank / fallback are unchanged.
 constexpr int CB2_RT = 64;             // index rows per tile (2 x 32-row MFMA tiles)
 constexpr int CB2_BK = 64;             // k per LDS stage (4 x 16-deep MFMA steps)
 constexpr int CB2_LDK = CB2_BK + 8;    // LDS row stride in bf16 (144 B: ds_read_b128 conflict-free)
@@ -961,15 +962,48 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
       if (k2 < bk[CB_L - 1]) insert(k2, row0 + (int)(v2 & 63u));
     }
   }
-  if (!qok) return;
-  float* okp = cand_key + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
-  int64_t* oip = cand_id + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
+  // One list per (query, block): lane li takes lane li + 32's list (the same query's other rows)
+  // and keeps the best CB_L of the 16.  Every row the merged list lacks has a key >= the new bound
+  // min(both lanes' bounds, the smallest key pushed out here), so the re-rank's test is unchanged
+  // and the select reads half the candidates.
+  float bound = fminf(bk[CB_L - 1], drop);
+  {
+    float ok[CB_L];
+    int oi[CB_L];
+#pragma unroll
+    for (int t = 0; t < CB_L; ++t) {
+      ok[t] = __shfl_xor(bk[t], 32, 64);
+      oi[t] = __shfl_xor(bi[t], 32, 64);
+    }
+    bound = fminf(bound, __shfl_xor(bound, 32, 64));
+    float pushed = INFINITY;
+#pragma unroll
+    for (int s = 0; s < CB_L; ++s) {
+      float ck = ok[s];
+      int ci = oi[s];
+#pragma unroll
+      for (int t = 0; t < CB_L; ++t) {
+        const bool sw = ck < bk[t];
+        const float tk = sw ? bk[t] : ck;
+        const int ti = sw ? bi[t] : ci;
+        bk[t] = sw ? ck : bk[t];
+        bi[t] = sw ? ci : bi[t];
+        ck = tk;
+        ci = ti;
+      }
+      pushed = fminf(pushed, ck);
+    }
+    bound = fminf(bound, pushed);
+  }
+  if (!qok || lh) return;
+  float* okp = cand_key + ((int64_t)q * RB + rb) * CB_L;
+  int64_t* oip = cand_id + ((int64_t)q * RB + rb) * CB_L;
 #pragma unroll
   for (int t = 0; t < CB_L; ++t) {
     okp[t] = bk[t];
     oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
   }
-  lane_bound[((int64_t)q * RB + rb) * 2 + lh] = fminf(bk[CB_L - 1], drop);
+  lane_bound[(int64_t)q * RB + rb] = bound;
 }
 
 // Coarse selection: block per query, the CB_C smallest of its n_cand lane-list keys (ids
@@ -1490,9 +1524,11 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     if (coarse_v2()) {
       const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
       const dim3 grid((unsigned)(nqt * RB)), blk((unsigned)(NW * 64));
-#define MPR_BF2(KS_, NW_)                                                                       \
-  hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, 4>), grid, blk, 0, s, xb, xnorm, n, row_offset, \
-                     w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
+      // prefetch depth: 4 stages (4 KiB per thread-slot at 8 waves); 2 at 4 waves, where each
+      // stage is two 16-byte loads per thread (the 256-VGPR budget of 2 blocks per CU)
+#define MPR_BF2(KS_, NW_)                                                                  \
+  hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, NW_ == 8 ? 4 : 2>), grid, blk, 0, s, xb, xnorm, \
+                     n, row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
       if (d == 512) {
         if (NW == 8) MPR_BF2(32, 8); else MPR_BF2(32, 4);
       } else {
@@ -1510,11 +1546,17 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
                            xnorm, n, row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb);
     }
     MPR_LAUNCHED();
-    const int n_cand = RB * 2 * CB_L;
+    const int lpb = coarse_v2() ? 1 : 2;  // candidate lists per (query, block)
+    const int n_cand = RB * lpb * CB_L;
     if (n_cand <= 256 * 16 && !getenv("MPR_COARSE_UNFUSED")) {
-      hipLaunchKernelGGL(coarse_rerank_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck, w.ci,
-                         n_cand, X, xnorm, d, row_offset, Q, w.lb, RB * 2, k, xmax, out_dist,
-                         out_ids, w.gate);
+      if (n_cand <= 256 * 8)
+        hipLaunchKernelGGL(coarse_rerank_kernel<8>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
+                           w.ci, n_cand, X, xnorm, d, row_offset, Q, w.lb, RB * lpb, k, xmax,
+                           out_dist, out_ids, w.gate);
+      else
+        hipLaunchKernelGGL(coarse_rerank_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
+                           w.ci, n_cand, X, xnorm, d, row_offset, Q, w.lb, RB * lpb, k, xmax,
+                           out_dist, out_ids, w.gate);
       MPR_LAUNCHED();
     } else {
       if (n_cand <= 256 * 16)
@@ -1525,7 +1567,7 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
                                w.sk, w.si, s));
       MPR_LAUNCHED();
       hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)b), dim3(256), 0, s, X, xnorm, d,
-                         row_offset, Q, w.sk, w.si, w.lb, RB * 2, k, xmax, out_dist, out_ids,
+                         row_offset, Q, w.sk, w.si, w.lb, RB * lpb, k, xmax, out_dist, out_ids,
                          w.gate);
       MPR_LAUNCHED();
     }
