@@ -249,3 +249,47 @@ def test_coarse_scan_falls_back_on_a_dense_neighbourhood(device):
     ix2 = DeviceIndex(syn.index_rows(34, n, d), device)
     ix2.search(q, k)
     assert 0 <= ix2.coarse_fallbacks() <= 1
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_c2_full_size_end_to_end_vs_oracle(device, k):
+    """Config C2 (C3's k = 3 too) end to end at full size: a 6,500 x 1,024 index, two seeded
+    ViT-B/32 towers + CLIP text, t5-small, batches of 16 with real-algorithm tokenizers and host
+    images — T5VisionModel.predict() and the retrieval prompts on the device against
+    oracle/pipeline.py (torch-CPU fp32 restatement of the reference path, the CPU baseline's
+    code) on the same weights and batches: retrieved prompts and greedy answers equal."""
+    from multimodalpromptretrieval_amd.dataset import VQARetrieval
+    from multimodalpromptretrieval_amd.model import T5VisionModel
+    from multimodalpromptretrieval_amd.tokenization import SpmT5Tokenizer, clip_tokenize
+    from oracle import pipeline
+    N, D, B = 6500, 1024, 16
+    retr_sd, tok_sd, t5_sd = syn.clip_state_dict(1), syn.clip_state_dict(2), syn.t5_state_dict(3)
+    X = syn.index_rows(4, N, D)
+    answers = syn.answers(N, 50)
+    info = {"question_id": [str(j) for j in range(N)], "question_type": ["open"] * N,
+            "question": [""] * N}
+    retr = VQARetrieval(device, clip_state_dict=retr_sd, clip_tokenizer=clip_tokenize)
+    retr.set_index(X, answers, info, k, is_training_phase=False)
+    model = T5VisionModel(device, clip_state_dict=tok_sd, t5_state_dict=t5_sd,
+                          tokenizer=SpmT5Tokenizer(),
+                          retrieval_function=retr.retrieve_closest_qa_pairs).eval()
+    rng = np.random.Generator(np.random.PCG64(77))
+    words = ["what", "is", "the", "organ", "shown", "in", "this", "image", "lung", "left",
+             "abnormal", "scan", "where", "does", "it", "appear", "brain", "chest", "liver"]
+    ref_tok = SpmT5Tokenizer()
+    ref_tok.add_tokens(["[itk]"])
+    for bi in range(2):
+        batch = {"image": syn.images(900 + bi, B),
+                 "question": [" ".join(rng.choice(words, size=int(rng.integers(5, 14)))) + "?"
+                              for _ in range(B)],
+                 "task": ["vqa"] * B, "answer": ["yes"] * B,
+                 "question_id": [str(bi * B + j) for j in range(B)],
+                 "question_type": ["open"] * B}
+        with torch.no_grad():
+            got = model.predict(batch)
+            got_prompts = retr.retrieve_closest_qa_pairs(batch)
+            preds, prompts, _ = pipeline.predict(
+                batch, retr_sd, tok_sd, t5_sd, 8, X, answers, info, k, False, clip_tokenize,
+                ref_tok, 20, forced_steps=True)
+        assert got_prompts == prompts, f"batch {bi}: retrieved prompts differ"
+        assert got == preds, f"batch {bi}: greedy answers differ"
