@@ -872,9 +872,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
       const int64_t row = row0 + r;
       rx[j][i] = *reinterpret_cast<const bf16x8*>(Xb + (row < n ? row : n - 1) * (int64_t)d + c);
     }
-    if (ks == 0) {
+    if (ks == 0) {  // unconditional load (a select on loaded data makes hipcc wait early)
       const int64_t nrow = row0 + (tid & (CB2_RT - 1));
-      rn[j] = nrow < n ? xnorm[nrow] : INFINITY;
+      rn[j] = xnorm[nrow < n ? nrow : n - 1];
     }
   };
   auto swrite = [&](int st, int j, int tt, int ks) {
@@ -883,7 +883,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
       const int idx = tid + i * NT, r = idx / CPR, c = (idx % CPR) * 8;
       *reinterpret_cast<bf16x8*>(&xs[st][r * CB2_LDK + c]) = rx[j][i];
     }
-    if (ks == 0 && tid < CB2_RT) xn_s[tt & 1][tid] = rn[j];
+    if (ks == 0 && tid < CB2_RT) {  // rows past n: infinite keys
+      const int64_t nrow = (int64_t)(rb + (int64_t)tt * RB) * CB2_RT + tid;
+      xn_s[tt & 1][tid] = nrow < n ? rn[j] : INFINITY;
+    }
   };
 
   f32x16 acc[2];
