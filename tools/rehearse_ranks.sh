@@ -6,9 +6,9 @@ set -e
 mkdir -p gpurun_out/rehearse
 run() {  # name, nproc, extra args...
   local name=$1 n=$2; shift 2
-  MPR_DIST_BACKEND=gloo timeout -k 10 170 python -m torch.distributed.run --nnodes=1 \
+  MPR_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n + ${#name})) \
-    bench.py --gpus $n --steps 5 --warmup 2 --no-cpu-baseline --no-probe "$@" \
+    bench.py --gpus $n --steps 5 --warmup 2 --no-cpu-baseline --no-probe --no-eos-leg "$@" \
     > gpurun_out/rehearse/$name.json 2> gpurun_out/rehearse/$name.err
   echo "$name done" >> gpurun_out/rehearse/steps.log
 }

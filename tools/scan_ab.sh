@@ -1,14 +1,15 @@
 #!/bin/bash
-# Coarse-scan A/B on the GPU box: the scan / coarse tests, then the C5 search (1M x 512, 256
-# queries, k = 5) and its 1/8 shard timed with the LDS-query kernel (MPR_COARSE_V1=1) and the
-# register-query kernel, then a rocprofv3 kernel-stats pass of the latter.
+# Coarse-scan A/B on the GPU box: the scan / coarse / merge tests, then the C5 search (1M x 512,
+# 256 queries, k = 5) and its 1/8 shard timed with the LDS-query kernel (MPR_COARSE_V1=1) and the
+# register-query kernel, then a rocprofv3 kernel-stats pass of the latter.  Every GPU step has its
+# own time limit; anything but a clean exit (or plain test failures, rc 1) ends the script.
 # usage: bash tools/scan_ab.sh <tag>
 TAG=${1:-scan}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_configs.py -q -m gpu \
-  -k "scan or coarse or c5" -rf --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1
+timeout -k 10 420 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_configs.py -v -m gpu \
+  -k "scan or coarse or c5 or merge" -rf --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1
 rc=$?; echo "pytest rc=$rc" >> "$OUT/steps.log"; [ $rc -le 1 ] || exit $rc
 for W in 1 8; do
   MPR_COARSE_V1=1 timeout -k 10 120 python tools/scan_c5.py $W >> "$OUT/c5.txt" 2>&1 || exit $?
@@ -17,5 +18,7 @@ done
 echo "c5 done" >> "$OUT/steps.log"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
   -- python tools/scan_c5.py 1 > "$OUT/prof.log" 2>&1 || exit $?
-rm -f "$OUT/prof/run_kernel_trace.csv"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv \
+  -- python tools/scan_c5.py 8 > "$OUT/prof8.log" 2>&1 || exit $?
+rm -f "$OUT"/prof*/run_kernel_trace.csv
 echo done >> "$OUT/steps.log"
