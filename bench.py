@@ -14,7 +14,8 @@ stage of the path, host included.  Weights are seeded random (no checkpoints off
 N > 1: one process per GPU (torch.distributed.run), each with its own batch of 16 (weak
 scaling); C2's 26.6 MB index is replicated per rank (no data-path collective; --index-sharding
 shard row-shards it with one exchange per batch).  The ``c5_scan`` line is the row-sharded 1M x
-512 search (strong scaling, one all_gather of per-shard top-k).
+512 search (strong scaling, one all_gather of per-shard top-k); its ``end_to_end_t5_base`` entry
+is config C5 end to end over the rows/N shards (weak: 256 questions per GPU per batch).
 
 Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel (the split-bf16 MFMA
 GEMM, fp32-accurate): the launches of a pass over the same steps are recorded and replayed back
@@ -632,7 +633,10 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_answers=None):
            "kind": "port",
            "sample": f"{n} batches x {cfg['B']} QA pairs of the same workload ({el:.1f} s), "
                      f"oracle/pipeline.py (torch-CPU fp32, KV-cached greedy, 20 forced steps)",
-           "cpu_model": model, "host_physical_cores": phys, "host_cpus_available": avail}
+           "cpu_model": model, "host_physical_cores": phys, "host_cpus_available": avail,
+           "cores_note": "threads = this job's CPU share on the GPU box (OMP_NUM_THREADS, 16 per "
+                         "GPU: the box's 8 GPUs' jobs share its physical cores; SURVEY.md §8(d) "
+                         "asks for the available cores)"}
     if gpu_answers is not None:
         # forced steps keep finished rows on pad, as the device loop does: the decoded answers
         # compare as strings
