@@ -51,15 +51,15 @@ dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 cfg = bench.CONFIGS["c2"]
 model, _, _ = bench.build(cfg, dev, None)
-batches = bench.make_batches(4, cfg["B"], dev, seed=100)
+batches = bench.make_batches(4, cfg["B"], seed=100)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 with torch.no_grad():
-    for _ in model.predict_many(batches[i % 4] for i in range(8)):
+    for _ in model.predict_many((batches[i % 4] for i in range(8)), eos_stop=False):
         pass
     torch.cuda.synchronize()
     time.sleep(0.05)
     t = time.perf_counter()
-    for _ in model.predict_many(batches[i % 4] for i in range(steps)):
+    for _ in model.predict_many((batches[i % 4] for i in range(steps)), eos_stop=False):
         pass
     torch.cuda.synchronize()
     print(f"{steps} steps: {(time.perf_counter() - t) / steps * 1e3:.3f} ms per step", flush=True)
