@@ -21,4 +21,14 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv \
   -- python tools/scan_c5.py 8 > "$OUT/prof8.log" 2>&1 || exit $?
 rm -f "$OUT"/prof*/run_kernel_trace.csv
+# HBM bytes of the coarse kernel (FETCH_SIZE x 2: the gfx950 half-count of 16-B streaming reads)
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "scan_bf" -d "$OUT/pmc" \
+  -o run --output-format csv -- python tools/scan_c5.py 1 > "$OUT/pmc.log" 2>&1 || exit $?
+python - "$OUT" >> "$OUT/c5.txt" 2>&1 <<'PY'
+import csv, glob, sys
+rows = list(csv.DictReader(open(glob.glob(sys.argv[1] + "/pmc/**/*counter_collection.csv", recursive=True)[0])))
+v = [float(r["Counter_Value"]) for r in rows if r["Counter_Name"].startswith("FETCH_SIZE")]
+print(f"scan_bf FETCH_SIZE: {len(v)} launches, {2 * sum(v) / len(v) * 1024 / 1e6:.1f} MB per launch (FETCH_SIZE KB x 2, gfx950 correction)")
+PY
+rm -f "$OUT"/pmc/*/*counter_collection.csv "$OUT"/pmc/*counter_collection.csv
 echo done >> "$OUT/steps.log"
