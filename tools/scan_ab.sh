@@ -16,6 +16,15 @@ for W in 1 8; do
   timeout -k 10 120 python tools/scan_c5.py $W >> "$OUT/c5.txt" 2>&1 || exit $?
 done
 echo "c5 done" >> "$OUT/steps.log"
+# the LDS-DMA ring variant: its coarse tests first, then timings (ids checksums must equal v2's)
+MPR_COARSE_GLDS=10 timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -v -m gpu \
+  -k "coarse or c5" -rf --timeout 200 --timeout-method thread > "$OUT/pytest_glds.log" 2>&1
+rc=$?; echo "pytest glds rc=$rc" >> "$OUT/steps.log"; [ $rc -le 1 ] || exit $rc
+for R in 6 10 12; do
+  MPR_COARSE_GLDS=$R timeout -k 10 120 python tools/scan_c5.py 1 >> "$OUT/c5.txt" 2>&1 || exit $?
+done
+MPR_COARSE_GLDS=10 timeout -k 10 120 python tools/scan_c5.py 8 >> "$OUT/c5.txt" 2>&1 || exit $?
+echo "glds done" >> "$OUT/steps.log"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
   -- python tools/scan_c5.py 1 > "$OUT/prof.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv \

@@ -24,5 +24,8 @@ for _ in range(10):
     ix.search(q, k)
 e1.record()
 torch.cuda.synchronize()
-print(f"[{"v1" if os.environ.get("MPR_COARSE_V1") else "v2"}] C5 search ({n} rows, {b} queries): {e0.elapsed_time(e1) / 10:.3f} ms, exact fallbacks {ix.coarse_fallbacks()}",
-      flush=True)
+_, ids = ix.search(q, k)
+tag = ("v1" if os.environ.get("MPR_COARSE_V1") else
+       f"glds{os.environ['MPR_COARSE_GLDS']}" if os.environ.get("MPR_COARSE_GLDS") else "v2")
+print(f"[{tag}] C5 search ({n} rows, {b} queries): {e0.elapsed_time(e1) / 10:.3f} ms, "
+      f"exact fallbacks {ix.coarse_fallbacks()}, ids checksum {int(ids.sum())}", flush=True)
