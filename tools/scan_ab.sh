@@ -1,30 +1,24 @@
 #!/bin/bash
-# Coarse-scan A/B on the GPU box: the scan / coarse / merge tests, then the C5 search (1M x 512,
-# 256 queries, k = 5) and its 1/8 shard timed with the LDS-query kernel (MPR_COARSE_V1=1) and the
-# register-query kernel, then a rocprofv3 kernel-stats pass of the latter.  Every GPU step has its
-# own time limit; anything but a clean exit (or plain test failures, rc 1) ends the script.
+# Coarse-scan A/B on the GPU box: the scan / coarse / merge tests (default kernel), then the C5
+# search (1M x 512, 256 queries, k = 5) and its 1/8 shard timed per kernel variant (env settings
+# in VARIANTS; ids checksums must agree), a rocprofv3 kernel-stats pass of the default at W = 1
+# and 8, and a FETCH_SIZE pass of the coarse kernel.  Every GPU step has its own time limit;
+# anything but a clean exit (or plain test failures, rc 1) ends the script.
 # usage: bash tools/scan_ab.sh <tag>
 TAG=${1:-scan}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+VARIANTS=${VARIANTS:-"MPR_COARSE_V1=1 MPR_COARSE_BF2=1 MPR_COARSE_GLDS=10 DEFAULT=1"}
 timeout -k 10 420 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_configs.py -v -m gpu \
   -k "scan or coarse or c5 or merge" -rf --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1
 rc=$?; echo "pytest rc=$rc" >> "$OUT/steps.log"; [ $rc -le 1 ] || exit $rc
 for W in 1 8; do
-  MPR_COARSE_V1=1 timeout -k 10 120 python tools/scan_c5.py $W >> "$OUT/c5.txt" 2>&1 || exit $?
-  timeout -k 10 120 python tools/scan_c5.py $W >> "$OUT/c5.txt" 2>&1 || exit $?
+  for V in $VARIANTS; do
+    env "$V" timeout -k 10 120 python tools/scan_c5.py $W >> "$OUT/c5.txt" 2>&1 || exit $?
+  done
 done
 echo "c5 done" >> "$OUT/steps.log"
-# the LDS-DMA ring variant: its coarse tests first, then timings (ids checksums must equal v2's)
-MPR_COARSE_GLDS=10 timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -v -m gpu \
-  -k "coarse or c5" -rf --timeout 200 --timeout-method thread > "$OUT/pytest_glds.log" 2>&1
-rc=$?; echo "pytest glds rc=$rc" >> "$OUT/steps.log"; [ $rc -le 1 ] || exit $rc
-for R in 6 10 12; do
-  MPR_COARSE_GLDS=$R timeout -k 10 120 python tools/scan_c5.py 1 >> "$OUT/c5.txt" 2>&1 || exit $?
-done
-MPR_COARSE_GLDS=10 timeout -k 10 120 python tools/scan_c5.py 8 >> "$OUT/c5.txt" 2>&1 || exit $?
-echo "glds done" >> "$OUT/steps.log"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
   -- python tools/scan_c5.py 1 > "$OUT/prof.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv \
