@@ -1674,6 +1674,206 @@ __global__ __launch_bounds__(256) void coarse_rerank_kernel(
                out_id, gate);
 }
 
+// Select + re-rank without a full selection (block per query, the one-list-per-block layout of
+// scan_bf2/bf4: n_lists sorted lists of CB_L, n_lists <= 512).  The re-rank only ever needs the
+// candidates whose coarse key is within T = s~(k) + 2E (rerank_block's bound), so:
+//  1. s~(k), the k-th smallest coarse key: each wave walks its lists' sorted heads for k rounds
+//     (wave-shuffle minima, no block barrier), then one wave takes the k-th of the 4 x k winners;
+//  2. |q|, the query's bf16 residual and E as rerank_block; T, Tcut;
+//  3. every entry <= Tcut is gathered (each list's qualifying entries are a prefix; a block scan
+//     places them) — at most CB_C, else the query is flagged for the exact scan;
+//  4. exact fp32 keys of the gathered rows, the best k by (key, id).
+// Sufficient when nothing was cut off: every list's bound > T and the gather did not overflow
+// (a row missing from every list has a key >= its lane's bound).  Same outputs as the select +
+// rerank_block pair whenever both are exact.
+template <int K>
+__global__ __launch_bounds__(256) void coarse_rerank2_kernel(
+    const float* __restrict__ cand_key, const int64_t* __restrict__ cand_id, int n_lists,
+    const float* __restrict__ X, const float* __restrict__ xnorm, int d, int64_t row_offset,
+    const float* __restrict__ Q, const float* __restrict__ lane_bound, int k, const float* xmax,
+    float* out_dist, int64_t* out_id, int* gate) {
+  constexpr int LPT = 2;  // lists per thread (n_lists <= 512)
+  __shared__ float qs[512];
+  __shared__ float wk[4][K];
+  __shared__ float red[3][4];
+  __shared__ int wcount[4];
+  __shared__ float keys[CB_C];
+  __shared__ int64_t ids[CB_C];
+  __shared__ float s_T;
+  const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* ck = cand_key + (int64_t)qi * n_lists * CB_L;
+  const int64_t* ci = cand_id + (int64_t)qi * n_lists * CB_L;
+  // this thread's lists: keys in registers (sorted ascending, +inf padded)
+  float lk[LPT][CB_L];
+  float lb = INFINITY;  // the smallest bound of this thread's lists
+#pragma unroll
+  for (int p = 0; p < LPT; ++p) {
+    const int l = tid + p * 256;
+#pragma unroll
+    for (int t = 0; t < CB_L; ++t) lk[p][t] = l < n_lists ? ck[(int64_t)l * CB_L + t] : INFINITY;
+    if (l < n_lists) lb = fminf(lb, lane_bound[(int64_t)qi * n_lists + l]);
+  }
+  // 1. the wave's k smallest keys: k rounds of "minimum head, its owner advances"
+  {
+    int h0 = 0, h1 = 0;  // heads of the thread's two lists
+    for (int r = 0; r < k; ++r) {
+      float a = h0 < CB_L ? lk[0][0] : INFINITY, b2 = h1 < CB_L ? lk[1][0] : INFINITY;
+      // (static indexing: the head value is rotated to slot 0 as a list advances, below)
+      const float mine = fminf(a, b2);
+      float m = mine;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
+      // the lowest lane holding the minimum advances one list
+      const uint64_t bal = __ballot(mine == m);
+      const int win = __ffsll((unsigned long long)bal) - 1;
+      if (lane == win) {
+        if (a <= b2) {
+#pragma unroll
+          for (int t = 0; t < CB_L - 1; ++t) lk[0][t] = lk[0][t + 1];
+          lk[0][CB_L - 1] = INFINITY;
+          ++h0;
+        } else {
+#pragma unroll
+          for (int t = 0; t < CB_L - 1; ++t) lk[1][t] = lk[1][t + 1];
+          lk[1][CB_L - 1] = INFINITY;
+          ++h1;
+        }
+      }
+      if (lane == 0) wk[wave][r] = m;
+    }
+  }
+  // 2. the query's norms and E (rerank_block's formulas and summation order)
+  const float* qp = Q + (int64_t)qi * d;
+  float ss = 0.f, ee = 0.f;
+  for (int c = tid; c < d; c += 256) {
+    const float v = qp[c];
+    const float r = (float)(__bf16)v - v;
+    qs[c] = v;
+    ss += v * v;
+    ee += r * r;
+  }
+  float lm = lb;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    ss += __shfl_xor(ss, off, 64);
+    ee += __shfl_xor(ee, off, 64);
+    lm = fminf(lm, __shfl_xor(lm, off, 64));
+  }
+  if (lane == 0) {
+    red[0][wave] = ss;
+    red[1][wave] = ee;
+    red[2][wave] = lm;
+  }
+  __syncthreads();
+  const float qn = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  if (wave == 0) {  // k-th smallest of the 4 waves' k smallest: one per lane, k wave minima
+    float v = lane < 4 * k ? wk[lane / k][lane % k] : INFINITY;
+    float kth = INFINITY;
+    for (int r = 0; r < k; ++r) {
+      float m = v;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
+      kth = m;
+      const uint64_t bal = __ballot(v == m);
+      if (lane == __ffsll((unsigned long long)bal) - 1) v = INFINITY;
+    }
+    const float qa = sqrtf(qn), ea = sqrtf((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+    const float Xm = sqrtf(xmax[0]), Rm = sqrtf(xmax[1]);
+    const float E = 2.0f * (ea * Xm + qa * Rm + ea * Rm + 2.0f * d * 5.9604645e-8f * (qa + ea) *
+                                                         (Xm + Rm)) * 1.01f +
+                    4.0f * 5.9604645e-8f * (Xm * Xm + 2.0f * qa * Xm + qa * qa);
+    if (lane == 0) s_T = kth * (1.0f + 3.0517578e-5f) + 2.0f * E;
+  }
+  __syncthreads();
+  const float T = s_T, Tcut = T * (1.0f + 1.5258789e-5f);
+  // 3. gather every entry <= Tcut (reload the lists: the registers were consumed in step 1)
+  int cnt[LPT], mycnt = 0;
+#pragma unroll
+  for (int p = 0; p < LPT; ++p) {
+    const int l = tid + p * 256;
+    cnt[p] = 0;
+    if (l < n_lists)
+#pragma unroll
+      for (int t = 0; t < CB_L; ++t) cnt[p] += ck[(int64_t)l * CB_L + t] <= Tcut ? 1 : 0;
+    mycnt += cnt[p];
+  }
+  int incl = mycnt;  // wave inclusive scan
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) wcount[wave] = incl;
+  for (int c = tid; c < CB_C; c += 256) {
+    keys[c] = INFINITY;
+    ids[c] = INT64_MAX;
+  }
+  __syncthreads();
+  int base = incl - mycnt;
+  for (int w = 0; w < wave; ++w) base += wcount[w];
+  const int total = (wcount[0] + wcount[1]) + (wcount[2] + wcount[3]);
+  // (candidate keys go to LDS as +inf-keyed placeholders first: their exact keys come in step 4)
+  int pos = base;
+#pragma unroll
+  for (int p = 0; p < LPT; ++p) {
+    const int l = tid + p * 256;
+    for (int t = 0; t < cnt[p]; ++t, ++pos)
+      if (pos < CB_C) ids[pos] = ci[(int64_t)l * CB_L + t];
+  }
+  __syncthreads();
+  const int need = min(total, CB_C);
+  // 4. exact keys (rerank_block's loop: 4 candidates per wave at a time, 64 lanes over the row)
+  constexpr int G = 4;
+  for (int c0 = wave * G; c0 < need; c0 += 4 * G) {
+    float xv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (c0 + g >= need) break;  // wave-uniform
+      const int64_t id = ids[c0 + g];
+      const float* xp = X + (id >= 0 ? id - row_offset : 0) * (int64_t)d;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = lane + 64 * j;
+        xv[g][j] = e < d ? xp[e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int c = c0 + g;
+      if (c >= need) break;  // wave-uniform
+      const int64_t id = ids[c];
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = lane + 64 * j;
+        dot += e < d ? qs[e] * xv[g][j] : 0.f;
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) dot += __shfl_xor(dot, off, 64);
+      if (lane == 0) {
+        keys[c] = id >= 0 ? sqrtf(fmaxf(qn + xnorm[id - row_offset] - 2.0f * dot, 0.0f))
+                          : INFINITY;
+        if (id < 0) ids[c] = INT64_MAX;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float lists_bound = fminf(fminf(red[2][0], red[2][1]), fminf(red[2][2], red[2][3]));
+    gate[qi] = (total <= CB_C && lists_bound > T) ? 0 : 1;
+  }
+  if (tid < CB_C) {
+    const float a = keys[tid];
+    const int64_t ia = ids[tid];
+    int rank = 0;
+    for (int c = 0; c < CB_C; ++c) rank += key_less(keys[c], ids[c], a, ia) ? 1 : 0;
+    if (rank < k) {
+      out_dist[(int64_t)qi * k + rank] = ia == INT64_MAX ? NAN : a;
+      out_id[(int64_t)qi * k + rank] = ia == INT64_MAX ? -1 : ia;
+    }
+  }
+}
+
 __global__ void sqnorm_kernel(const float* X, int64_t n, int d, float* out) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -1983,7 +2183,14 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     MPR_LAUNCHED();
     const int lpb = coarse_v2() ? 1 : 2;  // candidate lists per (query, block)
     const int n_cand = RB * lpb * CB_L;
-    if (n_cand <= 256 * 16 && !getenv("MPR_COARSE_UNFUSED")) {
+    static const bool radix = getenv("MPR_COARSE_RADIX") != nullptr;
+    if (lpb == 1 && RB <= 512 && !radix) {
+      // threshold gather over the sorted per-block lists (no full selection)
+      hipLaunchKernelGGL(coarse_rerank2_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
+                         w.ci, RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids,
+                         w.gate);
+      MPR_LAUNCHED();
+    } else if (n_cand <= 256 * 16 && !getenv("MPR_COARSE_UNFUSED")) {
       if (n_cand <= 256 * 8)
         hipLaunchKernelGGL(coarse_rerank_kernel<8>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
                            w.ci, n_cand, X, xnorm, d, row_offset, Q, w.lb, RB * lpb, k, xmax,
