@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 VARIANTS=${VARIANTS:-"MPR_COARSE_BF2=1 MPR_COARSE_RADIX=1 DEFAULT=1"}
 timeout -k 10 420 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_configs.py -v -m gpu \
   -k "scan or coarse or c5 or merge" -rf --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1
-rc=$?; echo "pytest rc=$rc" >> "$OUT/steps.log"; [ $rc -le 1 ] || exit $rc
+rc=$?; echo "pytest rc=$rc" >> "$OUT/steps.log"; [ $rc -eq 0 ] || exit $rc
 for W in 1 8; do
   for V in $VARIANTS; do
     env "$V" timeout -k 10 120 python tools/scan_c5.py $W >> "$OUT/c5.txt" 2>&1 || exit $?
