@@ -1009,401 +1009,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
   lane_bound[(int64_t)q * RB + rb] = bound;
 }
 
-// scan_bf2_kernel with the key epilogue taken off the MFMA pipe's critical path.  In scan_bf2 every
-// wave reaches a 64-row tile's end at the same barrier and then runs ~400 VALU of key work with no
-// MFMA to overlap (measured 337 us per C5 launch against ~125 us of MFMA issue).  Here a tile is
-// 32 rows (one 32x32 accumulator), the tiles alternate between two accumulators, and the keys of
-// tile t are formed right after the MFMAs of tile t+1's first stage are issued: the VALU work
-// co-executes with those MFMAs.  Stages are 32 rows x 128 deep (8 KiB, 272-B LDS rows:
-// ds_read_b128 conflict-free; each row's 256 B read by 16 consecutive lanes), 8 MFMAs per wave per
-// stage as before.  Row tag 5 bits (quantisation < 2^-18, inside the re-rank margin).  Keys, lists,
-// bound and outputs are scan_bf2_kernel's.
-constexpr int CB4_RT = 32;             // index rows per tile (one 32-row MFMA tile)
-constexpr int CB4_BK = 128;            // k per LDS stage (8 x 16-deep MFMA steps)
-constexpr int CB4_LDK = CB4_BK + 8;    // LDS row stride in bf16 (272 B)
-constexpr int CB4_STAGE = CB4_RT * CB4_LDK;
-
-template <int KS, int D>
-__global__ __launch_bounds__(512, 1) void scan_bf4_kernel(const __bf16* __restrict__ Xb,
-                                                          const float* __restrict__ xnorm,
-                                                          int64_t n, int64_t row_offset,
-                                                          const __bf16* __restrict__ Qb, int b,
-                                                          const float* __restrict__ qnorm,
-                                                          int nqt, int RB, float* cand_key,
-                                                          int64_t* cand_id, float* lane_bound) {
-  constexpr int NW = 8, NT = 512, d = KS * 16;
-  constexpr int SPT = d / CB4_BK;       // stages per row tile
-  constexpr int CPR = CB4_BK / 8;       // 16-byte chunks per staged row (16)
-  constexpr int US = CB4_BK / 16;       // MFMA k-steps per stage (8)
-  static_assert(CB4_RT * CPR == NT, "one 16-byte load per thread per stage");
-  static_assert(SPT >= 2 && SPT % D == 0, "stage slots repeat per row tile");
-  __shared__ __attribute__((aligned(16))) __bf16 xs[2][CB4_STAGE];
-  __shared__ float xn_s[2][CB4_RT];
-  int qt, rb;
-  {
-    const int total = gridDim.x, hw = blockIdx.x;
-    const int xcd = hw & 7, slot = hw >> 3, q8 = total >> 3, r8 = total & 7;
-    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-    qt = t % nqt;
-    rb = t / nqt;
-  }
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 31, lh = lane >> 5;
-  const int64_t ntile = (n + CB4_RT - 1) / CB4_RT;
-  const int ntb = (int)((ntile - rb + RB - 1) / RB);
-
-  const int q = qt * NW * 32 + wave * 32 + li;
-  const bool qok = q < b;
-  const float qn_l = qok ? qnorm[q] : 0.f;
-  bf16x8 qf[KS];
-  {
-    const __bf16* qp = Qb + (int64_t)(qok ? q : b - 1) * d + 8 * lh;
-#pragma unroll
-    for (int j = 0; j < KS; ++j) qf[j] = *reinterpret_cast<const bf16x8*>(qp + 16 * j);
-  }
-
-  bf16x8 rx[D];
-  float rn[D];
-  const int lr = tid / CPR, lc = (tid % CPR) * 8;  // this thread's staged row / column
-  auto gload = [&](int j, int tt, int ks) {
-    const int64_t row = (int64_t)(rb + (int64_t)tt * RB) * CB4_RT + lr;
-    rx[j] = *reinterpret_cast<const bf16x8*>(Xb + (row < n ? row : n - 1) * (int64_t)d +
-                                             ks * CB4_BK + lc);
-    if (ks == 0) {  // unconditional load; the past-n mask is applied at the LDS write
-      const int64_t nrow = (int64_t)(rb + (int64_t)tt * RB) * CB4_RT + (tid & (CB4_RT - 1));
-      rn[j] = xnorm[nrow < n ? nrow : n - 1];
-    }
-  };
-  auto swrite = [&](int st, int j, int tt, int ks) {
-    *reinterpret_cast<bf16x8*>(&xs[st][lr * CB4_LDK + lc]) = rx[j];
-    if (ks == 0 && tid < CB4_RT) {
-      const int64_t nrow = (int64_t)(rb + (int64_t)tt * RB) * CB4_RT + tid;
-      xn_s[tt & 1][tid] = nrow < n ? rn[j] : INFINITY;
-    }
-  };
-
-  float bk[CB_L];
-  int bi[CB_L];
-#pragma unroll
-  for (int t = 0; t < CB_L; ++t) {
-    bk[t] = INFINITY;
-    bi[t] = INT_MAX;
-  }
-  float drop = INFINITY;
-  // keys of row tile tt from its accumulator (zeroed for reuse): the lane's best two enter its
-  // list, the third bounds what it dropped (scan_bf_kernel's rule)
-  auto keys = [&](f32x16& acc, int tt) {
-    uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rr = (r & 3) + 8 * (r >> 2) + 4 * lh;
-      const float key = fmaxf(fmaf(-2.0f, acc[r], xn_s[tt & 1][rr]) + qn_l, 0.0f);
-      acc[r] = 0.f;
-      const uint32_t v = (__float_as_uint(key) & ~31u) | (uint32_t)rr;
-      v3 = min(v3, max(v2, v));
-      v2 = min(v2, max(v1, v));
-      v1 = min(v1, v);
-    }
-    drop = fminf(drop, __uint_as_float(v3 & ~31u));
-    auto insert = [&](float ck, int ci) {
-#pragma unroll
-      for (int t = 0; t < CB_L; ++t) {
-        const bool sw = ck < bk[t];
-        const float tk = sw ? bk[t] : ck;
-        const int ti = sw ? bi[t] : ci;
-        bk[t] = sw ? ck : bk[t];
-        bi[t] = sw ? ci : bi[t];
-        ck = tk;
-        ci = ti;
-      }
-    };
-    const int row0 = (rb + tt * RB) * CB4_RT;  // n < 2^31 (checked by the launcher)
-    const float k1 = __uint_as_float(v1 & ~31u), k2 = __uint_as_float(v2 & ~31u);
-    if (k1 < bk[CB_L - 1]) insert(k1, row0 + (int)(v1 & 31u));
-    if (k2 < bk[CB_L - 1]) insert(k2, row0 + (int)(v2 & 31u));
-  };
-
-  f32x16 acc0, acc1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
-
-  // prologue: stage 0 in LDS buffer 0, stages 1..D in flight (stage s >= 1 in slot (s - 1) % D)
-  gload(0, 0, 0);
-  swrite(0, 0, 0, 0);
-#pragma unroll
-  for (int j = 0; j < D; ++j) gload(j, (1 + j) / SPT, (1 + j) % SPT);
-  __syncthreads();
-  // one row tile into `acc`; after its first stage's MFMAs are issued, the keys of the previous
-  // tile (in `prev`) are formed while they run
-  auto tile = [&](int tt, f32x16& acc, f32x16& prev, bool has_prev) {
-#pragma clang loop unroll(full)
-    for (int ks = 0; ks < SPT; ++ks) {
-      const int st = ks & 1;  // SPT even: a tile's first stage is in buffer 0
-#pragma unroll
-      for (int u = 0; u < US; ++u) {
-        const bf16x8 fa =
-            *reinterpret_cast<const bf16x8*>(&xs[st][li * CB4_LDK + 16 * u + 8 * lh]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, qf[ks * US + u], acc, 0, 0, 0);
-      }
-      // fragment reads and MFMAs alternate (at most two fragments live: the 256-VGPR budget)
-#pragma unroll
-      for (int u = 0; u < US; ++u) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-      }
-      if (ks == 0 && has_prev) keys(prev, tt - 1);
-      const int j1 = ks % D;
-      swrite(st ^ 1, j1, tt + (ks + 1) / SPT, (ks + 1) % SPT);
-      gload(j1, tt + (ks + 1 + D) / SPT, (ks + 1 + D) % SPT);
-      __syncthreads();
-    }
-  };
-  // tiles in pairs; an odd count runs one tile past the block's last (its rows are past n:
-  // infinite keys, nothing enters a list)
-  int tt = 0;
-  for (; tt < ntb; tt += 2) {
-    tile(tt, acc0, acc1, tt > 0);
-    tile(tt + 1, acc1, acc0, true);
-  }
-  if (ntb > 0) keys(acc1, tt - 1);
-
-  float bound = fminf(bk[CB_L - 1], drop);
-  {
-    float ok[CB_L];
-    int oi[CB_L];
-#pragma unroll
-    for (int t = 0; t < CB_L; ++t) {
-      ok[t] = __shfl_xor(bk[t], 32, 64);
-      oi[t] = __shfl_xor(bi[t], 32, 64);
-    }
-    bound = fminf(bound, __shfl_xor(bound, 32, 64));
-    float pushed = INFINITY;
-#pragma unroll
-    for (int s = 0; s < CB_L; ++s) {
-      float ck = ok[s];
-      int ci = oi[s];
-#pragma unroll
-      for (int t = 0; t < CB_L; ++t) {
-        const bool sw = ck < bk[t];
-        const float tk = sw ? bk[t] : ck;
-        const int ti = sw ? bi[t] : ci;
-        bk[t] = sw ? ck : bk[t];
-        bi[t] = sw ? ci : bi[t];
-        ck = tk;
-        ci = ti;
-      }
-      pushed = fminf(pushed, ck);
-    }
-    bound = fminf(bound, pushed);
-  }
-  if (!qok || lh) return;
-  float* okp = cand_key + ((int64_t)q * RB + rb) * CB_L;
-  int64_t* oip = cand_id + ((int64_t)q * RB + rb) * CB_L;
-#pragma unroll
-  for (int t = 0; t < CB_L; ++t) {
-    okp[t] = bk[t];
-    oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
-  }
-  lane_bound[(int64_t)q * RB + rb] = bound;
-}
-
-// scan_bf2_kernel with the index streamed by LDS-DMA (`global_load_lds_dwordx4`) into a ring of
-// S stages (8 KiB each), so S - 2 stages are in flight without staging VGPRs (scan_bf2's register
-// prefetch stops at 4: its waves spend 128 VGPRs on queries).  8 waves; per stage each wave DMAs
-// 8 rows x 128 B (one wave-instruction, lane-linear in LDS), with the 16-byte chunk of lane L
-// fetched from chunk (L % 8) ^ ((row >> 1) & 7) of its row: the XOR swizzle on the SOURCE address
-// keeps the A-fragment ds_read_b128 conflict-free on an unpadded 128-B row.  Wave 0 also DMAs the
-// stage's tile row norms (64 x 4 B) into the stage's norm slot.  Per stage: a counted
-// `s_waitcnt vmcnt` retires this wave's DMAs of stage g, one raw s_barrier (no __syncthreads:
-// its implied vmcnt(0) would drain the ring), then the DMA of stage g + S - 1 into the slot read
-// at g - 1, then the MFMAs of stage g.  Keys, lists, bound and outputs are scan_bf2_kernel's.
-constexpr int CB3_STAGE_B = CB2_RT * CB2_BK * 2;  // bytes per ring stage (unpadded 128-B rows)
-
-template <int KS, int S>
-__global__ __launch_bounds__(512, 1) void scan_bf3_kernel(const __bf16* __restrict__ Xb,
-                                                          const float* __restrict__ xnorm,
-                                                          int64_t n, int64_t row_offset,
-                                                          const __bf16* __restrict__ Qb, int b,
-                                                          const float* __restrict__ qnorm,
-                                                          int nqt, int RB, float* cand_key,
-                                                          int64_t* cand_id, float* lane_bound) {
-  constexpr int NW = 8, d = KS * 16, SPT = d / CB2_BK;
-  static_assert(S >= 3 && SPT >= 2, "ring depth");
-  // ONE shared array (a second __shared__ object makes hipcc wait vmcnt(0) before LDS reads):
-  // [S][8 KiB index stage] then [S][64 floats of row norms]
-  __shared__ __attribute__((aligned(16))) char lds[S * CB3_STAGE_B + S * CB2_RT * 4];
-  int qt, rb;
-  {
-    const int total = gridDim.x, hw = blockIdx.x;
-    const int xcd = hw & 7, slot = hw >> 3, q8 = total >> 3, r8 = total & 7;
-    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-    qt = t % nqt;
-    rb = t / nqt;
-  }
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 31, lh = lane >> 5;
-  const int64_t ntile = (n + CB2_RT - 1) / CB2_RT;
-  const int ntb = (int)((ntile - rb + RB - 1) / RB);
-  const int nst = ntb * SPT;  // stages of this block
-
-  const int q = qt * NW * 32 + wave * 32 + li;
-  const bool qok = q < b;
-  const float qn_l = qok ? qnorm[q] : 0.f;
-  bf16x8 qf[KS];
-  {
-    const __bf16* qp = Qb + (int64_t)(qok ? q : b - 1) * d + 8 * lh;
-#pragma unroll
-    for (int j = 0; j < KS; ++j) qf[j] = *reinterpret_cast<const bf16x8*>(qp + 16 * j);
-  }
-  // the queries land before the first DMA: no ordinary load is outstanding beside the ring
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // this lane's DMA piece of a stage: row 8 wave + L / 8 of the tile, 16-byte chunk (L % 8) ^ f
-  const int prow = wave * 8 + (lane >> 3);
-  const int pchunk = (lane & 7) ^ ((prow >> 1) & 7);
-  auto issue = [&](int g) {  // stage g of the block: tile g / SPT, k-stage g % SPT
-    const int tt = g / SPT, ks = g - tt * SPT, slot = g % S;
-    const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB2_RT;
-    const int64_t row = row0 + prow;
-    const __bf16* src = Xb + (row < n ? row : n - 1) * (int64_t)d + ks * CB2_BK + pchunk * 8;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (void*)(lds + slot * CB3_STAGE_B + wave * 1024), 16, 0, 0);
-    if (wave == 0) {  // the tile's 64 row norms (every stage of the tile: a uniform count)
-      const int64_t nrow = row0 + lane;
-      __builtin_amdgcn_global_load_lds((const void*)(xnorm + (nrow < n ? nrow : n - 1)),
-                                       (void*)(lds + S * CB3_STAGE_B + slot * CB2_RT * 4), 4, 0,
-                                       0);
-    }
-  };
-
-  f32x16 acc[2];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[mi][r] = 0.f;
-  float bk[CB_L];
-  int bi[CB_L];
-#pragma unroll
-  for (int t = 0; t < CB_L; ++t) {
-    bk[t] = INFINITY;
-    bi[t] = INT_MAX;
-  }
-  float drop = INFINITY;
-
-  for (int g = 0; g < S - 1; ++g)
-    if (g < nst) issue(g);
-  for (int tt = 0; tt < ntb; ++tt) {
-#pragma clang loop unroll(full)
-    for (int ks = 0; ks < SPT; ++ks) {
-      const int g = tt * SPT + ks, slot = g % S;
-      // retire this wave's DMAs of stage g: after them it issued stages g+1 .. g+S-2 (one
-      // instruction each, two for wave 0), unless the ring is draining at the block's end
-      if (g + S - 2 < nst) {
-        if (wave == 0)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (S - 2)) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S - 2) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();  // every wave's stage g landed; stage g-1 read by all
-      __builtin_amdgcn_sched_barrier(0);
-      if (g + S - 1 < nst) issue(g + S - 1);  // into slot (g - 1) % S
-      const char* sb = lds + slot * CB3_STAGE_B;
-#pragma unroll
-      for (int u = 0; u < CB2_BK / 16; ++u) {
-        bf16x8 fa[2];
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          const int r = mi * 32 + li, c = 2 * u + lh;
-          fa[mi] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-        }
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-          acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi], qf[ks * (CB2_BK / 16) + u],
-                                                            acc[mi], 0, 0, 0);
-      }
-      if (ks == SPT - 1) {  // keys of this row tile (norms from this stage's slot)
-        const float* xn = reinterpret_cast<const float*>(lds + S * CB3_STAGE_B) + slot * CB2_RT;
-        const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB2_RT;
-        uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rr = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const float xv = row0 + rr < n ? xn[rr] : INFINITY;  // rows past n: infinite keys
-            const float key = fmaxf(fmaf(-2.0f, acc[mi][r], xv) + qn_l, 0.0f);
-            acc[mi][r] = 0.f;
-            const uint32_t v = (__float_as_uint(key) & ~63u) | (uint32_t)rr;
-            v3 = min(v3, max(v2, v));
-            v2 = min(v2, max(v1, v));
-            v1 = min(v1, v);
-          }
-        drop = fminf(drop, __uint_as_float(v3 & ~63u));
-        auto insert = [&](float ck, int ci) {
-#pragma unroll
-          for (int t = 0; t < CB_L; ++t) {
-            const bool sw = ck < bk[t];
-            const float tk = sw ? bk[t] : ck;
-            const int ti = sw ? bi[t] : ci;
-            bk[t] = sw ? ck : bk[t];
-            bi[t] = sw ? ci : bi[t];
-            ck = tk;
-            ci = ti;
-          }
-        };
-        const int r0 = (int)row0;  // n < 2^31 (checked by the launcher)
-        const float k1 = __uint_as_float(v1 & ~63u), k2 = __uint_as_float(v2 & ~63u);
-        if (k1 < bk[CB_L - 1]) insert(k1, r0 + (int)(v1 & 63u));
-        if (k2 < bk[CB_L - 1]) insert(k2, r0 + (int)(v2 & 63u));
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block
-  float bound = fminf(bk[CB_L - 1], drop);
-  {
-    float ok[CB_L];
-    int oi[CB_L];
-#pragma unroll
-    for (int t = 0; t < CB_L; ++t) {
-      ok[t] = __shfl_xor(bk[t], 32, 64);
-      oi[t] = __shfl_xor(bi[t], 32, 64);
-    }
-    bound = fminf(bound, __shfl_xor(bound, 32, 64));
-    float pushed = INFINITY;
-#pragma unroll
-    for (int s = 0; s < CB_L; ++s) {
-      float ck = ok[s];
-      int ci = oi[s];
-#pragma unroll
-      for (int t = 0; t < CB_L; ++t) {
-        const bool sw = ck < bk[t];
-        const float tk = sw ? bk[t] : ck;
-        const int ti = sw ? bi[t] : ci;
-        bk[t] = sw ? ck : bk[t];
-        bi[t] = sw ? ci : bi[t];
-        ck = tk;
-        ci = ti;
-      }
-      pushed = fminf(pushed, ck);
-    }
-    bound = fminf(bound, pushed);
-  }
-  if (!qok || lh) return;
-  float* okp = cand_key + ((int64_t)q * RB + rb) * CB_L;
-  int64_t* oip = cand_id + ((int64_t)q * RB + rb) * CB_L;
-#pragma unroll
-  for (int t = 0; t < CB_L; ++t) {
-    okp[t] = bk[t];
-    oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
-  }
-  lane_bound[(int64_t)q * RB + rb] = bound;
-}
-
 // Coarse selection: block per query, the CB_C smallest of its n_cand lane-list keys (ids
 // alongside), sorted by (key, id).  The CB_C-th key is found by a bisection over the keys' order
 // bits (counts by a block reduction), then the <= CB_C keys at or below it are ranked.
@@ -1675,7 +1280,7 @@ __global__ __launch_bounds__(256) void coarse_rerank_kernel(
 }
 
 // Select + re-rank without a full selection (block per query, the one-list-per-block layout of
-// scan_bf2/bf4: n_lists sorted lists of CB_L, n_lists <= 512).  The re-rank only ever needs the
+// scan_bf2: n_lists sorted lists of CB_L, n_lists <= 512).  The re-rank only ever needs the
 // candidates whose coarse key is within T = s~(k) + 2E (rerank_block's bound), so:
 //  1. s~(k), the k-th smallest coarse key: each wave walks its lists' sorted heads for k rounds
 //     (wave-shuffle minima, no block barrier), then one wave takes the k-th of the 4 x k winners;
@@ -1982,24 +1587,10 @@ bool coarse_v2() {
   return v;
 }
 int coarse_waves(int b) { return b <= 128 ? 4 : 8; }
-// 8-wave blocks run scan_bf4_kernel (32-row tiles, overlapped key epilogue) unless MPR_COARSE_BF2
-// asks for scan_bf2_kernel (64-row tiles) or MPR_COARSE_GLDS for the LDS-DMA ring
-int coarse_glds() {
-  static const int ring = [] {
-    const char* e = getenv("MPR_COARSE_GLDS");
-    return e ? atoi(e) : 0;
-  }();
-  return ring;
-}
-bool coarse_bf4(int b) {
-  static const bool off = getenv("MPR_COARSE_BF2") != nullptr;
-  return coarse_v2() && coarse_waves(b) == 8 && coarse_glds() == 0 && !off;
-}
 int coarse_rowblocks(int64_t n, int b) {
   if (coarse_v2()) {
     // one 8-wave block (two at 4 waves) per CU, every lane seeing >= 8 row tiles
-    const int rt = coarse_bf4(b) ? CB4_RT : CB2_RT;
-    const int64_t ntile = (n + rt - 1) / rt;
+    const int64_t ntile = (n + CB2_RT - 1) / CB2_RT;
     const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
     const int64_t per = std::max<int64_t>(1, (NW == 4 ? 512 : 256) / nqt);
     return (int)std::max<int64_t>(1, std::min<int64_t>(per, ntile / 8));
@@ -2133,30 +1724,7 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     MPR_LAUNCHED();
     qn_pre = w.qn;
     const __bf16* xb = reinterpret_cast<const __bf16*>(Xb);
-    const int ring = coarse_glds();  // MPR_COARSE_GLDS=6|10|12: the LDS-DMA ring kernel (A/B)
-    if (coarse_bf4(b)) {
-      const int nqt = (int)cdiv(b, 8 * 32);
-      const dim3 grid((unsigned)(nqt * RB)), blk(512);
-      if (d == 512)
-        hipLaunchKernelGGL((scan_bf4_kernel<32, 2>), grid, blk, 0, s, xb, xnorm, n, row_offset,
-                           w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb);
-      else
-        hipLaunchKernelGGL((scan_bf4_kernel<16, 2>), grid, blk, 0, s, xb, xnorm, n, row_offset,
-                           w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb);
-    } else if (coarse_v2() && ring > 0 && coarse_waves(b) == 8) {
-      const int nqt = (int)cdiv(b, 8 * 32);
-      const dim3 grid((unsigned)(nqt * RB)), blk(512);
-#define MPR_BF3(KS_, S_)                                                                     \
-  hipLaunchKernelGGL((scan_bf3_kernel<KS_, S_>), grid, blk, 0, s, xb, xnorm, n, row_offset, \
-                     w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
-      if (d == 512) {
-        // (S = 8 spills 21 VGPRs under hipcc 7.2; 6, 10 and 12 do not)
-        if (ring <= 6) MPR_BF3(32, 6); else if (ring >= 12) MPR_BF3(32, 12); else MPR_BF3(32, 10);
-      } else {
-        MPR_BF3(16, 8);
-      }
-#undef MPR_BF3
-    } else if (coarse_v2()) {
+    if (coarse_v2()) {
       const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
       const dim3 grid((unsigned)(nqt * RB)), blk((unsigned)(NW * 64));
       // prefetch depth: 4 stages (4 KiB per thread-slot at 8 waves); 2 at 4 waves, where each

@@ -13,5 +13,5 @@ run() {  # name, nproc, extra args...
   echo "$name done" >> gpurun_out/rehearse/steps.log
 }
 run bench_n2 2
-run bench_n4 4
+[ -n "$WITH_N4" ] && run bench_n4 4
 run shard_n2 2 --index-sharding shard --no-c5 --no-index-build
