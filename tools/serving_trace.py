@@ -18,12 +18,14 @@ if len(sys.argv) > 2 and sys.argv[1] == "--report":
     segs = [ts[a:b] for a, b in zip([0] + cuts, cuts + [len(ts)])]
     win = max(segs, key=len)
     t0, t1 = win[0][0], max(e for _, e, _ in win)
-    busy, end = 0, t0
+    busy, end, last = 0, t0, ""
     idle = []
     for s, e, n in win:
         if s > end:
-            idle.append((s - end, (end - t0) / 1e3, n[:60]))
+            idle.append((s - end, (end - t0) / 1e3, n[:60] + "  (after " + last[:50] + ")"))
         busy += max(0, e - max(s, end))
+        if e >= end:
+            last = n
         end = max(end, e)
     print(f"window {(t1 - t0) / 1e6:.2f} ms, {len(win)} kernels, busy {busy / 1e6:.2f} ms "
           f"({busy / (t1 - t0) * 100:.1f} %), idle {sum(g for g, _, _ in idle) / 1e6:.2f} ms")
