@@ -173,11 +173,36 @@ class DeviceT5:
         B, L, _ = embeds.shape
         if B > 16:
             chunks = [(embeds[i:i + 16], mask[i:i + 16]) for i in range(0, B, 16)]
+            groups = [chunks[g:g + 8] for g in range(0, len(chunks), 8)]
             outs = []
-            for g in range(0, len(chunks), 8):
-                outs += self.generate_batches_padded(chunks[g:g + 8], max_new_tokens,
-                                                     decoder_start_token_id, eos_token_id,
-                                                     pad_token_id, slot)
+            if len(groups) == 1 or os.environ.get("MPR_SPLIT_SLOTS", "1") == "0":
+                for grp in groups:
+                    outs += self.generate_batches_padded(grp, max_new_tokens,
+                                                         decoder_start_token_id, eos_token_id,
+                                                         pad_token_id, slot)
+                return torch.cat(outs)
+            # more than 128 rows (config C5's 256 questions): the 128-row decode loops are
+            # latency-bound chains of launches that leave CUs idle, so consecutive loops run on
+            # two workspace slots and streams at once (each loop's rows bit-identical to a call
+            # of its own; the caller's stream waits for both)
+            cur = torch.cuda.current_stream(self.device)
+            sts = [_lib.role_stream(self.device, f"gen:{j}") for j in range(2)]
+            for st in sts:
+                st.wait_stream(cur)
+            for gi, grp in enumerate(groups):
+                st = sts[gi % 2]
+                for e, m in grp:
+                    e.record_stream(st)
+                    m.record_stream(st)
+                with torch.cuda.stream(st):
+                    o = self.generate_batches_padded(grp, max_new_tokens, decoder_start_token_id,
+                                                     eos_token_id, pad_token_id,
+                                                     slot=(slot + gi) % 2)
+                for t in o:
+                    t.record_stream(cur)
+                outs += o
+            for st in sts:
+                cur.wait_stream(st)
             return torch.cat(outs)
         out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
         _lib.call("mpr_t5_generate_slot", self._h, int(slot), _lib.ptr(embeds), _lib.ptr(mask),

@@ -463,6 +463,23 @@ def test_t5_generate_pair_matches_single(device, t5_sd, monkeypatch, graphs):
     assert torch.equal(m.generate_padded(*big, 20).cpu(), want_big)
 
 
+def test_t5_generate_over_128_rows_two_slots(device, t5_sd, monkeypatch):
+    """More than 128 rows (config C5's 256 questions): the 128-row decode loops run on two
+    slots and streams at once; tokens equal the one-slot sequential run bit for bit."""
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    m = DeviceT5(t5_sd, device)
+    A = _t5_batch(t5_sd, 16, 71)
+    emb = torch.cat([A[0]] * 12 + [A[0][:5]])   # 197 rows: loops of 128 + 69
+    emb = emb + 1e-3 * torch.randn(emb.shape, generator=torch.Generator().manual_seed(5))
+    fm = torch.cat([A[1]] * 12 + [A[1][:5]])
+    monkeypatch.setenv("MPR_SPLIT_SLOTS", "0")
+    want = m.generate_padded(emb, fm, 20).cpu()
+    monkeypatch.setenv("MPR_SPLIT_SLOTS", "1")
+    got = m.generate_padded(emb, fm, 20).cpu()
+    assert got.shape == (197, 21)
+    assert torch.equal(got, want)
+
+
 def test_t5_embed_and_loss(device, t5_sd):
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     m = DeviceT5(t5_sd, device)
