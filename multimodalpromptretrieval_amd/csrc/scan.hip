@@ -820,7 +820,7 @@ constexpr int CB2_BK = 64;             // k per LDS stage (4 x 16-deep MFMA step
 constexpr int CB2_LDK = CB2_BK + 8;    // LDS row stride in bf16 (144 B: ds_read_b128 conflict-free)
 constexpr int CB2_STAGE = CB2_RT * CB2_LDK;
 
-template <int KS, int NW, int D>
+template <int KS, int NW, int D, int BK = CB2_BK>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16* __restrict__ Xb,
                                                               const float* __restrict__ xnorm,
                                                               int64_t n, int64_t row_offset,
@@ -829,11 +829,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
                                                               int nqt, int RB, float* cand_key,
                                                               int64_t* cand_id, float* lane_bound) {
   constexpr int d = KS * 16, NT = NW * 64;
-  constexpr int SPT = d / CB2_BK;                   // stages per row tile
-  constexpr int LPS = CB2_RT * CB2_BK / 8 / NT;     // 16-byte loads per thread per stage
-  constexpr int CPR = CB2_BK / 8;                   // 16-byte chunks per staged row
+  constexpr int SPT = d / BK;                       // stages per row tile
+  constexpr int LPS = CB2_RT * BK / 8 / NT;         // 16-byte loads per thread per stage
+  constexpr int CPR = BK / 8;                       // 16-byte chunks per staged row
+  constexpr int LDK = BK + 8;                       // LDS row stride (bf16): conflict-free
+  constexpr int STAGE = CB2_RT * LDK;
   static_assert(LPS >= 1 && SPT % D == 0, "stage slots repeat per row tile");
-  __shared__ __attribute__((aligned(16))) __bf16 xs[2][CB2_STAGE];
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][STAGE];
   __shared__ float xn_s[2][CB2_RT];
   int qt, rb;
   {
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
     const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB2_RT;
 #pragma unroll
     for (int i = 0; i < LPS; ++i) {
-      const int idx = tid + i * NT, r = idx / CPR, c = ks * CB2_BK + (idx % CPR) * 8;
+      const int idx = tid + i * NT, r = idx / CPR, c = ks * BK + (idx % CPR) * 8;
       const int64_t row = row0 + r;
       rx[j][i] = *reinterpret_cast<const bf16x8*>(Xb + (row < n ? row : n - 1) * (int64_t)d + c);
     }
@@ -881,7 +883,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
 #pragma unroll
     for (int i = 0; i < LPS; ++i) {
       const int idx = tid + i * NT, r = idx / CPR, c = (idx % CPR) * 8;
-      *reinterpret_cast<bf16x8*>(&xs[st][r * CB2_LDK + c]) = rx[j][i];
+      *reinterpret_cast<bf16x8*>(&xs[st][r * LDK + c]) = rx[j][i];
     }
     if (ks == 0 && tid < CB2_RT) {  // rows past n: infinite keys
       const int64_t nrow = (int64_t)(rb + (int64_t)tt * RB) * CB2_RT + tid;
@@ -914,15 +916,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
     for (int ks = 0; ks < SPT; ++ks) {
       const int st = ks & 1;  // SPT is even: a tile's first stage is always in buffer 0
 #pragma unroll
-      for (int u = 0; u < CB2_BK / 16; ++u) {
+      for (int u = 0; u < BK / 16; ++u) {
         bf16x8 fa[2];
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
           fa[mi] = *reinterpret_cast<const bf16x8*>(
-              &xs[st][(mi * 32 + li) * CB2_LDK + 16 * u + 8 * lh]);
+              &xs[st][(mi * 32 + li) * LDK + 16 * u + 8 * lh]);
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
-          acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi], qf[ks * (CB2_BK / 16) + u],
+          acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi], qf[ks * (BK / 16) + u],
                                                             acc[mi], 0, 0, 0);
       }
       // stage g+1 (held in slot g % D = ks % D) into the other buffer, then re-arm that slot with
@@ -1729,13 +1731,27 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
       const dim3 grid((unsigned)(nqt * RB)), blk((unsigned)(NW * 64));
       // prefetch depth: 4 stages (4 KiB per thread-slot at 8 waves); 2 at 4 waves, where each
       // stage is two 16-byte loads per thread (the 256-VGPR budget of 2 blocks per CU)
-#define MPR_BF2(KS_, NW_)                                                                  \
-  hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, NW_ == 8 ? 4 : 2>), grid, blk, 0, s, xb, xnorm, \
-                     n, row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
+#define MPR_BF2(KS_, NW_, D_, BK_)                                                          \
+  hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, D_, BK_>), grid, blk, 0, s, xb, xnorm, n,     \
+                     row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
+      // 8 waves: 128-deep stages (16 MFMAs per wave between barriers), 2 stages of two loads
+      // per thread in flight; MPR_COARSE_BK=64 the 64-deep stages with 4 in flight (same bytes)
+      static const bool bk64 = [] {
+        const char* e = getenv("MPR_COARSE_BK");
+        return e && atoi(e) == 64;
+      }();
       if (d == 512) {
-        if (NW == 8) MPR_BF2(32, 8); else MPR_BF2(32, 4);
+        if (NW == 8) {
+          if (bk64) MPR_BF2(32, 8, 4, 64); else MPR_BF2(32, 8, 2, 128);
+        } else {
+          MPR_BF2(32, 4, 2, 64);
+        }
       } else {
-        if (NW == 8) MPR_BF2(16, 8); else MPR_BF2(16, 4);
+        if (NW == 8) {
+          if (bk64) MPR_BF2(16, 8, 4, 64); else MPR_BF2(16, 8, 2, 128);
+        } else {
+          MPR_BF2(16, 4, 2, 64);
+        }
       }
 #undef MPR_BF2
     } else {

@@ -268,7 +268,7 @@ class T5VisionModel(nn.Module):
                 and (enc.width, enc.patch, enc.image_size, enc.layers)
                 == (vit.width, vit.patch, vit.image_size, vit.layers))
 
-    def _prefetch(self, batches, slot: int = 0):
+    def _prefetch(self, batches, slot: int = 0, vit=None):
         """Serving-loop lookahead: with a ``VQARetrieval`` retrieval function, enqueue the
         batches' towers (one pass over 1-2 batches; the token-feature ViT paired with the
         retrieval's when pairable), index scans and top-k copies now
@@ -279,7 +279,7 @@ class T5VisionModel(nn.Module):
         fn = getattr(retr, "prefetch_many", None)
         if fn is None or getattr(retr, "index", None) is None:
             return [None] * len(batches)
-        vit = self._device_vit()
+        vit = vit if vit is not None else self._device_vit()
         other = vit if self.use_image_info and self._pairable(retr, vit) else None
         return fn(batches, other, TOKENS, slot)
 

@@ -43,6 +43,7 @@ class ServingOptions:
     eos_stop: bool = True   # stop a call's decode once every row emitted eos
     stop_chunk: int = 4     # decode steps per chunk (eos_stop)
     stop_ahead: int = 3     # chunks kept queued ahead of the flags read (eos_stop)
+    ahead_passes: int = 1   # tower passes kept enqueued ahead of the batch being prepared
 
     @staticmethod
     def resolve(decodes_in_flight=2, pair_decodes=None, lookahead=None, tower_slots=None,
@@ -72,7 +73,8 @@ class ServingOptions:
                                                      4 // max(1, min(int(tower_batches), 2)))),
                               eos_stop=bool(eos_stop),
                               stop_chunk=max(1, int(env("MPR_EOS_STOP_CHUNK", "4"))),
-                              stop_ahead=max(1, min(16, int(env("MPR_EOS_AHEAD", "3")))))
+                              stop_ahead=max(1, min(16, int(env("MPR_EOS_AHEAD", "3")))),
+                              ahead_passes=max(1, min(3, int(env("MPR_LOOKAHEAD_PASSES", "1")))))
 
 
 class _Call:
@@ -111,6 +113,14 @@ class ServingLoop:
         self.upcoming = deque()  # pulled from the source, images submitted to the uploader
         self.src_done = False
         self.uploader = staging.uploader(model.device)
+        self._hs = None  # (device ViT, device T5), fetched once per decode group (_handles)
+
+    def _handles(self, refresh=False):
+        """The model's device handles.  Each fetch checks every parameter for updates (~0.13 ms
+        of host time); inside one pass of the loop they are fetched once per decode group."""
+        if refresh or self._hs is None:
+            self._hs = (self.m._device_vit(), self.m._device_t5())
+        return self._hs
 
     def _pull(self):
         """The next source batch; the STAGE_AHEAD batches after it already have their images on
@@ -129,7 +139,10 @@ class ServingLoop:
     def _refill(self):
         """Keep the next tower pass enqueued before the host blocks on a retrieval result."""
         per_pass = self.o.tower_batches if self.o.lookahead else 1
-        while not self.exhausted and len(self.ready) < per_pass:
+        # (more than one pass ahead: the passes share the tower workspace on one stream, and
+        # every batch's outputs are tensors of its own)
+        keep = per_pass * (self.o.ahead_passes if self.o.lookahead else 1)
+        while not self.exhausted and len(self.ready) < keep:
             chunk = []
             while len(chunk) < per_pass:
                 b = self._pull()
@@ -145,7 +158,8 @@ class ServingLoop:
                 with torch.cuda.stream(m._s_prep):
                     # a pass on slot s uses text workspaces s .. s + per_pass - 1: passes in
                     # flight together must not share one, so slots step by per_pass
-                    pres = m._prefetch(chunk, (self.passes % self.o.tower_slots) * per_pass)
+                    pres = m._prefetch(chunk, (self.passes % self.o.tower_slots) * per_pass,
+                                       vit=self._handles()[0])
                 self.passes += 1
             else:
                 pres = [None] * len(chunk)
@@ -168,7 +182,7 @@ class ServingLoop:
         if call.items is not None:
             return True
         with torch.cuda.stream(call.stream):
-            done, steps = self.m._device_t5().generate_poll(call.slot, wait)
+            done, steps = self._handles()[1].generate_poll(call.slot, wait)
             if done:
                 call.steps = steps
                 self.steps_run.append(steps)
@@ -193,7 +207,7 @@ class ServingLoop:
             for combined, mask in inputs:
                 combined.record_stream(sg)
                 mask.record_stream(sg)
-            t5 = m._device_t5()
+            t5 = self._handles(refresh=True)[1]
             if self.o.eos_stop:
                 toks = t5.generate_begin(inputs, m.max_new_tokens, slot=slot,
                                          stop_chunk=self.o.stop_chunk, ahead=self.o.stop_ahead)
@@ -255,7 +269,7 @@ class ServingLoop:
             m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
             with torch.cuda.stream(m._s_prep):
                 with torch.no_grad():
-                    combined, mask, _ = m.prepare_input(batch, _pre=pre)
+                    combined, mask, _ = m.prepare_input(batch, _pre=pre, _handles=self._handles())
             self._pump()
             if not self._add((combined, mask)):
                 continue
