@@ -53,6 +53,13 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
   } while (0)
 
 // Owning device buffer (hipMalloc'd).  Grows, never shrinks; not copyable.
+// Bumped by every device buffer (re)allocation: a captured graph bakes buffer addresses in, so
+// one captured at an older generation may point at freed memory and is re-captured.
+inline uint64_t& alloc_generation() {
+  static uint64_t g = 0;
+  return g;
+}
+
 struct DevBuf {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -69,6 +76,7 @@ struct DevBuf {
     if (want <= bytes) return MPR_OK;
     release();
     if (want == 0) return MPR_OK;
+    ++alloc_generation();
     hipError_t e = hipMalloc(&ptr, want);
     if (e != hipSuccess) {
       ptr = nullptr;

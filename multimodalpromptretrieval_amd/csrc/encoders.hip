@@ -10,6 +10,9 @@
 //   ResidualAttentionBlock: x = x + out_proj(MHA(ln_1(x)));  x = x + c_proj(QuickGELU(c_fc(ln_2(x))))
 // Data layout in HBM: activations [B*L, width] fp32 row-major; QKV [B*L, 3*width] with head h
 // of q/k/v at columns h*64, width + h*64, 2*width + h*64 (nn.MultiheadAttention in_proj order).
+#include <map>
+#include <vector>
+
 #include "models.h"
 
 namespace mpr {
@@ -176,7 +179,8 @@ int encode_towers(VitModel* const* v, const int* modes, float* const* outs,
                              &out_t, &out_t_bs, s, slot);
 }
 
-int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs,
+namespace {
+int encode_towers_eager(VitModel* const* v, const int* modes, float* const* outs,
                         const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
                         int nt, const int32_t* const* toks, const int* Bts, const int* Lts,
                         float* const* out_ts, const int64_t* out_t_bss, hipStream_t s,
@@ -297,6 +301,130 @@ int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs
     pj.N = tm->out_dim; pj.K = W; pj.C = out_t[j]; pj.ldc = out_t_bs[j];
   }
   MPR_TRY(gemm_group(pg, s));
+  return MPR_OK;
+}
+
+// A tower pass launches ~200 kernels (two ViTs and the text tower, 12 blocks each): ~1 ms of
+// host time per pass, which a serving loop feeding the GPU from one host thread cannot spare.
+// With MPR_TOWER_GRAPHS=1 the pass is captured once per shape into a hipGraph over staged
+// inputs and outputs (library-owned buffers: the images, the token ids and the outputs are
+// copied in and out around the replay, device to device) and replayed with one launch.  The
+// same kernels with the same arguments run: outputs are bit-identical to the eager pass.  Not
+// while a GEMM probe records launches (the bench roofline), not for the batches of the first
+// sighting of a shape (run eagerly, which also sizes every workspace before the capture).
+struct TowerGraph {
+  hipGraphExec_t exec;
+  uint64_t gen;
+};
+std::map<std::vector<int64_t>, TowerGraph> g_tower_graphs;
+hipStream_t g_tower_cap = nullptr;
+constexpr size_t MAX_TOWER_GRAPHS = 64;
+
+bool tower_graphs_on() {
+  const char* e = getenv("MPR_TOWER_GRAPHS");
+  return e && e[0] == '1' && probe_kind() == 0;
+}
+}  // namespace
+
+int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs,
+                        const int64_t* out_bs, int nv, const float* img, int B, TextModel* tm,
+                        int nt, const int32_t* const* toks, const int* Bts, const int* Lts,
+                        float* const* out_ts, const int64_t* out_t_bss, hipStream_t s,
+                        int slot) {
+  if (!tower_graphs_on() || nv < 0 || nv > 2 || nt < 0 || nt > MAX_TEXT_RUNS || slot < 0 ||
+      slot >= TOWER_SLOTS || (nv > 0 && B == 0))
+    return encode_towers_eager(v, modes, outs, out_bs, nv, img, B, tm, nt, toks, Bts, Lts, out_ts,
+                               out_t_bss, s, slot);
+  // the staged operands: images and outputs in ViT 0's / each model's workspace of this slot,
+  // every text run's tokens and output in the text workspace of its slot (as the eager pass)
+  const int ctx = tm ? tm->ctx : 0;
+  std::vector<int64_t> key = {nv, B, nt, slot, (int64_t)(intptr_t)tm};
+  for (int i = 0; i < nv; ++i) {
+    key.push_back((int64_t)(intptr_t)v[i]);
+    key.push_back(modes[i]);
+  }
+  for (int j = 0; j < nt; ++j) {
+    key.push_back(Bts[j]);
+    key.push_back(Lts[j]);
+  }
+  const float* s_img = img;
+  float* s_out[2] = {nullptr, nullptr};
+  int64_t s_bs[2] = {0, 0};
+  const int32_t* s_tok[MAX_TEXT_RUNS];
+  float* s_outt[MAX_TEXT_RUNS];
+  int64_t s_tbs[MAX_TEXT_RUNS];
+  if (nv > 0) {
+    VitModel& a0 = *v[0];
+    const size_t img_elems = (size_t)B * 3 * a0.image * a0.image;
+    MPR_TRY(a0.ws[slot].img_in.ensure(img_elems * 4));
+    s_img = a0.ws[slot].img_in.as<float>();
+    for (int i = 0; i < nv; ++i) {
+      const int T = v[i]->grid * v[i]->grid + 1;
+      s_bs[i] = modes[i] == 0 ? v[i]->out_dim : (int64_t)T * v[i]->out_dim;
+      MPR_TRY(v[i]->ws[slot].out_st.ensure((size_t)B * s_bs[i] * 4));
+      s_out[i] = v[i]->ws[slot].out_st.as<float>();
+    }
+  }
+  for (int j = 0; j < nt; ++j) {
+    TowerWs& w = tm->ws[(slot + j) % TOWER_SLOTS];
+    MPR_TRY(w.tok_in.ensure((size_t)std::max(Bts[j], 1) * ctx * 4));
+    MPR_TRY(w.out_st.ensure((size_t)std::max(Bts[j], 1) * tm->out_dim * 4));
+    s_tok[j] = w.tok_in.as<int32_t>();
+    s_outt[j] = w.out_st.as<float>();
+    s_tbs[j] = tm->out_dim;
+  }
+  auto body = [&](hipStream_t c) {
+    return encode_towers_eager(v, modes, s_out, s_bs, nv, s_img, B, tm, nt, s_tok, Bts, Lts,
+                               s_outt, s_tbs, c, slot);
+  };
+  // stage the inputs
+  if (nv > 0)
+    MPR_HIP(hipMemcpyAsync(const_cast<float*>(s_img), img,
+                           (size_t)B * 3 * v[0]->image * v[0]->image * 4,
+                           hipMemcpyDeviceToDevice, s));
+  for (int j = 0; j < nt; ++j)
+    if (Bts[j] > 0)
+      MPR_HIP(hipMemcpyAsync(const_cast<int32_t*>(s_tok[j]), toks[j],
+                             (size_t)Bts[j] * ctx * 4, hipMemcpyDeviceToDevice, s));
+  auto it = g_tower_graphs.find(key);
+  if (it != g_tower_graphs.end() && it->second.gen != alloc_generation()) {
+    (void)hipGraphExecDestroy(it->second.exec);
+    g_tower_graphs.erase(it);
+    it = g_tower_graphs.end();
+  }
+  if (it != g_tower_graphs.end()) {
+    MPR_HIP(hipGraphLaunch(it->second.exec, s));
+  } else {
+    // first sighting of this shape: run eagerly (sizes every workspace), then capture
+    MPR_TRY(body(s));
+    if (g_tower_graphs.size() >= MAX_TOWER_GRAPHS) {
+      for (auto& kv : g_tower_graphs) (void)hipGraphExecDestroy(kv.second.exec);
+      g_tower_graphs.clear();
+    }
+    if (!g_tower_cap) MPR_HIP(hipStreamCreateWithFlags(&g_tower_cap, hipStreamNonBlocking));
+    const uint64_t gen = alloc_generation();
+    hipGraph_t graph = nullptr;
+    MPR_HIP(hipStreamBeginCapture(g_tower_cap, hipStreamCaptureModeThreadLocal));
+    const int rc = body(g_tower_cap);
+    const hipError_t ec = hipStreamEndCapture(g_tower_cap, &graph);
+    if (rc != MPR_OK || ec != hipSuccess || alloc_generation() != gen) {
+      if (graph) (void)hipGraphDestroy(graph);  // not cached: the eager run already computed
+    } else {
+      hipGraphExec_t exec = nullptr;
+      const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      if (ei == hipSuccess) g_tower_graphs.emplace(key, TowerGraph{exec, gen});
+    }
+  }
+  // copy the outputs out to the caller's strided rows
+  for (int i = 0; i < nv; ++i)
+    MPR_HIP(hipMemcpy2DAsync(outs[i], (size_t)out_bs[i] * 4, s_out[i], (size_t)s_bs[i] * 4,
+                             (size_t)s_bs[i] * 4, B, hipMemcpyDeviceToDevice, s));
+  for (int j = 0; j < nt; ++j)
+    if (Bts[j] > 0)
+      MPR_HIP(hipMemcpy2DAsync(out_ts[j], (size_t)out_t_bss[j] * 4, s_outt[j],
+                               (size_t)s_tbs[j] * 4, (size_t)tm->out_dim * 4, Bts[j],
+                               hipMemcpyDeviceToDevice, s));
   return MPR_OK;
 }
 

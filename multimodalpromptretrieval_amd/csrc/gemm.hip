@@ -987,6 +987,8 @@ int probed(int kind, double flops, double bytes, hipStream_t s, F&& launch) {
 
 }  // namespace
 
+int probe_kind() { return g_probe_kind; }
+
 int probe_enable(int kind) {
   g_probe_kind = kind;
   return MPR_OK;

@@ -78,6 +78,7 @@ int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 // Kernel probe (bench roofline): hipEvent pairs around every launch of one GEMM kind.
 enum ProbeKind : int { PROBE_OFF = 0, PROBE_GEMM = 1, PROBE_SKINNY = 2, PROBE_RECORD = 3 };
 int probe_enable(int kind);
+int probe_kind();  // the probed GEMM kind (0: off)
 int probe_read(double* ms, int64_t* launches, double* flops, double* bytes);
 // Re-launch the tiled-GEMM groups recorded under PROBE_RECORD back to back on one stream
 // (outputs to a scratch buffer), hipEvents around each; marker kernels bracket the replay.

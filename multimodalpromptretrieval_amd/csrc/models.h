@@ -43,6 +43,7 @@ struct TowerWs {
   DevBuf h, qkv, ao, mlp;             // transformer layer activations
   DevBuf cols, patches, x, tmp, pooled;  // ViT im2col / patch embeddings / residual stream;
                                          // text residual stream / pooled EOT rows
+  DevBuf img_in, tok_in, out_st;         // graph-captured passes: staged inputs and outputs
 };
 
 struct ClipTower;

@@ -250,6 +250,43 @@ def test_encode_towers_multi_matches_per_batch(device, clip_sd):
                             tokens=[toks[0], toks[1][:5]])
 
 
+def test_tower_graphs_match_eager(device, clip_sd, monkeypatch):
+    """MPR_TOWER_GRAPHS=1: a tower pass captured into a hipGraph over staged inputs / outputs
+    (first sighting eager + capture, then replays) gives the eager pass's outputs bit for bit,
+    for strided outputs (the retrieval's [img | txt] query rows) and a new shape."""
+    from multimodalpromptretrieval_amd.encoders import (CLS, TOKENS, DeviceCLIPText, DeviceViT,
+                                                         encode_towers_multi)
+    a, b = DeviceViT(clip_sd, device), DeviceViT(syn.clip_state_dict(14), device)
+    txt = DeviceCLIPText(clip_sd, device)
+    imgs = torch.cat([syn.images(70, 8), syn.images(71, 8)]).to(device)
+    toks = [syn.clip_tokens(72, 8), syn.clip_tokens(73, 8)]
+
+    def run():
+        q = torch.full((16, 1024), float("nan"), device=device)
+        _, tb, _ = encode_towers_multi(a, imgs, CLS, out_a=q, out_a_bstride=1024, vit_b=b,
+                                       mode_b=TOKENS, text=txt, tokens=toks,
+                                       out_t=[q[:8, 512:], q[8:, 512:]],
+                                       out_t_bstride=[1024, 1024])
+        torch.cuda.synchronize()
+        return q.cpu(), tb.cpu()
+
+    monkeypatch.delenv("MPR_TOWER_GRAPHS", raising=False)
+    want_q, want_t = run()
+    monkeypatch.setenv("MPR_TOWER_GRAPHS", "1")
+    for _ in range(3):  # eager + capture, then graph replays
+        q, t = run()
+        assert torch.equal(q, want_q) and torch.equal(t, want_t)
+    toks[1] = toks[1].clone()
+    toks[1][:, 5:] = 0
+    toks[1][:, 4] = int(toks[0].max())       # a shorter text run: a new shape
+    monkeypatch.delenv("MPR_TOWER_GRAPHS", raising=False)
+    want_q, want_t = run()
+    monkeypatch.setenv("MPR_TOWER_GRAPHS", "1")
+    for _ in range(2):
+        q, t = run()
+        assert torch.equal(q, want_q) and torch.equal(t, want_t)
+
+
 def test_encode_towers_slots_run_concurrently(device, clip_sd):
     """Two batches' lockstep passes on workspace slots 0 and 1 on two streams at once (repeated,
     so the passes overlap): each equals its pass run alone, bit for bit."""
