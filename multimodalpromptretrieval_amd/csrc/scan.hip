@@ -817,8 +817,6 @@ __global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restric
 // so select / re-rank / fallback are unchanged.
 constexpr int CB2_RT = 64;             // index rows per tile (2 x 32-row MFMA tiles)
 constexpr int CB2_BK = 64;             // k per LDS stage (4 x 16-deep MFMA steps)
-constexpr int CB2_LDK = CB2_BK + 8;    // LDS row stride in bf16 (144 B: ds_read_b128 conflict-free)
-constexpr int CB2_STAGE = CB2_RT * CB2_LDK;
 
 template <int KS, int NW, int D, int BK = CB2_BK>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16* __restrict__ Xb,
@@ -1734,11 +1732,11 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
 #define MPR_BF2(KS_, NW_, D_, BK_)                                                          \
   hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, D_, BK_>), grid, blk, 0, s, xb, xnorm, n,     \
                      row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
-      // 8 waves: 128-deep stages (16 MFMAs per wave between barriers), 2 stages of two loads
-      // per thread in flight; MPR_COARSE_BK=64 the 64-deep stages with 4 in flight (same bytes)
+      // 8 waves: 64-deep stages, 4 in flight; MPR_COARSE_BK=128: 128-deep stages (16 MFMAs per
+      // wave between barriers) with 2 of two loads per thread in flight (the same bytes)
       static const bool bk64 = [] {
         const char* e = getenv("MPR_COARSE_BK");
-        return e && atoi(e) == 64;
+        return !(e && atoi(e) == 128);
       }();
       if (d == 512) {
         if (NW == 8) {
