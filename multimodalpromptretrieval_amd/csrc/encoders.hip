@@ -332,7 +332,7 @@ int encode_towers_multi(VitModel* const* v, const int* modes, float* const* outs
                         float* const* out_ts, const int64_t* out_t_bss, hipStream_t s,
                         int slot) {
   if (!tower_graphs_on() || nv < 0 || nv > 2 || nt < 0 || nt > MAX_TEXT_RUNS || slot < 0 ||
-      slot >= TOWER_SLOTS || (nv > 0 && B == 0))
+      slot >= TOWER_SLOTS || (nv > 0 && B == 0) || (nt > 0 && !tm))  // (errors: the eager path)
     return encode_towers_eager(v, modes, outs, out_bs, nv, img, B, tm, nt, toks, Bts, Lts, out_ts,
                                out_t_bss, s, slot);
   // the staged operands: images and outputs in ViT 0's / each model's workspace of this slot,
