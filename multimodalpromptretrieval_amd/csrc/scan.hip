@@ -1308,16 +1308,42 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* ck = cand_key + (int64_t)qi * n_lists * CB_L;
   const int64_t* ci = cand_id + (int64_t)qi * n_lists * CB_L;
-  // this thread's lists: keys in registers (sorted ascending, +inf padded)
-  float lk[LPT][CB_L];
+  // Every global operand needed before the exact keys is loaded up front (this thread's lists'
+  // keys and ids, their bounds, the query, xmax), so the block waits on memory twice — these,
+  // then the gathered rows — instead of once per step.
+  static_assert(CB_L == 8, "two float4 per list");
+  float lk[LPT][CB_L], lkc[LPT][CB_L];
+  int64_t lid[LPT][CB_L];
   float lb = INFINITY;  // the smallest bound of this thread's lists
 #pragma unroll
   for (int p = 0; p < LPT; ++p) {
     const int l = tid + p * 256;
+    if (l < n_lists) {
+      const f32x4* k4 = reinterpret_cast<const f32x4*>(ck + (int64_t)l * CB_L);
+      const f32x4 k0 = k4[0], k1 = k4[1];
 #pragma unroll
-    for (int t = 0; t < CB_L; ++t) lk[p][t] = l < n_lists ? ck[(int64_t)l * CB_L + t] : INFINITY;
-    if (l < n_lists) lb = fminf(lb, lane_bound[(int64_t)qi * n_lists + l]);
+      for (int t = 0; t < 4; ++t) {
+        lk[p][t] = k0[t];
+        lk[p][4 + t] = k1[t];
+      }
+#pragma unroll
+      for (int t = 0; t < CB_L; ++t) lid[p][t] = ci[(int64_t)l * CB_L + t];
+      lb = fminf(lb, lane_bound[(int64_t)qi * n_lists + l]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < CB_L; ++t) {
+        lk[p][t] = INFINITY;
+        lid[p][t] = -1;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < CB_L; ++t) lkc[p][t] = lk[p][t];
   }
+  const float* qp = Q + (int64_t)qi * d;
+  float qv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) qv[j] = tid + 256 * j < d ? qp[tid + 256 * j] : 0.f;
+  const float xm0 = xmax[0], xm1 = xmax[1];
   // 1. the wave's k smallest keys: k rounds of "minimum head, its owner advances"
   {
     int h0 = 0, h1 = 0;  // heads of the thread's two lists
@@ -1348,14 +1374,17 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
     }
   }
   // 2. the query's norms and E (rerank_block's formulas and summation order)
-  const float* qp = Q + (int64_t)qi * d;
   float ss = 0.f, ee = 0.f;
-  for (int c = tid; c < d; c += 256) {
-    const float v = qp[c];
-    const float r = (float)(__bf16)v - v;
-    qs[c] = v;
-    ss += v * v;
-    ee += r * r;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = tid + 256 * j;
+    if (c < d) {
+      const float v = qv[j];
+      const float r = (float)(__bf16)v - v;
+      qs[c] = v;
+      ss += v * v;
+      ee += r * r;
+    }
   }
   float lm = lb;
 #pragma unroll
@@ -1383,7 +1412,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
       if (lane == __ffsll((unsigned long long)bal) - 1) v = INFINITY;
     }
     const float qa = sqrtf(qn), ea = sqrtf((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
-    const float Xm = sqrtf(xmax[0]), Rm = sqrtf(xmax[1]);
+    const float Xm = sqrtf(xm0), Rm = sqrtf(xm1);
     const float E = 2.0f * (ea * Xm + qa * Rm + ea * Rm + 2.0f * d * 5.9604645e-8f * (qa + ea) *
                                                          (Xm + Rm)) * 1.01f +
                     4.0f * 5.9604645e-8f * (Xm * Xm + 2.0f * qa * Xm + qa * qa);
@@ -1391,7 +1420,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   }
   __syncthreads();
   const float T = s_T, Tcut = T * (1.0f + 1.5258789e-5f);
-  // 3. gather every entry <= Tcut (reload the lists: the registers were consumed in step 1)
+  // 3. gather every entry <= Tcut (from the kept copy of the lists: step 1 consumed lk)
   int cnt[LPT], mycnt = 0;
 #pragma unroll
   for (int p = 0; p < LPT; ++p) {
@@ -1399,7 +1428,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
     cnt[p] = 0;
     if (l < n_lists)
 #pragma unroll
-      for (int t = 0; t < CB_L; ++t) cnt[p] += ck[(int64_t)l * CB_L + t] <= Tcut ? 1 : 0;
+      for (int t = 0; t < CB_L; ++t) cnt[p] += lkc[p][t] <= Tcut ? 1 : 0;
     mycnt += cnt[p];
   }
   int incl = mycnt;  // wave inclusive scan
@@ -1417,25 +1446,30 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   int base = incl - mycnt;
   for (int w = 0; w < wave; ++w) base += wcount[w];
   const int total = (wcount[0] + wcount[1]) + (wcount[2] + wcount[3]);
-  // (candidate keys go to LDS as +inf-keyed placeholders first: their exact keys come in step 4)
+  // (candidate keys go to LDS as +inf-keyed placeholders first: their exact keys come in step 4;
+  // a list's qualifying entries are a prefix, so static register indices suffice)
   int pos = base;
 #pragma unroll
   for (int p = 0; p < LPT; ++p) {
-    const int l = tid + p * 256;
-    for (int t = 0; t < cnt[p]; ++t, ++pos)
-      if (pos < CB_C) ids[pos] = ci[(int64_t)l * CB_L + t];
+#pragma unroll
+    for (int t = 0; t < CB_L; ++t)
+      if (t < cnt[p] && pos + t < CB_C) ids[pos + t] = lid[p][t];
+    pos += cnt[p];
   }
   __syncthreads();
   const int need = min(total, CB_C);
-  // 4. exact keys (rerank_block's loop: 4 candidates per wave at a time, 64 lanes over the row)
-  constexpr int G = 4;
+  // 4. exact keys (rerank_block's summation: 64 lanes over the row), 8 candidates per wave with
+  // their rows and norms loaded together: one memory round trip for up to 32 candidates
+  constexpr int G = 8;
   for (int c0 = wave * G; c0 < need; c0 += 4 * G) {
-    float xv[G][8];
+    float xv[G][8], xn[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (c0 + g >= need) break;  // wave-uniform
       const int64_t id = ids[c0 + g];
-      const float* xp = X + (id >= 0 ? id - row_offset : 0) * (int64_t)d;
+      const int64_t r = id >= 0 ? id - row_offset : 0;
+      const float* xp = X + r * (int64_t)d;
+      xn[g] = xnorm[r];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int e = lane + 64 * j;
@@ -1456,8 +1490,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) dot += __shfl_xor(dot, off, 64);
       if (lane == 0) {
-        keys[c] = id >= 0 ? sqrtf(fmaxf(qn + xnorm[id - row_offset] - 2.0f * dot, 0.0f))
-                          : INFINITY;
+        keys[c] = id >= 0 ? sqrtf(fmaxf(qn + xn[g] - 2.0f * dot, 0.0f)) : INFINITY;
         if (id < 0) ids[c] = INT64_MAX;
       }
     }
