@@ -167,6 +167,10 @@ int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hip
 // tokens[b*tok_ld + col] = next; unfinished[b] &= next != eos;
 // x[b, :] = table[next, :] (decoder input embedding of the next step, may be null).
 // (x: the next step's input rows, row stride x_ld)
+// Row argmax of logits [M, N] (row stride ld) in P parts per row: pv/pi[row * P + part], the
+// part's largest value and its lowest column (greedy_step's partials layout).
+int argmax_parts(const float* L, int64_t ld, int M, int N, int P, float* pv, int32_t* pi,
+                 hipStream_t s);
 int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int M,
                 int32_t* unfinished, int32_t* tokens, int64_t tok_ld, int col, int eos, int pad,
                 const float* table, int D, float* x, hipStream_t s, int64_t x_ld = -1);

@@ -336,6 +336,111 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
   }
 }
 
+// attention_decode_kernel's arithmetic for many (batch, head) pairs with few keys (Lk <= 128,
+// grouped decodes of 64-128 rows): one wave per pair, 4 pairs per block, no block barrier.  Lane
+// i scores keys i and 64 + i with the same expression; the softmax max / sum and the P.V partials
+// combine in the block kernel's order (its waves 2-3, and waves / key groups past Lk, contribute
+// exact zeros), so outputs are bit-identical to attention_decode_kernel's.  The block kernel
+// issues 48 clamped 16-byte loads per thread for every key slot of its 256 whatever Lk: at 128
+// rows x 12 heads that load issue, not the bytes, was its 13.6 us.
+__global__ __launch_bounds__(256) void attention_decode_wave_kernel(AttnArgs a) {
+  __shared__ float Ps[4][128];
+  __shared__ __attribute__((aligned(16))) float Os[4][8][ATT_D];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pr = blockIdx.x * 4 + wave;
+  if (pr >= a.B * a.H) return;  // wave-uniform; no block barrier below
+  const int b = pr / a.H, h = pr % a.H;
+  const float* qp = a.q + (int64_t)b * a.q_bs + h * ATT_D;
+  const int qpos = a.q_pos0;
+  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
+  const float* kb = a.k + (int64_t)b * a.k_bs + h * ATT_D;
+  const float* vb = a.v + (int64_t)b * a.v_bs + h * ATT_D;
+  int lk_end = a.Lk;
+  if (a.causal) lk_end = min(lk_end, qpos + 1);
+  const bool two = lk_end > 64;  // wave-uniform
+  float qscale = a.scale, qpart = 0.f;
+  if (a.q_rms_part && lane < a.q_rms_nparts) qpart = a.q_rms_part[(int64_t)b * a.q_rms_nparts + lane];
+  // scores of keys lane and 64 + lane (clamped rows / words as the block kernel's)
+  f32x4 qv[ATT_D / 4], kr[2][ATT_D / 4];
+  float mraw[2], braw[2];
+#pragma unroll
+  for (int d = 0; d < ATT_D / 4; ++d) qv[d] = *reinterpret_cast<const f32x4*>(qp + 4 * d);
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf == 1 && !two) break;
+    const int j = hf * 64 + lane;
+    const int jc = j < lk_end ? j : 0;
+    const float* kp = kb + (int64_t)jc * a.k_rs;
+#pragma unroll
+    for (int d = 0; d < ATT_D / 4; ++d) kr[hf][d] = *reinterpret_cast<const f32x4*>(kp + 4 * d);
+    const float* mp = maskb ? maskb + jc : kp;
+    const float* bp = a.rel_tab ? a.rel_tab + (int64_t)(jc - qpos + a.lut_radius) * a.H + h : kp;
+    mraw[hf] = *mp;
+    braw[hf] = *bp;
+  }
+  if (a.q_rms_part)
+    qscale = a.scale * (1.0f / sqrtf(wave_sum(qpart) / (float)a.q_rms_n + a.q_rms_eps));
+  float sc[2] = {-INFINITY, -INFINITY};
+  bool valid[2] = {false, false};
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf == 1 && !two) break;
+    const int j = hf * 64 + lane;
+    const float mk = maskb ? mraw[hf] : 1.f, rb = a.rel_tab ? braw[hf] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < ATT_D / 4; ++d)
+      s += qv[d][0] * kr[hf][d][0] + qv[d][1] * kr[hf][d][1] + qv[d][2] * kr[hf][d][2] +
+           qv[d][3] * kr[hf][d][3];
+    valid[hf] = j < lk_end && mk != 0.f;
+    sc[hf] = valid[hf] ? s * qscale + rb : -INFINITY;
+  }
+  const float mnew = fmaxf(wave_max(sc[0]), wave_max(sc[1]));
+  float p[2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) p[hf] = valid[hf] ? expf(sc[hf] - mnew) : 0.f;
+  // the block kernel: l = 0 * alpha + ((w0 + w1) + (w2 + w3)), waves 2-3 (and 1 when Lk <= 64)
+  // summing zeros
+  const float l = (wave_sum(p[0]) + wave_sum(p[1])) + (0.f + 0.f);
+  Ps[wave][lane] = p[0];
+  Ps[wave][64 + lane] = p[1];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // P.V: lane (dg, kq) sums dims 4 dg .. +3 over key group kq (and 4 + kq), 16 keys each, as the
+  // block kernel's thread (dg, kg) does (o starts at 0 * alpha = 0)
+  const int dg = lane & 15, kq = lane >> 4;
+  f32x4 vr[2][16];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf == 1 && !two) break;
+    const int jv0 = (hf * 4 + kq) * 16;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int jv = jv0 + u < lk_end ? jv0 + u : 0;
+      vr[hf][u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)jv * a.v_rs + 4 * dg);
+    }
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf == 1 && !two) break;
+    const int g = hf * 4 + kq;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 16; ++u) o += Ps[wave][g * 16 + u] * vr[hf][u];
+    *reinterpret_cast<f32x4*>(&Os[wave][g][4 * dg]) = o;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the block kernel's sum over its 16 key groups in order (groups past Lk add exact zeros)
+  float acc = 0.f;
+  const int ng = two ? 8 : 4;
+  for (int g = 0; g < ng; ++g) acc += Os[wave][g][lane];
+  a.o[(int64_t)b * a.o_bs + h * ATT_D + lane] = acc / l;
+}
+
 // ---- short-sequence attention on MFMA ----------------------------------------------------------
 // Block = one (batch, head) and up to 64 queries (4 waves x 16-query tiles), Lk <= ATT_MFMA_MAXK,
 // head dim 64, on v_mfma_f32_16x16x4_f32 (exact f32 products, 4-deep k steps).  The block stages
@@ -807,8 +912,18 @@ int attention(const AttnArgs& a, hipStream_t s) {
                                 a.q_rms_nparts <= 64),
               "attention: a query row scale only on the one-query decode path");
   if (a.Lq == 1) {
-    // (A wave-per-(b, h) form without block barriers measured slower: 4.4 / 5.3 us self / cross
-    // against 3.8 / 4.1 — a quarter of the loads in flight per (b, h).)
+    // Few pairs (one batch's decode): the block kernel (a wave-per-(b, h) form measured slower at
+    // 16 rows: 4.4 / 5.3 us self / cross against 3.8 / 4.1, a quarter of the loads in flight per
+    // pair).  Many pairs with few keys (grouped decodes): the wave form, bit-identical.
+    const char* we = getenv("MPR_ATT_WAVE");  // read per call (a captured graph keeps its form)
+    const bool wave_ok = !(we && we[0] == '0');
+    const int lk_end = a.causal ? std::min(a.Lk, a.q_pos0 + 1) : a.Lk;
+    if (wave_ok && lk_end <= 128 && (int64_t)a.B * a.H >= 512) {
+      hipLaunchKernelGGL(attention_decode_wave_kernel,
+                         dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(256), 0, s, a);
+      MPR_LAUNCHED();
+      return MPR_OK;
+    }
     hipLaunchKernelGGL(attention_decode_kernel, dim3((unsigned)((int64_t)a.B * a.H)), dim3(256),
                        0, s, a);
     MPR_LAUNCHED();
@@ -904,6 +1019,73 @@ int eot_gather(const float* x, const int32_t* tok, int B, int L, int ctx, int D,
 int argmax_rows(const float* logits, int M, int V, int64_t ld, int32_t* out, hipStream_t s) {
   if (M == 0) return MPR_OK;
   hipLaunchKernelGGL(argmax_rows_kernel, dim3(M), dim3(256), 0, s, logits, V, ld, out);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+// Row argmax of a logits matrix in P parts per row (the tiled decode head, t5.hip): part p of
+// row r covers columns [p * seg, min(N, (p + 1) * seg)); its largest value, ties to the lowest
+// column (greedy_step's rule, which then reduces the P parts of each row).
+__global__ __launch_bounds__(256) void argmax_parts_kernel(const float* __restrict__ L,
+                                                           int64_t ld, int N, int seg,
+                                                           float* __restrict__ pv,
+                                                           int32_t* __restrict__ pi) {
+  const int p = blockIdx.x, row = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const float* lr = L + (int64_t)row * ld;
+  const int c0 = p * seg, c1 = min(N, c0 + seg);
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int b0 = c0; b0 < c1; b0 += 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // all loads first, lane-contiguous
+      const int c = b0 + u * 256 + tid;
+      v[u] = c < c1 ? lr[c] : -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = b0 + u * 256 + tid;
+      if (c < c1 && (v[u] > best || (v[u] == best && c < bi))) {
+        best = v[u];
+        bi = c;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(best, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ov > best || (ov == best && oi < bi)) {
+      best = ov;
+      bi = oi;
+    }
+  }
+  __shared__ float wv[4];
+  __shared__ int wi[4];
+  if (lane == 0) {
+    wv[wave] = best;
+    wi[wave] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (wv[w] > best || (wv[w] == best && wi[w] < bi)) {
+        best = wv[w];
+        bi = wi[w];
+      }
+    const int64_t o = (int64_t)row * gridDim.x + p;
+    pv[o] = best;
+    pi[o] = bi == 0x7fffffff ? c0 : bi;
+  }
+}
+
+int argmax_parts(const float* L, int64_t ld, int M, int N, int P, float* pv, int32_t* pi,
+                 hipStream_t s) {
+  MPR_REQUIRE(M >= 0 && N > 0 && P >= 1 && P <= N, "argmax_parts: M=%d N=%d P=%d", M, N, P);
+  if (M == 0) return MPR_OK;
+  hipLaunchKernelGGL(argmax_parts_kernel, dim3((unsigned)P, (unsigned)M), dim3(256), 0, s, L, ld,
+                     N, (int)cdiv(N, P), pv, pi);
   MPR_LAUNCHED();
   return MPR_OK;
 }

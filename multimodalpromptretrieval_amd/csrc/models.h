@@ -127,6 +127,7 @@ struct T5Work {
   ~T5Work();
   DevBuf x, h, qkv, ao, ff, enc_out, cross_kv, cache, dx, dq, unfinished, cur_tok;
   DevBuf enc_in, mask_in, part_val, part_idx, tok_buf;
+  DevBuf logits;  // [B, V] of the tiled decode head (T5Model::tiled_head)
   DevBuf mask_enc, enc_tmp;  // a group's encoder mask / output when several groups share a decode
   DevBuf ax, yq, hz;  // folded decode chain rows: [a | x], [c | h | u], [h2 | z]
   DevBuf x1ss, x2ss;  // their residual rows' per-16-column sums of squares
@@ -169,6 +170,7 @@ struct T5Model : mpr_model {
   // layer instead of 8; MPR_DECODE_FOLD=0 keeps the 8-launch chain): see decode_body.
   bool fold = false;
   bool fold_rows(int B) const;  // fold and B <= MPR_DECODE_FOLD_ROWS (16)
+  bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
   int build_folded();
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
   DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)

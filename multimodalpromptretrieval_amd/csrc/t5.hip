@@ -86,6 +86,17 @@ bool T5Model::fold_rows(int B) const {
   return fold && B <= max_rows;
 }
 
+// The argmax head of a grouped decode (> 32 rows) as RMSNorm + the tiled split-bf16 GEMM into a
+// logits buffer + a row argmax, instead of the skinny GEMV (which stages the rows once per 16
+// columns: 8,032 blocks re-reading 96 KB of rows for t5-base's 128-row head, 201 us).  Default
+// from d >= 768 (t5-base and up); MPR_TILED_HEAD=0 / 1 forces it off / on (read per call; a
+// captured decode graph keeps the head it was captured with).
+bool T5Model::tiled_head(int B) const {
+  const char* e = getenv("MPR_TILED_HEAD");
+  const bool on = e ? e[0] == '1' : d >= 768;
+  return on && B > 32 && !fold_rows(B);
+}
+
 int T5Model::build_folded() {
   const int K = inner + d;
   DevBuf tmp;
@@ -326,6 +337,24 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       fo.wpk = ly.pk_wo.as<float>();
       MPR_TRY(gemm_skinny(fo, s));
     }
+    if (tiled_head(B)) {
+      // logits = rms(x) . lm_head^T on the tiled GEMM, then the row argmax in 16 parts per row
+      // (out_scale > 0 multiplies every logit of a row alike: the argmax does not need it)
+      constexpr int HP = 16;
+      float* hb = ws->h.as<float>();
+      float* lg = ws->logits.as<float>();
+      MPR_TRY(rmsnorm(xp, d, B, d, dec_final.as<float>(), T5_EPS, hb, d, s));
+      GemmArgs g;
+      g.A = hb; g.lda = d; g.W = lm_head.as<float>(); g.ldw = d;
+      g.C = lg; g.ldc = V; g.M = B; g.N = V; g.K = d;
+      MPR_TRY(gemm(g, s));
+      MPR_TRY(argmax_parts(lg, V, B, V, HP, ws->part_val.as<float>(), ws->part_idx.as<int32_t>(),
+                           s));
+      MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), HP, B, unf, toks,
+                          T1, t + 1, eos, pad, shared.as<float>(), d,
+                          t + 1 < max_new ? xp : nullptr, s));
+      continue;
+    }
     // The argmax head, one launch for all rows (gemm_skinny splits more than 32 rows over blocks
     // of 16; as two 64-row launches it cost 2 x 42 us against 80.8 us per 128-row step).
     SkinnyArgs hd;
@@ -532,6 +561,7 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
   MPR_TRY(grow(ws->unfinished, (size_t)16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->cur_tok, (size_t)16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->tok_buf, (size_t)B * T1 * 4));
+  if (tiled_head(B)) MPR_TRY(grow(ws->logits, (size_t)B * V * 4));
   if (n > 1) {
     MPR_TRY(grow(ws->mask_enc, (size_t)Mg * 4));
     MPR_TRY(grow(ws->enc_tmp, (size_t)Mg * d * 4));

@@ -517,6 +517,54 @@ def test_t5_generate_over_128_rows_two_slots(device, t5_sd, monkeypatch):
     assert torch.equal(got, want)
 
 
+@pytest.fixture(scope="module")
+def grouped_40(t5_sd):
+    """40 distinct prompts (three 16-row groups sharing one decode loop) and the oracle's greedy
+    ids and per-step logits for them."""
+    ids, mask, img_tok = _t5_inputs(40, 61)
+    emb = torch.cat([img_tok, t5_sd["shared.weight"][ids]], 1)
+    fm = torch.cat([torch.ones(40, 50, dtype=torch.long), mask], 1)
+    ref_toks, step_logits = ot5.generate(t5_sd, emb, fm, 8, 20)
+    return emb, fm, ref_toks, step_logits
+
+
+@pytest.mark.parametrize("tiled", ["1", "0"])
+def test_t5_grouped_decode_head_vs_oracle(device, t5_sd, grouped_40, monkeypatch, tiled):
+    """The argmax head of a decode over > 32 rows: RMSNorm + the tiled GEMM + a row argmax
+    (MPR_TILED_HEAD=1, the default from d >= 768) or the skinny GEMV (0).  Greedy ids equal the
+    oracle's per row up to (and including) its first step with a top-2 margin <= 1e-3."""
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    monkeypatch.setenv("MPR_TILED_HEAD", tiled)
+    m = DeviceT5(t5_sd, device)
+    emb, fm, ref_toks, step_logits = grouped_40
+    toks = m.generate_padded(emb, fm, 20).cpu().long()
+    margins = torch.stack([s.topk(2).values[:, 0] - s.topk(2).values[:, 1]
+                           for s in step_logits], 1)
+    compared = 0
+    for r in range(emb.shape[0]):
+        close = (margins[r] <= 1e-3).nonzero()
+        n = int(close[0]) if len(close) else margins.shape[1]
+        assert torch.equal(toks[r, :n + 1], ref_toks[r, :n + 1]), r
+        compared += n
+    assert compared > 200
+
+
+def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
+    """Decodes over >= 64 rows (>= 512 batch x head pairs) run the decode attention one wave per
+    pair (attention_decode_wave_kernel), whose outputs are bit-identical to the block kernel's
+    (MPR_ATT_WAVE=0): the greedy tokens of 128 + 69 rows are equal."""
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    A = _t5_batch(t5_sd, 16, 73)
+    emb = torch.cat([A[0]] * 12 + [A[0][:5]])
+    emb = emb + 1e-3 * torch.randn(emb.shape, generator=torch.Generator().manual_seed(6))
+    fm = torch.cat([A[1]] * 12 + [A[1][:5]])
+    monkeypatch.setenv("MPR_ATT_WAVE", "0")
+    want = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
+    monkeypatch.setenv("MPR_ATT_WAVE", "1")
+    got = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
+    assert torch.equal(got, want)
+
+
 def test_t5_embed_and_loss(device, t5_sd):
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     m = DeviceT5(t5_sd, device)

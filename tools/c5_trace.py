@@ -1,0 +1,56 @@
+"""Kernel trace of config C5's end-to-end leg alone (development aid): three 256-question
+predict() calls of bench.c5_serving's model, host sleeps around them.  Run under
+``rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c5t -- python tools/c5_trace.py``
+then ``python tools/serving_trace.py --report gpurun_out/c5t`` (busy / idle over the window, the
+longest idle gaps, kernel time by name); ``--cprofile`` adds a cProfile of one more predict()."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from multimodalpromptretrieval_amd import synthetic as syn  # noqa: E402
+from multimodalpromptretrieval_amd.encoders import DeviceCLIPText  # noqa: E402
+from multimodalpromptretrieval_amd.index import DeviceIndex  # noqa: E402
+from multimodalpromptretrieval_amd.model import T5VisionModel  # noqa: E402
+from multimodalpromptretrieval_amd.tokenization import SpmT5Tokenizer  # noqa: E402
+
+dev = torch.device("cuda:0")
+torch.cuda.set_device(dev)
+n, d, B, k = bench.C5["N"], bench.C5["D"], bench.C5["B"], bench.C5["k"]
+ix = DeviceIndex(syn.index_rows_device(7, 0, n, d, dev), dev)
+text = DeviceCLIPText(syn.clip_state_dict(1), dev)
+retr = bench._C5Retrieval(text, ix, syn.answers(n, 50), k)
+m = T5VisionModel(dev, T5_version="t5-base", use_image_info=False,
+                  clip_state_dict=syn.clip_state_dict(2),
+                  t5_state_dict=syn.t5_state_dict(5, syn.T5_BASE),
+                  tokenizer=SpmT5Tokenizer(), retrieval_function=retr).eval()
+pool = bench.make_batches(4, B, seed=500, n_images=1)
+os.environ["MPR_EOS_STOP_CHUNK"] = "0"
+with torch.no_grad():
+    m.predict(pool[0])
+    torch.cuda.synchronize()
+    time.sleep(0.05)
+    t = time.perf_counter()
+    parts = []
+    for b in pool[1:]:
+        t1 = time.perf_counter()
+        m.predict(b)
+        torch.cuda.synchronize()
+        parts.append((time.perf_counter() - t1) * 1e3)
+    print(f"{len(pool) - 1} batches: {(time.perf_counter() - t) / (len(pool) - 1) * 1e3:.2f} ms per "
+          f"batch ({', '.join(f'{p:.1f}' for p in parts)})", flush=True)
+    time.sleep(0.05)
+    torch.zeros(1, device=dev).add_(1)
+    torch.cuda.synchronize()
+    if "--cprofile" in sys.argv:  # where one predict()'s host time goes
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        m.predict(pool[1])
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
