@@ -772,7 +772,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   if constexpr (RES) {
     if (wave < NT * MR)
       rres = *reinterpret_cast<const f32x4*>(a.R + (int64_t)(row0 + min(er * 16 + i, M - 1)) * a.ldr +
-                                             (blockIdx.x * NT + et) * 16 + h * 4);
+                                             min((int)blockIdx.x * NT + et, ntiles - 1) * 16 + h * 4);
   }
   // RSCALE: the rows' partial sums of squares (<= 64 per row): wave w loads those of rows w,
   // w + 8, ... (lane = partial), issued with the first loads, summed after the main loop
@@ -926,7 +926,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
       for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
     }
     if constexpr (RES) v = rres + v;
-    if (m < M) *reinterpret_cast<f32x4*>(a.C + (int64_t)(row0 + m) * a.ldc + n0 + h * 4) = v;
+    if (m < M && n0 < N) *reinterpret_cast<f32x4*>(a.C + (int64_t)(row0 + m) * a.ldc + n0 + h * 4) = v;
     if constexpr (SSQ) {
       // the tile's 16 columns of row m: this lane's 4, then the 4 lane groups (h) of the row
       float q = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
@@ -1232,7 +1232,11 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, un
     hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP, MR>), dim3(grid, gy), dim3(512), 0, s, sa); \
     break;
   if constexpr (NT > 1) {
-    switch (F) { MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS) default: break; }
+    switch (F) {
+      MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS)
+      MPR_SK(0) MPR_SK(SKF_RMS) MPR_SK(SKF_RES) MPR_SK(SKF_RMS | SKF_RELU)
+      default: break;
+    }
   } else {
     switch (F) {
       MPR_SK(0) MPR_SK(1) MPR_SK(2) MPR_SK(3) MPR_SK(4) MPR_SK(5) MPR_SK(6) MPR_SK(7)
@@ -1332,7 +1336,15 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
         else
           launch_skinny<16, 1, true>(sa, F, (unsigned)tiles, s, gy);
       } else {
-        if (amax && tiles >= 1024 && per <= 4)
+        // MPR_SKINNY_NT=4: four 16-column tiles per block share each staged row slab (the
+        // 32-row slab is otherwise staged once per 16 columns: for t5-base's 128-row qkv 56 MB
+        // of slab traffic against 7 MB of weights).  Same chunk order per accumulator chain
+        // (4-chunk passes; the padding chunks add exact zeros): bit-identical outputs.
+        const char* nte = getenv("MPR_SKINNY_NT");  // per call: a captured graph keeps its form
+        const bool nt4 = nte && atoi(nte) == 4;
+        if (nt4 && !amax && (F == 0 || F == SKF_RMS || F == SKF_RES || F == (SKF_RMS | SKF_RELU)))
+          launch_skinny<4, 4, true, 2>(sa, F, (unsigned)cdiv(tiles, 4), s, gy);
+        else if (amax && tiles >= 1024 && per <= 4)
           launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
         else if (per <= 4)
           launch_skinny<4, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU call: the GPU test suite, the C5 end-to-end trace with the grouped-decode changes
-# (tiled argmax head, wave-per-pair decode attention) against both off, the serving loop timed
-# with the wave attention on / off (alternating), then the driver's bench command.  Each GPU step
+# (tiled argmax head, wave-per-pair decode attention, 4-tile skinny blocks) against them off, the
+# serving loop timed with each (alternating), then the driver's bench command.  Each GPU step
 # has its own time limit; a failure ends the script.
 # usage: bash tools/round_j.sh <tag>
 TAG=${1:-r03_j}
@@ -17,15 +17,15 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/c5t" -o 
 step c5_trace $?
 python tools/serving_trace.py --report "$OUT/c5t" >> "$OUT/c5_trace.txt" 2>&1
 rm -f "$OUT"/c5t/*kernel_trace.csv "$OUT"/c5t/*/*kernel_trace.csv
-for v in "MPR_TILED_HEAD=0 MPR_ATT_WAVE=0" "MPR_TILED_HEAD=1 MPR_ATT_WAVE=0" "MPR_TILED_HEAD=0 MPR_ATT_WAVE=1" "MPR_TILED_HEAD=1 MPR_ATT_WAVE=1"; do
+for v in "MPR_TILED_HEAD=0 MPR_ATT_WAVE=0" "MPR_TILED_HEAD=1 MPR_ATT_WAVE=0" "MPR_TILED_HEAD=0 MPR_ATT_WAVE=1" "MPR_SKINNY_NT=4 MPR_TILED_HEAD=0 MPR_ATT_WAVE=0" "MPR_SKINNY_NT=4" "MPR_DEFAULTS=1"; do
   echo "[$v]" >> "$OUT/c5_ab.txt"
   env $v timeout -k 10 200 python tools/c5_trace.py >> "$OUT/c5_ab.txt" 2>&1
   step "c5 $v" $?
 done
 for r in 1 2; do
-  for v in MPR_ATT_WAVE=0 MPR_ATT_WAVE=1; do
+  for v in MPR_ATT_WAVE=0 MPR_DEFAULTS=1 MPR_SKINNY_NT=4; do
     echo "[$v]" >> "$OUT/serving_ab.txt"
-    env $v timeout -k 10 200 python tools/serving_trace.py 60 >> "$OUT/serving_ab.txt" 2>&1
+    env $v timeout -k 10 200 python tools/serving_trace.py 40 >> "$OUT/serving_ab.txt" 2>&1
     step "serving $v" $?
   done
 done
