@@ -195,8 +195,13 @@ def c5_projection(device, iters: int = 20):
         # the merge's cost on the GPU timeline: search + merge back to back minus the search (a
         # merge timed alone is a host-bound Python call, ~11 us against a ~4 us kernel)
         t_alone = timed(lambda: topk_merge(cd, ci, k))
-        t_both = timed(lambda: (ix.search(q, k), topk_merge(cd, ci, k)))
-        t_merge = max(0.0, t_both - t_search)
+        # the difference of two timed loops: median over 5 alternations (one pair is +-10 us)
+        diffs, searches = [], []
+        for _ in range(5):
+            searches.append(timed(lambda: ix.search(q, k)))
+            diffs.append(timed(lambda: (ix.search(q, k), topk_merge(cd, ci, k))) - searches[-1])
+        t_search = float(np.median(searches))
+        t_merge = max(0.0, float(np.median(diffs)))
         ix.close()
         torch.cuda.empty_cache()
         ag_bytes = W * B * k * 16

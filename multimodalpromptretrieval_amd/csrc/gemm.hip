@@ -1232,11 +1232,7 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, un
     hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP, MR>), dim3(grid, gy), dim3(512), 0, s, sa); \
     break;
   if constexpr (NT > 1) {
-    switch (F) {
-      MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS)
-      MPR_SK(0) MPR_SK(SKF_RMS) MPR_SK(SKF_RES) MPR_SK(SKF_RMS | SKF_RELU)
-      default: break;
-    }
+    switch (F) { MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS) default: break; }
   } else {
     switch (F) {
       MPR_SK(0) MPR_SK(1) MPR_SK(2) MPR_SK(3) MPR_SK(4) MPR_SK(5) MPR_SK(6) MPR_SK(7)
@@ -1336,15 +1332,10 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
         else
           launch_skinny<16, 1, true>(sa, F, (unsigned)tiles, s, gy);
       } else {
-        // MPR_SKINNY_NT=4: four 16-column tiles per block share each staged row slab (the
-        // 32-row slab is otherwise staged once per 16 columns: for t5-base's 128-row qkv 56 MB
-        // of slab traffic against 7 MB of weights).  Same chunk order per accumulator chain
-        // (4-chunk passes; the padding chunks add exact zeros): bit-identical outputs.
-        const char* nte = getenv("MPR_SKINNY_NT");  // per call: a captured graph keeps its form
-        const bool nt4 = nte && atoi(nte) == 4;
-        if (nt4 && !amax && (F == 0 || F == SKF_RMS || F == SKF_RES || F == (SKF_RMS | SKF_RELU)))
-          launch_skinny<4, 4, true, 2>(sa, F, (unsigned)cdiv(tiles, 4), s, gy);
-        else if (amax && tiles >= 1024 && per <= 4)
+        // (Four 16-column tiles per block sharing each staged 32-row slab — the slab is staged
+        // once per 16 columns — measured slower: C5's t5-base 128-row decodes 84.0 -> 96.3 ms
+        // per batch, the serving loop 3.77-3.79 -> 3.86-3.88 ms per step.)
+        if (amax && tiles >= 1024 && per <= 4)
           launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
         else if (per <= 4)
           launch_skinny<4, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
