@@ -1335,12 +1335,14 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
         // (Four 16-column tiles per block sharing each staged 32-row slab — the slab is staged
         // once per 16 columns — measured slower: C5's t5-base 128-row decodes 84.0 -> 96.3 ms
         // per batch, the serving loop 3.77-3.79 -> 3.86-3.88 ms per step.)
-        // MPR_SKINNY_MAXC=4 (read per call): 4-chunk passes above 4 chunks per wave, so the
-        // block's slabs take 70 KB of LDS instead of 136 KB and two blocks fit per CU (the 8-chunk
-        // slab holds one: t5-base's 576-block 128-row qkv runs in ~3 rounds of blocks).  Same
-        // chunk order per accumulator chain, padding chunks add exact zeros: bit-identical.
+        // 4-chunk passes above 4 chunks per wave, so the block's slabs take 70 KB of LDS instead
+        // of 136 KB and two blocks fit per CU (the 8-chunk slab holds one: t5-base's 576-block
+        // 128-row qkv ran in ~3 rounds of blocks).  Same chunk order per accumulator chain,
+        // padding chunks add exact zeros: bit-identical.  C5 end to end 72.1-73.1 -> 68.4-69.3
+        // ms per batch, the serving loop unchanged (3.69-3.71 ms per step either way).
+        // MPR_SKINNY_MAXC=8 (read per call) restores the 8-chunk slabs.
         const char* mce = getenv("MPR_SKINNY_MAXC");
-        const bool c4 = mce && atoi(mce) == 4;
+        const bool c4 = !(mce && atoi(mce) == 8);
         if (amax && tiles >= 1024 && per <= 4)
           launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
         else if (per <= 4)

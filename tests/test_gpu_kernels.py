@@ -566,17 +566,17 @@ def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
 
 
 def test_grouped_decode_skinny_maxc4_matches(device, t5_sd, monkeypatch):
-    """MPR_SKINNY_MAXC=4 (4-chunk passes for the grouped decode's 32-row GEMV blocks: t5-small's
-    K = 2048 FFN-out here) sums every output in the default kernel's order: the greedy tokens of
-    128 + 69 rows are equal."""
+    """The grouped decode's 32-row GEMV blocks in 4-chunk passes (the default; t5-small's K = 2048
+    FFN-out here) sum every output in the 8-chunk kernel's order (MPR_SKINNY_MAXC=8): the greedy
+    tokens of 128 + 69 rows are equal."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     A = _t5_batch(t5_sd, 16, 75)
     emb = torch.cat([A[0]] * 12 + [A[0][:5]])
     emb = emb + 1e-3 * torch.randn(emb.shape, generator=torch.Generator().manual_seed(7))
     fm = torch.cat([A[1]] * 12 + [A[1][:5]])
-    monkeypatch.delenv("MPR_SKINNY_MAXC", raising=False)
+    monkeypatch.setenv("MPR_SKINNY_MAXC", "8")
     want = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
-    monkeypatch.setenv("MPR_SKINNY_MAXC", "4")
+    monkeypatch.delenv("MPR_SKINNY_MAXC", raising=False)
     got = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
     assert torch.equal(got, want)
 
