@@ -575,6 +575,7 @@ __global__ void qprep_kernel(const float* __restrict__ Q, int b, int d, __bf16* 
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (q >= b) return;
   float s = 0.f;
+#pragma unroll 8  // d <= 512 in one batch of loads (the sum keeps qnorm_kernel's order)
   for (int c = lane; c < d; c += 64) {
     const float v = Q[(int64_t)q * d + c];
     qb[(int64_t)q * d + c] = (__bf16)v;
