@@ -178,7 +178,7 @@ int mpr_t5_generate(mpr_model* m, const float* embeds_dev, const float* mask_dev
                     int32_t L, int32_t max_new, int32_t decoder_start, int32_t eos, int32_t pad,
                     int32_t* out_tokens_dev, void* stream);
 /* Teacher-forced decoder logits: dec_in_dev [b,T] int32 decoder input ids -> logits [b,T,vocab]. */
-/* mpr_t5_generate on workspace slot `slot` (0 <= slot < 4; mpr_t5_generate uses slot 0).  Each
+/* mpr_t5_generate on workspace slot `slot` (0 <= slot < 6; mpr_t5_generate uses slot 0).  Each
  * slot has its own activations, decode caches and captured graphs, so calls on different slots
  * may be in flight on the device at the same time (a serving loop decoding two batches at once);
  * calls on one slot must be ordered by their streams. */
@@ -315,6 +315,22 @@ int mpr_gather_rows(const float* table, const int32_t* ids, int64_t n, int32_t d
                     void* stream);
 int mpr_embed_bwd(const float* dY, int32_t d, const int32_t* uniq, const int32_t* offs,
                   const int32_t* pos, int32_t n_uniq, float* dW, void* stream);
+
+/* ---- decode-step projection (the kernel behind the decoder projections of mpr_t5_generate*,
+ * architectures/T5VisionModel.py:200-205; exposed for kernel-level tests and benchmarks) ----
+ *   mpr_planes_bytes / mpr_planes_pack: the three-bf16-plane image of W [n, k] (k % 32 == 0;
+ *   fp32 W, row-major) into `planes` (16-byte aligned, mpr_planes_bytes(n, k) bytes).
+ *   mpr_rows_gemm: C[M,N] = R + act(s_m * sum_k A'[m,k] W[n,k]) on that image, fp32-accurate:
+ *   A' = rms_w * A and s_m = rsqrt(mean_k A[m,:]^2 + eps) when rms_w is given (T5's RMSNorm
+ *   folded into the projection), else A' = A, s_m = 1; act 0 none / 2 relu; R optional (may alias
+ *   C).  With amax_val/amax_idx (C, R null): per row the best column (lowest on ties) of each of
+ *   *nparts column parts, [M, *nparts].  Each row's results depend only on K, not on M. */
+int64_t mpr_planes_bytes(int64_t n, int32_t k);
+int mpr_planes_pack(const float* W, int64_t n, int32_t k, void* planes, void* stream);
+int mpr_rows_gemm(const float* A, int64_t lda, const void* planes, float* C, int64_t ldc,
+                  int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr, int32_t act,
+                  const float* rms_w, float eps, float* amax_val, int32_t* amax_idx,
+                  int32_t* nparts, void* stream);
 
 /* ---- measurement (bench.py roofline; no reference counterpart) --------------------------------
  * kind 1 = tiled f32-MFMA GEMM, 2 = skinny (decode) GEMM, 0 = off.  While enabled, every launch

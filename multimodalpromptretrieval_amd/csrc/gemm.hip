@@ -18,6 +18,7 @@
 #include <cstring>
 
 #include "kernels.h"
+#include "x3.h"
 
 namespace mpr {
 namespace {
@@ -259,46 +260,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, flo
 // Structure as gemm_tile: BM x BN block tile, WM x WN 32x32 accumulators per wave, BK-deep K
 // tiles staged fp32 global -> registers (D tiles in flight) -> split -> 3 bf16 planes in LDS (two
 // stages), KW wave groups splitting each K tile (partials summed through LDS).
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// RNE bf16 of (a, b) packed in one word (one v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
-}
-// fp32 value of the low / high bf16 of a packed word
-__device__ __forceinline__ float lo_f(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
-__device__ __forceinline__ float hi_f(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
-
-// v = h0 + h1 + h2 exactly (each an RNE bf16 of the remainder).  Written on packed words: the
-// plain vector form (convert, convert back, subtract) compiled to a convert per element and a
-// second convert + shift for the way back, 32 VALU per float4 in place of these 18 (the tile
-// loop was VALU-issue bound: SQ counters); same roundings, bit-identical planes.
-__device__ __forceinline__ void split3(const f32x4& v, bf16x4& h0, bf16x4& h1, bf16x4& h2) {
-  u32x2 p0, p1, p2;
-  f32x4 r1, r2;
-  p0[0] = pk_bf16(v[0], v[1]);
-  p0[1] = pk_bf16(v[2], v[3]);
-  r1[0] = v[0] - lo_f(p0[0]);
-  r1[1] = v[1] - hi_f(p0[0]);
-  r1[2] = v[2] - lo_f(p0[1]);
-  r1[3] = v[3] - hi_f(p0[1]);
-  p1[0] = pk_bf16(r1[0], r1[1]);
-  p1[1] = pk_bf16(r1[2], r1[3]);
-  r2[0] = r1[0] - lo_f(p1[0]);
-  r2[1] = r1[1] - hi_f(p1[0]);
-  r2[2] = r1[2] - lo_f(p1[1]);
-  r2[3] = r1[3] - hi_f(p1[1]);
-  p2[0] = pk_bf16(r2[0], r2[1]);
-  p2[1] = pk_bf16(r2[2], r2[3]);
-  h0 = __builtin_bit_cast(bf16x4, p0);
-  h1 = __builtin_bit_cast(bf16x4, p1);
-  h2 = __builtin_bit_cast(bf16x4, p2);
-}
+using x3::bf16x4;
+using x3::bf16x8;
+using x3::split3;
 
 template <int BM, int BN, int BK>
 constexpr int x3_lds_floats() {

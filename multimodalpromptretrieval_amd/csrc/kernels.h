@@ -75,6 +75,21 @@ struct SkinnyArgs {
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
+// Decode-step projections at any row count (decode_gemm.hip): gemm_skinny's contract (fused
+// RMSNorm, residual, ReLU, argmax head, folded-chain flags), computed on the bf16 matrix cores as
+// the fp32-accurate three-way split (x3.h) with the weight's three bf16 planes pre-split once at
+// load (pack_planes).  The K range of every output element is split into 8 fixed contiguous
+// slices summed in slice order, whatever the row count or the block tile: a row's results do not
+// depend on how many rows share the launch (a 16-row predict() and the same rows inside a 128-row
+// serving-loop decode are bit-identical).  K % 32 == 0 (gemm_rows_ok).  Argmax mode writes
+// *amax_nparts partials per row (amax_val/idx[row * nparts + part]).
+//   planes image: Wp[((t * K/32 + s) * 3 + p) * 512 + l * 8 + j] = plane p of
+//                 W[16t + (l & 15)][32s + 8(l >> 4) + j]  (0 past N), bf16
+bool gemm_rows_ok(int K);
+int64_t packed_planes_elems(int64_t N, int64_t K);  // bf16 elements of the planes image
+int pack_planes(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, hipStream_t s);
+int gemm_rows(const SkinnyArgs& a, const void* wpl, hipStream_t s, int* amax_nparts = nullptr);
+
 // Kernel probe (bench roofline): hipEvent pairs around every launch of one GEMM kind.
 enum ProbeKind : int { PROBE_OFF = 0, PROBE_GEMM = 1, PROBE_SKINNY = 2, PROBE_RECORD = 3 };
 int probe_enable(int kind);

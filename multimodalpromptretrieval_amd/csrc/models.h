@@ -118,6 +118,9 @@ struct T5Layer {
   //   W_ocq  = [[o | I_d], [cq diag(ln1) o | cq diag(ln1)]]     [d + inner, inner + d]
   //   W_cowi = [[co | I_d], [wi diag(ln2) co | wi diag(ln2)]]   [d + d_ff, inner + d]
   DevBuf pk_ocq, pk_cowi;
+  // decoder only: pack_planes images (three bf16 planes, decode_gemm.hip) of the same weights
+  // for the row-count independent decode GEMM (T5Model::rows)
+  DevBuf pl_qkv, pl_o, pl_cq, pl_co, pl_wi, pl_wo, pl_ocq, pl_cowi;
 };
 
 // Per-call workspace of generate(): activations, decode caches, captured graphs and the decode
@@ -161,7 +164,8 @@ struct T5Work {
 };
 
 struct T5Model : mpr_model {
-  static constexpr int MAX_SLOTS = 4;
+  // slots 0..3: serving-loop calls in flight; 4 (and 5 for > 128 rows): predict()'s own
+  static constexpr int MAX_SLOTS = 6;
   static constexpr int MAX_GROUPS = 8;  // batches (<= 16 rows each) sharing one decode loop
   T5Model() : mpr_model(T5) { use_slot(0); }
   int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
@@ -169,11 +173,18 @@ struct T5Model : mpr_model {
   // The decode chain with its RMSNorms folded into the preceding projections (6 launches per
   // layer instead of 8; MPR_DECODE_FOLD=0 keeps the 8-launch chain): see decode_body.
   bool fold = false;
-  bool fold_rows(int B) const;  // fold and B <= MPR_DECODE_FOLD_ROWS (16)
+  bool fold_rows(int B) const;  // the folded chain for a B-row decode
+  // Decode projections on gemm_rows (decode_gemm.hip) at every row count (MPR_DECODE_GEMM=skinny
+  // keeps the round-3 GEMV kernels): a row's tokens are then the same whatever decode group it
+  // is in, so the fold and the head are chosen per model, never per call.
+  bool rows = false;
+  int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& pl, hipStream_t s,
+               int* amax_nparts = nullptr) const;
   bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
   int build_folded();
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
   DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
+  DevBuf pl_lm_head;  // pack_planes image of lm_head (rows)
   // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
   DevBuf enc_tab, dec_tab;
   std::vector<std::unique_ptr<T5Layer>> enc, dec;

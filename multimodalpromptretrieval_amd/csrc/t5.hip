@@ -78,12 +78,28 @@ __global__ void fold_weights_kernel(const float* __restrict__ top, const float* 
 // The folded chain trades launches for MACs (its two merged GEMMs read 50 % more weight per
 // layer): it wins for the latency-bound decodes of one batch and loses for the grouped
 // 128-row decodes of a serving loop, where the launches overlap other work (measured).
+// On gemm_rows the choice is per model (MPR_ROWS_FOLD, default on): a batch's rows then take the
+// same chain alone or in a grouped decode.  On the skinny kernels it follows the row count.
 bool T5Model::fold_rows(int B) const {
   static const int max_rows = [] {
     const char* e = getenv("MPR_DECODE_FOLD_ROWS");
     return e ? atoi(e) : 16;
   }();
+  static const bool rows_fold = [] {
+    const char* e = getenv("MPR_ROWS_FOLD");
+    return !(e && e[0] == '0');
+  }();
+  if (rows) return fold && rows_fold;
   return fold && B <= max_rows;
+}
+
+int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& pl, hipStream_t s,
+                      int* amax_nparts) const {
+  if (rows) return gemm_rows(a, pl.ptr, s, amax_nparts);
+  SkinnyArgs b = a;
+  b.wpk = pk.as<float>();
+  if (amax_nparts) *amax_nparts = (int)cdiv(a.g.N, 16);
+  return gemm_skinny(b, s);
 }
 
 // The argmax head of a grouped decode (> 32 rows) as RMSNorm + the tiled split-bf16 GEMM into a
@@ -92,6 +108,7 @@ bool T5Model::fold_rows(int B) const {
 // from d >= 768 (t5-base and up); MPR_TILED_HEAD=0 / 1 forces it off / on (read per call; a
 // captured decode graph keeps the head it was captured with).
 bool T5Model::tiled_head(int B) const {
+  if (rows) return false;  // gemm_rows' argmax head serves every row count
   const char* e = getenv("MPR_TILED_HEAD");
   const bool on = e ? e[0] == '1' : d >= 768;
   return on && B > 32 && !fold_rows(B);
@@ -108,15 +125,20 @@ int T5Model::build_folded() {
                        top.as<float>(), bot.as<float>(), w.as<float>(), d, inner, N2,
                        tmp.as<float>());
     MPR_LAUNCHED();
-    MPR_TRY(dst.ensure((size_t)packed_rows16_elems(d + N2, K) * 4));
-    MPR_TRY(pack_rows16(tmp.as<float>(), d + N2, K, K, dst.as<float>(), nullptr));
+    if (rows) {
+      MPR_TRY(dst.ensure((size_t)packed_planes_elems(d + N2, K) * 2));
+      MPR_TRY(pack_planes(tmp.as<float>(), d + N2, K, K, dst.ptr, nullptr));
+    } else {
+      MPR_TRY(dst.ensure((size_t)packed_rows16_elems(d + N2, K) * 4));
+      MPR_TRY(pack_rows16(tmp.as<float>(), d + N2, K, K, dst.as<float>(), nullptr));
+    }
     MPR_HIP(hipStreamSynchronize(nullptr));  // tmp is reused by the next fold
     return MPR_OK;
   };
   for (auto& lp : dec) {
     T5Layer& ly = *lp;
-    MPR_TRY(fold(ly.pk_ocq, ly.o, ly.cq, ly.ln1, inner));
-    MPR_TRY(fold(ly.pk_cowi, ly.co, ly.wi, ly.ln2, dff));
+    MPR_TRY(fold(rows ? ly.pl_ocq : ly.pk_ocq, ly.o, ly.cq, ly.ln1, inner));
+    MPR_TRY(fold(rows ? ly.pl_cowi : ly.pk_cowi, ly.co, ly.wi, ly.ln2, dff));
   }
   return MPR_OK;
 }
@@ -269,7 +291,6 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
   if (t1 < 0 || t1 > max_new) t1 = max_new;
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
-  const int nparts = (int)cdiv(V, 16);
   const float* maskp = ws->mask_in.as<float>();
   float* xp = ws->dx.as<float>();
   float* qp = ws->dq.as<float>();
@@ -290,8 +311,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       sq.g.A = xp; sq.g.lda = d;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      sq.wpk = ly.pk_qkv.as<float>();
-      MPR_TRY(gemm_skinny(sq, s));
+      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.pl_qkv, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
       at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -304,14 +324,12 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       SkinnyArgs so;
       so.g.A = ap; so.g.lda = inner; so.g.R = xp;
       so.g.ldr = d; so.g.C = xp; so.g.ldc = d; so.g.M = B; so.g.N = d; so.g.K = inner;
-      so.wpk = ly.pk_o.as<float>();
-      MPR_TRY(gemm_skinny(so, s));
+      MPR_TRY(dec_gemm(so, ly.pk_o, ly.pl_o, s));
       SkinnyArgs cq;
       cq.g.A = xp; cq.g.lda = d; cq.g.C = qp;
       cq.g.ldc = inner; cq.g.M = B; cq.g.N = inner; cq.g.K = d; cq.rms_w = ly.ln1.as<float>();
       cq.rms_eps = T5_EPS;
-      cq.wpk = ly.pk_cq.as<float>();
-      MPR_TRY(gemm_skinny(cq, s));
+      MPR_TRY(dec_gemm(cq, ly.pk_cq, ly.pl_cq, s));
       AttnArgs ca;
       ca.q = qp; ca.q_bs = inner; ca.q_rs = inner;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -323,19 +341,16 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       SkinnyArgs co;
       co.g.A = ap; co.g.lda = inner; co.g.R = xp;
       co.g.ldr = d; co.g.C = xp; co.g.ldc = d; co.g.M = B; co.g.N = d; co.g.K = inner;
-      co.wpk = ly.pk_co.as<float>();
-      MPR_TRY(gemm_skinny(co, s));
+      MPR_TRY(dec_gemm(co, ly.pk_co, ly.pl_co, s));
       SkinnyArgs fi;
       fi.g.A = xp; fi.g.lda = d; fi.g.C = fp;
       fi.g.ldc = dff; fi.g.M = B; fi.g.N = dff; fi.g.K = d; fi.g.act = ACT_RELU;
       fi.rms_w = ly.ln2.as<float>(); fi.rms_eps = T5_EPS;
-      fi.wpk = ly.pk_wi.as<float>();
-      MPR_TRY(gemm_skinny(fi, s));
+      MPR_TRY(dec_gemm(fi, ly.pk_wi, ly.pl_wi, s));
       SkinnyArgs fo;
       fo.g.A = fp; fo.g.lda = dff; fo.g.R = xp;
       fo.g.ldr = d; fo.g.C = xp; fo.g.ldc = d; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
-      fo.wpk = ly.pk_wo.as<float>();
-      MPR_TRY(gemm_skinny(fo, s));
+      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.pl_wo, s));
     }
     if (tiled_head(B)) {
       // logits = rms(x) . lm_head^T on the tiled GEMM, then the row argmax in 16 parts per row
@@ -362,9 +377,9 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
     hd.rms_w = dec_final.as<float>(); hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
     hd.amax_val = ws->part_val.as<float>();
     hd.amax_idx = ws->part_idx.as<int32_t>();
-    hd.wpk = pk_lm_head.as<float>();
-    MPR_TRY(gemm_skinny(hd, s));
-    MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), nparts, B, unf, toks, T1,
+    int np = 0;
+    MPR_TRY(dec_gemm(hd, pk_lm_head, pl_lm_head, s, &np));
+    MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks, T1,
                         t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,
                         s));
   }
@@ -379,7 +394,6 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
                                 int t0, int t1) {
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
-  const int nparts = (int)cdiv(V, 16);
   const float* maskp = ws->mask_in.as<float>();
   const int64_t ldA = inner + d, ldY = 2 * inner + d, ldZ = d + dff;
   float* ax = ws->ax.as<float>();  // [a | x]
@@ -401,8 +415,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       sq.g.A = xp; sq.g.lda = ldA;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      sq.wpk = ly.pk_qkv.as<float>();
-      MPR_TRY(gemm_skinny(sq, s));
+      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.pl_qkv, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
       at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -415,9 +428,8 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       SkinnyArgs so;  // [x1 | u] = [a | x] W_ocq^T
       so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
       so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
-      so.wpk = ly.pk_ocq.as<float>();
       so.ssq_out = x1ss; so.ssq_cols = d;  // x1's per-tile sums of squares (its RMS)
-      MPR_TRY(gemm_skinny(so, s));
+      MPR_TRY(dec_gemm(so, ly.pk_ocq, ly.pl_ocq, s));
       AttnArgs ca;  // c = attention(u / rms_scale(x1), K_enc, V_enc)
       ca.q = yq + inner + d; ca.q_bs = ldY; ca.q_rs = ldY;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -430,25 +442,23 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       SkinnyArgs cw;  // [x2 | z] = [c | x1] W_cowi^T
       cw.g.A = yq; cw.g.lda = ldY; cw.g.C = hz; cw.g.ldc = ldZ;
       cw.g.M = B; cw.g.N = d + dff; cw.g.K = inner + d;
-      cw.wpk = ly.pk_cowi.as<float>();
       cw.ssq_out = x2ss; cw.ssq_cols = d;
-      MPR_TRY(gemm_skinny(cw, s));
+      MPR_TRY(dec_gemm(cw, ly.pk_cowi, ly.pl_cowi, s));
       SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
       fo.g.A = hz + d; fo.g.lda = ldZ; fo.g.R = hz; fo.g.ldr = ldZ;
       fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
       fo.relu_in = true; fo.rs_part = x2ss; fo.rs_nparts = d / 16; fo.rs_n = d;
       fo.rms_eps = T5_EPS;
-      fo.wpk = ly.pk_wo.as<float>();
-      MPR_TRY(gemm_skinny(fo, s));
+      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.pl_wo, s));
     }
     SkinnyArgs hd;
     hd.g.A = xp; hd.g.lda = ldA; hd.g.C = nullptr; hd.g.M = B; hd.g.N = V; hd.g.K = d;
     hd.rms_w = dec_final.as<float>(); hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
     hd.amax_val = ws->part_val.as<float>();
     hd.amax_idx = ws->part_idx.as<int32_t>();
-    hd.wpk = pk_lm_head.as<float>();
-    MPR_TRY(gemm_skinny(hd, s));
-    MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), nparts, B, unf, toks,
+    int np = 0;
+    MPR_TRY(dec_gemm(hd, pk_lm_head, pl_lm_head, s, &np));
+    MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks,
                         T1, t + 1, eos, pad, shared.as<float>(), d,
                         t + 1 < max_new ? xp : nullptr, s, ldA));
   }

@@ -245,7 +245,8 @@ class T5VisionModel(nn.Module):
             dev = DeviceT5(sd, self.device)
             if _lib.separate_decode_stream(self.device.index if self.device.index is not None
                                            else torch.cuda.current_device()):
-                dev.set_decode_stream(_lib.role_stream(self.device, "decode"))
+                dev.set_decode_stream(_lib.role_stream(self.device, "decode"),
+                                      slot=DeviceT5.PREDICT_SLOT)
             return dev
         return self._handle("t5", "T5_model.", build, lambda dev, sd: dev.update(sd))
 

@@ -78,14 +78,15 @@ class ServingOptions:
 
 
 class _Call:
-    """One generate call of the loop: its slot and stream, device token tensors and, once the
-    call is over, the pinned host copies + their event."""
-    __slots__ = ("slot", "stream", "toks", "items", "steps")
+    """One generate call of the loop: its slot and stream, device token tensors (one per <= 16-row
+    piece) and, once the call is over, the pinned host copies + their event."""
+    __slots__ = ("slot", "stream", "toks", "items", "steps", "refs")
 
     def __init__(self, slot, stream, toks):
         self.slot, self.stream, self.toks = slot, stream, toks
         self.items = None   # [(pinned host tokens, done event), ...] when finished
         self.steps = None   # decode steps launched
+        self.refs = 0       # batches not yet handed out that own one of its pieces
 
 
 class ServingLoop:
@@ -103,6 +104,7 @@ class ServingLoop:
         while len(model._s_gen) < opts.depth:
             model._s_gen.append(_lib.role_stream(model.device, f"gen:{len(model._s_gen)}"))
         self.pending = deque()  # one _Call per generate call, in launch order
+        self.order = deque()    # per batch, in order: its pieces [(call, piece index), ...]
         self.held = []          # prepared batches waiting for the rest of their decode group
         self.ready = deque()    # (batch, prefetched handles) in order
         self.calls = 0
@@ -195,6 +197,7 @@ class ServingLoop:
                 self._advance(call)
 
     def _launch(self, inputs):
+        """One generate call over 1-8 pieces of <= 16 rows; returns its _Call."""
         m = self.m
         slot = self.calls % self.o.depth
         self.calls += 1
@@ -222,62 +225,102 @@ class ServingLoop:
                 self.steps_run.append(call.steps)
                 self._copy_out(call)
         self.pending.append(call)
+        return call
+
+    def _flush_held(self):
+        """Launch the held batches' decode group (one piece each)."""
+        if not self.held:
+            return
+        call = self._launch(self.held)
+        for j in range(len(self.held)):
+            call.refs += 1
+            self.order.append([(call, j)])
+        self.held = []
 
     def _add(self, prepared) -> bool:
-        """Queue a prepared batch: grouped with its neighbours (<= 16 rows) or alone.  Returns
-        whether a generate call was launched."""
-        if self.o.decode_group > 1 and prepared[0].shape[0] <= 16:
+        """Queue a prepared batch: grouped with its neighbours (<= 16 rows) or alone.  A batch of
+        more than 16 rows (a DataLoader with batch_size > 16, a C5 batch of 256 questions) is
+        decoded as 16-row pieces, up to 8 per generate call, as predict() decodes it; its answers
+        come out once every piece is done.  Returns whether a generate call was launched."""
+        combined, mask = prepared
+        rows = combined.shape[0]
+        if self.o.decode_group > 1 and rows <= 16:
             self.held.append(prepared)
             if len(self.held) < self.o.decode_group:
                 return False
-            self._launch(self.held)
-            self.held = []
+            self._flush_held()
             return True
-        if self.held:
-            self._launch(self.held)
-            self.held = []
-        self._launch([prepared])
+        self._flush_held()
+        pieces = [(combined[i:i + 16], mask[i:i + 16]) for i in range(0, max(rows, 1), 16)]
+        owned = []
+        for g in range(0, len(pieces), 8):
+            call = self._launch(pieces[g:g + 8])
+            call.refs += 1
+            owned += [(call, j) for j in range(len(pieces[g:g + 8]))]
+        self.order.append(owned)
         return True
 
     def _hand_out(self, drain=False):
-        """Answers of the oldest calls whose host copies are complete, in order (the host
-        blocks on the oldest only when more than depth + 2 calls are outstanding, or at the end:
-        a slot's next call is ordered behind its previous one, and a blocked host would leave
+        """Answers of the oldest batches whose pieces' host copies are complete, in order (the
+        host blocks on the oldest only when more than depth + 2 calls are outstanding, or at the
+        end: a slot's next call is ordered behind its previous one, and a blocked host would leave
         the tower stream without its next pass)."""
         m = self.m
-        while self.pending:
-            call = self.pending[0]
+        while self.order:
+            owned = self.order[0]
+            calls = list(dict.fromkeys(c for c, _ in owned))
             if not (drain or len(self.pending) > self.o.depth + 2):
-                if call.items is None or not call.items[-1][1].query():
+                if any(c.items is None or not c.items[-1][1].query() for c in calls):
                     return
-            self._advance(call, wait=True)
-            self.pending.popleft()
-            for item in call.items:
-                yield m._finish(*item)
+            for c in calls:
+                self._advance(c, wait=True)
+            self.order.popleft()
+            for c in calls:
+                c.refs -= 1
+            while self.pending and self.pending[0].refs == 0 and self.pending[0].items is not None:
+                self.pending.popleft()
+            if len(owned) == 1:
+                c, j = owned[0]
+                yield m._finish(*c.items[j])
+            else:  # a batch decoded as pieces: its rows back in order, trimmed as one batch
+                for c, j in owned:
+                    c.items[j][1].synchronize()
+                host = torch.cat([c.items[j][0] for c, j in owned])
+                yield m._finish(host, owned[-1][0].items[owned[-1][1]][1])
+
+    def drain(self):
+        """Finish every generate call still in flight (their slots free for other work)."""
+        for call in list(self.pending):
+            if call.items is None:
+                self._advance(call, wait=True)
 
     def run(self, batches):
         m = self.m
         self.it = iter(batches)
-        while True:
-            self._pump()
-            if not self.ready:
+        try:
+            while True:
+                self._pump()
+                if not self.ready:
+                    self._refill()
+                if not self.ready:
+                    break
+                batch, pre = self.ready.popleft()
                 self._refill()
-            if not self.ready:
-                break
-            batch, pre = self.ready.popleft()
-            self._refill()
-            m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
-            with torch.cuda.stream(m._s_prep):
-                with torch.no_grad():
-                    combined, mask, _ = m.prepare_input(batch, _pre=pre, _handles=self._handles())
-            self._pump()
-            if not self._add((combined, mask)):
-                continue
-            yield from self._hand_out()
-        if self.held:
-            self._launch(self.held)
-            self.held = []
-        yield from self._hand_out(drain=True)
+                m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
+                with torch.cuda.stream(m._s_prep):
+                    with torch.no_grad():
+                        combined, mask, _ = m.prepare_input(batch, _pre=pre,
+                                                            _handles=self._handles())
+                self._pump()
+                if not self._add((combined, mask)):
+                    continue
+                yield from self._hand_out()
+            self._flush_held()
+            yield from self._hand_out(drain=True)
+        finally:
+            # a consumer that stops early (or drops the generator) leaves no decode in flight
+            # on the loop's slots: a later generate on one of them would be refused
+            self.drain()
 
 
 def lookahead(batches, model):

@@ -48,6 +48,11 @@ def _layers(sd: dict, stack: str) -> int:
 class DeviceT5:
     """T5ForConditionalGeneration arithmetic on one GPU (handle into libmpr)."""
 
+    # generate() (predict()) decodes on workspace slots of its own (4, and 5 for more than 128
+    # rows): a serving loop's calls in flight on slots 0-3 never block it, and it never blocks
+    # them
+    PREDICT_SLOT = 4
+
     def __init__(self, sd: dict, device, scale_decoder_outputs: bool = True,
                  max_distance: int = 128):
         _lib.ensure_device(device)
@@ -186,7 +191,8 @@ class DeviceT5:
             # two workspace slots and streams at once (each loop's rows bit-identical to a call
             # of its own; the caller's stream waits for both)
             cur = torch.cuda.current_stream(self.device)
-            sts = [_lib.role_stream(self.device, f"gen:{j}") for j in range(2)]
+            sts = [_lib.role_stream(self.device, f"gen:{j}" if slot < self.PREDICT_SLOT
+                                    else f"pgen:{j}") for j in range(2)]
             for st in sts:
                 st.wait_stream(cur)
             for gi, grp in enumerate(groups):
@@ -197,7 +203,7 @@ class DeviceT5:
                 with torch.cuda.stream(st):
                     o = self.generate_batches_padded(grp, max_new_tokens, decoder_start_token_id,
                                                      eos_token_id, pad_token_id,
-                                                     slot=(slot + gi) % 2)
+                                                     slot=slot + gi % 2)
                 for t in o:
                     t.record_stream(cur)
                 outs += o
@@ -304,12 +310,13 @@ class DeviceT5:
         B, L, _ = embeds_.shape
         if chunk <= 0 or B > 16 or max_new_tokens <= chunk:
             toks = self.generate_padded(embeds, mask, max_new_tokens, decoder_start_token_id,
-                                        eos_token_id, pad_token_id)
+                                        eos_token_id, pad_token_id, slot=self.PREDICT_SLOT)
             self.last_steps_run = int(max_new_tokens)
             return self.trim(toks, eos_token_id)
         out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
         steps = ctypes.c_int32(0)
-        _lib.call("mpr_t5_generate_stop", self._h, 0, _lib.ptr(embeds_), _lib.ptr(mask_), B, L,
+        _lib.call("mpr_t5_generate_stop", self._h, self.PREDICT_SLOT, _lib.ptr(embeds_),
+                  _lib.ptr(mask_), B, L,
                   int(max_new_tokens), int(decoder_start_token_id), int(eos_token_id),
                   int(pad_token_id), chunk, _lib.ptr(out), ctypes.byref(steps), self._stream())
         self.last_steps_run = int(steps.value)
