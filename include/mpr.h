@@ -63,7 +63,8 @@ int mpr_index_destroy(mpr_index* index);
 int64_t mpr_index_rows(const mpr_index* index);
 /* Top-k nearest rows for each of b queries q_dev [b, d] (fp32, device).  ids_dev [b, k] int64,
  * dist_dev [b, k] fp32: L2 distance (sqrt(max(|q|^2+|x|^2-2q.x, 0)), cdist mm-path) or cosine
- * similarity.  Order: best first; exact ties broken by lowest id.  1 <= k <= 64, k <= n. */
+ * similarity.  Order: best first; exact ties broken by lowest id.  1 <= k <= 16384, k <= n
+ * (k > 64: the full score rows, then a per-query radix select). */
 int mpr_index_search(mpr_index* index, const float* q_dev, int32_t b, int32_t k, int64_t* ids_dev,
                      float* dist_dev, void* stream);
 /* Queries of the last search on `stream` that took the exact fallback of the coarse large-batch
@@ -316,21 +317,33 @@ int mpr_gather_rows(const float* table, const int32_t* ids, int64_t n, int32_t d
 int mpr_embed_bwd(const float* dY, int32_t d, const int32_t* uniq, const int32_t* offs,
                   const int32_t* pos, int32_t n_uniq, float* dW, void* stream);
 
-/* ---- decode-step projection (the kernel behind the decoder projections of mpr_t5_generate*,
- * architectures/T5VisionModel.py:200-205; exposed for kernel-level tests and benchmarks) ----
- *   mpr_planes_bytes / mpr_planes_pack: the three-bf16-plane image of W [n, k] (k % 32 == 0;
- *   fp32 W, row-major) into `planes` (16-byte aligned, mpr_planes_bytes(n, k) bytes).
- *   mpr_rows_gemm: C[M,N] = R + act(s_m * sum_k A'[m,k] W[n,k]) on that image, fp32-accurate:
- *   A' = rms_w * A and s_m = rsqrt(mean_k A[m,:]^2 + eps) when rms_w is given (T5's RMSNorm
- *   folded into the projection), else A' = A, s_m = 1; act 0 none / 2 relu; R optional (may alias
- *   C).  With amax_val/amax_idx (C, R null): per row the best column (lowest on ties) of each of
- *   *nparts column parts, [M, *nparts].  Each row's results depend only on K, not on M. */
-int64_t mpr_planes_bytes(int64_t n, int32_t k);
-int mpr_planes_pack(const float* W, int64_t n, int32_t k, void* planes, void* stream);
-int mpr_rows_gemm(const float* A, int64_t lda, const void* planes, float* C, int64_t ldc,
-                  int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr, int32_t act,
-                  const float* rms_w, float eps, float* amax_val, int32_t* amax_idx,
-                  int32_t* nparts, void* stream);
+/* ---- cosine_similarity with broadcasting (utils.py:57-62, every layout the reference takes;
+ * the aligned-rows and [B,1,D] x [1,N,D] forms run mpr_cosine_rows / the index scan) ----
+ *   mpr_dot_reduce: out[o] = sum_t a[off_a(o) + t * a_axis_stride] * b[off_b(o) + t *
+ *   b_axis_stride], t < axis_len (sqrt of it with take_sqrt), for every o of the row-major
+ *   out_shape [nd], off_x(o) = sum_d o_d * x_strides[d] (element strides, 0 = broadcast).
+ *   mpr_cos_combine: out[o] = w12[.] / max(n1[.] * n2[.], eps) over out_shape, each operand by
+ *   its own strides (the broadcasting of the three reductions). */
+int mpr_dot_reduce(const float* a, const float* b, int32_t nd, const int64_t* out_shape,
+                   const int64_t* a_strides, const int64_t* b_strides, int64_t axis_len,
+                   int64_t a_axis_stride, int64_t b_axis_stride, int32_t take_sqrt, float* out,
+                   void* stream);
+int mpr_cos_combine(const float* w12, const float* n1, const float* n2, int32_t nd,
+                    const int64_t* out_shape, const int64_t* w12_strides,
+                    const int64_t* n1_strides, const int64_t* n2_strides, float eps, float* out,
+                    void* stream);
+
+/* ---- grouped-decode projection (the kernel behind the decoder projections of
+ * mpr_t5_generate_batches / _begin for more than 16 rows, architectures/T5VisionModel.py:200-205;
+ * exposed for kernel-level tests and benchmarks) ----
+ *   mpr_dec_gemm: C[M,N] = R + act(s_m * sum_k A'[m,k] W[n,k]), M <= 256, K % 32 == 0,
+ *   N % 16 == 0, fp32 W [N, K] (row stride ldw), fp32-accurate: A' = rms_w * A and
+ *   s_m = rsqrt(mean_k A[m,:]^2 + eps) when rms_w is given (T5's RMSNorm folded into the
+ *   projection), else A' = A, s_m = 1; act 0 none / 2 relu; R optional (may alias C).  Each row's
+ *   results depend only on (K, N), not on M. */
+int mpr_dec_gemm(const float* A, int64_t lda, const float* W, int64_t ldw, float* C, int64_t ldc,
+                 int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr, int32_t act,
+                 const float* rms_w, float eps, void* stream);
 
 /* ---- measurement (bench.py roofline; no reference counterpart) --------------------------------
  * kind 1 = tiled f32-MFMA GEMM, 2 = skinny (decode) GEMM, 0 = off.  While enabled, every launch

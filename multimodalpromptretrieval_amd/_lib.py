@@ -123,11 +123,13 @@ SIGNATURES = [
     ("mpr_gather_rows", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     ("mpr_embed_bwd", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                                 c_void_p, c_void_p]),
-    ("mpr_planes_bytes", c_int64, [c_int64, c_int32]),
-    ("mpr_planes_pack", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
-    ("mpr_rows_gemm", c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32, c_int32,
-                                c_int32, c_void_p, c_int64, c_int32, c_void_p, c_float, c_void_p,
-                                c_void_p, POINTER(c_int32), c_void_p]),
+    ("mpr_dot_reduce", c_int32, [c_void_p, c_void_p, c_int32, I64P, I64P, I64P, c_int64,
+                                 c_int64, c_int64, c_int32, c_void_p, c_void_p]),
+    ("mpr_cos_combine", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, I64P, I64P, I64P, I64P,
+                                  c_float, c_void_p, c_void_p]),
+    ("mpr_dec_gemm", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32,
+                               c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p, c_float,
+                               c_void_p]),
 ]
 
 

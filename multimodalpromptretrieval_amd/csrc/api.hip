@@ -141,8 +141,8 @@ int mpr_index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_
     MPR_REQUIRE(ix != nullptr, "search: null index");
     MPR_REQUIRE(b == 0 || (q && ids && dist), "search: null buffer");
     if (b == 0) return MPR_OK;
-    MPR_REQUIRE(k >= 1 && k <= 64 && k <= ix->n, "search: k=%d (1..64, <= %lld rows)", k,
-                (long long)ix->n);
+    MPR_REQUIRE(k >= 1 && k <= SELECT_MAX_K && k <= ix->n, "search: k=%d (1..%d, <= %lld rows)",
+                k, SELECT_MAX_K, (long long)ix->n);
     auto& slot = ix->ws[stream];
     if (!slot) slot = std::make_unique<DevBuf>();
     // a growth frees the old buffer: hipFree waits for the device, so work of earlier searches
@@ -411,21 +411,7 @@ int t5_load(T5Model* m, const float* const* t, const int32_t* enc_lut, const int
     MPR_TRY(dst.ensure((size_t)packed_rows16_elems(n, k) * 4));
     return pack_rows16(src.as<float>(), n, k, k, dst.as<float>(), nullptr);
   };
-  // three-bf16-plane images of the same weights for the row-count independent decode GEMM
-  auto planes = [](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
-    MPR_TRY(dst.ensure((size_t)packed_planes_elems(n, k) * 2));
-    return pack_planes(src.as<float>(), n, k, k, dst.ptr, nullptr);
-  };
   for (auto& ly : m->dec) {
-    if (m->rows) {
-      MPR_TRY(planes(ly->pl_qkv, ly->qkv, 3 * inner, d));
-      MPR_TRY(planes(ly->pl_o, ly->o, d, inner));
-      MPR_TRY(planes(ly->pl_cq, ly->cq, inner, d));
-      MPR_TRY(planes(ly->pl_co, ly->co, d, inner));
-      MPR_TRY(planes(ly->pl_wi, ly->wi, dff, d));
-      MPR_TRY(planes(ly->pl_wo, ly->wo, d, dff));
-      continue;
-    }
     MPR_TRY(pack(ly->pk_qkv, ly->qkv, 3 * inner, d));
     MPR_TRY(pack(ly->pk_o, ly->o, d, inner));
     MPR_TRY(pack(ly->pk_cq, ly->cq, inner, d));
@@ -433,10 +419,7 @@ int t5_load(T5Model* m, const float* const* t, const int32_t* enc_lut, const int
     MPR_TRY(pack(ly->pk_wi, ly->wi, dff, d));
     MPR_TRY(pack(ly->pk_wo, ly->wo, d, dff));
   }
-  if (m->rows)
-    MPR_TRY(planes(m->pl_lm_head, m->lm_head, m->V, d));
-  else
-    MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
+  MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
   if (m->fold) MPR_TRY(m->build_folded());
   MPR_HIP(hipDeviceSynchronize());
   return MPR_OK;
@@ -471,8 +454,8 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
       m->fold = !(e && e[0] == '0');
       // the decode projections on gemm_rows whenever every contraction length allows it
       const char* g = getenv("MPR_DECODE_GEMM");
-      m->rows = !(g && strcmp(g, "skinny") == 0) && gemm_rows_ok(d) && gemm_rows_ok(m->inner) &&
-                gemm_rows_ok(dff) && gemm_rows_ok(m->inner + d);
+      m->rows = !(g && strcmp(g, "skinny") == 0) && gemm_dec_ok(d, 3 * m->inner) &&
+                gemm_dec_ok(m->inner, d) && gemm_dec_ok(dff, d) && gemm_dec_ok(d, dff);
     }
     MPR_TRY(t5_load(m.get(), t, enc_lut, dec_lut, /*fresh=*/true));
     *out = m.release();

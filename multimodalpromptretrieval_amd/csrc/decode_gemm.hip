@@ -1,31 +1,30 @@
-// decode_gemm.hip — the decode-step projections of T5 greedy search at any row count (gfx950).
+// decode_gemm.hip — the decoder projections of grouped greedy decodes (32-256 rows per step).
 //
 // Reference: the per-token decoder of transformers' T5 as driven by
 // architectures/T5VisionModel.py:200-205 (generate, greedy, max_new_tokens=20): every step runs
-// q|k|v, o, cross-q, cross-o, wi, wo of every decoder layer and the tied lm_head over the rows of
-// the batch.  A 16-row predict() puts 16 rows through each projection; the serving loop's grouped
-// decodes 128 (eight batches), config C5's 256-question batches 128-256.
+// q|k|v, o, cross-q, cross-o, wi, wo of every decoder layer over the rows of the batch.  The serving
+// loop's grouped decodes put 128 rows (eight 16-row batches) through every projection, config C5's
+// 256-question batches 256; a 16-row predict() keeps the skinny GEMV chain (gemm.hip).
 //
-// C[m, n] = R[m, n] + act(scale_m * sum_k A'[m, k] W[n, k])   on v_mfma_f32_16x16x32_bf16, fp32
-// accurate: W arrives as three bf16 planes pre-split once at load (pack_planes, fragment order,
-// one contiguous 1 KiB per plane and wave load), each A fragment is split into three planes in
-// registers as it is loaded (x3.h), and the six cross products are accumulated in fp32 (x3.h).
+//   C[m, n] = R[m, n] + act(s_m * sum_k A'[m, k] W[n, k])      (T5's RMSNorm folded: A' = ln_w A,
+//                                                              s_m = rsqrt(mean_k A[m,:]^2 + eps))
+// on v_mfma_f32_16x16x32_bf16, fp32 accurate: both operands split into three bf16 planes (x3.h),
+// six cross products accumulated in fp32.
 //
-// Block = 8 waves over one output tile of WM x WN 16x16 sub-tiles; wave w owns the contiguous
-// k-step slice [w * nks / 8, (w + 1) * nks / 8) of the 32-deep k steps and keeps every sub-tile
-// of the block in its accumulators, loading its operands straight into registers (no LDS
-// staging: no operand is shared between the waves of a block).  The eight partial tiles are
-// summed through LDS in wave order.  So every output element is summed in one order fixed by K
-// alone — the block tile and the row count only decide which block computes it — and rows are
-// independent: a batch's rows give the same bits alone or inside a grouped decode.
-//
-// The options are gemm_skinny's (kernels.h, SkinnyArgs), each a template flag:
-//   RMS      A' = ln_w * A, scale_m = rsqrt(mean_k A[m,:]^2 + eps) (sums of squares of the loaded
-//            A values: per lane, across the 4 lanes of a row, across waves in order)
-//   RES      + R[m, n] (R may alias C)      RELU   max(., 0) before RES
-//   AMAX     per (row, block) best column (lowest index on ties) instead of C: greedy head
-//   RELU_IN  A' = max(A, 0)                  RSCALE scale_m from another launch's partial sums
-//   SSQ      per (row, 16-column tile < ssq_cols) sums of squares of the output (folded chain)
+// What bounds a decode projection at these row counts is how many CUs stream distinct weight bytes
+// (~25 GB/s per CU from HBM; measured: a 144-block launch over t5-base's q|k|v ran 12 us at
+// 0.9 TB/s), so the work is cut along N AND K into >= ~200 blocks, every weight element read by
+// exactly one block, and every block covers ALL rows of the launch:
+//   * block (column block cb, K slice ks): 16 * DN output columns x every row, K range
+//     [ks * Kb, (ks + 1) * Kb).  Its fp32 weight slice is loaded once, split into three bf16 planes
+//     in LDS (fragment order: one conflict-free ds_read_b128 per plane and lane);
+//   * each wave owns (row tile, column tiles) pairs and sums its outputs sequentially over the K
+//     slice, its A fragments loaded straight from L2 into registers and split there;
+//   * KS = K / Kb > 1: partial tiles go to a workspace [KS][M][N] and dec_finish_kernel sums them
+//     in slice order and applies the epilogue (row scale, ReLU, residual).
+// The K partition (Kb) is a function of (K, N) only (dec_plan): a row's result does not depend on
+// how many rows share the launch — a batch's rows give the same bits in a 128-row serving-loop
+// group and in a 256-row C5 decode.
 #include <algorithm>
 #include <cstdlib>
 
@@ -35,390 +34,292 @@
 namespace mpr {
 namespace {
 
+using x3::bf16x4;
 using x3::bf16x8;
 using x3::f32x4;
 
-constexpr int RW = 8;  // waves per block; the K range of every output splits into RW slices
+constexpr int DW = 8;        // waves per block
+constexpr int DN = 2;        // 16-column tiles per block
+constexpr int KB_MAX = 512;  // LDS: 3 planes x DN tiles x Kb x 2 B = 96 KiB at 512
 
-enum : int { RF_RMS = 1, RF_RES = 2, RF_RELU = 4, RF_AMAX = 8, RF_RELU_IN = 16,
-             RF_RSCALE = 32, RF_SSQ = 64 };
+enum : int { DF_RMS = 1, DF_RES = 2, DF_RELU = 4 };
 
-__global__ __launch_bounds__(256) void pack_planes_kernel(const float* __restrict__ W, int64_t N,
-                                                          int64_t K, int64_t ldw, int64_t nks,
-                                                          __bf16* __restrict__ out) {
-  // one (16-column tile t, 32-deep step s, lane l) per thread: 8 values -> 3 planes
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = cdiv(N, 16) * nks * 64;
-  if (q >= total) return;
-  const int l = (int)(q & 63);
-  const int64_t ts = q >> 6, t = ts / nks, s = ts % nks;
-  const int64_t row = t * 16 + (l & 15), k0 = s * 32 + 8 * (l >> 4);
-  f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
-  if (row < N) {
-    lo = *reinterpret_cast<const f32x4*>(W + row * ldw + k0);
-    hi = *reinterpret_cast<const f32x4*>(W + row * ldw + k0 + 4);
-  }
-  bf16x8 h0, h1, h2;
-  x3::split8(lo, hi, h0, h1, h2);
-  bf16x8* o = reinterpret_cast<bf16x8*>(out + (ts * 3) * 512) + l;
-  o[0] = h0;
-  o[64] = h1;
-  o[128] = h2;
-}
+struct DecArgs {
+  const float* A;
+  int64_t lda;
+  const float* W;  // [N, K] fp32, row-major
+  int64_t ldw;
+  const float* R;  // residual (may alias C)
+  int64_t ldr;
+  float* C;
+  int64_t ldc;
+  const float* rms_w;
+  float eps;
+  int M, N, K, Kb, KS;
+  float* part;     // [KS][M][N] (KS > 1)
+  float* part_ss;  // [KS][M] partial sums of squares of the A rows (RMS, KS > 1)
+};
 
-template <int WM, int WN, int F>
-__global__ __launch_bounds__(512) void gemm_rows_kernel(SkinnyArgs sa, const __bf16* wpl) {
-  constexpr bool RMS = (F & RF_RMS) != 0, RES = (F & RF_RES) != 0, RELU = (F & RF_RELU) != 0,
-                 AMAX = (F & RF_AMAX) != 0, RELU_IN = (F & RF_RELU_IN) != 0,
-                 RSCALE = (F & RF_RSCALE) != 0, SSQ = (F & RF_SSQ) != 0;
-  static_assert(!(RMS && RSCALE), "one row-scale source");
-  constexpr int ROWS = 16 * WM;
-  // LDS: partial tiles [RW][WM][WN][64 lanes] f32x4 | row sums of squares [RW][ROWS] | row scales
-  __shared__ __attribute__((aligned(16))) float smem[RW * WM * WN * 256 + RW * ROWS + ROWS];
-  f32x4* red = reinterpret_cast<f32x4*>(smem);
-  float* ssq_s = smem + RW * WM * WN * 256;
-  float* rsc_s = ssq_s + RW * ROWS;
-
-  const GemmArgs& a = sa.g;
-  const int M = a.M, N = a.N, K = a.K;
-  const int nks = K >> 5;
-  const int ntiles = (N + 15) >> 4;
-  const int nrb = (M + ROWS - 1) / ROWS;
-  // XCD-aware order: blocks are dealt round-robin over the 8 XCDs; tile t (column block major,
-  // row block minor) goes so that each XCD walks a contiguous run, i.e. the row blocks of one
-  // column block (same weight columns) share an XCD's L2
-  const int total = gridDim.x, hw = blockIdx.x;
-  const int xcd = hw & 7, slot = hw >> 3, qq = total >> 3, rr = total & 7;
-  const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
-  const int cb = t / nrb, rb = t - cb * nrb;
-  const int m0 = rb * ROWS;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 15, lg = lane >> 4;
-  const int s_lo = wave * nks / RW, s_hi = (wave + 1) * nks / RW;
-
-  // RSCALE: the rows' partial sums of squares (<= 64 per row), lane = partial; wave w takes
-  // rows w, w + 8, ... of the block; loaded first, summed after the main loop
-  constexpr int RPW = (ROWS + RW - 1) / RW;
-  float rsp[RSCALE ? RPW : 1];
-  if constexpr (RSCALE) {
+// One (row tile i, the wave's column tiles) work unit: A fragments of the K slice straight into
+// registers (a batch of loads issued first), then per 32-deep step the split and 6 MFMAs per
+// column tile against the LDS planes.  *ss = the row's sum of squares over the slice (RMS).
+template <int F, int NTW>
+__device__ __forceinline__ void dec_unit(const DecArgs& a, const __bf16* wl, int nsb, int k0,
+                                         int i, int j0, f32x4 (&acc)[NTW], float* ss) {
+  constexpr bool RMS = (F & DF_RMS) != 0;
+  const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+  const int row = i * 16 + li;
+  const bool rok = row < a.M;
+  const float* ar = a.A + (int64_t)min(row, a.M - 1) * a.lda + k0 + 8 * lg;
+  const float* gr = RMS ? a.rms_w + k0 + 8 * lg : nullptr;
+  const int PL = nsb * DN * 64;  // bf16x8 per plane
 #pragma unroll
-    for (int u = 0; u < RPW; ++u) {
-      const int r = wave + u * RW, row = min(m0 + r, M - 1);
-      rsp[u] = (r < ROWS && lane < sa.rs_nparts) ? sa.rs_part[(int64_t)row * sa.rs_nparts + lane]
-                                                 : 0.f;
-    }
-  }
-
-  const float* arow[WM];
-  bool rok[WM];
+  for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float s2 = 0.f;
+  constexpr int PS = 4;  // k steps per batch of loads
+  for (int s0 = 0; s0 < nsb; s0 += PS) {
+    f32x4 va[PS][2], vg[PS][2];
 #pragma unroll
-  for (int i = 0; i < WM; ++i) {
-    const int row = m0 + i * 16 + li;
-    rok[i] = row < M;
-    arow[i] = a.A + (int64_t)min(row, M - 1) * a.lda + 8 * lg;
-  }
-  const __bf16* wrow[WN];
-#pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int ct = min(cb * WN + j, ntiles - 1);  // a tile past N re-reads the last; not stored
-    wrow[j] = wpl + (int64_t)ct * nks * 3 * 512 + lane * 8;
-  }
-
-  f32x4 acc[WM][WN];
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss[WM];
-#pragma unroll
-  for (int i = 0; i < WM; ++i) ss[i] = 0.f;
-
-  // two k steps in flight: slot b holds step s's weight planes, A values (and RMS weights)
-  bf16x8 rw[2][WN][3];
-  f32x4 ra[2][WM][2];
-  f32x4 rg[2][RMS ? 2 : 1];
-  auto load = [&](int b, int s) {
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        rw[b][j][p] = *reinterpret_cast<const bf16x8*>(wrow[j] + (int64_t)(s * 3 + p) * 512);
-#pragma unroll
-    for (int i = 0; i < WM; ++i) {
-      ra[b][i][0] = *reinterpret_cast<const f32x4*>(arow[i] + s * 32);
-      ra[b][i][1] = *reinterpret_cast<const f32x4*>(arow[i] + s * 32 + 4);
-    }
-    if constexpr (RMS) {
-      rg[b][0] = *reinterpret_cast<const f32x4*>(sa.rms_w + s * 32 + 8 * lg);
-      rg[b][1] = *reinterpret_cast<const f32x4*>(sa.rms_w + s * 32 + 8 * lg + 4);
-    }
-  };
-  auto compute = [&](int b) {
-#pragma unroll
-    for (int i = 0; i < WM; ++i) {
-      f32x4 v0 = ra[b][i][0], v1 = ra[b][i][1];
-      if (!rok[i]) v0 = v1 = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (RELU_IN) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v0[e] = v0[e] > 0.f ? v0[e] : 0.f;
-          v1[e] = v1[e] > 0.f ? v1[e] : 0.f;
-        }
+    for (int u = 0; u < PS; ++u) {
+      const int s = min(s0 + u, nsb - 1);
+      va[u][0] = *reinterpret_cast<const f32x4*>(ar + s * 32);
+      va[u][1] = *reinterpret_cast<const f32x4*>(ar + s * 32 + 4);
+      if constexpr (RMS) {
+        vg[u][0] = *reinterpret_cast<const f32x4*>(gr + s * 32);
+        vg[u][1] = *reinterpret_cast<const f32x4*>(gr + s * 32 + 4);
       }
+    }
+#pragma unroll
+    for (int u = 0; u < PS; ++u) {
+      const int s = s0 + u;
+      if (s >= nsb) break;
+      f32x4 v0 = va[u][0], v1 = va[u][1];
+      if (!rok) v0 = v1 = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (RMS) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ss[i] += v0[e] * v0[e];
+        for (int e = 0; e < 4; ++e) s2 += v0[e] * v0[e];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ss[i] += v1[e] * v1[e];
-        v0 = rg[b][0] * v0;
-        v1 = rg[b][1] * v1;
+        for (int e = 0; e < 4; ++e) s2 += v1[e] * v1[e];
+        v0 = vg[u][0] * v0;
+        v1 = vg[u][1] * v1;
       }
       bf16x8 a0, a1, a2;
       x3::split8(v0, v1, a0, a1, a2);
 #pragma unroll
-      for (int j = 0; j < WN; ++j) {
+      for (int t = 0; t < NTW; ++t) {
+        // planes image in LDS: [plane][step][tile][lane] bf16x8
+        const bf16x8* wp = reinterpret_cast<const bf16x8*>(wl) + ((s * DN + j0 + t) * 64 + lane);
+        const bf16x8 w0 = wp[0], w1 = wp[PL], w2 = wp[2 * PL];
+        f32x4 c = acc[t];
         // D[row = weight column n][col = activation row m]; terms in increasing magnitude
-        f32x4 c = acc[i][j];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[b][j][2], a0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[b][j][1], a1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[b][j][0], a2, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[b][j][1], a0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[b][j][0], a1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[b][j][0], a0, c, 0, 0, 0);
-        acc[i][j] = c;
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, a0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, a1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, a2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, a0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, a1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, a0, c, 0, 0, 0);
+        acc[t] = c;
       }
     }
-  };
-  if (s_lo < s_hi) load(0, s_lo);
-  for (int s = s_lo; s < s_hi; s += 2) {
-    if (s + 1 < s_hi) load(1, s + 1);
-    compute(0);
-    if (s + 1 < s_hi) {
-      if (s + 2 < s_hi) load(0, s + 2);
-      compute(1);
-    }
   }
-
-  // partial tiles and row sums of squares to LDS, summed in wave order below
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j) red[((wave * WM + i) * WN + j) * 64 + lane] = acc[i][j];
   if constexpr (RMS) {
-#pragma unroll
-    for (int i = 0; i < WM; ++i) {
-      float v = ss[i];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (lane < 16) ssq_s[wave * ROWS + i * 16 + lane] = v;
-    }
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    *ss = s2;
   }
-  if constexpr (RSCALE) {
+}
+
+template <int F>
+__device__ __forceinline__ void dec_store(const DecArgs& a, int ks, int i, int n0, f32x4 v,
+                                          float ss, bool ss_writer) {
+  constexpr bool RMS = (F & DF_RMS) != 0, RES = (F & DF_RES) != 0, RELU = (F & DF_RELU) != 0;
+  const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+  const int m = i * 16 + li;
+  if (m >= a.M || n0 >= a.N) return;
+  const int n = n0 + 4 * lg;
+  if (a.KS > 1) {
+    *reinterpret_cast<f32x4*>(a.part + ((int64_t)ks * a.M + m) * a.N + n) = v;
+    if (RMS && ss_writer && lg == 0) a.part_ss[(int64_t)ks * a.M + m] = ss;
+    return;
+  }
+  if constexpr (RMS) v = v * (1.0f / sqrtf(ss / (float)a.K + a.eps));
+  if constexpr (RELU) {
 #pragma unroll
-    for (int u = 0; u < RPW; ++u) {
-      float v = rsp[u];
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-      const int r = wave + u * RW;
-      if (lane == 0 && r < ROWS)
-        rsc_s[r] = 1.0f / sqrtf(v / (float)sa.rs_n + sa.rms_eps);
+    for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+  }
+  if constexpr (RES) v = *reinterpret_cast<const f32x4*>(a.R + (int64_t)m * a.ldr + n) + v;
+  *reinterpret_cast<f32x4*>(a.C + (int64_t)m * a.ldc + n) = v;
+}
+
+template <int F>
+__global__ __launch_bounds__(512) void dec_part_kernel(DecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 dec_lds[];
+  const int ncb = (a.N + 16 * DN - 1) / (16 * DN);
+  // XCD-aware order: each XCD walks a contiguous run of (ks major, cb minor): its L2 holds the
+  // A columns of about one K slice
+  const int total = gridDim.x, hw = blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, qq = total >> 3, rr = total & 7;
+  const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + slot;
+  const int ks = t / ncb, cb = t - ks * ncb;
+  const int k0 = ks * a.Kb, nsb = a.Kb >> 5;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // stage the weight slice: 16 * DN rows x Kb fp32 -> three bf16 planes in fragment order
+  {
+    const int n0 = cb * 16 * DN;
+    const int q4 = a.Kb >> 2;  // float4 per weight row
+    const int nq = 16 * DN * q4;
+    const int PL = nsb * DN * 512;  // bf16 per plane
+    for (int q = tid; q < nq; q += DW * 64) {
+      const int r = q / q4, k = (q - r * q4) * 4;
+      const int n = min(n0 + r, a.N - 1);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(a.W + (int64_t)n * a.ldw + k0 + k);
+      bf16x4 h0, h1, h2;
+      x3::split3(v, h0, h1, h2);
+      const int s = k >> 5, j = r >> 4;
+      const int l = (r & 15) + 16 * ((k & 31) >> 3);
+      __bf16* p = dec_lds + ((s * DN + j) * 64 + l) * 8 + (k & 7);
+      *reinterpret_cast<bf16x4*>(p) = h0;
+      *reinterpret_cast<bf16x4*>(p + PL) = h1;
+      *reinterpret_cast<bf16x4*>(p + 2 * PL) = h2;
     }
   }
   __syncthreads();
 
-  // epilogue: wave q finishes sub-tiles q, q + 8, ... (argmax: row tiles, all WN column tiles)
-  constexpr int NQ = AMAX ? WM : WM * WN;
-  for (int q = wave; q < NQ; q += RW) {
-    const int i = AMAX ? q : q / WN;
-    const int m = m0 + i * 16 + li;  // the lane's row; its columns n0 + 4 lg .. + 3
-    float scale = sa.a_scale;
-    if constexpr (RMS) {
-      float tt = 0.f;
+  // work split: row tiles over waves; with fewer row tiles than waves, the waves of a row tile
+  // split its DN column tiles (each output is still summed by one wave over the whole slice)
+  const int nrt = (a.M + 15) >> 4;
+  if (nrt > DW / DN) {
+    for (int i = wave; i < nrt; i += DW) {
+      f32x4 acc[DN];
+      float ss = 0.f;
+      dec_unit<F, DN>(a, dec_lds, nsb, k0, i, 0, acc, &ss);
 #pragma unroll
-      for (int w = 0; w < RW; ++w) tt += ssq_s[w * ROWS + i * 16 + li];
-      scale = (1.0f / sqrtf(tt / (float)K + sa.rms_eps)) * sa.a_scale;
+      for (int j = 0; j < DN; ++j)
+        dec_store<F>(a, ks, i, (cb * DN + j) * 16, acc[j], ss, cb == 0 && j == 0);
     }
-    if constexpr (RSCALE) scale = rsc_s[i * 16 + li] * sa.a_scale;
-    if constexpr (AMAX) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
-#pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        f32x4 sum = red[(i * WN + j) * 64 + lane];
-#pragma unroll
-        for (int w = 1; w < RW; ++w) sum += red[((w * WM + i) * WN + j) * 64 + lane];
-        const int n0 = (cb * WN + j) * 16 + 4 * lg;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = sum[r] * scale;
-          const int n = n0 + r;
-          if (n < N && (v > bv || (v == bv && n < bi))) {
-            bv = v;
-            bi = n;
-          }
-        }
-      }
-#pragma unroll
-      for (int off = 16; off <= 32; off <<= 1) {
-        const float ov = __shfl_xor(bv, off, 64);
-        const int oi = __shfl_xor(bi, off, 64);
-        if (ov > bv || (ov == bv && oi < bi)) {
-          bv = ov;
-          bi = oi;
-        }
-      }
-      const int nparts = (N + 16 * WN - 1) / (16 * WN);
-      if (lane < 16 && m < M) {
-        sa.amax_val[(int64_t)m * nparts + cb] = bv;
-        sa.amax_idx[(int64_t)m * nparts + cb] = bi;
-      }
-    } else {
-      const int j = q % WN;
-      const int tile = cb * WN + j, n0 = tile * 16;
-      f32x4 sum = red[(i * WN + j) * 64 + lane];
-#pragma unroll
-      for (int w = 1; w < RW; ++w) sum += red[((w * WM + i) * WN + j) * 64 + lane];
-      f32x4 v = sum * scale;
-      if constexpr (RELU) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-      }
-      const bool ok = m < M && n0 < N;
-      if constexpr (RES) {
-        if (ok) v = *reinterpret_cast<const f32x4*>(a.R + (int64_t)m * a.ldr + n0 + 4 * lg) + v;
-      }
-      if (ok) *reinterpret_cast<f32x4*>(a.C + (int64_t)m * a.ldc + n0 + 4 * lg) = v;
-      if constexpr (SSQ) {
-        float sq = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
-        sq += __shfl_xor(sq, 16, 64);
-        sq += __shfl_xor(sq, 32, 64);
-        if (n0 < sa.ssq_cols && lane < 16 && m < M)
-          sa.ssq_out[(int64_t)m * (sa.ssq_cols / 16) + tile] = sq;
-      }
+  } else {  // <= 4 row tiles: one (row tile, column tile) pair per wave
+    const int i = wave / DN, j = wave % DN;
+    if (i < nrt) {
+      f32x4 acc[1];
+      float ss = 0.f;
+      dec_unit<F, 1>(a, dec_lds, nsb, k0, i, j, acc, &ss);
+      dec_store<F>(a, ks, i, (cb * DN + j) * 16, acc[0], ss, cb == 0 && j == 0);
     }
   }
 }
 
-struct RowsTile {
-  int wm, wn;
+// KS > 1: out[m, n] = epilogue(sum_ks part[ks][m][n]) in slice order; one block per row
+template <int F>
+__global__ __launch_bounds__(256) void dec_finish_kernel(DecArgs a) {
+  constexpr bool RMS = (F & DF_RMS) != 0, RES = (F & DF_RES) != 0, RELU = (F & DF_RELU) != 0;
+  const int m = blockIdx.x;
+  float scale = 1.f;
+  if constexpr (RMS) {
+    float ss = 0.f;
+    for (int ks = 0; ks < a.KS; ++ks) ss += a.part_ss[(int64_t)ks * a.M + m];
+    scale = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+  }
+  const int n4 = a.N >> 2;
+  for (int q = threadIdx.x; q < n4; q += 256) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(a.part + (int64_t)m * a.N + 4 * q);
+    for (int ks = 1; ks < a.KS; ++ks)
+      v += *reinterpret_cast<const f32x4*>(a.part + ((int64_t)ks * a.M + m) * a.N + 4 * q);
+    if constexpr (RMS) v = v * scale;
+    if constexpr (RELU) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+    }
+    if constexpr (RES) v = *reinterpret_cast<const f32x4*>(a.R + (int64_t)m * a.ldr + 4 * q) + v;
+    *reinterpret_cast<f32x4*>(a.C + (int64_t)m * a.ldc + 4 * q) = v;
+  }
+}
+
+struct DecPlan {
+  int Kb, KS, ncb;
 };
 
-// The block tile of a launch: the largest of these (weight bytes per A byte, VALU of the A split
-// per MFMA both fall with the tile) whose grid still puts a block on every CU; failing that the
-// one with the most blocks.  MPR_ROWS_TILE=WMxWN forces one (measurements), MPR_ROWS_BLOCKS sets
-// the target grid.
-constexpr RowsTile kTiles[] = {{2, 4}, {4, 2}, {2, 2}, {1, 4}, {4, 1}, {1, 2}, {2, 1}, {1, 1}};
-
-RowsTile pick_tile(int M, int N) {
-  static const RowsTile forced = [] {
-    const char* e = getenv("MPR_ROWS_TILE");
-    RowsTile t{0, 0};
-    if (e && sscanf(e, "%dx%d", &t.wm, &t.wn) == 2) {
-      for (const RowsTile& c : kTiles)
-        if (c.wm == t.wm && c.wn == t.wn) return t;
-    }
-    return RowsTile{0, 0};
-  }();
-  if (forced.wm) return forced;
+// The K partition of a launch: the fewest K slices (each <= KB_MAX deep, a divisor of the
+// 32-deep steps) that give the launch >= MPR_DEC_BLOCKS blocks (default 192).  A function of
+// (K, N) only, never of the row count.
+DecPlan dec_plan(int N, int K) {
   static const int target = [] {
-    const char* e = getenv("MPR_ROWS_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 240;
+    const char* e = getenv("MPR_DEC_BLOCKS");
+    return e ? std::max(1, atoi(e)) : 192;
   }();
-  RowsTile best{1, 1};
-  int64_t best_blocks = -1;
-  for (const RowsTile& c : kTiles) {
-    if (c.wm > 1 && 16 * c.wm > ((M + 15) / 16) * 16) continue;  // no mostly-empty row tiles
-    const int64_t blocks = cdiv(M, 16 * c.wm) * cdiv(N, 16 * c.wn);
-    if (blocks >= target) return c;
-    if (blocks > best_blocks) {
-      best_blocks = blocks;
-      best = c;
-    }
+  const int nks = K / 32;
+  const int ncb = (N + 16 * DN - 1) / (16 * DN);
+  int best = nks;
+  for (int d = 1; d <= nks; ++d) {
+    if (nks % d || K / d > KB_MAX) continue;
+    best = d;
+    if ((int64_t)ncb * d >= target) break;
   }
-  return best;
+  return DecPlan{K / best, best, ncb};
 }
 
-template <int WM, int WN>
-int launch_rows(const SkinnyArgs& sa, const __bf16* wpl, int F, hipStream_t s) {
-  const GemmArgs& a = sa.g;
-  const unsigned blocks = (unsigned)(cdiv(a.M, 16 * WM) * cdiv(a.N, 16 * WN));
-#define MPR_RK(f)                                                                        \
-  case f:                                                                                \
-    hipLaunchKernelGGL((gemm_rows_kernel<WM, WN, f>), dim3(blocks), dim3(512), 0, s, sa, \
-                       wpl);                                                             \
-    break;
-  switch (F) {
-    MPR_RK(RF_RMS)
-    MPR_RK(RF_RES)
-    MPR_RK(RF_RMS | RF_RELU)
-    MPR_RK(RF_AMAX | RF_RMS)
-    MPR_RK(RF_SSQ)
-    MPR_RK(RF_RELU_IN | RF_RSCALE | RF_RES)
-    default:
-      set_error("gemm_rows: option set %d is not instantiated", F);
-      return MPR_EINVAL;
-  }
-#undef MPR_RK
+template <int F>
+int launch_dec(const DecArgs& a, const DecPlan& p, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(dec_part_kernel<F>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3 * DN * KB_MAX * 2));
+  MPR_HIP(attr);
+  const size_t lds = (size_t)3 * DN * p.Kb * 2;
+  hipLaunchKernelGGL(dec_part_kernel<F>, dim3((unsigned)(p.ncb * p.KS)), dim3(DW * 64), lds, s,
+                     a);
   MPR_LAUNCHED();
+  if (p.KS > 1) {
+    hipLaunchKernelGGL(dec_finish_kernel<F>, dim3((unsigned)a.M), dim3(256), 0, s, a);
+    MPR_LAUNCHED();
+  }
   return MPR_OK;
 }
 
 }  // namespace
 
-bool gemm_rows_ok(int K) { return K > 0 && K % 32 == 0; }
+bool gemm_dec_ok(int K, int N) { return K > 0 && K % 32 == 0 && N > 0 && N % 16 == 0; }
 
-int64_t packed_planes_elems(int64_t N, int64_t K) { return cdiv(N, 16) * (K / 32) * 3 * 512; }
-
-int pack_planes(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, hipStream_t s) {
-  MPR_REQUIRE(N > 0 && K > 0 && K % 32 == 0 && ldw >= K && ldw % 4 == 0 && aligned16(W),
-              "pack_planes: bad shape N=%lld K=%lld", (long long)N, (long long)K);
-  const int64_t q = cdiv(N, 16) * (K / 32) * 64;
-  hipLaunchKernelGGL(pack_planes_kernel, dim3((unsigned)cdiv(q, 256)), dim3(256), 0, s, W, N, K,
-                     ldw, K / 32, reinterpret_cast<__bf16*>(out));
-  MPR_LAUNCHED();
-  return MPR_OK;
+size_t gemm_dec_ws_floats(int M, int N, int K) {
+  const DecPlan p = dec_plan(N, K);
+  return p.KS > 1 ? (size_t)p.KS * M * (N + 1) : 0;
 }
 
-int gemm_rows(const SkinnyArgs& sa, const void* wpl, hipStream_t s, int* amax_nparts) {
-  const GemmArgs& a = sa.g;
-  MPR_REQUIRE(a.M >= 0 && a.N >= 0 && gemm_rows_ok(a.K), "gemm_rows: bad shape M=%d N=%d K=%d",
-              a.M, a.N, a.K);
-  MPR_REQUIRE(wpl && aligned16(wpl), "gemm_rows: needs the 16-byte aligned planes image");
-  MPR_REQUIRE(a.lda % 4 == 0 && aligned16(a.A) && (!sa.rms_w || aligned16(sa.rms_w)),
-              "gemm_rows: lda must be a multiple of 4, operands 16-byte aligned");
-  MPR_REQUIRE(!a.bias && (a.act == ACT_NONE || a.act == ACT_RELU),
-              "gemm_rows: no bias, activation none or relu (the T5 decoder's projections)");
-  const bool amax = sa.amax_val != nullptr;
-  MPR_REQUIRE(!amax || (sa.amax_idx && !a.R && !a.C && a.act == ACT_NONE),
-              "gemm_rows: argmax mode takes plain logits and stores no C");
-  MPR_REQUIRE(amax || (a.C && a.N % 16 == 0 && a.ldc % 4 == 0 && aligned16(a.C) &&
-                       (!a.R || (a.ldr % 4 == 0 && aligned16(a.R)))),
-              "gemm_rows: N must be a multiple of 16, C/R rows 16-byte aligned");
-  MPR_REQUIRE(!sa.rs_part || (!sa.rms_w && !amax && sa.rs_n > 0 && sa.rs_nparts > 0 &&
-                               sa.rs_nparts <= 64),
-              "gemm_rows: an external row scale excludes the fused RMSNorm / argmax; at most "
-              "64 partials per row");
-  MPR_REQUIRE(!sa.ssq_out || (sa.ssq_cols % 16 == 0 && sa.ssq_cols <= a.N),
-              "gemm_rows: ssq columns %d", sa.ssq_cols);
-  const int F = (sa.rms_w ? RF_RMS : 0) | (a.R ? RF_RES : 0) | (a.act == ACT_RELU ? RF_RELU : 0) |
-                (amax ? RF_AMAX : 0) | (sa.relu_in ? RF_RELU_IN : 0) |
-                (sa.rs_part ? RF_RSCALE : 0) | (sa.ssq_out ? RF_SSQ : 0);
-  const RowsTile tl = pick_tile(a.M, a.N);
-  if (amax_nparts) *amax_nparts = (int)cdiv(a.N, 16 * tl.wn);
-  if (a.M == 0 || a.N == 0) return MPR_OK;
-  const __bf16* w = reinterpret_cast<const __bf16*>(wpl);
-  switch (tl.wm * 8 + tl.wn) {
-    case 1 * 8 + 1: return launch_rows<1, 1>(sa, w, F, s);
-    case 1 * 8 + 2: return launch_rows<1, 2>(sa, w, F, s);
-    case 1 * 8 + 4: return launch_rows<1, 4>(sa, w, F, s);
-    case 2 * 8 + 1: return launch_rows<2, 1>(sa, w, F, s);
-    case 2 * 8 + 2: return launch_rows<2, 2>(sa, w, F, s);
-    case 2 * 8 + 4: return launch_rows<2, 4>(sa, w, F, s);
-    case 4 * 8 + 1: return launch_rows<4, 1>(sa, w, F, s);
-    default: return launch_rows<4, 2>(sa, w, F, s);
+int gemm_dec(const SkinnyArgs& sa, float* ws, size_t ws_floats, hipStream_t s) {
+  const GemmArgs& g = sa.g;
+  MPR_REQUIRE(g.M >= 0 && g.M <= 256 && gemm_dec_ok(g.K, g.N),
+              "gemm_dec: bad shape M=%d N=%d K=%d (M <= 256, K %% 32 == 0, N %% 16 == 0)", g.M,
+              g.N, g.K);
+  MPR_REQUIRE(g.W && aligned16(g.W) && g.ldw % 4 == 0 && g.lda % 4 == 0 && aligned16(g.A) &&
+                  g.C && aligned16(g.C) && g.ldc % 4 == 0 &&
+                  (!g.R || (aligned16(g.R) && g.ldr % 4 == 0)) &&
+                  (!sa.rms_w || aligned16(sa.rms_w)),
+              "gemm_dec: operands must be 16-byte aligned, leading dims multiples of 4");
+  MPR_REQUIRE(!g.bias && (g.act == ACT_NONE || g.act == ACT_RELU) && !sa.amax_val &&
+                  !sa.ssq_out && !sa.rs_part && !sa.relu_in && sa.a_scale == 1.f,
+              "gemm_dec: the plain decode projections (RMSNorm prologue, ReLU, residual) only");
+  if (g.M == 0 || g.N == 0) return MPR_OK;
+  const DecPlan p = dec_plan(g.N, g.K);
+  DecArgs a;
+  a.A = g.A; a.lda = g.lda; a.W = g.W; a.ldw = g.ldw; a.R = g.R; a.ldr = g.ldr;
+  a.C = g.C; a.ldc = g.ldc; a.rms_w = sa.rms_w; a.eps = sa.rms_eps;
+  a.M = g.M; a.N = g.N; a.K = g.K; a.Kb = p.Kb; a.KS = p.KS;
+  a.part = ws;
+  a.part_ss = ws ? ws + (size_t)p.KS * g.M * g.N : nullptr;
+  MPR_REQUIRE(p.KS == 1 || (ws && ws_floats >= gemm_dec_ws_floats(g.M, g.N, g.K) &&
+                            aligned16(ws)),
+              "gemm_dec: split-K workspace too small");
+  const int F = (sa.rms_w ? DF_RMS : 0) | (g.R ? DF_RES : 0) | (g.act == ACT_RELU ? DF_RELU : 0);
+  switch (F) {
+    case 0: return launch_dec<0>(a, p, s);
+    case DF_RELU: return launch_dec<DF_RELU>(a, p, s);
+    case DF_RMS: return launch_dec<DF_RMS>(a, p, s);
+    case DF_RMS | DF_RELU: return launch_dec<DF_RMS | DF_RELU>(a, p, s);
+    case DF_RES: return launch_dec<DF_RES>(a, p, s);
+    default: break;
   }
+  set_error("gemm_dec: option set %d is not instantiated", F);
+  return MPR_EINVAL;
 }
 
 }  // namespace mpr
@@ -426,37 +327,25 @@ int gemm_rows(const SkinnyArgs& sa, const void* wpl, hipStream_t s, int* amax_np
 // ---- C ABI (kernel-level tests and benchmarks of the decode projection) ----------------------
 extern "C" {
 
-int64_t mpr_planes_bytes(int64_t n, int32_t k) {
-  return k > 0 && k % 32 == 0 && n > 0 ? mpr::packed_planes_elems(n, k) * 2 : 0;
-}
-
-int mpr_planes_pack(const float* W, int64_t n, int32_t k, void* planes, void* stream) {
+int mpr_dec_gemm(const float* A, int64_t lda, const float* W, int64_t ldw, float* C, int64_t ldc,
+                 int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr, int32_t act,
+                 const float* rms_w, float eps, void* stream) {
   try {
-    MPR_REQUIRE(planes && mpr::aligned16(planes), "planes_pack: output must be 16-byte aligned");
-    return mpr::pack_planes(W, n, k, k, planes, reinterpret_cast<hipStream_t>(stream));
-  } catch (...) {
-    mpr::set_error("planes_pack: exception");
-    return MPR_EINVAL;
-  }
-}
-
-int mpr_rows_gemm(const float* A, int64_t lda, const void* planes, float* C, int64_t ldc,
-                  int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr, int32_t act,
-                  const float* rms_w, float eps, float* amax_val, int32_t* amax_idx,
-                  int32_t* nparts, void* stream) {
-  try {
-    MPR_REQUIRE(act == mpr::ACT_NONE || act == mpr::ACT_RELU, "rows_gemm: act %d", act);
-    mpr::SkinnyArgs sa;
-    sa.g.A = A; sa.g.lda = lda; sa.g.C = C; sa.g.ldc = ldc; sa.g.M = M; sa.g.N = N; sa.g.K = K;
-    sa.g.R = R; sa.g.ldr = ldr; sa.g.act = act;
+    using namespace mpr;
+    MPR_REQUIRE(act == ACT_NONE || act == ACT_RELU, "dec_gemm: act %d", act);
+    SkinnyArgs sa;
+    sa.g.A = A; sa.g.lda = lda; sa.g.W = W; sa.g.ldw = ldw; sa.g.C = C; sa.g.ldc = ldc;
+    sa.g.M = M; sa.g.N = N; sa.g.K = K; sa.g.R = R; sa.g.ldr = ldr; sa.g.act = act;
     sa.rms_w = rms_w; sa.rms_eps = eps;
-    sa.amax_val = amax_val; sa.amax_idx = amax_idx;
-    int np = 0;
-    const int rc = mpr::gemm_rows(sa, planes, reinterpret_cast<hipStream_t>(stream), &np);
-    if (nparts) *nparts = np;
-    return rc;
+    static DevBuf ws;  // the split-K partials of these calls (ordered on their stream)
+    const size_t need = gemm_dec_ws_floats(M, N, K);
+    if (need * 4 > ws.bytes) {
+      MPR_HIP(hipDeviceSynchronize());
+      MPR_TRY(ws.ensure(need * 4));
+    }
+    return gemm_dec(sa, ws.as<float>(), ws.bytes / 4, reinterpret_cast<hipStream_t>(stream));
   } catch (...) {
-    mpr::set_error("rows_gemm: exception");
+    mpr::set_error("dec_gemm: exception");
     return MPR_EINVAL;
   }
 }

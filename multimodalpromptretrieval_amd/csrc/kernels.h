@@ -75,20 +75,15 @@ struct SkinnyArgs {
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
-// Decode-step projections at any row count (decode_gemm.hip): gemm_skinny's contract (fused
-// RMSNorm, residual, ReLU, argmax head, folded-chain flags), computed on the bf16 matrix cores as
-// the fp32-accurate three-way split (x3.h) with the weight's three bf16 planes pre-split once at
-// load (pack_planes).  The K range of every output element is split into 8 fixed contiguous
-// slices summed in slice order, whatever the row count or the block tile: a row's results do not
-// depend on how many rows share the launch (a 16-row predict() and the same rows inside a 128-row
-// serving-loop decode are bit-identical).  K % 32 == 0 (gemm_rows_ok).  Argmax mode writes
-// *amax_nparts partials per row (amax_val/idx[row * nparts + part]).
-//   planes image: Wp[((t * K/32 + s) * 3 + p) * 512 + l * 8 + j] = plane p of
-//                 W[16t + (l & 15)][32s + 8(l >> 4) + j]  (0 past N), bf16
-bool gemm_rows_ok(int K);
-int64_t packed_planes_elems(int64_t N, int64_t K);  // bf16 elements of the planes image
-int pack_planes(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, hipStream_t s);
-int gemm_rows(const SkinnyArgs& a, const void* wpl, hipStream_t s, int* amax_nparts = nullptr);
+// Decoder projections of grouped decodes (decode_gemm.hip, 17-256 rows): gemm_skinny's plain
+// contract (fused RMSNorm prologue, ReLU, residual; no argmax / folded-chain options) on the fp32
+// weight [N, K] (g.W, g.ldw), fp32-accurate on the bf16 matrix cores (x3.h).  The work is split
+// along N and K into ~200+ blocks (every weight element read by one block, every block all rows);
+// K slices > 1 need the workspace (gemm_dec_ws_floats) and a second, finishing launch.  The K
+// partition depends on (K, N) only: a row's results do not depend on the row count of the launch.
+bool gemm_dec_ok(int K, int N);  // K % 32 == 0, N % 16 == 0
+size_t gemm_dec_ws_floats(int M, int N, int K);
+int gemm_dec(const SkinnyArgs& a, float* ws, size_t ws_floats, hipStream_t s);
 
 // Kernel probe (bench roofline): hipEvent pairs around every launch of one GEMM kind.
 enum ProbeKind : int { PROBE_OFF = 0, PROBE_GEMM = 1, PROBE_SKINNY = 2, PROBE_RECORD = 3 };
@@ -204,6 +199,11 @@ int scale_inplace(float* p, int64_t n, float scale, hipStream_t s);
 int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
                 const int* gate);
+// k > 64: per row the k smallest (sign * key, id) of n (ids null: id = column + id_offset),
+// ascending, ties to the lowest id; values written as given (sign undone).
+constexpr int SELECT_MAX_K = 16384;
+int select_large(const float* keys, const int64_t* ids, int b, int64_t n, int k, float sign,
+                 int64_t id_offset, float* od, int64_t* oi, hipStream_t s);
 int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
               int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
               float* out_dist, int64_t* out_ids, hipStream_t s, const void* Xb = nullptr,

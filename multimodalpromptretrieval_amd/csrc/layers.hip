@@ -1094,7 +1094,7 @@ int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int 
                 int32_t* unfinished, int32_t* tokens, int64_t tok_ld, int col, int eos, int pad,
                 const float* table, int D, float* x, hipStream_t s, int64_t x_ld) {
   if (M == 0) return MPR_OK;
-  MPR_REQUIRE(M <= 128, "greedy_step: %d rows > 128", M);
+  MPR_REQUIRE(M <= 256, "greedy_step: %d rows > 256", M);
   hipLaunchKernelGGL(greedy_step_kernel, dim3(M), dim3(256), 0, s, part_val, part_idx, nparts,
                      unfinished, tokens, tok_ld, col, eos, pad, table, D, x,
                      x_ld < 0 ? (int64_t)D : x_ld);

@@ -118,9 +118,6 @@ struct T5Layer {
   //   W_ocq  = [[o | I_d], [cq diag(ln1) o | cq diag(ln1)]]     [d + inner, inner + d]
   //   W_cowi = [[co | I_d], [wi diag(ln2) co | wi diag(ln2)]]   [d + d_ff, inner + d]
   DevBuf pk_ocq, pk_cowi;
-  // decoder only: pack_planes images (three bf16 planes, decode_gemm.hip) of the same weights
-  // for the row-count independent decode GEMM (T5Model::rows)
-  DevBuf pl_qkv, pl_o, pl_cq, pl_co, pl_wi, pl_wo, pl_ocq, pl_cowi;
 };
 
 // Per-call workspace of generate(): activations, decode caches, captured graphs and the decode
@@ -134,13 +131,14 @@ struct T5Work {
   DevBuf mask_enc, enc_tmp;  // a group's encoder mask / output when several groups share a decode
   DevBuf ax, yq, hz;  // folded decode chain rows: [a | x], [c | h | u], [h2 | z]
   DevBuf x1ss, x2ss;  // their residual rows' per-16-column sums of squares
+  DevBuf dec_ws;      // split-K partials of the grouped decode's projections (gemm_dec)
   uint64_t gen = 0;  // bumped by every buffer growth: invalidates captured graphs
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {
     hipGraphExec_t exec;
     uint64_t gen;
   };
-  using GraphKey = std::tuple<int, int, int, int, int, int>;  // (part, B, L, max_new, ., .)
+  using GraphKey = std::vector<int>;  // (part, B, L, max_new, ...)
   std::map<GraphKey, GraphEnt> graphs;
   hipStream_t dec_stream = nullptr;  // not owned
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -157,8 +155,8 @@ struct T5Work {
     int ahead = 2;                  // chunks kept launched but unread
     int steps = 0;                  // decode steps launched by the last finished call
     int n = 0;
-    int32_t* outs[8] = {};
-    int row0[8] = {}, rows[8] = {};
+    int32_t* outs[16] = {};
+    int row0[16] = {}, rows[16] = {};
     hipStream_t ds = nullptr;
   } pend;
 };
@@ -166,7 +164,7 @@ struct T5Work {
 struct T5Model : mpr_model {
   // slots 0..3: serving-loop calls in flight; 4 (and 5 for > 128 rows): predict()'s own
   static constexpr int MAX_SLOTS = 6;
-  static constexpr int MAX_GROUPS = 8;  // batches (<= 16 rows each) sharing one decode loop
+  static constexpr int MAX_GROUPS = 16;  // batches (<= 16 rows each) sharing one decode loop
   T5Model() : mpr_model(T5) { use_slot(0); }
   int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1;
   int inner = 0, lut_radius = 0;
@@ -174,17 +172,16 @@ struct T5Model : mpr_model {
   // layer instead of 8; MPR_DECODE_FOLD=0 keeps the 8-launch chain): see decode_body.
   bool fold = false;
   bool fold_rows(int B) const;  // the folded chain for a B-row decode
-  // Decode projections on gemm_rows (decode_gemm.hip) at every row count (MPR_DECODE_GEMM=skinny
-  // keeps the round-3 GEMV kernels): a row's tokens are then the same whatever decode group it
-  // is in, so the fold and the head are chosen per model, never per call.
+  // Grouped decodes (> 16 rows) run their layer projections on gemm_dec (decode_gemm.hip) when
+  // every contraction allows it (MPR_DECODE_GEMM=skinny keeps the round-3 GEMV kernels); 16-row
+  // decodes (predict()) keep the skinny GEMVs and the folded chain.
   bool rows = false;
-  int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& pl, hipStream_t s,
+  int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& w, hipStream_t s,
                int* amax_nparts = nullptr) const;
   bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
   int build_folded();
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
   DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
-  DevBuf pl_lm_head;  // pack_planes image of lm_head (rows)
   // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
   DevBuf enc_tab, dec_tab;
   std::vector<std::unique_ptr<T5Layer>> enc, dec;

@@ -1724,6 +1724,7 @@ bool use_scan_small(int64_t n, int d, int b) {
 }
 
 size_t scan_topk_workspace(int64_t n, int b, int k) {
+  if (k > 64) return (size_t)b * n * sizeof(float) + 256;  // the full score rows (select_large)
   const int K = list_cap(k);
   const int64_t per_q = std::max<int64_t>(
       std::max<int64_t>(scan_blocks(n), small_regime(n, b) ? cdiv(n, 16) : 0),
@@ -1738,12 +1739,19 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
               int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
               float* out_dist, int64_t* out_ids, hipStream_t s, const void* Xb,
               const float* xmax) {
-  MPR_REQUIRE(k >= 1 && k <= 64, "search: k=%d must be in [1, 64]", k);
+  MPR_REQUIRE(k >= 1 && k <= SELECT_MAX_K, "search: k=%d must be in [1, %d]", k, SELECT_MAX_K);
   MPR_REQUIRE(k <= n, "search: k=%d exceeds index rows %lld", k, (long long)n);
   MPR_REQUIRE(d % 16 == 0 && d <= 8192, "search: d=%d must be a multiple of 16", d);
   MPR_REQUIRE(b >= 0, "search: b<0");
   if (b == 0) return MPR_OK;
   MPR_REQUIRE(ws_bytes >= scan_topk_workspace(n, b, k), "search: workspace too small");
+  if (k > 64) {
+    // a retrieval_k past the fused kernels' register lists: the full score rows (the exact scan
+    // kernel's arithmetic, as mpr_index_scores), then a per-query radix select + sort
+    MPR_TRY(scan_scores(X, xnorm, n, d, metric, Q, b, ws, s));
+    return select_large(ws, nullptr, b, n, k, metric == 1 ? -1.f : 1.f, row_offset, out_dist,
+                        out_ids, s);
+  }
   const int K = list_cap(k);
   const int* gate = nullptr;
   const float* qn_pre = nullptr;  // |q|^2 already computed by the coarse path
@@ -1920,7 +1928,8 @@ int row_sqnorms(const float* X, int64_t n, int d, float* out, hipStream_t s) {
 
 int topk_merge(const float* cand_d, const int64_t* cand_i, int b, int64_t n_cand, int k,
                int metric, float* out_d, int64_t* out_i, hipStream_t s) {
-  MPR_REQUIRE(k >= 1 && k <= 64 && k <= n_cand, "merge: k=%d n_cand=%lld", k, (long long)n_cand);
+  MPR_REQUIRE(k >= 1 && k <= SELECT_MAX_K && k <= n_cand, "merge: k=%d n_cand=%lld", k,
+              (long long)n_cand);
   if (b == 0) return MPR_OK;
   return merge_dispatch(cand_d, cand_i, b, n_cand, k, /*keys_are_values=*/1, metric, out_d, out_i,
                         s);

@@ -149,6 +149,103 @@ __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
   }
 }
 
+
+// Large k (> 64; the reference slices any retrieval_k out of a full argsort,
+// dataset/VQAFeatureDataset.py:194-197): per query one block finds the k smallest 64-bit words
+// (key order bits, id) — unique, so the set is exact with ties going to the lowest id — by a
+// radix select over 8 passes of 8-bit digits (MSB first, LDS histograms), gathers them into LDS
+// and sorts them there (bitonic, padded to a power of two).  ids == null: candidate c of the row
+// has id c (a full score row), output ids + id_offset.  Ids are < 2^32 (n < 2^31 everywhere).
+constexpr int SL_NT = 1024;
+
+__device__ __forceinline__ uint64_t sl_word(float key, uint32_t id) {
+  return ((uint64_t)order_bits(key + 0.0f) << 32) | id;
+}
+
+__global__ __launch_bounds__(SL_NT) void select_large_kernel(const float* keys,
+                                                             const int64_t* ids, int64_t n,
+                                                             int k, int P, float sign,
+                                                             int64_t id_offset, float* out_val,
+                                                             int64_t* out_id) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sl_lds[];
+  uint64_t* items = sl_lds;                                 // [P]
+  uint32_t* hist = reinterpret_cast<uint32_t*>(sl_lds + P);  // [256]
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_rem, s_count;
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const float* kr = keys + (int64_t)q * n;
+  const int64_t* ir = ids ? ids + (int64_t)q * n : nullptr;
+  auto word_at = [&](int64_t c, bool& ok) -> uint64_t {
+    if (ir) {
+      const int64_t id = ir[c];
+      ok = id >= 0;
+      return sl_word(sign * kr[c], (uint32_t)id);
+    }
+    ok = true;
+    return sl_word(sign * kr[c], (uint32_t)c);
+  };
+  if (tid == 0) {
+    s_prefix = 0;
+    s_rem = (uint32_t)k;
+  }
+  uint64_t mask = 0;
+  for (int pass = 7; pass >= 0; --pass) {
+    for (int i = tid; i < 256; i += SL_NT) hist[i] = 0;
+    __syncthreads();
+    const uint64_t prefix = s_prefix;
+    const int sh = pass * 8;
+    for (int64_t c = tid; c < n; c += SL_NT) {
+      bool ok;
+      const uint64_t w = word_at(c, ok);
+      if (ok && (w & mask) == prefix) atomicAdd(&hist[(w >> sh) & 255], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {  // the digit whose cumulative count reaches the rank still to place
+      uint32_t rem = s_rem, cum = 0;
+      int dgt = 0;
+      for (; dgt < 256; ++dgt) {
+        if (cum + hist[dgt] >= rem) break;
+        cum += hist[dgt];
+      }
+      s_rem = rem - cum;
+      s_prefix = prefix | ((uint64_t)dgt << sh);
+    }
+    mask |= (uint64_t)255 << sh;
+    __syncthreads();
+  }
+  const uint64_t thr = s_prefix;  // the k-th smallest word
+  if (tid == 0) s_count = 0;
+  for (int i = tid; i < P; i += SL_NT) items[i] = ~0ull;
+  __syncthreads();
+  for (int64_t c = tid; c < n; c += SL_NT) {
+    bool ok;
+    const uint64_t w = word_at(c, ok);
+    if (ok && w <= thr) items[atomicAdd(&s_count, 1u)] = w;
+  }
+  __syncthreads();
+  // bitonic sort of the P words (ascending)
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P / 2; i += SL_NT) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t a = items[lo], b = items[hi];
+        if ((a > b) == up) {
+          items[lo] = b;
+          items[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = tid; t < k; t += SL_NT) {
+    const uint64_t w = items[t];
+    out_val[(int64_t)q * k + t] = sign * word_key(w);
+    out_id[(int64_t)q * k + t] = (int64_t)(uint32_t)w + (ir ? 0 : id_offset);
+  }
+}
+
 template <int K>
 int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                  int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
@@ -182,8 +279,27 @@ int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k
     MPR_MG(1) MPR_MG(2) MPR_MG(4) MPR_MG(8) MPR_MG(32) MPR_MG(64)
   }
 #undef MPR_MG
-  set_error("top-k: k=%d unsupported (1..64)", k);
-  return MPR_EUNSUP;
+  MPR_REQUIRE(!gate, "top-k: gated merge of k=%d > 64", k);
+  const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
+  return select_large(ck, ci, b, n_cand, k, sign, 0, od, oi, s);
+}
+
+int select_large(const float* keys, const int64_t* ids, int b, int64_t n, int k, float sign,
+                 int64_t id_offset, float* od, int64_t* oi, hipStream_t s) {
+  MPR_REQUIRE(k >= 1 && k <= SELECT_MAX_K && k <= n, "top-k: k=%d (1..%d, <= %lld candidates)",
+              k, SELECT_MAX_K, (long long)n);
+  MPR_REQUIRE(n < ((int64_t)1 << 31), "top-k: %lld candidates per row", (long long)n);
+  if (b == 0) return MPR_OK;
+  int P = 1;
+  while (P < k) P <<= 1;
+  const size_t lds = (size_t)P * 8 + 256 * 4;
+  if (lds > 64 * 1024)
+    MPR_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(select_large_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(select_large_kernel, dim3((unsigned)b), dim3(SL_NT), lds, s, keys, ids, n, k,
+                     P, sign, id_offset, od, oi);
+  MPR_LAUNCHED();
+  return MPR_OK;
 }
 
 }  // namespace mpr

@@ -78,24 +78,24 @@ __global__ void fold_weights_kernel(const float* __restrict__ top, const float* 
 // The folded chain trades launches for MACs (its two merged GEMMs read 50 % more weight per
 // layer): it wins for the latency-bound decodes of one batch and loses for the grouped
 // 128-row decodes of a serving loop, where the launches overlap other work (measured).
-// On gemm_rows the choice is per model (MPR_ROWS_FOLD, default on): a batch's rows then take the
-// same chain alone or in a grouped decode.  On the skinny kernels it follows the row count.
 bool T5Model::fold_rows(int B) const {
   static const int max_rows = [] {
     const char* e = getenv("MPR_DECODE_FOLD_ROWS");
     return e ? atoi(e) : 16;
   }();
-  static const bool rows_fold = [] {
-    const char* e = getenv("MPR_ROWS_FOLD");
-    return !(e && e[0] == '0');
-  }();
-  if (rows) return fold && rows_fold;
   return fold && B <= max_rows;
 }
 
-int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& pl, hipStream_t s,
+// A decode projection: gemm_dec for grouped decodes (> 16 rows; not the argmax head or the folded
+// chain's options), else the skinny GEMV on the packed weight.
+int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& w, hipStream_t s,
                       int* amax_nparts) const {
-  if (rows) return gemm_rows(a, pl.ptr, s, amax_nparts);
+  if (rows && a.g.M > 16 && !a.amax_val && !a.ssq_out && !a.rs_part) {
+    SkinnyArgs b = a;
+    b.g.W = w.as<float>();
+    b.g.ldw = a.g.K;
+    return gemm_dec(b, ws->dec_ws.as<float>(), ws->dec_ws.bytes / 4, s);
+  }
   SkinnyArgs b = a;
   b.wpk = pk.as<float>();
   if (amax_nparts) *amax_nparts = (int)cdiv(a.g.N, 16);
@@ -108,7 +108,6 @@ int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& pl, h
 // from d >= 768 (t5-base and up); MPR_TILED_HEAD=0 / 1 forces it off / on (read per call; a
 // captured decode graph keeps the head it was captured with).
 bool T5Model::tiled_head(int B) const {
-  if (rows) return false;  // gemm_rows' argmax head serves every row count
   const char* e = getenv("MPR_TILED_HEAD");
   const bool on = e ? e[0] == '1' : d >= 768;
   return on && B > 32 && !fold_rows(B);
@@ -125,20 +124,15 @@ int T5Model::build_folded() {
                        top.as<float>(), bot.as<float>(), w.as<float>(), d, inner, N2,
                        tmp.as<float>());
     MPR_LAUNCHED();
-    if (rows) {
-      MPR_TRY(dst.ensure((size_t)packed_planes_elems(d + N2, K) * 2));
-      MPR_TRY(pack_planes(tmp.as<float>(), d + N2, K, K, dst.ptr, nullptr));
-    } else {
-      MPR_TRY(dst.ensure((size_t)packed_rows16_elems(d + N2, K) * 4));
-      MPR_TRY(pack_rows16(tmp.as<float>(), d + N2, K, K, dst.as<float>(), nullptr));
-    }
+    MPR_TRY(dst.ensure((size_t)packed_rows16_elems(d + N2, K) * 4));
+    MPR_TRY(pack_rows16(tmp.as<float>(), d + N2, K, K, dst.as<float>(), nullptr));
     MPR_HIP(hipStreamSynchronize(nullptr));  // tmp is reused by the next fold
     return MPR_OK;
   };
   for (auto& lp : dec) {
     T5Layer& ly = *lp;
-    MPR_TRY(fold(rows ? ly.pl_ocq : ly.pk_ocq, ly.o, ly.cq, ly.ln1, inner));
-    MPR_TRY(fold(rows ? ly.pl_cowi : ly.pk_cowi, ly.co, ly.wi, ly.ln2, dff));
+    MPR_TRY(fold(ly.pk_ocq, ly.o, ly.cq, ly.ln1, inner));
+    MPR_TRY(fold(ly.pk_cowi, ly.co, ly.wi, ly.ln2, dff));
   }
   return MPR_OK;
 }
@@ -311,7 +305,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       sq.g.A = xp; sq.g.lda = d;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.pl_qkv, s));
+      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.qkv, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
       at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -324,12 +318,12 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       SkinnyArgs so;
       so.g.A = ap; so.g.lda = inner; so.g.R = xp;
       so.g.ldr = d; so.g.C = xp; so.g.ldc = d; so.g.M = B; so.g.N = d; so.g.K = inner;
-      MPR_TRY(dec_gemm(so, ly.pk_o, ly.pl_o, s));
+      MPR_TRY(dec_gemm(so, ly.pk_o, ly.o, s));
       SkinnyArgs cq;
       cq.g.A = xp; cq.g.lda = d; cq.g.C = qp;
       cq.g.ldc = inner; cq.g.M = B; cq.g.N = inner; cq.g.K = d; cq.rms_w = ly.ln1.as<float>();
       cq.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(cq, ly.pk_cq, ly.pl_cq, s));
+      MPR_TRY(dec_gemm(cq, ly.pk_cq, ly.cq, s));
       AttnArgs ca;
       ca.q = qp; ca.q_bs = inner; ca.q_rs = inner;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -341,16 +335,16 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       SkinnyArgs co;
       co.g.A = ap; co.g.lda = inner; co.g.R = xp;
       co.g.ldr = d; co.g.C = xp; co.g.ldc = d; co.g.M = B; co.g.N = d; co.g.K = inner;
-      MPR_TRY(dec_gemm(co, ly.pk_co, ly.pl_co, s));
+      MPR_TRY(dec_gemm(co, ly.pk_co, ly.co, s));
       SkinnyArgs fi;
       fi.g.A = xp; fi.g.lda = d; fi.g.C = fp;
       fi.g.ldc = dff; fi.g.M = B; fi.g.N = dff; fi.g.K = d; fi.g.act = ACT_RELU;
       fi.rms_w = ly.ln2.as<float>(); fi.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(fi, ly.pk_wi, ly.pl_wi, s));
+      MPR_TRY(dec_gemm(fi, ly.pk_wi, ly.wi, s));
       SkinnyArgs fo;
       fo.g.A = fp; fo.g.lda = dff; fo.g.R = xp;
       fo.g.ldr = d; fo.g.C = xp; fo.g.ldc = d; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
-      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.pl_wo, s));
+      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.wo, s));
     }
     if (tiled_head(B)) {
       // logits = rms(x) . lm_head^T on the tiled GEMM, then the row argmax in 16 parts per row
@@ -378,7 +372,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
     hd.amax_val = ws->part_val.as<float>();
     hd.amax_idx = ws->part_idx.as<int32_t>();
     int np = 0;
-    MPR_TRY(dec_gemm(hd, pk_lm_head, pl_lm_head, s, &np));
+    MPR_TRY(dec_gemm(hd, pk_lm_head, lm_head, s, &np));
     MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks, T1,
                         t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,
                         s));
@@ -415,7 +409,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       sq.g.A = xp; sq.g.lda = ldA;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.pl_qkv, s));
+      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.qkv, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
       at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -429,7 +423,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
       so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
       so.ssq_out = x1ss; so.ssq_cols = d;  // x1's per-tile sums of squares (its RMS)
-      MPR_TRY(dec_gemm(so, ly.pk_ocq, ly.pl_ocq, s));
+      MPR_TRY(dec_gemm(so, ly.pk_ocq, ly.pk_ocq, s));
       AttnArgs ca;  // c = attention(u / rms_scale(x1), K_enc, V_enc)
       ca.q = yq + inner + d; ca.q_bs = ldY; ca.q_rs = ldY;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -443,13 +437,13 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       cw.g.A = yq; cw.g.lda = ldY; cw.g.C = hz; cw.g.ldc = ldZ;
       cw.g.M = B; cw.g.N = d + dff; cw.g.K = inner + d;
       cw.ssq_out = x2ss; cw.ssq_cols = d;
-      MPR_TRY(dec_gemm(cw, ly.pk_cowi, ly.pl_cowi, s));
+      MPR_TRY(dec_gemm(cw, ly.pk_cowi, ly.pk_cowi, s));
       SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
       fo.g.A = hz + d; fo.g.lda = ldZ; fo.g.R = hz; fo.g.ldr = ldZ;
       fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
       fo.relu_in = true; fo.rs_part = x2ss; fo.rs_nparts = d / 16; fo.rs_n = d;
       fo.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.pl_wo, s));
+      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.wo, s));
     }
     SkinnyArgs hd;
     hd.g.A = xp; hd.g.lda = ldA; hd.g.C = nullptr; hd.g.M = B; hd.g.N = V; hd.g.K = d;
@@ -457,7 +451,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
     hd.amax_val = ws->part_val.as<float>();
     hd.amax_idx = ws->part_idx.as<int32_t>();
     int np = 0;
-    MPR_TRY(dec_gemm(hd, pk_lm_head, pl_lm_head, s, &np));
+    MPR_TRY(dec_gemm(hd, pk_lm_head, lm_head, s, &np));
     MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks,
                         T1, t + 1, eos, pad, shared.as<float>(), d,
                         t + 1 < max_new ? xp : nullptr, s, ldA));
@@ -566,6 +560,13 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
     MPR_TRY(grow(ws->x1ss, (size_t)B * (d / 16) * 4));
     MPR_TRY(grow(ws->x2ss, (size_t)B * (d / 16) * 4));
   }
+  if (rows && B > 16) {
+    size_t wsf = 0;
+    const int shapes[6][2] = {{3 * inner, d}, {d, inner}, {inner, d}, {d, inner}, {dff, d},
+                              {d, dff}};
+    for (const auto& nk : shapes) wsf = std::max(wsf, gemm_dec_ws_floats(B, nk[0], nk[1]));
+    if (wsf) MPR_TRY(grow(ws->dec_ws, wsf * 4));
+  }
   MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->unfinished, (size_t)16 * MAX_GROUPS * 4));
@@ -583,7 +584,7 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
     const Grp& g = gr[0];
     MPR_TRY(stage_rows(ws->enc_in.as<float>(), g.e, B, g.L, L, d, s));
     MPR_TRY(stage_rows(ws->mask_in.as<float>(), g.m, B, g.L, L, 1, s));
-    MPR_TRY(run(std::make_tuple(0, B, L, max_new, start, 0), s,
+    MPR_TRY(run(GraphKey{0, B, L, max_new, start, 0}, s,
                 [&](hipStream_t c) { return encode_body(B, L, max_new, start, c); }));
   } else {
     float* eo = ws->enc_out.as<float>();
@@ -592,7 +593,7 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
     for (int k = 1; k < n; ++k) ragged |= gr[k].Lb != gr[0].Lb;
     if (ragged) MPR_HIP(hipMemsetAsync(eo, 0, (size_t)M * d * 4, s));
     // every batch's inputs at its own bucket, back to back; one grouped encoder pass
-    int bs[MAX_GROUPS], lbs[MAX_GROUPS], pack[MAX_GROUPS / 2] = {0, 0, 0, 0};
+    int bs[MAX_GROUPS], lbs[MAX_GROUPS], pack[MAX_GROUPS / 2] = {};
     int64_t r = 0;
     for (int k = 0; k < n; ++k) {
       const Grp& g = gr[k];
@@ -606,7 +607,9 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
       pack[k / 2] |= (g.B | (g.Lb << 5)) << (16 * (k % 2));  // B <= 16, Lb <= 1024
       r += (int64_t)g.B * g.Lb;
     }
-    MPR_TRY(run(std::make_tuple(2, n, pack[0], pack[1], pack[2], pack[3]), s,
+    GraphKey key{2, n};
+    for (int k = 0; k < (n + 1) / 2; ++k) key.push_back(pack[k]);
+    MPR_TRY(run(key, s,
                 [&](hipStream_t c) {
                   // grouped passes of up to GEMM_GROUP batches over the stacked rows
                   int64_t rr = 0;
@@ -627,7 +630,7 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
                                (size_t)g.Lb * d * 4, g.B, hipMemcpyDeviceToDevice, s));
       r += (int64_t)g.B * g.Lb;
     }
-    MPR_TRY(run(std::make_tuple(3, B, L, max_new, start, 0), s,
+    MPR_TRY(run(GraphKey{3, B, L, max_new, start, 0}, s,
                 [&](hipStream_t c) { return init_body(B, L, max_new, start, c); }));
   }
   hipStream_t ds = ws->dec_stream ? ws->dec_stream : s;
@@ -646,7 +649,7 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
   }
   if (stop_chunk <= 0 || max_new <= stop_chunk) {
     // one graph of all max_new steps: nothing to poll
-    MPR_TRY(run_graph(std::make_tuple(1, B, L, max_new, eos, pad), ds,
+    MPR_TRY(run_graph(GraphKey{1, B, L, max_new, eos, pad}, ds,
                       [&](hipStream_t c) { return decode_body(B, L, max_new, eos, pad, c); }));
     P.chunk = 0;
     P.nch = P.launched = 1;
@@ -678,7 +681,7 @@ int T5Model::launch_chunk(int c) {
   T5Work::Pending& P = ws->pend;
   const int t0 = c * P.chunk, t1 = std::min(P.max_new, t0 + P.chunk);
   const int B = P.B, L = P.L, max_new = P.max_new, eos = P.eos, pad = P.pad;
-  MPR_TRY(run_graph(std::make_tuple(100 + c, B, L, max_new * 1024 + P.chunk, eos, pad), P.ds,
+  MPR_TRY(run_graph(GraphKey{100 + c, B, L, max_new * 1024 + P.chunk, eos, pad}, P.ds,
                     [&](hipStream_t cs) {
                       return decode_body(B, L, max_new, eos, pad, cs, t0, t1);
                     }));

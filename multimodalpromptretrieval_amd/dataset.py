@@ -229,7 +229,7 @@ class VQARetrieval:
         rows = [sum(sizes[:j]) for j in range(len(sizes))]
         q = torch.empty((img.shape[0], self.embed_dim), device=self.device, dtype=torch.float32)
         di = self.image_encoder.out_dim
-        kk = self.retrieval_k + (1 if self.is_training_phase else 0)
+        kk = self._search_k()
         s_img.wait_stream(cur)
         img.record_stream(s_img)
         q.record_stream(s_img)
@@ -462,7 +462,7 @@ class VQARetrieval:
                 return ent[0]
         if self.index is None:
             raise RuntimeError("create_retrieval_dataset() / set_index() first")
-        kk = self.retrieval_k + (1 if self.is_training_phase else 0)
+        kk = self._search_k()
         pre = self._prefetched.pop(key, None)
         if pre is not None and pre[0] is not None:  # prefetch(): scan + copy already enqueued
             pre[1].synchronize()
@@ -481,6 +481,15 @@ class VQARetrieval:
         while len(self._recent) > self.RECENT:
             self._recent.pop(next(iter(self._recent)))
         return val
+
+    def _search_k(self) -> int:
+        """Columns of the search: retrieval_k (+ the skipped self-match in the training phase),
+        at most the index rows — the reference slices argsort(...)[:, s:s + retrieval_k] out of
+        a full sort, which holds only N columns (dataset/VQAFeatureDataset.py:194-197)."""
+        kk = self.retrieval_k + (1 if self.is_training_phase else 0)
+        answers = getattr(self, "retrieval_answers", None)
+        n = len(answers) if answers else kk
+        return max(1, min(kk, n))
 
     def retrieve_closest_qa_pairs(self, batch, return_ans=False, return_info=None,
                                   return_dists=False, use_quantifier=True):

@@ -19,8 +19,11 @@ overlapped across batches on their own streams:
   20-step headline);
 * answers are handed out in order as their calls complete (``_finish``).
 
-Every batch gets exactly the answers ``predict()`` gives it (the grouped launches keep each
-batch's arithmetic: tests/test_gpu_golden.py).
+Every batch gets ``predict()``'s answers up to fp32 near-ties: a grouped decode (more than 16
+rows) runs its layer projections on gemm_dec (csrc/decode_gemm.hip), whose summation order differs
+from the 16-row GEMV chain's (both fp32-accurate and pinned to the reference's goldens G3 / G7 /
+G8); its results do not depend on how many batches share the decode, so every grouping of the same
+batches gives the same bits (tests/test_gpu_serving.py, tests/test_gpu_golden.py).
 """
 from __future__ import annotations
 
@@ -31,6 +34,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib, staging
+from .t5 import pieces_per_call
 
 
 @dataclass(frozen=True)
@@ -197,7 +201,7 @@ class ServingLoop:
                 self._advance(call)
 
     def _launch(self, inputs):
-        """One generate call over 1-8 pieces of <= 16 rows; returns its _Call."""
+        """One generate call over 1-16 pieces of <= 16 rows; returns its _Call."""
         m = self.m
         slot = self.calls % self.o.depth
         self.calls += 1
@@ -240,8 +244,9 @@ class ServingLoop:
     def _add(self, prepared) -> bool:
         """Queue a prepared batch: grouped with its neighbours (<= 16 rows) or alone.  A batch of
         more than 16 rows (a DataLoader with batch_size > 16, a C5 batch of 256 questions) is
-        decoded as 16-row pieces, up to 8 per generate call, as predict() decodes it; its answers
-        come out once every piece is done.  Returns whether a generate call was launched."""
+        decoded as 16-row pieces, pieces_per_call() per generate call, as predict() decodes it;
+        its answers come out once every piece is done.  Returns whether a generate call was
+        launched."""
         combined, mask = prepared
         rows = combined.shape[0]
         if self.o.decode_group > 1 and rows <= 16:
@@ -253,10 +258,11 @@ class ServingLoop:
         self._flush_held()
         pieces = [(combined[i:i + 16], mask[i:i + 16]) for i in range(0, max(rows, 1), 16)]
         owned = []
-        for g in range(0, len(pieces), 8):
-            call = self._launch(pieces[g:g + 8])
+        per = pieces_per_call()
+        for g in range(0, len(pieces), per):
+            call = self._launch(pieces[g:g + per])
             call.refs += 1
-            owned += [(call, j) for j in range(len(pieces[g:g + 8]))]
+            owned += [(call, j) for j in range(len(pieces[g:g + per]))]
         self.order.append(owned)
         return True
 

@@ -18,6 +18,14 @@ import torch
 from . import _lib
 
 LUT_RADIUS = 1024  # covers encoder lengths up to 512 and any decode length here
+MAX_PIECES = 16    # batches of <= 16 rows sharing one decode loop (T5Model::MAX_GROUPS)
+
+
+def pieces_per_call() -> int:
+    """<= 16-row pieces per decode loop for a batch of more than 16 rows (predict() of a large
+    batch, the serving loop's large batches): MPR_GEN_PIECES, default 16 (one 256-row loop for a
+    256-question batch, every decode weight streamed once per step for all rows)."""
+    return max(1, min(MAX_PIECES, int(os.environ.get("MPR_GEN_PIECES", "16"))))
 
 
 def relative_position_bucket(rel: torch.Tensor, bidirectional: bool, num_buckets: int = 32,
@@ -173,12 +181,13 @@ class DeviceT5:
         """All max_new_tokens greedy steps on device: int32 [B, 1+max_new] (no host sync).
         ``slot`` picks one of the model's independent workspaces (two batches of a serving
         loop decode concurrently on different slots and streams).  A batch of more than 16 rows
-        runs as 16-row chunks sharing decode loops (up to 8 chunks per loop)."""
+        runs as 16-row chunks sharing decode loops (pieces_per_call() chunks per loop)."""
         embeds, mask = self._inputs(embeds, mask)
         B, L, _ = embeds.shape
         if B > 16:
             chunks = [(embeds[i:i + 16], mask[i:i + 16]) for i in range(0, B, 16)]
-            groups = [chunks[g:g + 8] for g in range(0, len(chunks), 8)]
+            per = pieces_per_call()
+            groups = [chunks[g:g + per] for g in range(0, len(chunks), per)]
             outs = []
             if len(groups) == 1 or os.environ.get("MPR_SPLIT_SLOTS", "1") == "0":
                 for grp in groups:
@@ -218,11 +227,11 @@ class DeviceT5:
 
     def generate_batches_padded(self, batches, max_new_tokens=20, decoder_start_token_id=0,
                                 eos_token_id=1, pad_token_id=0, slot: int = 0):
-        """generate_padded() of 1-8 batches [(embeds, mask), ...] (<= 16 rows each) with one
+        """generate_padded() of 1-16 batches [(embeds, mask), ...] (<= 16 rows each) with one
         shared decode loop (mpr_t5_generate_batches): a list of [B_i, 1+max_new] int32, each
         bit-identical to its own call."""
-        if not 1 <= len(batches) <= 8:
-            raise ValueError(f"generate_batches: {len(batches)} batches (1 to 8)")
+        if not 1 <= len(batches) <= MAX_PIECES:
+            raise ValueError(f"generate_batches: {len(batches)} batches (1 to {MAX_PIECES})")
         ins = [self._inputs(e, m) for e, m in batches]
         for e, _ in ins:
             if e.shape[0] > 16:
@@ -245,8 +254,8 @@ class DeviceT5:
         the current stream; ``generate_poll(slot)`` advances the call.  Returns the [B_i,
         1+max_new] int32 output tensors, valid on the current stream once a poll reports done
         (each equal to generate_batches_padded's)."""
-        if not 1 <= len(batches) <= 8:
-            raise ValueError(f"generate_begin: {len(batches)} batches (1 to 8)")
+        if not 1 <= len(batches) <= MAX_PIECES:
+            raise ValueError(f"generate_begin: {len(batches)} batches (1 to {MAX_PIECES})")
         ins = [self._inputs(e, m) for e, m in batches]
         for e, _ in ins:
             if e.shape[0] > 16:

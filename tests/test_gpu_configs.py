@@ -52,6 +52,127 @@ def test_g5_cosine_similarity_product(device):
         assert np.abs(got.cpu().numpy() - z[name]).max() <= 2e-6, name
 
 
+@pytest.mark.parametrize("s1,s2,dim", [((8, 64), (1, 64), 1),        # [B,D] x [1,D]
+                                       ((64,), (10, 64), -1),       # a vector against rows
+                                       ((5, 3, 32), (5, 1, 32), 2),
+                                       ((7, 40, 3), (1, 40, 3), 1),  # reduce a middle axis
+                                       ((6, 33), (6, 33), 0),        # aligned, dim 0
+                                       ((4, 1, 16), (1, 9, 16), 2),  # D % 16 != 0 not needed
+                                       ((3, 5), (5,), -1),           # fewer dims
+                                       ((2, 3, 4), (1, 4), 1),       # positive dim, fewer dims
+                                       ((2, 3, 4), (3, 1), -2),
+                                       ((2, 1, 5), (3, 1), -1),      # size-1 reduced axis
+                                       ((), (), 0)])
+def test_cosine_similarity_broadcasting(device, s1, s2, dim):
+    """utils.cosine_similarity over the reference's general broadcasting (utils.py:57-62):
+    every layout against the oracle restatement of the reference formula in fp64."""
+    from multimodalpromptretrieval_amd.utils import cosine_similarity
+    from oracle import retrieval as oret
+    g = torch.Generator().manual_seed(len(s1) * 10 + len(s2) + dim)
+    x1 = torch.randn(s1, generator=g)
+    x2 = torch.randn(s2, generator=g)
+    if len(s1) == 2 and s1[0] == 8:
+        x1[3] = 0  # the eps clamp
+    want = oret.cosine_similarity(x1.double(), x2.double(), dim=dim)
+    got = cosine_similarity(x1.to(device), x2.to(device), dim=dim)
+    assert got.device.type == "cuda" and got.dtype == torch.float32
+    assert tuple(got.shape) == tuple(want.shape)
+    assert (got.cpu().double() - want).abs().max() <= 2e-6
+    # host tensors in, host tensor out (computed on the GPU); the inputs' dtype out
+    h = cosine_similarity(x1.half(), x2.half(), dim=dim)
+    assert h.device.type == "cpu" and h.dtype == torch.float16
+    assert (h.double() - oret.cosine_similarity(x1.half().double(), x2.half().double(),
+                                                dim=dim)).abs().max() <= 1e-3
+
+
+def test_cosine_similarity_errors_as_torch(device):
+    from multimodalpromptretrieval_amd.utils import cosine_similarity
+    from oracle import retrieval as oret
+    with pytest.raises(IndexError):  # the reference too: norm(x2, 2, 1) of a 1-d x2
+        oret.cosine_similarity(torch.randn(3, 5), torch.randn(5), dim=1)
+    with pytest.raises(IndexError):
+        cosine_similarity(torch.randn(3, 5, device=device), torch.randn(5, device=device), dim=1)
+    a = torch.randn(4, 8, device=device)
+    with pytest.raises(RuntimeError):
+        cosine_similarity(a, torch.randn(3, 8, device=device))  # not broadcastable
+    with pytest.raises(IndexError):
+        cosine_similarity(a, a, dim=2)
+    with pytest.raises(RuntimeError):
+        cosine_similarity(a, a.cpu())
+
+
+def _check_topk(ids, vals, ref64, k, descending=False):
+    """ids/vals [b, k] against an fp64 score matrix: the selected rows' fp64 scores equal the
+    reference's sorted top-k within fp32 rounding (so the set and the order are right up to
+    near-ties), every distinct id, and the returned values are those rows' scores."""
+    ids = ids.cpu().long()
+    order = torch.argsort(-ref64 if descending else ref64, dim=1, stable=True)[:, :k]
+    want = torch.gather(ref64, 1, order)
+    got = torch.gather(ref64, 1, ids)
+    tol = 1e-5 * ref64.abs().max()
+    assert (got - want).abs().max() <= tol
+    assert all(len(set(r)) == k for r in ids.tolist())
+    assert (vals.cpu().double() - got).abs().max() <= tol
+
+
+@pytest.mark.parametrize("n,d,b,k", [(6500, 1024, 16, 100), (300, 64, 5, 300),
+                                     (20000, 512, 3, 4096), (70000, 256, 2, 65)])
+def test_scan_large_k(device, n, d, b, k):
+    """k > 64 (the reference slices any retrieval_k out of a full argsort,
+    dataset/VQAFeatureDataset.py:194-197): the selected rows and their order against fp64 up to
+    fp32 near-ties, exact duplicates to the lowest id, both metrics, and the merge of two shards'
+    candidates (a sharded search's second stage)."""
+    from multimodalpromptretrieval_amd.index import COSINE, DeviceIndex, topk_merge
+    X = syn.index_rows(21, n, d)
+    X[n // 2] = X[n // 3]  # an exact tie
+    q = syn.index_rows(22, b, d)
+    q[0] = X[n // 3]
+    ref64 = torch.cdist(q.double(), X.double())
+    ix = DeviceIndex(X, device)
+    dist, ids = ix.search(q.to(device), k)
+    _check_topk(ids, dist, ref64, k)
+    assert ids[0, :2].cpu().tolist() == [n // 3, n // 2]  # the tie: lowest id first
+    Xn, qn = X.double() / X.double().norm(dim=1, keepdim=True), q.double()
+    sim64 = (qn / qn.norm(dim=1, keepdim=True)) @ Xn.T
+    sim, idc = DeviceIndex(X, device, metric=COSINE).search(q.to(device), k)
+    _check_topk(idc, sim, sim64, k, descending=True)
+    half = n // 2
+    d0, i0 = DeviceIndex(X[:half], device).search(q.to(device), min(k, half))
+    d1, i1 = DeviceIndex(X[half:], device, row_offset=half).search(q.to(device), min(k, n - half))
+    md, mi = topk_merge(torch.cat([d0, d1], 1), torch.cat([i0, i1], 1), k)
+    _check_topk(mi, md, ref64, k)
+    assert torch.equal(mi.cpu(), ids.cpu())
+
+
+def test_retrieval_k_beyond_rows(device):
+    """retrieval_k larger than the index (and k = 100): the reference's argsort slice returns
+    what there is; answers / prompts / dists as the oracle's."""
+    from multimodalpromptretrieval_amd.dataset import VQARetrieval
+    from oracle import retrieval as oret
+    ccfg, clip_sd, *_ = gi.g2_models()
+    for N, k, train in ((40, 100, False), (40, 100, True), (300, 100, False)):
+        # well separated distances (|x_j| = 1 + 0.05 j in shuffled order, queries near 0): the
+        # order is the same in any precision
+        g = torch.Generator().manual_seed(N + k)
+        u = torch.randn(N, 2 * ccfg.embed_dim, generator=g)
+        scale = 1 + 0.05 * torch.randperm(N, generator=g).float()
+        X = u / u.norm(dim=1, keepdim=True) * scale[:, None]
+        answers = syn.answers(N, 7)
+        info = {"question_id": [str(j) for j in range(N)],
+                "question_type": ["open"] * N, "question": [f"q{j}" for j in range(N)]}
+        r = VQARetrieval(device, clip_state_dict=clip_sd, clip_tokenizer=syn.hash_clip_tokenize)
+        r.set_index(X, answers, info, k, train)
+        q = torch.randn(6, 2 * ccfg.embed_dim, generator=g) * 1e-3
+        r.encode_queries = lambda batch, q=q: q.to(device)
+        batch = {"image": torch.zeros(6, 1), "question": [f"x{i}" for i in range(6)]}
+        s = 1 if train else 0
+        ids = oret.topk_ids(oret.cdist(q, X), N, skip_first=False)[:, s:s + k]
+        want_ans = [[answers[j] for j in row] for row in ids.tolist()]
+        assert r.retrieve_closest_qa_pairs(batch, return_ans=True) == want_ans
+        dists = r.retrieve_closest_qa_pairs(batch, return_dists=True)
+        assert all(len(dd) == min(k, N) for _, dd in dists)
+
+
 def _g2_parts(device):
     from multimodalpromptretrieval_amd.dataset import VQARetrieval
     ccfg, clip_sd, tcfg, tok_sd, t5cfg, t5_sd = gi.g2_models()

@@ -1,13 +1,12 @@
-"""GPU: the decode-step projection kernel (mpr_rows_gemm, csrc/decode_gemm.hip) behind every
-decoder projection of greedy generation (architectures/T5VisionModel.py:200-205).
+"""GPU: the grouped-decode projection kernel (mpr_dec_gemm, csrc/decode_gemm.hip) behind the
+decoder projections of decodes of more than 16 rows (architectures/T5VisionModel.py:200-205).
 
 * values vs an fp64 reference of the same op: max|gpu - ref| <= 2e-6 * max_n sum_k |a w| per
-  row (the split-bf16 product is fp32-accurate: ~1e-7 of sum |a w|);
-* argmax head: the index equals the fp64 argmax wherever the top-2 gap exceeds that bound;
-* row-count independence: a row's results are bit-identical whatever else shares the launch (16
-  rows alone vs the same rows inside 37 / 128 / 256-row launches, which take other block tiles):
-  the property that makes a batch's greedy tokens the same alone (predict()) and grouped (the
-  serving loop).
+  row (the split-bf16 product is fp32-accurate: ~1e-7 of sum |a w|), with and without the
+  split-K finishing launch;
+* row-count independence: a row's results are bit-identical whatever else shares the launch (the
+  same 16 rows inside 32 / 69 / 128 / 256-row launches): a batch's rows give the same bits in a
+  128-row serving-loop group and in a 256-row decode.
 """
 import ctypes
 
@@ -20,33 +19,15 @@ pytestmark = pytest.mark.gpu
 VAL_TOL = 2e-6
 
 
-def _planes(W: torch.Tensor) -> torch.Tensor:
-    n, k = W.shape
-    nbytes = _lib.load().mpr_planes_bytes(n, k)
-    assert nbytes > 0
-    pl = torch.empty(nbytes, dtype=torch.uint8, device=W.device)
-    _lib.call("mpr_planes_pack", _lib.ptr(W), n, k, _lib.ptr(pl), _lib.stream_ptr(W.device))
-    return pl
-
-
-def _rows_gemm(A, pl, N, R=None, act=0, rms_w=None, amax=False, eps=1e-6):
+def _dec_gemm(A, W, R=None, act=0, rms_w=None, eps=1e-6, out=None):
     M, K = A.shape
-    dev = A.device
-    C = None if amax else torch.empty((M, N), device=dev, dtype=torch.float32)
-    av = ai = None
-    if amax:
-        av = torch.full((M, N // 16), float("nan"), device=dev)
-        ai = torch.full((M, N // 16), -1, device=dev, dtype=torch.int32)
-    np_ = ctypes.c_int32(0)
-    _lib.call("mpr_rows_gemm", _lib.ptr(A), A.stride(0), _lib.ptr(pl),
-              _lib.ptr(C) if C is not None else None, N, M, N, K,
-              _lib.ptr(R) if R is not None else None, R.stride(0) if R is not None else 0, act,
-              _lib.ptr(rms_w) if rms_w is not None else None, eps,
-              _lib.ptr(av) if av is not None else None, _lib.ptr(ai) if ai is not None else None,
-              ctypes.byref(np_), _lib.stream_ptr(dev))
+    N = W.shape[0]
+    C = torch.empty((M, N), device=A.device, dtype=torch.float32) if out is None else out
+    _lib.call("mpr_dec_gemm", _lib.ptr(A), A.stride(0), _lib.ptr(W), W.stride(0), _lib.ptr(C),
+              C.stride(0), M, N, K, _lib.ptr(R) if R is not None else None,
+              R.stride(0) if R is not None else 0, act,
+              _lib.ptr(rms_w) if rms_w is not None else None, eps, _lib.stream_ptr(A.device))
     torch.cuda.synchronize()
-    if amax:
-        return av[:, :np_.value].cpu(), ai[:, :np_.value].cpu()
     return C.cpu()
 
 
@@ -65,76 +46,48 @@ def _ref(A, W, R=None, act=0, rms_w=None, eps=1e-6):
     return out, bound
 
 
-@pytest.mark.parametrize("M,N,K", [(16, 512, 512), (1, 512, 512), (37, 1536, 512),
+@pytest.mark.parametrize("M,N,K", [(17, 512, 512), (32, 512, 512), (37, 1536, 512),
                                    (128, 512, 2048), (128, 3072, 768), (256, 768, 3072),
-                                   (200, 1024, 1024), (16, 256, 128), (48, 128, 64)])
-def test_rows_gemm_values(device, M, N, K):
+                                   (200, 1024, 1024), (128, 2304, 768), (64, 256, 128),
+                                   (48, 128, 64), (256, 32, 32)])
+def test_dec_gemm_values(device, M, N, K):
     g = torch.Generator().manual_seed(M * 7 + N + K)
     A = torch.randn(M, K, generator=g).to(device)
     W = (torch.randn(N, K, generator=g) * K ** -0.5).to(device)
     R = torch.randn(M, N, generator=g).to(device)
-    pl = _planes(W)
-    for kw in (dict(), dict(R=R), dict(act=2), dict(
-            rms_w=(torch.rand(K, generator=g) + 0.5).to(device))):
-        got = _rows_gemm(A, pl, N, **kw).double()
+    w = (torch.rand(K, generator=g) + 0.5).to(device)
+    for kw in (dict(), dict(R=R), dict(act=2), dict(rms_w=w), dict(rms_w=w, act=2)):
+        got = _dec_gemm(A, W, **kw).double()
         ref, bound = _ref(A, W, **kw)
         err = ((got - ref).abs() / bound).max().item()
         assert err <= VAL_TOL, (kw.keys(), err)
 
 
-def test_rows_gemm_residual_in_place(device):
-    """R aliasing C (the decode chain's residual stream updated in place)."""
+def test_dec_gemm_residual_in_place(device):
+    """R aliasing C (the decode chain's residual stream updated in place), split-K and not."""
     g = torch.Generator().manual_seed(5)
-    M, N, K = 64, 512, 512
-    A = torch.randn(M, K, generator=g).to(device)
-    W = (torch.randn(N, K, generator=g) * 0.05).to(device)
-    X = torch.randn(M, N, generator=g).to(device)
-    want = _rows_gemm(A, _planes(W), N, R=X.clone())
-    pl = _planes(W)
-    np_ = ctypes.c_int32(0)
-    _lib.call("mpr_rows_gemm", _lib.ptr(A), K, _lib.ptr(pl), _lib.ptr(X), N, M, N, K,
-              _lib.ptr(X), N, 0, None, 1e-6, None, None, ctypes.byref(np_),
-              _lib.stream_ptr(device))
-    torch.cuda.synchronize()
-    assert torch.equal(X.cpu(), want)
+    for M, N, K in ((64, 512, 512), (128, 2304, 256)):
+        A = torch.randn(M, K, generator=g).to(device)
+        W = (torch.randn(N, K, generator=g) * 0.05).to(device)
+        X = torch.randn(M, N, generator=g).to(device)
+        want = _dec_gemm(A, W, R=X.clone())
+        assert torch.equal(_dec_gemm(A, W, R=X, out=X), want)
 
 
-@pytest.mark.parametrize("M,N,K", [(16, 32128, 512), (128, 32128, 768), (5, 4096, 256)])
-def test_rows_gemm_argmax_head(device, M, N, K):
-    g = torch.Generator().manual_seed(N + M)
-    A = torch.randn(M, K, generator=g).to(device)
-    W = torch.randn(N, K, generator=g).to(device)
-    w = (torch.rand(K, generator=g) + 0.5).to(device)
-    pv, pi = _rows_gemm(A, _planes(W), N, rms_w=w, amax=True)
-    best = pv.argmax(1)  # parts hold disjoint column ranges in order: first max = lowest column
-    idx = pi.gather(1, best[:, None])[:, 0]
-    ref, bound = _ref(A, W, rms_w=w)
-    top2 = ref.topk(2, dim=1).values
-    sep = (top2[:, 0] - top2[:, 1]) > 4 * VAL_TOL * bound[:, 0]
-    assert sep.sum() >= M - 1
-    assert torch.equal(idx[sep].long(), ref.argmax(1)[sep])
-    # the winning value is the row's logit at that column (fp32-accurate)
-    v = ref.gather(1, idx.long()[:, None])[:, 0]
-    assert ((pv.gather(1, best[:, None])[:, 0].double() - v).abs() <= VAL_TOL * bound[:, 0]).all()
-
-
-def test_rows_gemm_row_count_independent(device):
-    """Rows 32..47 of a 128-row launch == the same 16 rows alone == inside 37 and 256-row
-    launches (different block tiles), bit for bit, in every mode the decode chain uses."""
+def test_dec_gemm_row_count_independent(device):
+    """Rows 32..47 inside launches of 48 / 69 / 128 / 256 rows, bit for bit, in every mode the
+    decode chain uses (split-K and single-slice shapes)."""
     g = torch.Generator().manual_seed(11)
-    K, N = 768, 2304
-    big = torch.randn(256, K, generator=g).to(device)
-    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(device)
-    R = torch.randn(256, N, generator=g).to(device)
-    w = (torch.rand(K, generator=g) + 0.5).to(device)
-    pl = _planes(W)
-    rows = slice(32, 48)
-    for kw in (dict(), dict(act=2), dict(rms_w=w)):
-        alone = _rows_gemm(big[rows].contiguous(), pl, N, **kw)
-        for M in (37 + 32, 128, 256):
-            A = big[:M].contiguous()
-            got = _rows_gemm(A, pl, N, **kw)[rows]
-            assert torch.equal(got, alone), (kw.keys(), M)
-    alone = _rows_gemm(big[rows].contiguous(), pl, N, R=R[rows].contiguous())
-    assert torch.equal(_rows_gemm(big[:128].contiguous(), pl, N, R=R[:128].contiguous())[rows],
-                       alone)
+    for K, N in ((768, 2304), (3072, 768), (512, 2048)):
+        big = torch.randn(256, K, generator=g).to(device)
+        W = (torch.randn(N, K, generator=g) * K ** -0.5).to(device)
+        R = torch.randn(256, N, generator=g).to(device)
+        w = (torch.rand(K, generator=g) + 0.5).to(device)
+        rows = slice(32, 48)
+        for kw in (dict(), dict(act=2), dict(rms_w=w), dict(rms_w=w, act=2)):
+            ref = _dec_gemm(big[:48].contiguous(), W, **kw)[rows]
+            for M in (69, 128, 256):
+                got = _dec_gemm(big[:M].contiguous(), W, **kw)[rows]
+                assert torch.equal(got, ref), (K, N, kw.keys(), M)
+        ref = _dec_gemm(big[:48].contiguous(), W, R=R[:48].contiguous())[rows]
+        assert torch.equal(_dec_gemm(big[:128].contiguous(), W, R=R[:128].contiguous())[rows], ref)

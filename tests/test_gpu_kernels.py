@@ -490,8 +490,8 @@ def test_t5_generate_pair_matches_single(device, t5_sd, monkeypatch, graphs):
     outs = m.generate_batches_padded([named[k] for k in "ABCDDCBA"], 20, slot=3)  # 114 rows
     for k, o in zip("ABCDDCBA", outs):
         assert torch.equal(o.cpu(), single[k]), ("ABCDDCBA", k)
-    with pytest.raises(ValueError):
-        m.generate_batches_padded([A, B, C, D, A, B, C, D, A], 20)
+    with pytest.raises(ValueError):  # at most 16 batches (256 rows) per decode loop
+        m.generate_batches_padded([A, B, C, D] * 4 + [A], 20)
     # a batch of more than 16 rows runs as 16-row chunks (here 16 + 8): each row as alone
     big = (torch.cat([C[0], A[0][:8]]), torch.cat([C[1], A[1][:8]])) if C[0].shape[1] == \
         A[0].shape[1] else (torch.cat([C[0], C[0][:8]]), torch.cat([C[1], C[1][:8]]))
