@@ -539,17 +539,8 @@ int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
     gx = std::max(gx, (int)cdiv(g.g[i].N, BN));
     gy = std::max(gy, (int)cdiv(g.g[i].M, BM));
   }
-  // MPR_GEMM_LDS_KB: reserve that much LDS per block (unused dynamic LDS beyond the static
-  // stages), capping the blocks per CU so the decode GEMVs of other streams fit beside them
-  // (41 KB = 3 blocks per CU measured 3012 vs 3028 QA pairs/s: off by default).
-  static const int lds_kb = [] {
-    const char* e = getenv("MPR_GEMM_LDS_KB");
-    return e ? atoi(e) : 0;
-  }();
-  constexpr int STATIC_LDS = 2 * (BM + BN) * (BK + 4) * 4;
-  const size_t pad = lds_kb * 1024 > STATIC_LDS ? (size_t)(lds_kb * 1024 - STATIC_LDS) : 0;
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, D, KW, XR>), dim3(gx, gy, g.n), dim3(NT),
-                     pad, s, g);
+                     0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -1043,12 +1034,6 @@ int probe_read(double* ms, int64_t* launches, double* flops, double* bytes) {
 
 namespace {
 // One launch of problems that share a tile configuration (probed / recorded as one launch).
-// MPR_KSPLIT32_ONLY=1: always the 32x32 K-split blocks (A/B switch for measurements and tests)
-const bool g_ksplit32_only = [] {
-  const char* e = getenv("MPR_KSPLIT32_ONLY");
-  return e && atoi(e) != 0;
-}();
-
 // Kernel families of one launch.  F32_*: exact f32 MFMA (v_mfma_f32_32x32x2_f32), the round-1
 // kernels, kept behind MPR_GEMM=f32.  X3_*: the split-bf16 kernels (default).  Within X3_WIDE /
 // X3_TALL (16-deep k steps in order, KW = 1) every output element is accumulated in the same
@@ -1083,7 +1068,7 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
     switch (kind) {
       case F32_BIG: return launch_gemm_group<64, 64, 1, 1, 32, 2, 1, true>(g, s);
       case F32_SMALL:
-        if (blocks32 >= 2048 && !g_ksplit32_only)
+        if (blocks32 >= 2048)
           return launch_gemm_group<64, 32, 1, 1, 64, 2, 4>(g, s);
         return launch_gemm_group<32, 32, 1, 1, 64, 2, 4>(g, s);
       case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>(g, s);
@@ -1149,14 +1134,10 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // half the barriers per K, same k order (bit-identical).  Replayed alone equal (0.79-0.80 of
   // 157.3 either way); in the serving loop the GEMMs run 0.64 -> 0.68 (a CU holding one leaves no
   // LDS for decode blocks) and the loop 4157-4165 -> 4212-4309 QA pairs/s at 40 steps.  Every
-  // 128x128 launch on 32-deep tiles (MPR_X3_BK32=2) halves the blocks per CU of the > 256-block
-  // launches: 4073-4127; 0 = 16-deep only.
-  static const int bk32 = [] {
-    const char* e = getenv("MPR_X3_BK32");
-    return e ? atoi(e) : 1;
-  }();
+  // 128x128 launch on 32-deep tiles halves the blocks per CU of the > 256-block launches
+  // (4073-4127, r02); 16-deep only is slower in the loop.
   if (fam.n)
-    MPR_TRY(gemm_launch(fam, b128 >= 160 && (bk32 == 2 || (bk32 == 1 && b128 <= 256))
+    MPR_TRY(gemm_launch(fam, b128 >= 160 && b128 <= 256
                                  ? X3_WIDE32
                              : b128 >= 160                     ? X3_WIDE
                              : (b64x128 < 128 || short_k) ? X3_SMALL
@@ -1213,7 +1194,7 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, un
 // blocks, made the two-decodes-in-flight serving loop 1-6% slower.)
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const GemmArgs& a = sa.g;
-  MPR_REQUIRE(a.M >= 0 && a.M <= 128 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
+  MPR_REQUIRE(a.M >= 0 && a.M <= 256 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
   if (a.M == 0 || a.N == 0) return MPR_OK;
   MPR_REQUIRE(sa.wpk && aligned16(sa.wpk), "gemm_skinny: needs the 16-byte aligned packed weight");
   MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && aligned16(a.A) &&
@@ -1243,94 +1224,37 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(!(F & SKF_SSQ) || F == SKF_SSQ, "gemm_skinny: ssq only on a plain projection");
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
-  // Above 32 rows (grouped decodes) the rows split over blocks of MPR_SKINNY_ROWS (32 default,
-  // or 16; 0 = one block column holds all rows, MR up to 8).  Serving loop, 20 steps: 3783-3831
-  // (0) -> 3893-3908 (32) / 3913-3932 (16) QA pairs/s; the 128-row o-proj 17.9 us at 32 blocks.
-  // At the bench's 80 steps, five alternating pairs on two boxes: 32 ahead by 0.3-1.2 % in
-  // every pair (4539-4551 vs 4493-4506; 4342-4393 vs 4292-4372), main loop 3.48-3.65 vs
-  // 3.52-3.67 ms.
-  static const int row_blk = [] {
-    const char* e = getenv("MPR_SKINNY_ROWS");
-    const int v = e ? atoi(e) : 32;
-    return v == 16 || v == 32 ? v : 0;
-  }();
-  MPR_REQUIRE(!sa.rs_part || a.M <= 32 || row_blk > 0,
-              "gemm_skinny: an external row scale needs row blocks of <= 32 rows");
-  static const bool small_lds = [] {
-    const char* e = getenv("MPR_SKINNY_SMALL");
-    return e && e[0] == '1';
-  }();
+  // Above 32 rows (grouped decodes on the skinny path: MPR_DECODE_GEMM=skinny) the rows split
+  // over blocks of 32 (serving loop, 20 steps: 3783-3831 with one block column of up to 8 row
+  // groups -> 3893-3908 QA pairs/s; 16-row blocks within 1 %).
   return probed(PROBE_SKINNY, 2.0 * a.M * a.N * a.K, gemm_bytes(a), s, [&]() {
-    // MPR_SKINNY_SMALL=1: <= 43 KB of LDS per block (fits beside 3 GEMM blocks on a CU) at the
-    // price of more, shorter passes; in the serving loop 3086 vs 3028 QA pairs/s (within the
-    // box-to-box spread), and the MAXC change moves the summation order: off by default.
     // (A K split of the K = 2048 GEMV over 4 blocks per tile, partials published with an
     // agent-scope fence and added by the last block, made a 16-row generate 5.49 -> 5.89 ms and
     // the serving loop 3050 -> 2830 QA pairs/s: the cross-XCD publish costs more than the
     // 32-block launch loses.)
-    if (small_lds) {
-      if (a.M > 32) {
-        if (per <= 1) launch_skinny<1, 1, false, 4>(sa, F, (unsigned)tiles, s);
-        else launch_skinny<1, 1, true, 4>(sa, F, (unsigned)tiles, s);
-      } else if (a.M > 16) {
-        if (per <= 2) launch_skinny<2, 1, false, 2>(sa, F, (unsigned)tiles, s);
-        else launch_skinny<2, 1, true, 2>(sa, F, (unsigned)tiles, s);
-      } else {
-        if (per <= 4) launch_skinny<4, 1, false>(sa, F, (unsigned)tiles, s);
-        else launch_skinny<4, 1, true>(sa, F, (unsigned)tiles, s);
-      }
-      MPR_LAUNCHED();
-      return MPR_OK;
-    }
-    if (a.M > 32 && row_blk > 0) {  // rows split over blocks of row_blk rows (grouped decodes)
-      const unsigned gy = (unsigned)cdiv(a.M, row_blk);
-      if (row_blk == 16) {
-        if (amax && tiles >= 1024 && per <= 4)
-          launch_skinny<4, 2, false>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
-        else if (per <= 4)
-          launch_skinny<4, 1, false>(sa, F, (unsigned)tiles, s, gy);
-        else if (per <= 8)
-          launch_skinny<8, 1, false>(sa, F, (unsigned)tiles, s, gy);
-        else if (per <= 16)
-          launch_skinny<16, 1, false>(sa, F, (unsigned)tiles, s, gy);
-        else
-          launch_skinny<16, 1, true>(sa, F, (unsigned)tiles, s, gy);
-      } else {
-        // (Four 16-column tiles per block sharing each staged 32-row slab — the slab is staged
-        // once per 16 columns — measured slower: C5's t5-base 128-row decodes 84.0 -> 96.3 ms
-        // per batch, the serving loop 3.77-3.79 -> 3.86-3.88 ms per step.)
-        // 4-chunk passes above 4 chunks per wave, so the block's slabs take 70 KB of LDS instead
-        // of 136 KB and two blocks fit per CU (the 8-chunk slab holds one: t5-base's 576-block
-        // 128-row qkv ran in ~3 rounds of blocks).  Same chunk order per accumulator chain,
-        // padding chunks add exact zeros: bit-identical.  C5 end to end 72.1-73.1 -> 68.4-69.3
-        // ms per batch, the serving loop unchanged (3.69-3.71 ms per step either way).
-        // MPR_SKINNY_MAXC=8 (read per call) restores the 8-chunk slabs.
-        const char* mce = getenv("MPR_SKINNY_MAXC");
-        const bool c4 = !(mce && atoi(mce) == 8);
-        if (amax && tiles >= 1024 && per <= 4)
-          launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
-        else if (per <= 4)
-          launch_skinny<4, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
-        else if (c4)
-          launch_skinny<4, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
-        else if (per <= 8)
-          launch_skinny<8, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
-        else
-          launch_skinny<8, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
-      }
-    } else if (a.M > 64) {  // eight row groups per weight load (up to 8 batches): 2-chunk passes fit
-      // (one tile per block also for the lm_head: two would spill registers)
-      if (per <= 2)
-        launch_skinny<2, 1, false, 8>(sa, F, (unsigned)tiles, s);
-      else
-        launch_skinny<2, 1, true, 8>(sa, F, (unsigned)tiles, s);
-    } else if (a.M > 32) {  // four row groups per weight load (up to 4 batches of <= 16 rows)
+    if (a.M > 32) {  // rows split over blocks of 32 rows (grouped decodes)
+      const unsigned gy = (unsigned)cdiv(a.M, 32);
+      // (Four 16-column tiles per block sharing each staged 32-row slab — the slab is staged
+      // once per 16 columns — measured slower: C5's t5-base 128-row decodes 84.0 -> 96.3 ms
+      // per batch, the serving loop 3.77-3.79 -> 3.86-3.88 ms per step.)
+      // 4-chunk passes above 4 chunks per wave, so the block's slabs take 70 KB of LDS instead
+      // of 136 KB and two blocks fit per CU (the 8-chunk slab holds one: t5-base's 576-block
+      // 128-row qkv ran in ~3 rounds of blocks).  Same chunk order per accumulator chain,
+      // padding chunks add exact zeros: bit-identical.  C5 end to end 72.1-73.1 -> 68.4-69.3
+      // ms per batch, the serving loop unchanged (3.69-3.71 ms per step either way).
+      // MPR_SKINNY_MAXC=8 (read per call) restores the 8-chunk slabs.
+      const char* mce = getenv("MPR_SKINNY_MAXC");
+      const bool c4 = !(mce && atoi(mce) == 8);
       if (amax && tiles >= 1024 && per <= 4)
-        launch_skinny<4, 2, false, 4>(sa, F, (unsigned)cdiv(tiles, 2), s);
+        launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
       else if (per <= 4)
-        launch_skinny<4, 1, false, 4>(sa, F, (unsigned)tiles, s);
-      else  // 4-chunk passes: a wider slab for 64 rows would not fit the 160 KiB LDS
-        launch_skinny<4, 1, true, 4>(sa, F, (unsigned)tiles, s);
+        launch_skinny<4, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
+      else if (c4)
+        launch_skinny<4, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
+      else if (per <= 8)
+        launch_skinny<8, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
+      else
+        launch_skinny<8, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
     } else if (a.M > 16) {  // two row groups per weight load (2 batches of <= 16 rows)
       if (amax && tiles >= 1024 && per <= 4)
         launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s);

@@ -554,14 +554,8 @@ __global__ void qnorm_kernel(const float* Q, int b, int d, float* out) {
 // a flag) — never a silently approximate id.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-constexpr int CB_RT = 128;             // index rows per block tile (4 x 32-row MFMA tiles)
-constexpr int CB_QT = 128;             // queries per block: 4 waves x 32
-constexpr int CB_BK = 32;              // k per LDS stage (two 16-deep MFMA steps)
-constexpr int CB_LDK = CB_BK + 8;      // LDS row stride in bf16 (16-byte pad: conflict-free)
-constexpr int CB_D = 8;                // stages of global loads in flight (1 wave per SIMD)
 constexpr int CB_L = 8;                // coarse candidates kept per lane list
 constexpr int CB_C = 64;               // coarse candidates re-ranked per query
-constexpr int CB_STAGE = CB_RT * CB_LDK;
 
 __global__ void to_bf16_kernel(const float* __restrict__ x, int64_t n4, bf16x4* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
@@ -619,203 +613,17 @@ __global__ __launch_bounds__(1024) void max_kernel(const float* __restrict__ x, 
   }
 }
 
-// Block = 4 waves = CB_QT queries (wave w: queries qt*128 + 32w + (lane & 31); the block's bf16
-// query rows resident in LDS, the B operand) x a strided set of 128-row index tiles (staged
-// through LDS, shared by the 4 waves, A operand).  Per row tile each lane turns its 64
-// accumulators into coarse keys and keeps a sorted list of its best CB_L; each query's two lists
-// (lane halves) leave the block.
-template <int KS>
-__global__ __launch_bounds__(256, 1) void scan_bf_kernel(const __bf16* __restrict__ Xb,
-                                                         const float* __restrict__ xnorm,
-                                                         int64_t n, int64_t row_offset,
-                                                         const __bf16* __restrict__ Qb, int b,
-                                                         const float* __restrict__ qnorm,
-                                                         int nqt, int RB, float* cand_key,
-                                                         int64_t* cand_id, float* lane_bound) {
-  constexpr int d = KS * 16, KQ = CB_BK / 8;  // 16-byte loads per staged row
-  constexpr int SPT = KS / 2;                  // stages per row tile
-  __shared__ __attribute__((aligned(16))) __bf16 xs[2][CB_STAGE];
-  __shared__ float xn_s[2][CB_RT];
-  int qt, rb;
-  {
-    const int total = gridDim.x, hw = blockIdx.x;
-    const int xcd = hw & 7, slot = hw >> 3, q8 = total >> 3, r8 = total & 7;
-    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-    qt = t % nqt;
-    rb = t / nqt;
-  }
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 31, lh = lane >> 5;
-  const int64_t ntile = (n + CB_RT - 1) / CB_RT;
-  const int ntb = (int)((ntile - rb + RB - 1) / RB);
-
-  // the block's query rows stay in LDS for the whole scan (row stride d + 8 bf16: the B-fragment
-  // reads of 32 rows are conflict-free); zero rows past b
-  extern __shared__ __attribute__((aligned(16))) __bf16 qs[];  // [CB_QT][d + 8]
-  constexpr int LDQ = d + 8;
-  const int q = qt * CB_QT + wave * 32 + li;
-  const bool qok = q < b;
-  const float qn_l = qok ? qnorm[q] : 0.f;
-  for (int idx = tid; idx < CB_QT * (d / 8); idx += 256) {
-    const int r = idx / (d / 8), c = (idx % (d / 8)) * 8, qq = qt * CB_QT + r;
-    bf16x8 v = bf16x8{};
-    if (qq < b) v = *reinterpret_cast<const bf16x8*>(Qb + (int64_t)qq * d + c);
-    *reinterpret_cast<bf16x8*>(&qs[r * LDQ + c]) = v;
-  }
-  // B[k = 16 s + 8 lh + j][col li] = Q~[wave's query li][16 s + 8 lh + j]
-  const __bf16* qrow = qs + (wave * 32 + li) * LDQ + 8 * lh;
-
-  // rows past n (and stages past the block's last tile) load row n-1: their keys are masked in the
-  // epilogue, and no select on the loaded data lets the compiler wait for a load early
-  bf16x8 rx[CB_D][2];
-  float rn0 = 0.f;  // a tile's first stage always lands in slot 0 (SPT % CB_D == 0)
-  // stage ks of the block's row tile tt (ks is a constant once the stage loop is unrolled)
-  auto gload = [&](int j, int tt, int ks) {
-    const int64_t row0 = (int64_t)(rb + (int64_t)tt * RB) * CB_RT;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = tid + i * 256, r = idx / KQ, c = ks * CB_BK + (idx % KQ) * 8;
-      const int64_t row = row0 + r;
-      rx[j][i] = *reinterpret_cast<const bf16x8*>(Xb + (row < n ? row : n - 1) * (int64_t)d + c);
-    }
-    if (ks == 0) {  // the tile's row norms ride with its first stage
-      const int64_t nrow = row0 + (tid & (CB_RT - 1));
-      rn0 = nrow < n ? xnorm[nrow] : INFINITY;  // rows past n: infinite keys
-    }
-  };
-  auto swrite = [&](int st, int j, int tt, int ks) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = tid + i * 256, r = idx / KQ, c = (idx % KQ) * 8;
-      *reinterpret_cast<bf16x8*>(&xs[st][r * CB_LDK + c]) = rx[j][i];
-    }
-    if (ks == 0 && tid < CB_RT) xn_s[tt & 1][tid] = rn0;
-  };
-  bf16x8 fa[4][2], na[4][2], fb[2], nb[2];
-  // fragments of stage `ks` of a row tile: the 4 row tiles' A from the staged rows, the wave's
-  // B from the resident query rows
-  auto sread = [&](int st, int ks, bf16x8(&xa)[4][2], bf16x8(&xb)[2]) {
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        xa[mi][u] = *reinterpret_cast<const bf16x8*>(&xs[st][(mi * 32 + li) * CB_LDK + 16 * u +
-                                                              8 * lh]);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      xb[u] = *reinterpret_cast<const bf16x8*>(qrow + CB_BK * ks + 16 * u);
-  };
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[mi][r] = 0.f;
-  // the lane's sorted best-CB_L list, in registers.  Per row tile only the lane's best two rows
-  // may enter it; the tile's third-best key goes into `drop`, so every row the lane did not keep
-  // has a key >= min(list's last key, drop) — the lane's bound the re-rank tests against.
-  float bk[CB_L];
-  int bi[CB_L];
-#pragma unroll
-  for (int t = 0; t < CB_L; ++t) {
-    bk[t] = INFINITY;
-    bi[t] = INT_MAX;
-  }
-  float drop = INFINITY;
-
-  gload(0, 0, 0);
-  swrite(0, 0, 0, 0);
-  gload(0, 0, 1);
-  swrite(1, 0, 0, 1);
-#pragma unroll
-  for (int j = 0; j < CB_D; ++j) gload(j, (2 + j) / SPT, (2 + j) % SPT);
-  __syncthreads();
-  sread(0, 0, fa, fb);
-  __syncthreads();
-  static_assert(SPT % CB_D == 0 && SPT % 2 == 0, "stage slots / LDS stages repeat per row tile");
-  // one barrier per stage: multiply stage t (fragments in registers), read stage t+1's
-  // fragments, write stage t+2 into stage t's LDS buffer, re-arm the register slot
-  for (int tt = 0; tt < ntb; ++tt) {
-#pragma clang loop unroll(full)
-    for (int ks = 0; ks < SPT; ++ks) {
-      const int st = ks & 1, j = ks % CB_D;
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          acc[mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][u], fb[u], acc[mi], 0, 0, 0);
-      sread(st ^ 1, (ks + 1) % SPT, na, nb);
-      swrite(st, j, tt + (ks + 2) / SPT, (ks + 2) % SPT);
-      gload(j, tt + (ks + 2 + CB_D) / SPT, (ks + 2 + CB_D) % SPT);
-      __syncthreads();
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        fa[mi][0] = na[mi][0];
-        fa[mi][1] = na[mi][1];
-      }
-      fb[0] = nb[0];
-      fb[1] = nb[1];
-    }
-    {  // coarse values of this row tile: v = max(|x|^2 - 2 q~.x~ + |q|^2, 0) with its 7 low
-       // mantissa bits replaced by the tile row (a nonnegative float orders as its bits; the
-       // quantisation, < 2^-16 relative, is in the re-rank's bound), so the best three are kept by
-       // integer min/median steps with no compare masks; best two -> the lane's list, third -> drop
-      uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rr = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const float key = fmaxf(fmaf(-2.0f, acc[mi][r], xn_s[tt & 1][rr]) + qn_l, 0.0f);
-          acc[mi][r] = 0.f;
-          const uint32_t v = (__float_as_uint(key) & ~127u) | (uint32_t)rr;
-          v3 = min(v3, max(v2, v));
-          v2 = min(v2, max(v1, v));
-          v1 = min(v1, v);
-        }
-      drop = fminf(drop, __uint_as_float(v3 & ~127u));
-      auto insert = [&](float ck, int ci) {
-#pragma unroll
-        for (int t = 0; t < CB_L; ++t) {
-          const bool sw = ck < bk[t];
-          const float tk = sw ? bk[t] : ck;
-          const int ti = sw ? bi[t] : ci;
-          bk[t] = sw ? ck : bk[t];
-          bi[t] = sw ? ci : bi[t];
-          ck = tk;
-          ci = ti;
-        }
-      };
-      const int row0 = (rb + tt * RB) * CB_RT;  // n < 2^31 (checked by the launcher)
-      const float k1 = __uint_as_float(v1 & ~127u), k2 = __uint_as_float(v2 & ~127u);
-      if (k1 < bk[CB_L - 1]) insert(k1, row0 + (int)(v1 & 127u));
-      if (k2 < bk[CB_L - 1]) insert(k2, row0 + (int)(v2 & 127u));
-    }
-  }
-  if (!qok) return;
-  float* okp = cand_key + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
-  int64_t* oip = cand_id + (((int64_t)q * RB + rb) * 2 + lh) * CB_L;
-#pragma unroll
-  for (int t = 0; t < CB_L; ++t) {
-    okp[t] = bk[t];
-    oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
-  }
-  lane_bound[((int64_t)q * RB + rb) * 2 + lh] = fminf(bk[CB_L - 1], drop);
-}
-
 // The coarse scan with the queries in REGISTERS, so one block covers up to 256 queries and the
-// bf16 index is streamed from HBM once per search (scan_bf_kernel holds 128 queries in LDS and
-// reads the index once per 128-query tile: twice at C5).  Block = NW waves x 32 queries; wave w's
+// bf16 index is streamed from HBM once per search (round 2's kernel held 128 queries in LDS and
+// read the index once per 128-query tile: twice at C5).  Block = NW waves x 32 queries; wave w's
 // lane keeps its query's bf16 row as the MFMA B operand for every 16-deep k-step (KS x 16 B:
 // 128 VGPRs at d = 512), so only the index tile passes through LDS: 64-row x 64-deep stages
 // (register prefetch CB2_D stages ahead, two LDS buffers, one barrier per stage), every wave reading
 // the A fragments of all 64 rows (1 KiB of LDS per 32x32x16 MFMA: 128 B/clk/CU at the MFMA rate,
 // half the array's 256).  Two waves per SIMD at NW = 8, so one wave's key epilogue runs beside the
-// other's MFMAs.  Keys, lists and the lane bound are scan_bf_kernel's (the row tag now 6 bits, so
-// the quantisation is < 2^-17 relative, inside the re-rank's 2^-16 margin); the outputs share its
-// layout with one list per (query, block) ([q][RB][CB_L]: the two lane halves merged in-kernel),
-// so select / re-rank / fallback are unchanged.
+// other's MFMAs.  Keys: the coarse value quantised with the row tag in its low 6 bits (so
+// the quantisation is < 2^-17 relative, inside the re-rank's 2^-16 margin); one sorted list of
+// CB_L per (query, block) ([q][RB][CB_L]: the two lane halves merged in-kernel) and its lane bound.
 constexpr int CB2_RT = 64;             // index rows per tile (2 x 32-row MFMA tiles)
 constexpr int CB2_BK = 64;             // k per LDS stage (4 x 16-deep MFMA steps)
 
@@ -933,7 +741,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
       gload(j1, tt + (ks + 1 + D) / SPT, (ks + 1 + D) % SPT);
       __syncthreads();
     }
-    {  // keys of this row tile (scan_bf_kernel's epilogue, 6-bit row tag)
+    {  // keys of this row tile (6-bit row tag)
       uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
@@ -1008,276 +816,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
     oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
   }
   lane_bound[(int64_t)q * RB + rb] = bound;
-}
-
-// Coarse selection: block per query, the CB_C smallest of its n_cand lane-list keys (ids
-// alongside), sorted by (key, id).  The CB_C-th key is found by a bisection over the keys' order
-// bits (counts by a block reduction), then the <= CB_C keys at or below it are ranked.
-
-// Block-wide: the best CB_C of one query's n_cand coarse candidates, sorted by (key, id), into
-// sel_key / sel_id (this query's rows; global memory or LDS), padded with (+inf, -1).
-template <int PER>
-__device__ __forceinline__ void select_block(const float* __restrict__ ck,
-                                             const int64_t* __restrict__ ci, int n_cand,
-                                             float* sel_key, int64_t* sel_id) {
-  __shared__ float sk[CB_C * 2];
-  __shared__ int64_t si[CB_C * 2];
-  __shared__ int nsel;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t u[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int c = tid + j * 256;
-    u[j] = c < n_cand && ci[c] >= 0 ? order_bits(ck[c]) : 0xFFFFFFFFu;
-  }
-  // smallest v with count(u <= v) >= CB_C: a radix select over the order bits, 8 bits per pass
-  // (4 passes of a 256-bin LDS histogram and one wave's prefix scan, instead of a 32-step
-  // bisection with a block reduction per step)
-  __shared__ int hist[256];
-  __shared__ uint32_t s_prefix;
-  __shared__ int s_below;
-  uint32_t lo;
-  if (n_cand < CB_C) {
-    lo = 0xFFFFFFFFu;  // every candidate is kept
-  } else {
-    uint32_t prefix = 0;
-    int below = 0;  // keys whose decided bits are below the prefix
-#pragma unroll 1
-    for (int pass = 0; pass < 4; ++pass) {
-      const int shift = 24 - 8 * pass;
-      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-      hist[tid] = 0;
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < PER; ++j)
-        if (tid + j * 256 < n_cand && (u[j] & hmask) == prefix)
-          atomicAdd(&hist[(u[j] >> shift) & 255u], 1);  // LDS atomic
-      __syncthreads();
-      if (wave == 0) {
-        const int c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2],
-                  c3 = hist[4 * lane + 3];
-        int inc = c0 + c1 + c2 + c3;  // inclusive scan of the lanes' 4-bin sums
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const int o = __shfl_up(inc, off, 64);
-          if (lane >= off) inc += o;
-        }
-        const int excl = below + inc - (c0 + c1 + c2 + c3);
-        const bool hit = excl < CB_C && below + inc >= CB_C;  // exactly one lane
-        if (hit) {
-          int run = excl, dgt = 4 * lane;
-          if (run + c0 < CB_C) {
-            run += c0;
-            ++dgt;
-            if (run + c1 < CB_C) {
-              run += c1;
-              ++dgt;
-              if (run + c2 < CB_C) {
-                run += c2;
-                ++dgt;
-              }
-            }
-          }
-          s_prefix = prefix | ((uint32_t)dgt << shift);
-          s_below = run;
-        }
-      }
-      __syncthreads();
-      prefix = s_prefix;
-      below = s_below;
-    }
-    lo = prefix;
-  }
-  if (tid == 0) nsel = 0;
-  __syncthreads();
-  // gather every key <= the threshold (ties past CB_C are ranked out below; at most 2 CB_C kept)
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int c = tid + j * 256;
-    if (u[j] <= lo && u[j] != 0xFFFFFFFFu) {
-      const int slot = atomicAdd(&nsel, 1);  // LDS atomic
-      if (slot < 2 * CB_C) {
-        sk[slot] = ck[c];
-        si[slot] = ci[c];
-      }
-    }
-  }
-  __syncthreads();
-  const int m = min(nsel, 2 * CB_C);
-  for (int c = tid; c < CB_C; c += 256) {  // pad a short list
-    sel_key[c] = INFINITY;
-    sel_id[c] = -1;
-  }
-  __syncthreads();
-  if (tid < m) {
-    const float a = sk[tid];
-    const int64_t ia = si[tid];
-    int rank = 0;
-    for (int c = 0; c < m; ++c) rank += key_less(sk[c], si[c], a, ia) ? 1 : 0;
-    if (rank < CB_C) {
-      sel_key[rank] = a;
-      sel_id[rank] = ia;
-    }
-  }
-}
-
-template <int PER>
-__global__ __launch_bounds__(256) void coarse_select_kernel(const float* __restrict__ cand_key,
-                                                            const int64_t* __restrict__ cand_id,
-                                                            int n_cand, float* sel_key,
-                                                            int64_t* sel_id) {
-  const int64_t qi = blockIdx.x;
-  select_block<PER>(cand_key + qi * n_cand, cand_id + qi * n_cand, n_cand, sel_key + qi * CB_C,
-                    sel_id + qi * CB_C);
-}
-
-// Exact re-rank: block per query over its CB_C coarse candidates (sorted coarse keys, global ids):
-// the sufficiency test (against the selected list and every lane's bound), the fp32 key
-// of every candidate (the exact scan's formula), the best k by (key, id); gate[q] = 1 asks the
-// exact scan for this query.
-__device__ __forceinline__ void rerank_block(const float* __restrict__ X,
-                                             const float* __restrict__ xnorm, int d,
-                                             int64_t row_offset, const float* __restrict__ Q,
-                                             const float* sk, const int64_t* si,
-                                             const float* lane_bound, int n_lists, int k,
-                                             const float* xmax, float* out_dist,
-                                             int64_t* out_id, int* gate) {
-  __shared__ float qs[512];
-  __shared__ float keys[CB_C];
-  __shared__ int64_t ids[CB_C];
-  __shared__ float part[4], epart[4], lmin[4];
-  const int qi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* qp = Q + (int64_t)qi * d;
-  float ss = 0.f, ee = 0.f;
-  for (int c = tid; c < d; c += 256) {
-    const float v = qp[c];
-    const float r = (float)(__bf16)v - v;  // the coarse scan's rounding of this component
-    qs[c] = v;
-    ss += v * v;
-    ee += r * r;
-  }
-  // the smallest last key over the query's lane lists
-  float lm = INFINITY;
-  const float* lb = lane_bound + (int64_t)qi * n_lists;
-  for (int l = tid; l < n_lists; l += 256) lm = fminf(lm, lb[l]);
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    ss += __shfl_xor(ss, off, 64);
-    ee += __shfl_xor(ee, off, 64);
-    lm = fminf(lm, __shfl_xor(lm, off, 64));
-  }
-  if (lane == 0) {
-    part[wave] = ss;
-    epart[wave] = ee;
-    lmin[wave] = lm;
-  }
-  __syncthreads();
-  const float qn = (part[0] + part[1]) + (part[2] + part[3]);
-  // The bound (below): a candidate whose coarse key exceeds T = s~(k) + 2E has an exact key above
-  // the exact k-th best, so only the prefix of the sorted list with keys <= T is re-scored (a
-  // margin of 2^-16 relative keeps the excluded keys distinct from the k-th after the sqrt); the
-  // rest rank last with key +inf.  Typically k + a few of the CB_C rows are read.
-  const float qa = sqrtf(qn), ea = sqrtf((epart[0] + epart[1]) + (epart[2] + epart[3]));
-  const float Xm = sqrtf(xmax[0]), Rm = sqrtf(xmax[1]);
-  const float E = 2.0f * (ea * Xm + qa * Rm + ea * Rm + 2.0f * d * 5.9604645e-8f * (qa + ea) *
-                                                       (Xm + Rm)) * 1.01f +
-                  4.0f * 5.9604645e-8f * (Xm * Xm + 2.0f * qa * Xm + qa * qa);
-  // coarse values are quantised down by < 2^-16 relative (scan_bf_kernel's low-bit row tag)
-  const float T = sk[k - 1] * (1.0f + 3.0517578e-5f) + 2.0f * E;
-  const float Tcut = T * (1.0f + 1.5258789e-5f);
-  int need = 0;  // sorted keys: the count of keys <= Tcut is a prefix length
-  for (int c = lane; c < CB_C; c += 64) need += sk[c] <= Tcut ? 1 : 0;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) need += __shfl_xor(need, off, 64);
-  need = max(need, min(k, CB_C));
-  for (int c = need + tid; c < CB_C; c += 256) {
-    keys[c] = INFINITY;
-    ids[c] = INT64_MAX;
-  }
-  // candidates round-robin over the 4 waves, 4 at a time with every load of the group in flight
-  // (d <= 512: 8 components per lane), 64 lanes over the row
-  constexpr int G = 4;
-  for (int c0 = wave * G; c0 < need; c0 += 4 * G) {
-    float xv[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (c0 + g >= need) break;  // wave-uniform
-      const int64_t id = si[c0 + g];
-      const float* xp = X + (id >= 0 ? id - row_offset : 0) * (int64_t)d;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int e = lane + 64 * j;
-        xv[g][j] = e < d ? xp[e] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int c = c0 + g;
-      if (c >= need) break;  // wave-uniform
-      const int64_t id = si[c];
-      float dot = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int e = lane + 64 * j;
-        dot += e < d ? qs[e] * xv[g][j] : 0.f;
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) dot += __shfl_xor(dot, off, 64);
-      if (lane == 0) {
-        keys[c] = id >= 0 ? sqrtf(fmaxf(qn + xnorm[id - row_offset] - 2.0f * dot, 0.0f))
-                          : INFINITY;
-        ids[c] = id >= 0 ? id : INT64_MAX;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int nvalid = 0;
-    for (int c = 0; c < CB_C; ++c) nvalid += si[c] >= 0 ? 1 : 0;
-    const float lists_last = fminf(fminf(lmin[0], lmin[1]), fminf(lmin[2], lmin[3]));
-    const bool enough = (nvalid < CB_C || sk[CB_C - 1] > T) && lists_last > T;
-    gate[qi] = enough ? 0 : 1;
-  }
-  // rank of each candidate among the CB_C by (exact key, id): the best k are written in order
-  if (tid < CB_C) {
-    const float a = keys[tid];
-    const int64_t ia = ids[tid];
-    int rank = 0;
-    for (int c = 0; c < CB_C; ++c) rank += key_less(keys[c], ids[c], a, ia) ? 1 : 0;
-    if (rank < k) {
-      out_dist[(int64_t)qi * k + rank] = ia == INT64_MAX ? NAN : a;
-      out_id[(int64_t)qi * k + rank] = ia == INT64_MAX ? -1 : ia;
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void rerank_kernel(const float* __restrict__ X,
-                                                     const float* __restrict__ xnorm, int d,
-                                                     int64_t row_offset,
-                                                     const float* __restrict__ Q,
-                                                     const float* sel_key, const int64_t* sel_id,
-                                                     const float* lane_bound, int n_lists, int k,
-                                                     const float* xmax, float* out_dist,
-                                                     int64_t* out_id, int* gate) {
-  const int64_t qi = blockIdx.x;
-  rerank_block(X, xnorm, d, row_offset, Q, sel_key + qi * CB_C, sel_id + qi * CB_C, lane_bound,
-               n_lists, k, xmax, out_dist, out_id, gate);
-}
-
-// select + re-rank in one block per query (n_cand <= 256 * PER): the sorted CB_C stay in LDS
-template <int PER>
-__global__ __launch_bounds__(256) void coarse_rerank_kernel(
-    const float* __restrict__ cand_key, const int64_t* __restrict__ cand_id, int n_cand,
-    const float* __restrict__ X, const float* __restrict__ xnorm, int d, int64_t row_offset,
-    const float* __restrict__ Q, const float* lane_bound, int n_lists, int k, const float* xmax,
-    float* out_dist, int64_t* out_id, int* gate) {
-  __shared__ float sel_k[CB_C];
-  __shared__ int64_t sel_i[CB_C];
-  const int64_t qi = blockIdx.x;
-  select_block<PER>(cand_key + qi * n_cand, cand_id + qi * n_cand, n_cand, sel_k, sel_i);
-  __syncthreads();
-  rerank_block(X, xnorm, d, row_offset, Q, sel_k, sel_i, lane_bound, n_lists, k, xmax, out_dist,
-               out_id, gate);
 }
 
 // Select + re-rank without a full selection (block per query, the one-list-per-block layout of
@@ -1614,25 +1152,14 @@ int launch_scan_mm(const float* X, int64_t n, int d, int64_t row_offset, int met
 }
 
 // ---- coarse path launchers --------------------------------------------------------------------
-// scan_bf2_kernel (queries in registers, the index read once per 256 queries) unless
-// MPR_COARSE_V1 asks for the LDS-resident-query kernel
-bool coarse_v2() {
-  static const bool v = getenv("MPR_COARSE_V1") == nullptr;
-  return v;
-}
 int coarse_waves(int b) { return b <= 128 ? 4 : 8; }
+// one 8-wave block (two at 4 waves) per CU, every lane seeing >= 8 row tiles (<= 512: the
+// threshold gather of coarse_rerank2_kernel walks at most 512 lists)
 int coarse_rowblocks(int64_t n, int b) {
-  if (coarse_v2()) {
-    // one 8-wave block (two at 4 waves) per CU, every lane seeing >= 8 row tiles
-    const int64_t ntile = (n + CB2_RT - 1) / CB2_RT;
-    const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
-    const int64_t per = std::max<int64_t>(1, (NW == 4 ? 512 : 256) / nqt);
-    return (int)std::max<int64_t>(1, std::min<int64_t>(per, ntile / 8));
-  }
-  // ~2 blocks per CU, but every lane sees >= 8 row tiles (its bound gets tight: few fallbacks)
-  const int64_t ntile = (n + CB_RT - 1) / CB_RT;
-  const int nqt = (int)cdiv(b, CB_QT);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(1, 512 / nqt), ntile / 8));
+  const int64_t ntile = (n + CB2_RT - 1) / CB2_RT;
+  const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
+  const int64_t per = std::max<int64_t>(1, (NW == 4 ? 512 : 256) / nqt);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(per, ntile / 8));
 }
 
 bool scan_coarse_eligible(int64_t n, int d, int b, int k, int metric) {
@@ -1766,77 +1293,25 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     MPR_LAUNCHED();
     qn_pre = w.qn;
     const __bf16* xb = reinterpret_cast<const __bf16*>(Xb);
-    if (coarse_v2()) {
-      const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
-      const dim3 grid((unsigned)(nqt * RB)), blk((unsigned)(NW * 64));
-      // prefetch depth: 4 stages (4 KiB per thread-slot at 8 waves); 2 at 4 waves, where each
-      // stage is two 16-byte loads per thread (the 256-VGPR budget of 2 blocks per CU)
+    const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
+    const dim3 grid((unsigned)(nqt * RB)), blk((unsigned)(NW * 64));
+    // prefetch depth: 4 stages (4 KiB per thread-slot at 8 waves); 2 at 4 waves, where each
+    // stage is two 16-byte loads per thread (the 256-VGPR budget of 2 blocks per CU)
 #define MPR_BF2(KS_, NW_, D_, BK_)                                                          \
   hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, D_, BK_>), grid, blk, 0, s, xb, xnorm, n,     \
                      row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
-      // 8 waves: 64-deep stages, 4 in flight; MPR_COARSE_BK=128: 128-deep stages (16 MFMAs per
-      // wave between barriers) with 2 of two loads per thread in flight (the same bytes)
-      static const bool bk64 = [] {
-        const char* e = getenv("MPR_COARSE_BK");
-        return !(e && atoi(e) == 128);
-      }();
-      if (d == 512) {
-        if (NW == 8) {
-          if (bk64) MPR_BF2(32, 8, 4, 64); else MPR_BF2(32, 8, 2, 128);
-        } else {
-          MPR_BF2(32, 4, 2, 64);
-        }
-      } else {
-        if (NW == 8) {
-          if (bk64) MPR_BF2(16, 8, 4, 64); else MPR_BF2(16, 8, 2, 128);
-        } else {
-          MPR_BF2(16, 4, 2, 64);
-        }
-      }
+    if (d == 512) {
+      if (NW == 8) MPR_BF2(32, 8, 4, 64); else MPR_BF2(32, 4, 2, 64);
+    } else {
+      if (NW == 8) MPR_BF2(16, 8, 4, 64); else MPR_BF2(16, 4, 2, 64);
+    }
 #undef MPR_BF2
-    } else {
-      const int nqt = (int)cdiv(b, CB_QT);
-      const size_t qlds = (size_t)CB_QT * (d + 8) * 2;
-      if (d == 512)
-        hipLaunchKernelGGL(scan_bf_kernel<32>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s, xb,
-                           xnorm, n, row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb);
-      else
-        hipLaunchKernelGGL(scan_bf_kernel<16>, dim3((unsigned)(nqt * RB)), dim3(256), qlds, s, xb,
-                           xnorm, n, row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb);
-    }
     MPR_LAUNCHED();
-    const int lpb = coarse_v2() ? 1 : 2;  // candidate lists per (query, block)
-    const int n_cand = RB * lpb * CB_L;
-    static const bool radix = getenv("MPR_COARSE_RADIX") != nullptr;
-    if (lpb == 1 && RB <= 512 && !radix) {
-      // threshold gather over the sorted per-block lists (no full selection)
-      hipLaunchKernelGGL(coarse_rerank2_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
-                         w.ci, RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids,
-                         w.gate);
-      MPR_LAUNCHED();
-    } else if (n_cand <= 256 * 16 && !getenv("MPR_COARSE_UNFUSED")) {
-      if (n_cand <= 256 * 8)
-        hipLaunchKernelGGL(coarse_rerank_kernel<8>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
-                           w.ci, n_cand, X, xnorm, d, row_offset, Q, w.lb, RB * lpb, k, xmax,
-                           out_dist, out_ids, w.gate);
-      else
-        hipLaunchKernelGGL(coarse_rerank_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
-                           w.ci, n_cand, X, xnorm, d, row_offset, Q, w.lb, RB * lpb, k, xmax,
-                           out_dist, out_ids, w.gate);
-      MPR_LAUNCHED();
-    } else {
-      if (n_cand <= 256 * 16)
-        hipLaunchKernelGGL(coarse_select_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck,
-                           w.ci, n_cand, w.sk, w.si);
-      else
-        MPR_TRY(merge_dispatch(w.ck, w.ci, b, n_cand, CB_C, /*keys_are_values=*/0, /*metric=*/0,
-                               w.sk, w.si, s));
-      MPR_LAUNCHED();
-      hipLaunchKernelGGL(rerank_kernel, dim3((unsigned)b), dim3(256), 0, s, X, xnorm, d,
-                         row_offset, Q, w.sk, w.si, w.lb, RB * lpb, k, xmax, out_dist, out_ids,
-                         w.gate);
-      MPR_LAUNCHED();
-    }
+    // threshold gather over the sorted per-block lists (no full selection) + exact re-rank
+    MPR_REQUIRE(RB <= 512, "search: %d coarse row blocks", RB);
+    hipLaunchKernelGGL(coarse_rerank2_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck, w.ci,
+                       RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids, w.gate);
+    MPR_LAUNCHED();
     gate = w.gate;
   }
   if (use_scan_mm(n, d, b, k) && !getenv("MPR_SCAN_MM_OFF")) {

@@ -29,7 +29,7 @@ import torch
 from . import _lib
 from .encoders import CLS, DeviceCLIPText, DeviceViT, encode_towers, encode_towers_multi  # noqa: F401,E501
 from .index import L2, DeviceIndex
-from .staging import to_device, uploader
+from .staging import to_device
 
 BUCKETS = ["very unlikely", "unlikely", "maybe", "likely", "very likely", "certainly"]
 
@@ -83,27 +83,6 @@ def read_pickled_data(path):
     a list of answer strings / a dict of lists.  Refuses anything that needs a global."""
     with open(path, "rb") as f:
         return _DataOnlyUnpickler(f).load()
-
-
-def _staged(batches, up, ahead: int = 2):
-    """Iterate ``batches`` with the next ``ahead`` batches' images already submitted to the
-    uploader (staging.ImageUploader), so their host -> device copies overlap this batch."""
-    if up is None:
-        yield from batches
-        return
-    from collections import deque
-    q = deque()
-    it = iter(batches)
-    while True:
-        while len(q) < ahead + 1:
-            b = next(it, None)
-            if b is None:
-                break
-            up.submit(b.get("image") if isinstance(b, dict) else None)
-            q.append(b)
-        if not q:
-            return
-        yield q.popleft()
 
 
 class VQARetrieval:
@@ -359,8 +338,7 @@ class VQARetrieval:
         pend = None
         npass = 0
         used = set()
-        up = uploader(self.device)
-        for batch in _staged(data_loader, up):
+        for batch in data_loader:
             answers.extend(batch["answer"])
             info["question_type"].extend(batch["question_type"])
             info["question_id"].extend(batch["question_id"])

@@ -33,7 +33,7 @@ from dataclasses import dataclass
 
 import torch
 
-from . import _lib, staging
+from . import _lib
 from .t5 import pieces_per_call
 
 
@@ -96,7 +96,7 @@ class _Call:
 class ServingLoop:
     """One pass of the pipeline over an iterable of batches (see the module docstring)."""
 
-    STAGE_AHEAD = 4  # batches whose host images are being uploaded ahead of their tower pass
+    STAGE_AHEAD = 4  # batches pulled from the source ahead of the one being prepared
 
     def __init__(self, model, opts: ServingOptions):
         self.m = model
@@ -118,7 +118,6 @@ class ServingLoop:
         self.steps_run = []     # decode steps launched per generate call
         self.upcoming = deque()  # pulled from the source, images submitted to the uploader
         self.src_done = False
-        self.uploader = staging.uploader(model.device)
         self._hs = None  # (device ViT, device T5), fetched once per decode group (_handles)
 
     def _handles(self, refresh=False):
@@ -129,15 +128,12 @@ class ServingLoop:
         return self._hs
 
     def _pull(self):
-        """The next source batch; the STAGE_AHEAD batches after it already have their images on
-        their way to the device (staging.ImageUploader), off this thread."""
+        """The next source batch (STAGE_AHEAD more are pulled ahead of it)."""
         while len(self.upcoming) < self.STAGE_AHEAD + 1 and not self.src_done:
             b = next(self.it, None)
             if b is None:
                 self.src_done = True
                 break
-            if self.uploader is not None:
-                self.uploader.submit(b["image"])
             self.upcoming.append(b)
         return self.upcoming.popleft() if self.upcoming else None
 

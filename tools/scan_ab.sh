@@ -9,7 +9,7 @@ TAG=${1:-scan}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-VARIANTS=${VARIANTS:-"MPR_COARSE_RADIX=1 DEFAULT=1"}
+VARIANTS=${VARIANTS:-"DEFAULT=1"}
 timeout -k 10 420 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_configs.py -v -m gpu \
   -k "scan or coarse or c5 or merge" -rf --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1
 rc=$?; echo "pytest rc=$rc" >> "$OUT/steps.log"; [ $rc -eq 0 ] || exit $rc

@@ -25,7 +25,6 @@ for _ in range(10):
 e1.record()
 torch.cuda.synchronize()
 _, ids = ix.search(q, k)
-tag = ("v1" if os.environ.get("MPR_COARSE_V1") else "bf2") + \
-    ("+radix" if os.environ.get("MPR_COARSE_RADIX") else "")
+tag = "bf2"
 print(f"[{tag}] C5 search ({n} rows, {b} queries): {e0.elapsed_time(e1) / 10:.3f} ms, "
       f"exact fallbacks {ix.coarse_fallbacks()}, ids checksum {int(ids.sum())}", flush=True)
