@@ -333,18 +333,6 @@ int mpr_cos_combine(const float* w12, const float* n1, const float* n2, int32_t 
                     const int64_t* n1_strides, const int64_t* n2_strides, float eps, float* out,
                     void* stream);
 
-/* ---- grouped-decode projection (the kernel behind the decoder projections of
- * mpr_t5_generate_batches / _begin for more than 16 rows, architectures/T5VisionModel.py:200-205;
- * exposed for kernel-level tests and benchmarks) ----
- *   mpr_dec_gemm: C[M,N] = R + act(s_m * sum_k A'[m,k] W[n,k]), M <= 256, K % 32 == 0,
- *   N % 16 == 0, fp32 W [N, K] (row stride ldw), fp32-accurate: A' = rms_w * A and
- *   s_m = rsqrt(mean_k A[m,:]^2 + eps) when rms_w is given (T5's RMSNorm folded into the
- *   projection), else A' = A, s_m = 1; act 0 none / 2 relu; R optional (may alias C).  Each row's
- *   results depend only on (K, N), not on M. */
-int mpr_dec_gemm(const float* A, int64_t lda, const float* W, int64_t ldw, float* C, int64_t ldc,
-                 int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr, int32_t act,
-                 const float* rms_w, float eps, void* stream);
-
 /* ---- measurement (bench.py roofline; no reference counterpart) --------------------------------
  * kind 1 = tiled f32-MFMA GEMM, 2 = skinny (decode) GEMM, 0 = off.  While enabled, every launch
  * of that kernel (outside graph capture) is bracketed by hipEvents on its own stream.

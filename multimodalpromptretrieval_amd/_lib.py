@@ -127,9 +127,6 @@ SIGNATURES = [
                                  c_int64, c_int64, c_int32, c_void_p, c_void_p]),
     ("mpr_cos_combine", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, I64P, I64P, I64P, I64P,
                                   c_float, c_void_p, c_void_p]),
-    ("mpr_dec_gemm", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32,
-                               c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p, c_float,
-                               c_void_p]),
 ]
 
 

@@ -452,10 +452,6 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
     {
       const char* e = getenv("MPR_DECODE_FOLD");
       m->fold = !(e && e[0] == '0');
-      // the decode projections on gemm_rows whenever every contraction length allows it
-      const char* g = getenv("MPR_DECODE_GEMM");
-      m->rows = !(g && strcmp(g, "skinny") == 0) && gemm_dec_ok(d, 3 * m->inner) &&
-                gemm_dec_ok(m->inner, d) && gemm_dec_ok(dff, d) && gemm_dec_ok(d, dff);
     }
     MPR_TRY(t5_load(m.get(), t, enc_lut, dec_lut, /*fresh=*/true));
     *out = m.release();

@@ -75,16 +75,6 @@ struct SkinnyArgs {
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
-// Decoder projections of grouped decodes (decode_gemm.hip, 17-256 rows): gemm_skinny's plain
-// contract (fused RMSNorm prologue, ReLU, residual; no argmax / folded-chain options) on the fp32
-// weight [N, K] (g.W, g.ldw), fp32-accurate on the bf16 matrix cores (x3.h).  The work is split
-// along N and K into ~200+ blocks (every weight element read by one block, every block all rows);
-// K slices > 1 need the workspace (gemm_dec_ws_floats) and a second, finishing launch.  The K
-// partition depends on (K, N) only: a row's results do not depend on the row count of the launch.
-bool gemm_dec_ok(int K, int N);  // K % 32 == 0, N % 16 == 0
-size_t gemm_dec_ws_floats(int M, int N, int K);
-int gemm_dec(const SkinnyArgs& a, float* ws, size_t ws_floats, hipStream_t s);
-
 // Kernel probe (bench roofline): hipEvent pairs around every launch of one GEMM kind.
 enum ProbeKind : int { PROBE_OFF = 0, PROBE_GEMM = 1, PROBE_SKINNY = 2, PROBE_RECORD = 3 };
 int probe_enable(int kind);

@@ -131,7 +131,6 @@ struct T5Work {
   DevBuf mask_enc, enc_tmp;  // a group's encoder mask / output when several groups share a decode
   DevBuf ax, yq, hz;  // folded decode chain rows: [a | x], [c | h | u], [h2 | z]
   DevBuf x1ss, x2ss;  // their residual rows' per-16-column sums of squares
-  DevBuf dec_ws;      // split-K partials of the grouped decode's projections (gemm_dec)
   uint64_t gen = 0;  // bumped by every buffer growth: invalidates captured graphs
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {
@@ -172,11 +171,8 @@ struct T5Model : mpr_model {
   // layer instead of 8; MPR_DECODE_FOLD=0 keeps the 8-launch chain): see decode_body.
   bool fold = false;
   bool fold_rows(int B) const;  // the folded chain for a B-row decode
-  // Grouped decodes (> 16 rows) run their layer projections on gemm_dec (decode_gemm.hip) when
-  // every contraction allows it (MPR_DECODE_GEMM=skinny keeps the round-3 GEMV kernels); 16-row
-  // decodes (predict()) keep the skinny GEMVs and the folded chain.
-  bool rows = false;
-  int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& w, hipStream_t s,
+  // A decode projection: the skinny GEMV on the packed weight (gemm_skinny)
+  int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
                int* amax_nparts = nullptr) const;
   bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
   int build_folded();

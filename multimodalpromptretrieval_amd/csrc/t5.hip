@@ -86,16 +86,8 @@ bool T5Model::fold_rows(int B) const {
   return fold && B <= max_rows;
 }
 
-// A decode projection: gemm_dec for grouped decodes (> 16 rows; not the argmax head or the folded
-// chain's options), else the skinny GEMV on the packed weight.
-int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, const DevBuf& w, hipStream_t s,
+int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
                       int* amax_nparts) const {
-  if (rows && a.g.M > 16 && !a.amax_val && !a.ssq_out && !a.rs_part) {
-    SkinnyArgs b = a;
-    b.g.W = w.as<float>();
-    b.g.ldw = a.g.K;
-    return gemm_dec(b, ws->dec_ws.as<float>(), ws->dec_ws.bytes / 4, s);
-  }
   SkinnyArgs b = a;
   b.wpk = pk.as<float>();
   if (amax_nparts) *amax_nparts = (int)cdiv(a.g.N, 16);
@@ -305,7 +297,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       sq.g.A = xp; sq.g.lda = d;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.qkv, s));
+      MPR_TRY(dec_gemm(sq, ly.pk_qkv, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
       at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -318,12 +310,12 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       SkinnyArgs so;
       so.g.A = ap; so.g.lda = inner; so.g.R = xp;
       so.g.ldr = d; so.g.C = xp; so.g.ldc = d; so.g.M = B; so.g.N = d; so.g.K = inner;
-      MPR_TRY(dec_gemm(so, ly.pk_o, ly.o, s));
+      MPR_TRY(dec_gemm(so, ly.pk_o, s));
       SkinnyArgs cq;
       cq.g.A = xp; cq.g.lda = d; cq.g.C = qp;
       cq.g.ldc = inner; cq.g.M = B; cq.g.N = inner; cq.g.K = d; cq.rms_w = ly.ln1.as<float>();
       cq.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(cq, ly.pk_cq, ly.cq, s));
+      MPR_TRY(dec_gemm(cq, ly.pk_cq, s));
       AttnArgs ca;
       ca.q = qp; ca.q_bs = inner; ca.q_rs = inner;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -335,16 +327,16 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       SkinnyArgs co;
       co.g.A = ap; co.g.lda = inner; co.g.R = xp;
       co.g.ldr = d; co.g.C = xp; co.g.ldc = d; co.g.M = B; co.g.N = d; co.g.K = inner;
-      MPR_TRY(dec_gemm(co, ly.pk_co, ly.co, s));
+      MPR_TRY(dec_gemm(co, ly.pk_co, s));
       SkinnyArgs fi;
       fi.g.A = xp; fi.g.lda = d; fi.g.C = fp;
       fi.g.ldc = dff; fi.g.M = B; fi.g.N = dff; fi.g.K = d; fi.g.act = ACT_RELU;
       fi.rms_w = ly.ln2.as<float>(); fi.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(fi, ly.pk_wi, ly.wi, s));
+      MPR_TRY(dec_gemm(fi, ly.pk_wi, s));
       SkinnyArgs fo;
       fo.g.A = fp; fo.g.lda = dff; fo.g.R = xp;
       fo.g.ldr = d; fo.g.C = xp; fo.g.ldc = d; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
-      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.wo, s));
+      MPR_TRY(dec_gemm(fo, ly.pk_wo, s));
     }
     if (tiled_head(B)) {
       // logits = rms(x) . lm_head^T on the tiled GEMM, then the row argmax in 16 parts per row
@@ -372,7 +364,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
     hd.amax_val = ws->part_val.as<float>();
     hd.amax_idx = ws->part_idx.as<int32_t>();
     int np = 0;
-    MPR_TRY(dec_gemm(hd, pk_lm_head, lm_head, s, &np));
+    MPR_TRY(dec_gemm(hd, pk_lm_head, s, &np));
     MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks, T1,
                         t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,
                         s));
@@ -409,7 +401,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       sq.g.A = xp; sq.g.lda = ldA;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(sq, ly.pk_qkv, ly.qkv, s));
+      MPR_TRY(dec_gemm(sq, ly.pk_qkv, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
       at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -423,7 +415,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
       so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
       so.ssq_out = x1ss; so.ssq_cols = d;  // x1's per-tile sums of squares (its RMS)
-      MPR_TRY(dec_gemm(so, ly.pk_ocq, ly.pk_ocq, s));
+      MPR_TRY(dec_gemm(so, ly.pk_ocq, s));
       AttnArgs ca;  // c = attention(u / rms_scale(x1), K_enc, V_enc)
       ca.q = yq + inner + d; ca.q_bs = ldY; ca.q_rs = ldY;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -437,13 +429,13 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       cw.g.A = yq; cw.g.lda = ldY; cw.g.C = hz; cw.g.ldc = ldZ;
       cw.g.M = B; cw.g.N = d + dff; cw.g.K = inner + d;
       cw.ssq_out = x2ss; cw.ssq_cols = d;
-      MPR_TRY(dec_gemm(cw, ly.pk_cowi, ly.pk_cowi, s));
+      MPR_TRY(dec_gemm(cw, ly.pk_cowi, s));
       SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
       fo.g.A = hz + d; fo.g.lda = ldZ; fo.g.R = hz; fo.g.ldr = ldZ;
       fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
       fo.relu_in = true; fo.rs_part = x2ss; fo.rs_nparts = d / 16; fo.rs_n = d;
       fo.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(fo, ly.pk_wo, ly.wo, s));
+      MPR_TRY(dec_gemm(fo, ly.pk_wo, s));
     }
     SkinnyArgs hd;
     hd.g.A = xp; hd.g.lda = ldA; hd.g.C = nullptr; hd.g.M = B; hd.g.N = V; hd.g.K = d;
@@ -451,7 +443,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
     hd.amax_val = ws->part_val.as<float>();
     hd.amax_idx = ws->part_idx.as<int32_t>();
     int np = 0;
-    MPR_TRY(dec_gemm(hd, pk_lm_head, lm_head, s, &np));
+    MPR_TRY(dec_gemm(hd, pk_lm_head, s, &np));
     MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks,
                         T1, t + 1, eos, pad, shared.as<float>(), d,
                         t + 1 < max_new ? xp : nullptr, s, ldA));
@@ -559,13 +551,6 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
     MPR_TRY(grow(ws->hz, (size_t)B * (d + dff) * 4));
     MPR_TRY(grow(ws->x1ss, (size_t)B * (d / 16) * 4));
     MPR_TRY(grow(ws->x2ss, (size_t)B * (d / 16) * 4));
-  }
-  if (rows && B > 16) {
-    size_t wsf = 0;
-    const int shapes[6][2] = {{3 * inner, d}, {d, inner}, {inner, d}, {d, inner}, {dff, d},
-                              {d, dff}};
-    for (const auto& nk : shapes) wsf = std::max(wsf, gemm_dec_ws_floats(B, nk[0], nk[1]));
-    if (wsf) MPR_TRY(grow(ws->dec_ws, wsf * 4));
   }
   MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * MAX_GROUPS * 4));

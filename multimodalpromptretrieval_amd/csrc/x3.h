@@ -1,5 +1,5 @@
 // x3.h — the three-way bf16 split of fp32 operands shared by the split-bf16 ("x3") MFMA kernels
-// (gemm.hip's tiled GEMM, decode_gemm.hip's decode-step projections).
+// (gemm.hip's tiled GEMM).
 //
 // Every fp32 value is a = a0 + a1 + a2 with each term the round-to-nearest bf16 of the remainder
 // (|a - a0| <= 2^-8 |a|, |a - a0 - a1| <= 2^-16 |a|, the rest <= 2^-24 |a|: fp32 input precision),

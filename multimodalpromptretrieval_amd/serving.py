@@ -19,11 +19,12 @@ overlapped across batches on their own streams:
   20-step headline);
 * answers are handed out in order as their calls complete (``_finish``).
 
-Every batch gets ``predict()``'s answers up to fp32 near-ties: a grouped decode (more than 16
-rows) runs its layer projections on gemm_dec (csrc/decode_gemm.hip), whose summation order differs
-from the 16-row GEMV chain's (both fp32-accurate and pinned to the reference's goldens G3 / G7 /
-G8); its results do not depend on how many batches share the decode, so every grouping of the same
-batches gives the same bits (tests/test_gpu_serving.py, tests/test_gpu_golden.py).
+Every batch gets ``predict()``'s answers up to fp32 near-ties: a 16-row predict() decodes with
+the decoder layer's RMSNorms folded into its projections (csrc/t5.hip), a grouped decode (more
+than 16 rows) without, and t5-base's grouped argmax head runs on the tiled GEMM — other
+fp32-accurate summation orders, all pinned to the reference's goldens G3 / G7 / G8.  A grouped
+decode's rows do not depend on how many batches share it: every grouping of the same batches gives
+the same bits (tests/test_gpu_serving.py, tests/test_gpu_golden.py).
 """
 from __future__ import annotations
 

@@ -6,8 +6,8 @@ consumers that stop early, and beside predict().
   answers (architectures/T5VisionModel.py:196-216);
 * a generator dropped mid-way leaves no decode in flight: later predict() calls and a new loop
   run (their workspace slots are free);
-* a batch's greedy tokens are the same decoded alone (16 rows) or inside a 128-row group, at
-  full t5-small size (the decode projections' arithmetic depends on K only: gemm_rows).
+* a batch's greedy tokens are the same in a 128-row and a 256-row group, and agree with its
+  own 16-row decode up to fp32 near-ties, at full t5-small size.
 """
 import os
 import sys
@@ -87,9 +87,9 @@ def _near_tie_free(dev, emb, mask, toks, rel=1e-4):
 
 @pytest.mark.slow
 def test_t5_small_grouped_rows_equal_alone(device):
-    """Full-size t5-small, eight 16-row batches: decoded as one 128-row group (gemm_dec) and as
-    one 256-row group they give bit-identical tokens (the grouped projections' arithmetic depends
-    on K and N only); against each batch's own 16-row decode (the skinny GEMV chain, another
+    """Full-size t5-small, eight 16-row batches: decoded as one 128-row group and as one 256-row
+    group they give bit-identical tokens (the grouped decode's GEMVs sum every row alike, in
+    32-row blocks); against each batch's own 16-row decode (the folded chain, another
     fp32-accurate summation order) every row agrees up to its first near-tie."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     sd = syn.t5_state_dict(gi.G3["t5_seed"], syn.T5Config())
