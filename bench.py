@@ -454,37 +454,50 @@ def train_leg(cfg, weights, retr, device, batches, steps: int = 10):
     m.train()
     timings = {"forward": 0.0, "predict": 0.0, "backward_step": 0.0}
 
-    def step(b, timed):
+    def step(b, parts=False):
+        # main.py:177-188 as written: loss.item() is the step's one read of a device value
         t0 = time.perf_counter()
         loss = m(b)
-        torch.cuda.synchronize()
+        if parts:
+            torch.cuda.synchronize()
         t1 = time.perf_counter()
         m.predict(b)
-        torch.cuda.synchronize()
+        if parts:
+            torch.cuda.synchronize()
         t2 = time.perf_counter()
         opt.zero_grad()
         loss.backward()
         opt.step()
-        torch.cuda.synchronize()
+        v = loss.item()
         t3 = time.perf_counter()
-        if timed:
+        if parts:
             timings["forward"] += t1 - t0
             timings["predict"] += t2 - t1
             timings["backward_step"] += t3 - t2
-        return float(loss.detach())
+        return v
 
     try:
-        for i in range(2):
-            step(batches[i % len(batches)], False)
-        _lib.probe_clear()
-        _lib.probe_enable(1)
+        for i in range(3):
+            step(batches[i % len(batches)])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        losses = [step(batches[i % len(batches)], True) for i in range(steps)]
+        losses = [step(batches[i % len(batches)]) for i in range(steps)]
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        # the same steps with a device sync after each part: where a step's time goes
+        n_parts = max(2, steps // 2)
+        for i in range(n_parts):
+            step(batches[i % len(batches)], parts=True)
+        # the tiled-GEMM launches of one step, recorded and replayed back to back (kernel time
+        # only: mpr_probe_replay) — their algorithmic flops over that time, and that time's share
+        # of the step
+        torch.cuda.synchronize()
+        _lib.probe_clear()
+        _lib.probe_enable(3)
+        step(batches[0])
+        torch.cuda.synchronize()
         _lib.probe_enable(0)
-        gms, gl, gflops, _ = _lib.probe_read()
+        gms, gl, gflops, _ = _lib.probe_replay(1, device)
         _lib.probe_clear()
     finally:
         retr.is_training_phase = phase
@@ -492,20 +505,24 @@ def train_leg(cfg, weights, retr, device, batches, steps: int = 10):
     torch.cuda.empty_cache()
     ms = el / steps * 1e3
     return {"workload": f"main.py:177-188 train step: t5-small + ViT-B/32 token features, batch "
-                        f"{cfg['B']}, dropout 0.1, forward + predict + backward + AdamW",
+                        f"{cfg['B']}, dropout 0.1, forward + predict + backward + AdamW + "
+                        f"loss.item()",
             "ms_per_step": round(ms, 2),
-            "ms_per_step_parts": {k: round(v / steps * 1e3, 2) for k, v in timings.items()},
+            "ms_per_step_parts_synced": {k: round(v / n_parts * 1e3, 2)
+                                         for k, v in timings.items()},
             "qa_pairs_per_s": round(cfg["B"] / (ms * 1e-3), 1),
             "loss_first_last": [round(losses[0], 4), round(losses[-1], 4)],
             "roofline": {"bound": "mfma", "kernel": "gemm_x3_kernel (tiled split-bf16 GEMM)",
-                         "gemm_launches_per_step": round(gl / steps, 1),
+                         "gemm_launches_per_step": gl,
+                         "gemm_ms_per_step": round(gms, 3),
                          "achieved": round(gflops / (gms * 1e-3) / 1e12, 2) if gms else None,
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(gflops / (gms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)
                          if gms else None,
-                         "gemm_share_of_wall": round(gms / (el * 1e3), 4),
-                         "note": "GEMM algorithmic flops / the GEMM launches' own time (hipEvents "
-                                 "per launch); gemm_share_of_wall = GEMM time / step wall time"}}
+                         "gemm_share_of_wall": round(gms / ms, 4),
+                         "note": "one step's tiled-GEMM launches recorded and replayed back to "
+                                 "back (mpr_probe_replay): algorithmic flops / replay time; "
+                                 "gemm_share_of_wall = replay time / step wall time"}}
 
 
 def index_build(cfg, weights, device, n_batches: int = 48):

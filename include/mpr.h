@@ -166,6 +166,12 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* tensors
  * step between training-mode predict() calls, main.py:179-187).  Waits for the device first. */
 int mpr_t5_update(mpr_model* m, const float* const* tensors, int32_t n_tensors,
                   const int32_t* enc_lut, const int32_t* dec_lut);
+/* mpr_t5_update without a host wait: every copy (device tensors: device to device), bias-table
+ * gather, pack and fold is enqueued on `stream` (the bucket luts of mpr_t5_create are kept).
+ * The caller orders `stream` after every call still reading this handle's weights and later
+ * calls after `stream`, and keeps the tensors alive until it completes. */
+int mpr_t5_update_async(mpr_model* m, const float* const* tensors, int32_t n_tensors,
+                        void* stream);
 /* Gather shared[ids] into out[b*out_bstride + (row0+t)*d + c] (T5VisionModel.py:169). */
 int mpr_t5_embed(mpr_model* m, const int32_t* ids_dev, int32_t b, int32_t len, float* out_dev,
                  int64_t out_bstride, int32_t row0, void* stream);
@@ -275,7 +281,16 @@ int mpr_model_destroy(mpr_model* m);
  *   through lut[2R + 1] (bucket of offset off - R).
  *   mpr_ce_train: per-row loss of logits [n, V] against labels [n] (-100 ignored) into row_loss,
  *   loss = sum * loss_scale; dlogits (optional, row stride ld_dlogits >= V, zero padded) =
- *   (softmax - onehot) * grad_scale.
+ *   (softmax - onehot) * (grad_scale * grad_mult[0]) (grad_mult: an optional device scalar, the
+ *   incoming gradient of the loss, read on the device: no host wait for it).
+ *   mpr_gemm_f32_splitk: mpr_gemm_f32 with K cut into `splits` chunks (multiples of 32) computed
+ *   side by side into partial [splits, M, N] and summed in chunk order (for few output tiles
+ *   over a long K, e.g. the tied lm_head's input gradient: K = vocab).
+ *   mpr_rmsnorm_bwd: dw_partial (optional, cdiv(M, 64) x D floats) sums dw over 64-row chunks
+ *   side by side first.
+ *   mpr_gemm_f32_many: n mpr_gemm_f32 problems, desc[12 i ..] = {A, lda, W, ldw, C, ldc, M, N, K,
+ *   R, ldr, act} (pointers as int64), GEMM_GROUP (4) per launch; each problem's result is
+ *   bit-identical to its own mpr_gemm_f32 (every tile sums in the same order).
  *   mpr_gather_rows / mpr_embed_bwd: embedding rows and the gradient of the gather (positions
  *   grouped per unique id: pos[offs[u] .. offs[u+1]) hold uniq[u]), added into dW. */
 int mpr_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, float* C, int64_t ldc,
@@ -287,7 +302,7 @@ int mpr_rmsnorm_fwd(const float* x, int32_t M, int32_t D, const float* w, float 
                     float* y, float* rstd, void* stream);
 int mpr_rmsnorm_bwd(const float* x, int32_t M, int32_t D, const float* w, const float* rstd,
                     const float* dy, float scale, float* dx, int32_t accumulate, float* dw,
-                    void* stream);
+                    float* dw_partial, void* stream);
 int mpr_attn_train_fwd(const float* q, int64_t q_bs, int64_t q_rs, const float* k, int64_t k_bs,
                        int64_t k_rs, const float* v, int64_t v_bs, int64_t v_rs, int32_t B,
                        int32_t H, int32_t Lq, int32_t Lk, int32_t causal, const float* key_mask,
@@ -310,8 +325,12 @@ int mpr_rel_scatter(const float* drel, const int32_t* lut, int32_t R, int32_t nu
 int mpr_relu_bwd(const float* y, const float* dy, int64_t n, float* dx, void* stream);
 int mpr_add(const float* a, const float* b, int64_t n, float* out, void* stream);
 int mpr_ce_train(const float* logits, int64_t n, int32_t V, const int32_t* labels,
-                 float loss_scale, float grad_scale, float* row_loss, float* loss,
-                 float* dlogits, int64_t ld_dlogits, void* stream);
+                 float loss_scale, float grad_scale, const float* grad_mult, float* row_loss,
+                 float* loss, float* dlogits, int64_t ld_dlogits, void* stream);
+int mpr_gemm_f32_many(int32_t n, const int64_t* desc, void* stream);
+int mpr_gemm_f32_splitk(const float* A, int64_t lda, const float* W, int64_t ldw, float* C,
+                        int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr,
+                        int32_t act, int32_t splits, float* partial, void* stream);
 int mpr_gather_rows(const float* table, const int32_t* ids, int64_t n, int32_t d, float* out,
                     void* stream);
 int mpr_embed_bwd(const float* dY, int32_t d, const int32_t* uniq, const int32_t* offs,

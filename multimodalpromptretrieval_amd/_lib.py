@@ -57,6 +57,7 @@ SIGNATURES = [
     ("mpr_t5_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32, I32P, I32P, c_int32,
                                 POINTER(c_void_p)]),
     ("mpr_t5_update", c_int32, [c_void_p, POINTER(c_void_p), c_int32, I32P, I32P]),
+    ("mpr_t5_update_async", c_int32, [c_void_p, POINTER(c_void_p), c_int32, c_void_p]),
     ("mpr_t5_embed", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_int32,
                                c_void_p]),
     ("mpr_t5_encode", c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
@@ -93,12 +94,16 @@ SIGNATURES = [
     ("mpr_probe_clear", c_int32, []),
     ("mpr_gemm_f32", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32,
                                c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p]),
+    ("mpr_gemm_f32_many", c_int32, [c_int32, c_void_p, c_void_p]),
+    ("mpr_gemm_f32_splitk", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                      c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
+                                      c_int32, c_void_p, c_void_p]),
     ("mpr_transpose", c_int32, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64,
                                 c_void_p]),
     ("mpr_rmsnorm_fwd", c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_float, c_float,
                                   c_void_p, c_void_p, c_void_p]),
     ("mpr_rmsnorm_bwd", c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
-                                  c_float, c_void_p, c_int32, c_void_p, c_void_p]),
+                                  c_float, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     ("mpr_attn_train_fwd", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
                                      c_void_p, c_int64, c_int64, c_int32, c_int32, c_int32,
                                      c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
@@ -119,7 +124,7 @@ SIGNATURES = [
     ("mpr_relu_bwd", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("mpr_add", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("mpr_ce_train", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_float, c_float, c_void_p,
-                               c_void_p, c_void_p, c_int64, c_void_p]),
+                               c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     ("mpr_gather_rows", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     ("mpr_embed_bwd", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                                 c_void_p, c_void_p]),

@@ -352,65 +352,92 @@ int mpr_clip_text_forward(mpr_model* m, const int32_t* tok, int32_t b, int32_t s
 namespace {
 // Weights of a T5 handle from the tensor list of mpr_t5_create (fresh: allocate the layers) or
 // into the same device buffers (an update: every pointer a captured graph holds stays valid).
+// Every copy, bias-table gather, pack and fold is enqueued on s; luts (host, 2 radius + 1 each)
+// are validated and uploaded when given, else the handle's device copies are used.  device_src:
+// every tensor is device memory — the copies and packs then go as batched kernels (copy_segments,
+// pack_many: ~10 launches instead of ~170).
 int t5_load(T5Model* m, const float* const* t, const int32_t* enc_lut, const int32_t* dec_lut,
-            bool fresh) {
+            bool fresh, hipStream_t s, bool device_src = false) {
   const int d = m->d, inner = m->inner, dff = m->dff, Le = m->Le, Ld = m->Ld;
-  const int radius = m->lut_radius;
+  const int64_t nr = 2 * (int64_t)m->lut_radius + 1;
+  if (enc_lut || dec_lut) {
+    MPR_REQUIRE(enc_lut && dec_lut, "t5_load: both bucket luts needed");
+    for (const int32_t* lut : {enc_lut, dec_lut})
+      for (int64_t r = 0; r < nr; ++r)
+        MPR_REQUIRE(lut[r] >= 0 && lut[r] < m->nb, "t5_load: lut bucket %d out of range", lut[r]);
+    MPR_TRY(m->enc_lut.ensure(nr * 4));
+    MPR_TRY(m->dec_lut.ensure(nr * 4));
+    MPR_HIP(hipMemcpy(m->enc_lut.ptr, enc_lut, nr * 4, hipMemcpyHostToDevice));
+    MPR_HIP(hipMemcpy(m->dec_lut.ptr, dec_lut, nr * 4, hipMemcpyHostToDevice));
+  }
+  MPR_REQUIRE(m->enc_lut.bytes >= (size_t)nr * 4, "t5_load: no bucket luts");
+  // count floats of src at float offset off of dst (a buffer of several tensors is sized first)
+  std::vector<CopySeg> segs;
+  std::vector<PackJob> packs;
+  auto put = [&](DevBuf& dst, size_t off, const float* src, size_t count) -> int {
+    MPR_REQUIRE(src != nullptr, "t5_load: null tensor pointer");
+    MPR_TRY(dst.ensure((off + count) * 4));
+    MPR_REQUIRE((off + count) * 4 <= dst.bytes, "t5_load: overflow");
+    if (device_src)
+      segs.push_back({src, dst.as<float>() + off, (int64_t)count});
+    else
+      MPR_HIP(hipMemcpyAsync(dst.as<float>() + off, src, count * 4, hipMemcpyDefault, s));
+    return MPR_OK;
+  };
   // Relative position bias by offset r = key - query: tab[(r + radius) * H + h] =
   // rel_bias[lut[r + radius], h] (the bucket gather done once here, not per score).
-  auto bias_table = [&](DevBuf& dst, const float* rel, const int32_t* lut) -> int {
-    std::vector<float> hrel((size_t)m->nb * m->H);
-    MPR_HIP(hipMemcpy(hrel.data(), rel, hrel.size() * 4, hipMemcpyDefault));
-    const size_t nr = (size_t)2 * radius + 1;
-    std::vector<int32_t> hl(nr);
-    MPR_HIP(hipMemcpy(hl.data(), lut, nr * 4, hipMemcpyDefault));
-    std::vector<float> tab(nr * m->H);
-    for (size_t r = 0; r < nr; ++r) {
-      MPR_REQUIRE(hl[r] >= 0 && hl[r] < m->nb, "t5_create: lut bucket %d out of range", hl[r]);
-      for (int hh = 0; hh < m->H; ++hh) tab[r * m->H + hh] = hrel[(size_t)hl[r] * m->H + hh];
-    }
-    return upload(dst, tab.data(), tab.size());
+  auto bias_table = [&](DevBuf& dst, const float* rel, const DevBuf& lut) -> int {
+    MPR_REQUIRE(rel != nullptr, "t5_load: null tensor pointer");
+    MPR_TRY(dst.ensure((size_t)nr * m->H * 4));
+    if (device_src)  // gathered straight from the tensor
+      return mpr_rel_gather(rel, lut.as<int32_t>(), m->lut_radius, m->H, dst.as<float>(), s);
+    if (m->nb * m->H > 0) MPR_TRY(m->rel_tmp.ensure((size_t)m->nb * m->H * 4));
+    MPR_HIP(hipMemcpyAsync(m->rel_tmp.ptr, rel, (size_t)m->nb * m->H * 4, hipMemcpyDefault, s));
+    return mpr_rel_gather(m->rel_tmp.as<float>(), lut.as<int32_t>(), m->lut_radius, m->H,
+                          dst.as<float>(), s);
   };
   int p = 0;
-  MPR_TRY(upload(m->shared, t[p++], (size_t)m->V * d));
-  MPR_TRY(bias_table(m->enc_tab, t[p++], enc_lut));
+  MPR_TRY(put(m->shared, 0, t[p++], (size_t)m->V * d));
+  MPR_TRY(bias_table(m->enc_tab, t[p++], m->enc_lut));
   for (int l = 0; l < Le; ++l) {
     if (fresh) m->enc.push_back(std::make_unique<T5Layer>());
     T5Layer& ly = *m->enc[l];
-    MPR_TRY(upload(ly.ln0, t[p++], d));
+    MPR_TRY(put(ly.ln0, 0, t[p++], d));
     MPR_TRY(ly.qkv.ensure((size_t)3 * inner * d * 4));
-    for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly.qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
-    MPR_TRY(upload(ly.o, t[p++], (size_t)d * inner));
-    MPR_TRY(upload(ly.ln1, t[p++], d));
-    MPR_TRY(upload(ly.wi, t[p++], (size_t)dff * d));
-    MPR_TRY(upload(ly.wo, t[p++], (size_t)d * dff));
+    for (int j = 0; j < 3; ++j) MPR_TRY(put(ly.qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(put(ly.o, 0, t[p++], (size_t)d * inner));
+    MPR_TRY(put(ly.ln1, 0, t[p++], d));
+    MPR_TRY(put(ly.wi, 0, t[p++], (size_t)dff * d));
+    MPR_TRY(put(ly.wo, 0, t[p++], (size_t)d * dff));
   }
-  MPR_TRY(upload(m->enc_final, t[p++], d));
-  MPR_TRY(bias_table(m->dec_tab, t[p++], dec_lut));
+  MPR_TRY(put(m->enc_final, 0, t[p++], d));
+  MPR_TRY(bias_table(m->dec_tab, t[p++], m->dec_lut));
   MPR_TRY(m->cross_kv_w.ensure((size_t)Ld * 2 * inner * d * 4));
   for (int l = 0; l < Ld; ++l) {
     if (fresh) m->dec.push_back(std::make_unique<T5Layer>());
     T5Layer& ly = *m->dec[l];
-    MPR_TRY(upload(ly.ln0, t[p++], d));
+    MPR_TRY(put(ly.ln0, 0, t[p++], d));
     MPR_TRY(ly.qkv.ensure((size_t)3 * inner * d * 4));
-    for (int j = 0; j < 3; ++j) MPR_TRY(upload_at(ly.qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
-    MPR_TRY(upload(ly.o, t[p++], (size_t)d * inner));
-    MPR_TRY(upload(ly.ln1, t[p++], d));
-    MPR_TRY(upload(ly.cq, t[p++], (size_t)inner * d));
-    MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l) * inner * d, t[p++], (size_t)inner * d));
-    MPR_TRY(upload_at(m->cross_kv_w, (size_t)(2 * l + 1) * inner * d, t[p++], (size_t)inner * d));
-    MPR_TRY(upload(ly.co, t[p++], (size_t)d * inner));
-    MPR_TRY(upload(ly.ln2, t[p++], d));
-    MPR_TRY(upload(ly.wi, t[p++], (size_t)dff * d));
-    MPR_TRY(upload(ly.wo, t[p++], (size_t)d * dff));
+    for (int j = 0; j < 3; ++j) MPR_TRY(put(ly.qkv, (size_t)j * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(put(ly.o, 0, t[p++], (size_t)d * inner));
+    MPR_TRY(put(ly.ln1, 0, t[p++], d));
+    MPR_TRY(put(ly.cq, 0, t[p++], (size_t)inner * d));
+    MPR_TRY(put(m->cross_kv_w, (size_t)(2 * l) * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(put(m->cross_kv_w, (size_t)(2 * l + 1) * inner * d, t[p++], (size_t)inner * d));
+    MPR_TRY(put(ly.co, 0, t[p++], (size_t)d * inner));
+    MPR_TRY(put(ly.ln2, 0, t[p++], d));
+    MPR_TRY(put(ly.wi, 0, t[p++], (size_t)dff * d));
+    MPR_TRY(put(ly.wo, 0, t[p++], (size_t)d * dff));
   }
-  MPR_TRY(upload(m->dec_final, t[p++], d));
-  MPR_TRY(upload(m->lm_head, t[p++], (size_t)m->V * d));
+  MPR_TRY(put(m->dec_final, 0, t[p++], d));
+  MPR_TRY(put(m->lm_head, 0, t[p++], (size_t)m->V * d));
   // lane-order images of the decoder projections for the decode-step GEMMs
-  auto pack = [](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
+  auto pack = [&](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
     MPR_TRY(dst.ensure((size_t)packed_rows16_elems(n, k) * 4));
-    return pack_rows16(src.as<float>(), n, k, k, dst.as<float>(), nullptr);
+    packs.push_back({src.as<float>(), dst.as<float>(), n, k});
+    return MPR_OK;
   };
+  MPR_TRY(copy_segments(segs, s));  // device_src: every tensor copy so far, batched
   for (auto& ly : m->dec) {
     MPR_TRY(pack(ly->pk_qkv, ly->qkv, 3 * inner, d));
     MPR_TRY(pack(ly->pk_o, ly->o, d, inner));
@@ -420,8 +447,8 @@ int t5_load(T5Model* m, const float* const* t, const int32_t* enc_lut, const int
     MPR_TRY(pack(ly->pk_wo, ly->wo, d, dff));
   }
   MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
-  if (m->fold) MPR_TRY(m->build_folded());
-  MPR_HIP(hipDeviceSynchronize());
+  MPR_TRY(pack_many(packs, s));
+  if (m->fold) MPR_TRY(m->build_folded(s));
   return MPR_OK;
 }
 }  // namespace
@@ -453,7 +480,8 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
       const char* e = getenv("MPR_DECODE_FOLD");
       m->fold = !(e && e[0] == '0');
     }
-    MPR_TRY(t5_load(m.get(), t, enc_lut, dec_lut, /*fresh=*/true));
+    MPR_TRY(t5_load(m.get(), t, enc_lut, dec_lut, /*fresh=*/true, nullptr));
+    MPR_HIP(hipDeviceSynchronize());
     *out = m.release();
     return MPR_OK;
   });
@@ -468,7 +496,25 @@ int mpr_t5_update(mpr_model* mm, const float* const* t, int32_t nt, const int32_
     const int expect = 2 + 8 * m->Le + 1 + 1 + 13 * m->Ld + 2;
     MPR_REQUIRE(nt == expect, "t5_update: expected %d tensors, got %d", expect, nt);
     MPR_HIP(hipDeviceSynchronize());  // no work in flight reads the weights being replaced
-    return t5_load(m, t, enc_lut, dec_lut, /*fresh=*/false);
+    MPR_TRY(t5_load(m, t, enc_lut, dec_lut, /*fresh=*/false, nullptr));
+    MPR_HIP(hipDeviceSynchronize());
+    return MPR_OK;
+  });
+}
+
+int mpr_t5_update_async(mpr_model* mm, const float* const* t, int32_t nt, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(mm && mm->kind == mpr_model::T5 && t, "t5_update_async: bad arguments");
+    T5Model* m = static_cast<T5Model*>(mm);
+    const int expect = 2 + 8 * m->Le + 1 + 1 + 13 * m->Ld + 2;
+    MPR_REQUIRE(nt == expect, "t5_update_async: expected %d tensors, got %d", expect, nt);
+    for (int i = 0; i < nt; ++i) {  // device memory only: the copies are kernels
+      hipPointerAttribute_t at;
+      MPR_REQUIRE(t[i] && hipPointerGetAttributes(&at, t[i]) == hipSuccess &&
+                      at.type == hipMemoryTypeDevice,
+                  "t5_update_async: tensor %d is not device memory", i);
+    }
+    return t5_load(m, t, nullptr, nullptr, /*fresh=*/false, S(stream), /*device_src=*/true);
   });
 }
 

@@ -511,6 +511,8 @@ __device__ __forceinline__ GemmArgs select_problem(const GemmGroup& grp, int z) 
   a.bias = MPR_SEL(bias); a.R = MPR_SEL(R); a.ldr = MPR_SEL(ldr); a.C = MPR_SEL(C);
   a.ldc = MPR_SEL(ldc); a.M = MPR_SEL(M); a.N = MPR_SEL(N); a.K = MPR_SEL(K);
   a.act = MPR_SEL(act); a.c_rpb = MPR_SEL(c_rpb); a.c_bs = MPR_SEL(c_bs);
+  a.batch = MPR_SEL(batch); a.a_bs = MPR_SEL(a_bs); a.w_bs = MPR_SEL(w_bs);
+  a.cb_bs = MPR_SEL(cb_bs);
 #undef MPR_SEL
   return a;
 }
@@ -569,15 +571,17 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
       const int gxi = (int)cdiv(i == 0 ? grp.g[0].N : i == 1 ? grp.g[1].N : i == 2 ? grp.g[2].N
                                                                                   : grp.g[3].N,
                                 BN);
-      if (t >= gxi * gyi) {
-        t -= gxi * gyi;
+      const int nbi = i == 0 ? grp.g[0].batch : i == 1 ? grp.g[1].batch : i == 2 ? grp.g[2].batch
+                                                                                 : grp.g[3].batch;
+      if (t >= gxi * gyi * nbi) {
+        t -= gxi * gyi * nbi;
         ++z;
       } else {
         gy = gyi;
       }
     }
   }
-  const GemmArgs a = select_problem(grp, z);
+  GemmArgs a = select_problem(grp, z);
   // Inside a problem the tiles go in bands of G row tiles, column-major inside a band, so the
   // contiguous run of ~total/8 tiles an XCD gets is about sqrt(run) rows x sqrt(run) columns:
   // its L2 then fetches ~2 sqrt(run) operand panels instead of all gy row panels plus run/gy
@@ -585,6 +589,13 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
   // never how: results are bit-identical.
   const int gx = (int)cdiv(z == 0 ? grp.g[0].N : z == 1 ? grp.g[1].N : z == 2 ? grp.g[2].N
                                                                        : grp.g[3].N, BN);
+  if (a.batch > 1) {  // batch copy b: the b-th run of gx * gy tiles
+    const int b = t / (gx * gy);
+    t -= b * gx * gy;
+    a.A += b * a.a_bs;
+    a.W += b * a.w_bs;
+    a.C += b * a.cb_bs;
+  }
   const int run = (total + 7) >> 3;
   int G = 1;
   while ((G + 1) * (G + 1) <= run) ++G;
@@ -610,7 +621,7 @@ int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   int64_t tiles = 0;
   bool kt = false;
   for (int i = 0; i < g.n; ++i) {
-    tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM);
+    tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM) * g.g[i].batch;
     kt = kt || g.g[i].K % BK != 0;
   }
   if (tiles == 0) return MPR_OK;
@@ -963,8 +974,8 @@ int probe_replay(int iters, hipStream_t s, double* ms, int64_t* launches, double
     for (int i = 0; i < g.n; ++i) {
       const GemmArgs& a = g.g[i];
       const int64_t r = a.M - 1;
-      const int64_t last = a.c_rpb ? (r / a.c_rpb) * a.c_bs + (r % a.c_rpb) * a.ldc + a.N
-                                   : r * a.ldc + a.N;
+      const int64_t last = (a.c_rpb ? (r / a.c_rpb) * a.c_bs + (r % a.c_rpb) * a.ldc + a.N
+                                    : r * a.ldc + a.N) + (int64_t)(a.batch - 1) * a.cb_bs;
       cmax = std::max(cmax, (size_t)last * sizeof(float));
     }
   static DevBuf scratch;
@@ -983,8 +994,8 @@ int probe_replay(int iters, hipStream_t s, double* ms, int64_t* launches, double
       for (int i = 0; i < g.n; ++i) {
         g.g[i].C = scratch.as<float>();
         if (g.g[i].R == g0.g[i].C) g.g[i].R = scratch.as<float>();  // in-place residual
-        f += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K;
-        by += gemm_bytes(g.g[i]);
+        f += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K * g.g[i].batch;
+        by += gemm_bytes(g.g[i]) * g.g[i].batch;
       }
       const int saved = g_probe_kind;
       g_probe_kind = PROBE_OFF;
@@ -1051,8 +1062,8 @@ const bool g_gemm_f32 = [] {
 int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
   double flops = 0, bytes = 0;
   for (int i = 0; i < g.n; ++i) {
-    flops += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K;
-    bytes += gemm_bytes(g.g[i]);
+    flops += 2.0 * g.g[i].M * g.g[i].N * g.g[i].K * g.g[i].batch;
+    bytes += gemm_bytes(g.g[i]) * g.g[i].batch;
   }
   if (g_probe_kind == PROBE_RECORD) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -1080,6 +1091,8 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
 }
 }  // namespace
 
+bool gemm_uniform_order() { return !g_gemm_f32; }
+
 int gemm_group(const GemmGroup& g, hipStream_t s) {
   MPR_REQUIRE(g.n >= 1 && g.n <= GEMM_GROUP, "gemm_group: %d problems", g.n);
   for (int i = 0; i < g.n; ++i) {
@@ -1089,8 +1102,14 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
     MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
                     aligned16(a.W),
                 "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
+    MPR_REQUIRE(a.batch >= 1 && (a.batch == 1 || (!a.R && !a.c_rpb && a.a_bs % 4 == 0 &&
+                                                   a.w_bs % 4 == 0)),
+                "gemm: batch %d needs no residual / row batching and 16-byte batch strides",
+                a.batch);
   }
   if (g_gemm_f32) {
+    for (int i = 0; i < g.n; ++i)
+      MPR_REQUIRE(g.g[i].batch == 1, "gemm: strided batches need the split-bf16 kernels");
     // Round-1 f32 MFMA tiles, per problem (tools/gbench.hip): 64x64 tiles (4 waves of 32x32,
     // BK 32) once the problem has >= 1.5 blocks per CU, else 32x32 tiles with the K tile split
     // over 4 waves.  A problem keeps its tile alone or grouped (bit-identical results).
@@ -1126,8 +1145,8 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
     const GemmArgs& a = g.g[i];
     if (a.M == 0 || a.N == 0) continue;
     fam.g[fam.n++] = a;
-    b128 += cdiv(a.M, 128) * cdiv(a.N, 128);
-    b64x128 += cdiv(a.M, 64) * cdiv(a.N, 128);
+    b128 += cdiv(a.M, 128) * cdiv(a.N, 128) * a.batch;
+    b64x128 += cdiv(a.M, 64) * cdiv(a.N, 128) * a.batch;
     short_k = short_k && a.K <= 512;
   }
   // A launch of <= 256 128x128 blocks (at most one per CU) takes 32-deep K tiles: 123 KB of LDS,

@@ -28,6 +28,11 @@ struct GemmArgs {
   // batches concatenated sets one batch's rows, so it gets the tile (summation order) each batch
   // gets alone: bit-identical results.
   int tile_m = 0;
+  // Strided batch (split-bf16 kernels only): `batch` copies of the problem, copy b reading
+  // A + b a_bs, W + b w_bs and writing C + b cb_bs (no residual) — e.g. the K chunks of a split-K
+  // GEMM side by side in one launch.
+  int batch = 1;
+  int64_t a_bs = 0, w_bs = 0, cb_bs = 0;
 };
 
 int gemm(const GemmArgs& a, hipStream_t s);
@@ -41,6 +46,10 @@ struct GemmGroup {
   int n = 1;
 };
 int gemm_group(const GemmGroup& g, hipStream_t s);
+// Every tiled-GEMM configuration sums each output element in the same order (the default
+// split-bf16 kernels; not MPR_GEMM=f32): rows may then be merged into one problem or split over
+// launches without changing any bit of the results.
+bool gemm_uniform_order();
 
 // Skinny GEMM for M <= 16 rows (decode steps): same contract as gemm() plus an optional fused
 // T5 RMSNorm of the A rows: A'[m,k] = ln_w[k] * (A[m,k] * rsqrt(mean_k A[m,:]^2 + eps)).

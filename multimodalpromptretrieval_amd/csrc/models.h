@@ -160,6 +160,28 @@ struct T5Work {
   } pend;
 };
 
+// Batched device copies / lane-order packs (the weight refresh of mpr_t5_update_async)
+struct CopySeg {
+  const float* src;
+  float* dst;
+  int64_t n;  // floats
+};
+constexpr int COPY_SEGS = 32;
+struct CopySegs {
+  CopySeg s[COPY_SEGS];
+};
+int copy_segments(const std::vector<CopySeg>& segs, hipStream_t s);
+struct PackJob {
+  const float* src;  // [N, K] row-major
+  float* dst;        // pack_rows16 image
+  int64_t N, K;
+};
+constexpr int PACK_JOBS = 16;
+struct PackJobs {
+  PackJob j[PACK_JOBS];
+};
+int pack_many(const std::vector<PackJob>& jobs, hipStream_t s);
+
 struct T5Model : mpr_model {
   // slots 0..3: serving-loop calls in flight; 4 (and 5 for > 128 rows): predict()'s own
   static constexpr int MAX_SLOTS = 6;
@@ -175,11 +197,13 @@ struct T5Model : mpr_model {
   int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
                int* amax_nparts = nullptr) const;
   bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
-  int build_folded();
+  int build_folded(hipStream_t s);  // stream-ordered
+  DevBuf rel_tmp;  // update scratch: a bias table
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
   DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
   // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
   DevBuf enc_tab, dec_tab;
+  DevBuf enc_lut, dec_lut;  // the bucket LUTs (2 lut_radius + 1 int32 each): device-side updates
   std::vector<std::unique_ptr<T5Layer>> enc, dec;
   std::vector<std::unique_ptr<T5Work>> work;
   T5Work* ws = nullptr;  // workspace of the call being enqueued

@@ -33,34 +33,155 @@ bool graphs_enabled() {
   return !(e && e[0] == '0');
 }
 
-// One folded decode-chain weight [d + N2, inner + d] (row-major):
+// Weight refresh after an optimizer step (mpr_t5_update_async): ~130 tensor copies and ~37
+// lane-order packs as hipMemcpyAsync / pack_rows16 launches cost ~5 us each of launch-bound GPU
+// time (0.75 + 0.26 ms per training step); these take up to 32 / 16 of them per launch, each
+// segment a row of blocks walking it grid-stride (float4 when aligned).
+__global__ __launch_bounds__(256) void copy_segments_kernel(const CopySegs segs) {
+  const CopySeg sg = segs.s[blockIdx.y];
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (((reinterpret_cast<uintptr_t>(sg.src) | reinterpret_cast<uintptr_t>(sg.dst)) & 15) == 0) {
+    const int64_t n4 = sg.n >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(sg.src);
+    float4* d4 = reinterpret_cast<float4*>(sg.dst);
+    for (int64_t i = t0; i < n4; i += stride) d4[i] = s4[i];
+    for (int64_t i = (n4 << 2) + t0; i < sg.n; i += stride) sg.dst[i] = sg.src[i];
+  } else {
+    for (int64_t i = t0; i < sg.n; i += stride) sg.dst[i] = sg.src[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_many_kernel(const PackJobs jobs) {
+  const PackJob jb = jobs.j[blockIdx.y];
+  const int64_t nch = (jb.K + 15) / 16;
+  const int64_t total = (jb.N + 15) / 16 * nch * 64;  // float4s of the image
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * 256) {
+    const int l = (int)(q & 63);
+    const int64_t tc = q >> 6, t = tc / nch, c = tc % nch;
+    const int64_t row = t * 16 + (l & 15), k0 = c * 16 + (l >> 4) * 4;
+    float4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < jb.N) {
+      if (k0 + 0 < jb.K) v.x = jb.src[row * jb.K + k0 + 0];
+      if (k0 + 1 < jb.K) v.y = jb.src[row * jb.K + k0 + 1];
+      if (k0 + 2 < jb.K) v.z = jb.src[row * jb.K + k0 + 2];
+      if (k0 + 3 < jb.K) v.w = jb.src[row * jb.K + k0 + 3];
+    }
+    reinterpret_cast<float4*>(jb.dst)[q] = v;
+  }
+}
+
+// One folded decode-chain weight [d + N2, inner + d]:
 //   rows n < d:       [top[n, :] | e_n]                      (top: [d, inner], the o / co weight)
 //   rows d + j < N2:  [sum_k bot[j, k] w[k] top[k, :] | bot[j, :] * w]
-// (bot: [N2, d], the cq / wi weight; w the RMSNorm weight between them).  The product is summed
-// in double and rounded once.
-__global__ void fold_weights_kernel(const float* __restrict__ top, const float* __restrict__ bot,
-                                    const float* __restrict__ w, int d, int inner, int N2,
-                                    float* __restrict__ out) {
+// (bot: [N2, d], the cq / wi weight; w the RMSNorm weight between them), written straight into
+// its pack_rows16 lane-order image (the decode GEMV's weight layout; d + N2 and inner + d are
+// multiples of 16, so there is no padding).  The product is summed in double and rounded once.
+// Every fold of the model goes in two launches (fold_copy_kernel: the copied / scaled parts;
+// fold_product_kernel: the product blocks as double-precision tiles through LDS, the next k
+// step's operands prefetched into registers): one
+// thread per element with a column of top re-read per output took 264 us per fold of t5-small's
+// 2048-row wi, 12 folds after every optimizer step.
+struct FoldJob {
+  const float* top;
+  const float* bot;
+  const float* w;
+  float* out;
+  int N2;
+};
+constexpr int FOLD_JOBS = 32;
+struct FoldJobs {
+  FoldJob j[FOLD_JOBS];
+};
+
+__device__ __forceinline__ int64_t packed16(int row, int col, int kc16) {
+  return ((int64_t)(row >> 4) * kc16 + (col >> 4)) * 256 + ((row & 15) + 16 * ((col & 15) >> 2)) * 4 +
+         (col & 3);
+}
+
+__global__ void fold_copy_kernel(const FoldJobs jobs, int d, int inner) {
+  const FoldJob jb = jobs.j[blockIdx.y];
   const int K = inner + d;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (int64_t)(d + N2) * K) return;
+  if (e >= (int64_t)(d + jb.N2) * K) return;
   const int row = (int)(e / K), col = (int)(e % K);
   float v;
-  if (row < d) {
-    v = col < inner ? top[(int64_t)row * inner + col] : (col - inner == row ? 1.f : 0.f);
-  } else {
-    const int j = row - d;
-    const float* br = bot + (int64_t)j * d;
-    if (col < inner) {
-      double acc = 0.0;
-      for (int k = 0; k < d; ++k)
-        acc += (double)br[k] * (double)w[k] * (double)top[(int64_t)k * inner + col];
-      v = (float)acc;
-    } else {
-      v = br[col - inner] * w[col - inner];
+  if (row < d)
+    v = col < inner ? jb.top[(int64_t)row * inner + col] : (col - inner == row ? 1.f : 0.f);
+  else if (col >= inner)
+    v = jb.bot[(int64_t)(row - d) * d + (col - inner)] * jb.w[col - inner];
+  else
+    return;  // fold_product_kernel
+  jb.out[packed16(row, col, K >> 4)] = v;
+}
+
+// 128 x 128 product tile per block, 8 x 8 per thread (rows ty + 16 r, columns tx + 16 q): 16 LDS
+// reads per 64 FMAs keeps the fp64 FMA pipe, not LDS, the limit (2 x 2 per thread: 690 us for
+// t5-small's 12 folds, LDS-bound).  k in ascending order per output: the same sum as one thread
+// looping over k.
+constexpr int FOLD_T = 128, FOLD_K = 8;
+__global__ __launch_bounds__(256) void fold_product_kernel(const FoldJobs jobs, int d, int inner) {
+  __shared__ double sb[FOLD_K][FOLD_T];  // bot[j0 + j, k0 + k] * w[k0 + k] at [k][j]
+  __shared__ double st[FOLD_K][FOLD_T];  // top[k0 + k, c0 + c] at [k][c]
+  const FoldJob jb = jobs.j[blockIdx.z];
+  const int N2 = jb.N2, K = inner + d;
+  const int j0 = blockIdx.y * FOLD_T, c0 = blockIdx.x * FOLD_T;
+  if (j0 >= N2) return;
+  const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+  constexpr int PER = FOLD_K * FOLD_T / 256;  // operand elements each thread stages per k step
+  double pb[PER], pt[PER];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int h = 0; h < PER; ++h) {
+      const int i = t + 256 * h;
+      const int kb = i % FOLD_K, jr = i / FOLD_K;
+      const int j = j0 + jr, k = k0 + kb;
+      pb[h] = (j < N2 && k < d) ? (double)jb.bot[(int64_t)j * d + k] * (double)jb.w[k] : 0.0;
+      const int ct = i % FOLD_T, kt = i / FOLD_T;
+      const int c = c0 + ct, k2 = k0 + kt;
+      pt[h] = (c < inner && k2 < d) ? (double)jb.top[(int64_t)k2 * inner + c] : 0.0;
+    }
+  };
+  double acc[8][8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[r][q] = 0.0;
+  load(0);
+  for (int k0 = 0; k0 < d; k0 += FOLD_K) {
+#pragma unroll
+    for (int h = 0; h < PER; ++h) {
+      const int i = t + 256 * h;
+      sb[i % FOLD_K][i / FOLD_K] = pb[h];
+      st[i / FOLD_T][i % FOLD_T] = pt[h];
+    }
+    __syncthreads();
+    if (k0 + FOLD_K < d) load(k0 + FOLD_K);
+#pragma unroll
+    for (int kk = 0; kk < FOLD_K; ++kk) {
+      double a[8], b[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) a[r] = sb[kk][ty + 16 * r];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) b[q] = st[kk][tx + 16 * q];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[r][q] += a[r] * b[q];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int j = j0 + ty + 16 * r;
+    if (j >= N2) continue;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = c0 + tx + 16 * q;
+      if (c < inner) jb.out[packed16(d + j, c, K >> 4)] = (float)acc[r][q];
     }
   }
-  out[e] = v;
 }
 }  // namespace
 
@@ -105,26 +226,70 @@ bool T5Model::tiled_head(int B) const {
   return on && B > 32 && !fold_rows(B);
 }
 
-int T5Model::build_folded() {
+int T5Model::build_folded(hipStream_t s) {
   const int K = inner + d;
-  DevBuf tmp;
-  MPR_TRY(tmp.ensure((size_t)(d + std::max(inner, dff)) * K * 4));
-  auto fold = [&](DevBuf& dst, const DevBuf& top, const DevBuf& bot, const DevBuf& w,
-                  int N2) -> int {
-    const int64_t n = (int64_t)(d + N2) * K;
-    hipLaunchKernelGGL(fold_weights_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, nullptr,
-                       top.as<float>(), bot.as<float>(), w.as<float>(), d, inner, N2,
-                       tmp.as<float>());
-    MPR_LAUNCHED();
-    MPR_TRY(dst.ensure((size_t)packed_rows16_elems(d + N2, K) * 4));
-    MPR_TRY(pack_rows16(tmp.as<float>(), d + N2, K, K, dst.as<float>(), nullptr));
-    MPR_HIP(hipStreamSynchronize(nullptr));  // tmp is reused by the next fold
-    return MPR_OK;
-  };
+  MPR_REQUIRE(d % 16 == 0 && inner % 16 == 0 && dff % 16 == 0, "fold: d=%d inner=%d dff=%d", d,
+              inner, dff);
+  std::vector<FoldJob> all;
   for (auto& lp : dec) {
     T5Layer& ly = *lp;
-    MPR_TRY(fold(ly.pk_ocq, ly.o, ly.cq, ly.ln1, inner));
-    MPR_TRY(fold(ly.pk_cowi, ly.co, ly.wi, ly.ln2, dff));
+    MPR_TRY(ly.pk_ocq.ensure((size_t)packed_rows16_elems(d + inner, K) * 4));
+    MPR_TRY(ly.pk_cowi.ensure((size_t)packed_rows16_elems(d + dff, K) * 4));
+    all.push_back({ly.o.as<float>(), ly.cq.as<float>(), ly.ln1.as<float>(), ly.pk_ocq.as<float>(),
+                   inner});
+    all.push_back({ly.co.as<float>(), ly.wi.as<float>(), ly.ln2.as<float>(),
+                   ly.pk_cowi.as<float>(), dff});
+  }
+  for (size_t j0 = 0; j0 < all.size(); j0 += FOLD_JOBS) {
+    FoldJobs jobs;
+    const int n = (int)std::min<size_t>(FOLD_JOBS, all.size() - j0);
+    int max_n2 = 0;
+    for (int j = 0; j < n; ++j) {
+      jobs.j[j] = all[j0 + j];
+      max_n2 = std::max(max_n2, jobs.j[j].N2);
+    }
+    const int64_t elems = (int64_t)(d + max_n2) * K;
+    hipLaunchKernelGGL(fold_copy_kernel, dim3((unsigned)cdiv(elems, 256), (unsigned)n), dim3(256),
+                       0, s, jobs, d, inner);
+    MPR_LAUNCHED();
+    hipLaunchKernelGGL(fold_product_kernel,
+                       dim3((unsigned)cdiv(inner, FOLD_T), (unsigned)cdiv(max_n2, FOLD_T), (unsigned)n),
+                       dim3(256), 0, s, jobs, d, inner);
+    MPR_LAUNCHED();
+  }
+  return MPR_OK;
+}
+
+int copy_segments(const std::vector<CopySeg>& segs, hipStream_t s) {
+  for (size_t i0 = 0; i0 < segs.size(); i0 += COPY_SEGS) {
+    CopySegs cs;
+    const int n = (int)std::min<size_t>(COPY_SEGS, segs.size() - i0);
+    int64_t mx = 1;
+    for (int i = 0; i < n; ++i) {
+      cs.s[i] = segs[i0 + i];
+      mx = std::max(mx, cs.s[i].n);
+    }
+    hipLaunchKernelGGL(copy_segments_kernel,
+                       dim3((unsigned)std::min<int64_t>(cdiv(cdiv(mx, 4), 256), 1024), (unsigned)n),
+                       dim3(256), 0, s, cs);
+    MPR_LAUNCHED();
+  }
+  return MPR_OK;
+}
+
+int pack_many(const std::vector<PackJob>& jobs, hipStream_t s) {
+  for (size_t i0 = 0; i0 < jobs.size(); i0 += PACK_JOBS) {
+    PackJobs pj;
+    const int n = (int)std::min<size_t>(PACK_JOBS, jobs.size() - i0);
+    int64_t mx = 1;
+    for (int i = 0; i < n; ++i) {
+      pj.j[i] = jobs[i0 + i];
+      mx = std::max(mx, packed_rows16_elems(pj.j[i].N, pj.j[i].K) / 4);
+    }
+    hipLaunchKernelGGL(pack_many_kernel, dim3((unsigned)std::min<int64_t>(cdiv(mx, 256), 1024),
+                                              (unsigned)n),
+                       dim3(256), 0, s, pj);
+    MPR_LAUNCHED();
   }
   return MPR_OK;
 }
@@ -164,13 +329,17 @@ int T5Model::encode(const float* embeds, const float* mask, int B, int L, float*
 }
 
 // The T5 encoder over n <= MAX_GROUPS batches at once: batch g's rows (B[g] x L[g]) follow
-// batch g-1's in `embeds`, `mask` and `out`.  Row-wise ops run once over all rows, every GEMM is
-// one grouped launch with a problem per batch (each keeps the tile it gets alone) and the
-// attentions are one grouped launch: each batch's result is bit-identical to encoding it alone.
+// batch g-1's in `embeds`, `mask` and `out`.  Row-wise ops run once over all rows; every projection
+// is ONE problem over all the batches' stacked rows when every tiled-GEMM configuration sums an
+// output in the same order (the split-bf16 kernels: gemm_uniform_order) — a 16-batch C5 group's
+// q|k|v is one 8,000-row launch that fills the chip instead of four 4-problem launches of ~500-row
+// problems — else one problem per batch (each keeps the tile it gets alone, GEMM_GROUP per
+// launch); the attentions go ATTN_GROUP batches per launch.  Each batch's result is bit-identical
+// to encoding it alone.
 int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embeds,
                           const float* mask, float* out, hipStream_t s) {
-  MPR_REQUIRE(n >= 1 && n <= GEMM_GROUP && n <= ATTN_GROUP, "t5 encode: %d batches", n);
-  int64_t row0[GEMM_GROUP + 1];
+  MPR_REQUIRE(n >= 1 && n <= MAX_GROUPS, "t5 encode: %d batches", n);
+  int64_t row0[MAX_GROUPS + 1];
   row0[0] = 0;
   for (int g = 0; g < n; ++g) {
     MPR_REQUIRE(Ls[g] >= 1, "t5 encode: L=%d", Ls[g]);
@@ -180,6 +349,7 @@ int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embe
   }
   const int64_t M = row0[n];
   if (M == 0) return MPR_OK;
+  MPR_REQUIRE(M < (int64_t)1 << 31, "t5 encode: %lld rows", (long long)M);
   MPR_TRY(grow(ws->x, (size_t)M * d * 4));
   MPR_TRY(grow(ws->h, (size_t)M * d * 4));
   MPR_TRY(grow(ws->qkv, (size_t)M * 3 * inner * 4));
@@ -190,48 +360,57 @@ int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embe
   float* qp = ws->qkv.as<float>();
   float* ap = ws->ao.as<float>();
   float* fp = ws->ff.as<float>();
+  const bool merged = gemm_uniform_order();
+  // one projection over rows [r0, r1) of the stacked batches
+  auto proj = [&](int64_t r0, int64_t r1, const float* A, int64_t lda, const float* W, int N,
+                  int K, const float* R, float* C, int act) {
+    GemmArgs g;
+    g.A = A + r0 * lda; g.lda = lda; g.W = W; g.ldw = K;
+    g.R = R ? R + r0 * N : nullptr; g.ldr = N; g.C = C + r0 * N; g.ldc = N;
+    g.M = (int)(r1 - r0); g.N = N; g.K = K; g.act = act;
+    return g;
+  };
+  auto run = [&](const float* A, int64_t lda, const float* W, int N, int K, const float* R,
+                 float* C, int act) -> int {
+    if (merged) return gemm(proj(0, M, A, lda, W, N, K, R, C, act), s);
+    for (int g0 = 0; g0 < n; g0 += GEMM_GROUP) {
+      GemmGroup gg;
+      gg.n = 0;
+      for (int g = g0; g < std::min(n, g0 + GEMM_GROUP); ++g)
+        if (row0[g + 1] > row0[g]) gg.g[gg.n++] = proj(row0[g], row0[g + 1], A, lda, W, N, K, R, C, act);
+      if (gg.n) MPR_TRY(gemm_group(gg, s));
+    }
+    return MPR_OK;
+  };
   MPR_HIP(hipMemcpyAsync(xp, embeds, (size_t)M * d * 4, hipMemcpyDeviceToDevice, s));
   for (auto& lp : enc) {
     const T5Layer& ly = *lp;
     MPR_TRY(rmsnorm(xp, d, (int)M, d, ly.ln0.as<float>(), T5_EPS, hp, d, s));
-    GemmGroup gq, go, gi, gw;
-    AttnGroup at;
-    gq.n = go.n = gi.n = gw.n = 0;
-    at.n = 0;
-    for (int g = 0; g < n; ++g) {
-      const int B = Bs[g], L = Ls[g], Mg = B * L;
-      if (Mg == 0) continue;
-      const int64_t r = row0[g];
-      GemmArgs& q = gq.g[gq.n++];
-      q.A = hp + r * d; q.lda = d; q.W = ly.qkv.as<float>(); q.ldw = d;
-      q.C = qp + r * 3 * inner; q.ldc = 3 * inner; q.M = Mg; q.N = 3 * inner; q.K = d;
-      AttnArgs& a = at.a[at.n++];
-      const float* qb = qp + r * 3 * inner;
-      a.q = qb; a.q_bs = (int64_t)L * 3 * inner; a.q_rs = 3 * inner;
-      a.k = qb + inner; a.k_bs = a.q_bs; a.k_rs = 3 * inner;
-      a.v = qb + 2 * inner; a.v_bs = a.q_bs; a.v_rs = 3 * inner;
-      a.o = ap + r * inner; a.o_bs = (int64_t)L * inner; a.o_rs = inner;
-      a.B = B; a.H = H; a.Lq = L; a.Lk = L; a.scale = 1.f;
-      a.key_mask = mask + r; a.mask_bs = L;
-      a.rel_tab = enc_tab.as<float>();
-      a.lut_radius = lut_radius;
-      GemmArgs& o = go.g[go.n++];
-      o.A = ap + r * inner; o.lda = inner; o.W = ly.o.as<float>(); o.ldw = inner;
-      o.R = xp + r * d; o.ldr = d; o.C = xp + r * d; o.ldc = d; o.M = Mg; o.N = d; o.K = inner;
-      GemmArgs& f = gi.g[gi.n++];
-      f.A = hp + r * d; f.lda = d; f.W = ly.wi.as<float>(); f.ldw = d; f.C = fp + r * dff;
-      f.ldc = dff; f.M = Mg; f.N = dff; f.K = d; f.act = ACT_RELU;
-      GemmArgs& w = gw.g[gw.n++];
-      w.A = fp + r * dff; w.lda = dff; w.W = ly.wo.as<float>(); w.ldw = dff; w.R = xp + r * d;
-      w.ldr = d; w.C = xp + r * d; w.ldc = d; w.M = Mg; w.N = d; w.K = dff;
+    MPR_TRY(run(hp, d, ly.qkv.as<float>(), 3 * inner, d, nullptr, qp, ACT_NONE));
+    for (int g0 = 0; g0 < n; g0 += ATTN_GROUP) {
+      AttnGroup at;
+      at.n = 0;
+      for (int g = g0; g < std::min(n, g0 + ATTN_GROUP); ++g) {
+        const int B = Bs[g], L = Ls[g];
+        if (B * L == 0) continue;
+        const int64_t r = row0[g];
+        AttnArgs& a = at.a[at.n++];
+        const float* qb = qp + r * 3 * inner;
+        a.q = qb; a.q_bs = (int64_t)L * 3 * inner; a.q_rs = 3 * inner;
+        a.k = qb + inner; a.k_bs = a.q_bs; a.k_rs = 3 * inner;
+        a.v = qb + 2 * inner; a.v_bs = a.q_bs; a.v_rs = 3 * inner;
+        a.o = ap + r * inner; a.o_bs = (int64_t)L * inner; a.o_rs = inner;
+        a.B = B; a.H = H; a.Lq = L; a.Lk = L; a.scale = 1.f;
+        a.key_mask = mask + r; a.mask_bs = L;
+        a.rel_tab = enc_tab.as<float>();
+        a.lut_radius = lut_radius;
+      }
+      if (at.n) MPR_TRY(attention_group(at, s));
     }
-    if (gq.n == 0) break;
-    MPR_TRY(gemm_group(gq, s));
-    MPR_TRY(attention_group(at, s));
-    MPR_TRY(gemm_group(go, s));
+    MPR_TRY(run(ap, inner, ly.o.as<float>(), d, inner, xp, xp, ACT_NONE));
     MPR_TRY(rmsnorm(xp, d, (int)M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
-    MPR_TRY(gemm_group(gi, s));
-    MPR_TRY(gemm_group(gw, s));
+    MPR_TRY(run(hp, d, ly.wi.as<float>(), dff, d, nullptr, fp, ACT_RELU));
+    MPR_TRY(run(fp, dff, ly.wo.as<float>(), d, dff, xp, xp, ACT_NONE));
   }
   MPR_TRY(rmsnorm(xp, d, (int)M, d, enc_final.as<float>(), T5_EPS, out, d, s));
   return MPR_OK;
@@ -596,16 +775,9 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
     for (int k = 0; k < (n + 1) / 2; ++k) key.push_back(pack[k]);
     MPR_TRY(run(key, s,
                 [&](hipStream_t c) {
-                  // grouped passes of up to GEMM_GROUP batches over the stacked rows
-                  int64_t rr = 0;
-                  for (int k0 = 0; k0 < n; k0 += GEMM_GROUP) {
-                    const int nk = std::min(GEMM_GROUP, n - k0);
-                    MPR_TRY(encode_multi(nk, bs + k0, lbs + k0, ws->enc_in.as<float>() + rr * d,
-                                         ws->mask_enc.as<float>() + rr,
-                                         ws->enc_tmp.as<float>() + rr * d, c));
-                    for (int k = k0; k < k0 + nk; ++k) rr += (int64_t)bs[k] * lbs[k];
-                  }
-                  return MPR_OK;
+                  // one grouped pass over every batch's stacked rows
+                  return encode_multi(n, bs, lbs, ws->enc_in.as<float>(),
+                                      ws->mask_enc.as<float>(), ws->enc_tmp.as<float>(), c);
                 }));
     r = 0;
     for (int k = 0; k < n; ++k) {

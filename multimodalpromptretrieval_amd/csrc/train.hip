@@ -118,6 +118,50 @@ __global__ __launch_bounds__(256) void rms_bwd_dw_kernel(const float* __restrict
                                (part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
+// The same sum over 64-row chunks: part[chunk, c] (grid D/64 x chunks: the chip fills at
+// training sizes, where one block per 64 columns walked ~2K rows at memory latency, 42 us), then
+// dw[c] = sum over chunks in chunk order.  Fixed order: deterministic.
+constexpr int RMS_DW_CHUNK = 64;
+__global__ __launch_bounds__(256) void rms_dw_part_kernel(const float* __restrict__ x, int M, int D,
+                                                          const float* __restrict__ rstd,
+                                                          const float* __restrict__ dy,
+                                                          float scale, float* __restrict__ part) {
+  __shared__ float ps[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * RMS_DW_CHUNK, r1 = min(M, r0 + RMS_DW_CHUNK);
+  float s = 0.f;
+  if (c < D)
+    for (int row = r0 + g; row < r1; row += 4)
+      s += (dy[(int64_t)row * D + c] * scale) * x[(int64_t)row * D + c] * rstd[row];
+  ps[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < D)
+    part[(int64_t)blockIdx.y * D + c] = (ps[0][threadIdx.x] + ps[1][threadIdx.x]) +
+                                        (ps[2][threadIdx.x] + ps[3][threadIdx.x]);
+}
+
+__global__ void sum_rows_kernel(const float* __restrict__ part, int rows, int64_t n,
+                                float* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= n) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += part[(int64_t)r * n + c];
+  out[c] = s;
+}
+
+// Split-K GEMM epilogue: C = act(sum_s part[s]) + R, splits summed in order
+__global__ void splitk_reduce_kernel(const float* __restrict__ part, int splits, int M, int N,
+                                     int act, const float* R, int64_t ldr, float* C, int64_t ldc) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)M * N) return;
+  const int64_t m = e / N, n = e % N;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[(int64_t)k * M * N + e];
+  if (act == ACT_RELU) s = fmaxf(s, 0.f);
+  if (R) s += R[m * ldr + n];
+  C[m * ldc + n] = s;
+}
+
 // Counter-based dropout mask (train mode: T5's nn.Dropout / functional dropout sites): element
 // idx of site `site` under a forward's seed is kept iff the top 24 bits of a splitmix64 mix of
 // (seed, site, idx) are >= thresh (= p * 2^24), kept elements scaled by 1 / (1 - p).  Nothing is
@@ -336,6 +380,7 @@ __global__ void add_kernel(const float* __restrict__ a, const float* __restrict_
 __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ logits, int64_t n,
                                                       int V, const int32_t* __restrict__ labels,
                                                       float grad_scale,
+                                                      const float* __restrict__ grad_mult,
                                                       float* __restrict__ row_loss,
                                                       float* __restrict__ dlogits, int64_t ldd) {
   __shared__ float red[4];
@@ -367,6 +412,7 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
   if (t == 0) row_loss[row] = lse - lr[lab];
   if (dr) {
     const float inv = 1.f / s;
+    if (grad_mult) grad_scale *= grad_mult[0];
     for (int c = t; c < ldd; c += 256)  // columns V .. ldd: zero padding (a GEMM K)
       dr[c] = c < V ? (expf(lr[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * grad_scale : 0.f;
   }
@@ -453,6 +499,75 @@ int mpr_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, float
   });
 }
 
+int mpr_gemm_f32_many(int32_t n, const int64_t* desc, void* stream) {
+  return guarded_call([&]() -> int {
+    MPR_REQUIRE(n >= 0 && n <= 64 && (n == 0 || desc), "gemm_many: %d problems", n);
+    GemmGroup g;
+    g.n = 0;
+    for (int i = 0; i < n; ++i) {
+      const int64_t* d = desc + 12 * i;
+      GemmArgs& a = g.g[g.n];
+      a = GemmArgs();
+      a.A = reinterpret_cast<const float*>(d[0]); a.lda = d[1];
+      a.W = reinterpret_cast<const float*>(d[2]); a.ldw = d[3];
+      a.C = reinterpret_cast<float*>(d[4]); a.ldc = d[5];
+      a.M = (int)d[6]; a.N = (int)d[7]; a.K = (int)d[8];
+      a.R = reinterpret_cast<const float*>(d[9]); a.ldr = d[10]; a.act = (int)d[11];
+      MPR_REQUIRE(a.act == ACT_NONE || a.act == ACT_RELU, "gemm_many: act %d", a.act);
+      MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm_many: bad shape M=%d N=%d K=%d", a.M,
+                  a.N, a.K);
+      if (a.M == 0 || a.N == 0) continue;
+      if (++g.n == GEMM_GROUP) {
+        MPR_TRY(gemm_group(g, S(stream)));
+        g.n = 0;
+      }
+    }
+    if (g.n) MPR_TRY(gemm_group(g, S(stream)));
+    return MPR_OK;
+  });
+}
+
+int mpr_gemm_f32_splitk(const float* A, int64_t lda, const float* W, int64_t ldw, float* C,
+                        int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr,
+                        int32_t act, int32_t splits, float* partial, void* stream) {
+  return guarded_call([&]() -> int {
+    MPR_REQUIRE(act == ACT_NONE || act == ACT_RELU, "gemm: act %d (none or relu)", act);
+    MPR_REQUIRE(splits >= 1 && splits <= 64 && partial, "gemm_splitk: splits=%d", splits);
+    MPR_REQUIRE(M >= 0 && N >= 0 && K > 0, "gemm_splitk: bad shape M=%d N=%d K=%d", M, N, K);
+    if (M == 0 || N == 0) return MPR_OK;
+    const int kc = (int)cdiv(cdiv(K, splits), 32) * 32;  // chunk: a multiple of every BK
+    const int full = K / kc, rem = K - full * kc, used = full + (rem > 0);
+    GemmGroup g;
+    g.n = 0;
+    auto chunk = [&](int k0, int kk, int nb) {
+      GemmArgs& a = g.g[g.n++];
+      a = GemmArgs();
+      a.A = A + k0; a.lda = lda; a.W = W + k0; a.ldw = ldw;
+      a.C = partial + (int64_t)(k0 / kc) * M * N; a.ldc = N;
+      a.M = M; a.N = N; a.K = kk;
+      a.batch = nb; a.a_bs = kc; a.w_bs = kc; a.cb_bs = (int64_t)M * N;
+    };
+    if (gemm_uniform_order()) {  // the full chunks as one strided batch, one launch
+      if (full) chunk(0, kc, full);
+      if (rem) chunk(full * kc, rem, 1);
+      MPR_TRY(gemm_group(g, S(stream)));
+    } else {
+      for (int c = 0; c < used; ++c) {
+        chunk(c * kc, std::min(kc, K - c * kc), 1);
+        if (g.n == GEMM_GROUP || c == used - 1) {
+          MPR_TRY(gemm_group(g, S(stream)));
+          g.n = 0;
+        }
+      }
+    }
+    const int64_t n = (int64_t)M * N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(stream),
+                       partial, used, M, N, act, R, ldr, C, ldc);
+    MPR_LAUNCHED();
+    return MPR_OK;
+  });
+}
+
 int mpr_transpose(const float* in, int64_t rows, int64_t cols, int64_t ld_in, float* out,
                   int64_t ld_out, void* stream) {
   MPR_REQUIRE(ld_out >= rows, "transpose: ld_out %lld < rows %lld", (long long)ld_out,
@@ -475,13 +590,23 @@ int mpr_rmsnorm_fwd(const float* x, int32_t M, int32_t D, const float* w, float 
 
 int mpr_rmsnorm_bwd(const float* x, int32_t M, int32_t D, const float* w, const float* rstd,
                     const float* dy, float scale, float* dx, int32_t accumulate, float* dw,
-                    void* stream) {
+                    float* dw_partial, void* stream) {
   if (M == 0) return MPR_OK;
   hipLaunchKernelGGL(rms_bwd_dx_kernel, dim3((unsigned)cdiv(M, 4)), dim3(256), 0, S(stream), x, M,
                      D, w, rstd, dy, scale, dx, accumulate);
   MPR_LAUNCHED();
-  hipLaunchKernelGGL(rms_bwd_dw_kernel, dim3((unsigned)cdiv(D, 64)), dim3(256), 0, S(stream), x, M,
-                     D, rstd, dy, scale, dw);
+  if (!dw_partial) {
+    hipLaunchKernelGGL(rms_bwd_dw_kernel, dim3((unsigned)cdiv(D, 64)), dim3(256), 0, S(stream), x,
+                       M, D, rstd, dy, scale, dw);
+    MPR_LAUNCHED();
+    return MPR_OK;
+  }
+  const int chunks = (int)cdiv(M, RMS_DW_CHUNK);
+  hipLaunchKernelGGL(rms_dw_part_kernel, dim3((unsigned)cdiv(D, 64), (unsigned)chunks), dim3(256),
+                     0, S(stream), x, M, D, rstd, dy, scale, dw_partial);
+  MPR_LAUNCHED();
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)cdiv(D, 256)), dim3(256), 0, S(stream),
+                     dw_partial, chunks, (int64_t)D, dw);
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -576,12 +701,12 @@ int mpr_add(const float* a, const float* b, int64_t n, float* out, void* stream)
 }
 
 int mpr_ce_train(const float* logits, int64_t n, int32_t V, const int32_t* labels,
-                 float loss_scale, float grad_scale, float* row_loss, float* loss,
-                 float* dlogits, int64_t ld_dlogits, void* stream) {
+                 float loss_scale, float grad_scale, const float* grad_mult, float* row_loss,
+                 float* loss, float* dlogits, int64_t ld_dlogits, void* stream) {
   MPR_REQUIRE(!dlogits || ld_dlogits >= V, "cross-entropy: dlogits row stride < V");
   if (n == 0) return MPR_OK;
   hipLaunchKernelGGL(ce_rows_kernel, dim3((unsigned)n), dim3(256), 0, S(stream), logits, n, V,
-                     labels, grad_scale, row_loss, dlogits, ld_dlogits);
+                     labels, grad_scale, grad_mult, row_loss, dlogits, ld_dlogits);
   MPR_LAUNCHED();
   hipLaunchKernelGGL(sum_scale_kernel, dim3(1), dim3(256), 0, S(stream), row_loss, n, loss_scale,
                      loss);

@@ -223,8 +223,19 @@ class T5VisionModel(nn.Module):
         key = self._params_key(prefix)
         ent = self._dev.get(name)
         if ent is None or ent[0] != key:
-            sd = {n[len(prefix):]: p.detach() for n, p in self.named_parameters()
-                  if n.startswith(prefix)}
+            if update is not None and ent is not None:
+                # an update candidate: the parameters from the cached slots (named_parameters()
+                # walks the module tree, ~1 ms per optimizer step), the same traversal order,
+                # tied parameters kept once under their first name as named_parameters() does
+                sd, seen = {}, set()
+                for full, params, pname in self._slots[prefix]:
+                    p = params.get(pname)
+                    if p is not None and id(p) not in seen:
+                        seen.add(id(p))
+                        sd[full[len(prefix):]] = p.detach()
+            else:
+                sd = {n[len(prefix):]: p.detach() for n, p in self.named_parameters()
+                      if n.startswith(prefix)}
             shapes = tuple((n, tuple(p.shape)) for n, p in sorted(sd.items()))
             if (update is not None and ent is not None and ent[2] == shapes
                     and [k[0] for k in ent[0]] == [k[0] for k in key]):
@@ -376,7 +387,8 @@ class T5VisionModel(nn.Module):
             ans = pipe.answers_for(batch)
             if ans is not None:
                 return ans
-        pre = self._take_hint(batch)
+        memo = self._take_forward_inputs(batch)
+        pre = self._take_hint(batch) if memo is None else None
         if pre is not None:
             # the retrieval stream may already hold the NEXT hinted batch's towers: the T5 part
             # runs on a stream of its own (the serving loop's first generate stream)
@@ -397,10 +409,15 @@ class T5VisionModel(nn.Module):
             # measured 10.8-13.4 ms per predict() depending on how the process's earlier streams
             # happened to map onto the 4 hardware queues; MPR_PREDICT_STREAM=private restores it).
             s_main = self._predict_stream()
-        s_main.wait_stream(torch.cuda.current_stream(self.device))
+        # the handles first: a T5 refreshed after an optimizer step enqueues its weight update
+        # on the current stream, which s_main then waits for
         handles = (self._device_vit(), self._device_t5())
+        s_main.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s_main), torch.no_grad():
-            combined, mask, _ = self.prepare_input(batch, _pre=pre, _handles=handles)
+            if memo is not None:
+                combined, mask = memo
+            else:
+                combined, mask, _ = self.prepare_input(batch, _pre=pre, _handles=handles)
             # T5_model.generate (:200-205) hands back a device tensor as GenerationMixin does;
             # the answers only need the host copy the device generate already made, so decode
             # that one (batch_decode over a device tensor pays a D2H copy + sync per row)
@@ -494,11 +511,33 @@ class T5VisionModel(nn.Module):
 
     def forward(self, batch):
         """architectures/T5VisionModel.py:219-234: the teacher-forced loss; differentiable when
-        grad mode is on and T5 parameters require grad (train.py), else the value only."""
+        grad mode is on and T5 parameters require grad (train.py), else the value only.
+        The labels stay on the host (T5Shell and train.py take host or device labels; the
+        reference's ``.to(device)`` copy then a ``.cpu()`` read back would wait for the GPU).
+        main.py:177-179 follows ``model(batch)`` with ``model.predict(batch)`` on the same batch
+        before any optimizer step: the inputs built here (retrieval, prompts, image tokens,
+        question embeddings) are kept for that predict(), which would rebuild the same values."""
         combined, mask, _ = self.prepare_input(batch, _pre=self._take_hint(batch))
+        self._fwd_inputs = (self._forward_key(batch), combined.detach(), mask)
         target = self.tokenizer(batch["answer"], padding="longest",
                                 max_length=self.max_target_length, truncation=True)
         labels = torch.tensor(target["input_ids"])
         labels[labels == self.tokenizer.pad_token_id] = -100
-        labels = labels.to(self.device)
         return self.T5_model(inputs_embeds=combined, attention_mask=mask, labels=labels).loss
+
+    def _forward_key(self, batch):
+        # what prepare_input's result depends on besides the batch: the tied embedding's values
+        # (its in-place version: an optimizer step changes it) and the retrieval phase
+        retr = self._retrieval_obj()
+        return (batch["image"], tuple(batch["question"]), tuple(batch["task"]),
+                self.T5_model.shared.weight._version, getattr(retr, "is_training_phase", None),
+                self.use_image_info, self.use_quantifier)
+
+    def _take_forward_inputs(self, batch):
+        ent = self.__dict__.pop("_fwd_inputs", None)
+        if ent is None:
+            return None
+        key = self._forward_key(batch)
+        if ent[0][0] is not key[0] or ent[0][1:] != key[1:]:
+            return None
+        return ent[1], ent[2]

@@ -67,6 +67,7 @@ class DeviceT5:
         self.device = torch.device(device)
         self.scale_out = scale_decoder_outputs
         self._h = None
+        self._seen = {}
         shared = sd["shared.weight"]
         self.vocab, self.d_model = shared.shape
         q0 = sd["encoder.block.0.layer.0.SelfAttention.q.weight"]
@@ -119,10 +120,23 @@ class DeviceT5:
         return host, self._luts[0], self._luts[1]
 
     def update(self, sd: dict) -> "DeviceT5":
-        """New parameter values (same shapes) into this handle's buffers (mpr_t5_update): its
-        captured generate graphs stay valid — an optimizer step costs a copy, not a rebuild."""
+        """New parameter values (same shapes) into this handle's buffers: its captured generate
+        graphs stay valid — an optimizer step costs a copy, not a rebuild.  Parameters on this
+        device (training, main.py:186-187): mpr_t5_update_async, enqueued on the current stream
+        after every stream this handle has run on, without a host wait; host tensors:
+        mpr_t5_update (waits for the device)."""
         host, enc_lut, dec_lut = self._tensors(sd)
-        _lib.call("mpr_t5_update", self._h, _lib.tensor_array(host), len(host), enc_lut, dec_lut)
+        if all(t.device == self.device for t in host):
+            cur = torch.cuda.current_stream(self.device)
+            for st in self._seen.values():
+                if st.cuda_stream != cur.cuda_stream:
+                    cur.wait_stream(st)
+            _lib.call("mpr_t5_update_async", self._h, _lib.tensor_array(host), len(host),
+                      _lib.c_void_p(cur.cuda_stream))
+            self._seen[cur.cuda_stream] = cur
+        else:
+            _lib.call("mpr_t5_update", self._h, _lib.tensor_array(host), len(host), enc_lut,
+                      dec_lut)
         return self
 
     def close(self):
@@ -137,7 +151,10 @@ class DeviceT5:
             pass
 
     def _stream(self):
-        return _lib.stream_ptr(self.device)
+        # streams this handle's work was enqueued on: update() orders itself after them
+        st = torch.cuda.current_stream(self.device)
+        self._seen[st.cuda_stream] = st
+        return _lib.c_void_p(st.cuda_stream)
 
     def set_decode_stream(self, stream=None, slot: int = 0):
         """Run the greedy decode loop of later generate calls on ``stream`` (a torch stream,
@@ -334,7 +351,7 @@ class DeviceT5:
     def logits(self, embeds, mask, decoder_input_ids) -> torch.Tensor:
         embeds, mask = self._inputs(embeds, mask)
         B, L, _ = embeds.shape
-        dec = decoder_input_ids.to(self.device, torch.int32).contiguous()
+        dec = _lib.to_device_async(decoder_input_ids, self.device, torch.int32).contiguous()
         T = dec.shape[1]
         out = torch.empty((B, T, self.vocab), device=self.device, dtype=torch.float32)
         _lib.call("mpr_t5_logits", self._h, _lib.ptr(embeds), _lib.ptr(mask), B, L,
@@ -342,7 +359,7 @@ class DeviceT5:
         return out
 
     def loss(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        lab = labels.to(self.device, torch.int32).contiguous()
+        lab = _lib.to_device_async(labels, self.device, torch.int32).contiguous()
         lg = logits.contiguous()
         out = torch.empty((), device=self.device, dtype=torch.float32)
         _lib.call("mpr_cross_entropy", _lib.ptr(lg), _lib.ptr(lab), lab.numel(),

@@ -112,13 +112,35 @@ def _empty(*shape, like):
     return torch.empty(shape, device=like.device, dtype=torch.float32)
 
 
-def gemm(A, W, R=None, act=0):
-    """A [M, K] @ W[N, K]^T (+ R), fp32-accurate tiled GEMM."""
+def _cdiv(a: int, b: int) -> int:
+    return -(-a // b)
+
+
+def _splits(M: int, N: int, K: int) -> int:
+    """K chunks for a GEMM with few output tiles over a long K (1: none): the dW GEMMs of a
+    [512, 512] weight over ~2K rows fill 64 of 256 CUs, the tied lm_head's input gradient
+    (M = B*T, N = d, K = vocab) 16."""
+    tiles = _cdiv(M, 64) * _cdiv(N, 64)
+    if tiles >= 128 or K < 1024:
+        return 1
+    return max(1, min(16, _cdiv(256, tiles), K // 256))
+
+
+def gemm(A, W, R=None, act=0, ldw=None):
+    """A [M, K] (row stride A.stride(0)) @ W[N, K]^T (+ R), fp32-accurate tiled GEMM (split
+    over K into chunks summed in order when the output has few tiles, ``_splits``)."""
     M, K = A.shape
     N = W.shape[0]
     C = _empty(M, N, like=A)
-    _lib.call("mpr_gemm_f32", _lib.ptr(A), K, _lib.ptr(W), W.shape[1], _lib.ptr(C), N, M, N, K,
-              _lib.ptr(R), N if R is not None else 0, act, _s())
+    sp = _splits(M, N, K)
+    if sp > 1:
+        part = _empty(sp, M, N, like=A)
+        _lib.call("mpr_gemm_f32_splitk", _lib.ptr(A), A.stride(0), _lib.ptr(W), W.stride(0),
+                  _lib.ptr(C), N, M, N, K, _lib.ptr(R), N if R is not None else 0, act, sp,
+                  _lib.ptr(part), _s())
+        return C
+    _lib.call("mpr_gemm_f32", _lib.ptr(A), A.stride(0), _lib.ptr(W), W.stride(0), _lib.ptr(C), N,
+              M, N, K, _lib.ptr(R), N if R is not None else 0, act, _s())
     return C
 
 
@@ -126,20 +148,22 @@ def _r4(n: int) -> int:
     return (n + 3) // 4 * 4
 
 
-def transpose(x):
-    """x [r, c] -> [c, r4] (r4 = r rounded up to 4, zero columns: the GEMM K-alignment)."""
-    r, c = x.shape
+def transpose(x, cols=None):
+    """x [r, c] (row stride x.stride(0); only the first ``cols`` columns) -> [c, r4] (r4 = r
+    rounded up to 4, zero columns: the GEMM K-alignment)."""
+    r = x.shape[0]
+    c = x.shape[1] if cols is None else cols
     out = _empty(c, _r4(r), like=x)
-    _lib.call("mpr_transpose", _lib.ptr(x), r, c, c, _lib.ptr(out), _r4(r), _s())
+    _lib.call("mpr_transpose", _lib.ptr(x), r, c, x.stride(0), _lib.ptr(out), _r4(r), _s())
     return out
 
 
-def linear_bwd(x, W, Wt, dy, dx_acc=None, need_dw=True, need_dx=True):
+def linear_bwd(x, W, Wt, dy, dx_acc=None, need_dw=True, need_dx=True, xt=None):
     """y = x W^T: (dx (+ dx_acc), dW).  Wt = transpose(W) [K, N4], staged once per backward;
-    dy's row stride must be N4 (N4 = N for every projection but the vocabulary)."""
+    dy's row stride must be N4 (N4 = N for every projection but the vocabulary); xt: x already
+    transposed (shared by the projections of one input)."""
     N, K = W.shape
-    dW = gemm(transpose(dy[:, :N].contiguous() if dy.shape[1] != N else dy),
-              transpose(x)) if need_dw else None
+    dW = gemm(transpose(dy, N), xt if xt is not None else transpose(x)) if need_dw else None
     dx = gemm(dy, Wt, R=dx_acc) if need_dx else None
     return dx, dW
 
@@ -157,31 +181,44 @@ def rms_bwd(x, w, rstd, dy, dx_acc=None, scale=1.0):
     M, D = x.shape
     dx = dx_acc if dx_acc is not None else _empty(M, D, like=x)
     dw = _empty(D, like=x)
+    part = _empty(_cdiv(M, 64), D, like=x)
     _lib.call("mpr_rmsnorm_bwd", _lib.ptr(x), M, D, _lib.ptr(w), _lib.ptr(rstd), _lib.ptr(dy),
-              float(scale), _lib.ptr(dx), 1 if dx_acc is not None else 0, _lib.ptr(dw), _s())
+              float(scale), _lib.ptr(dx), 1 if dx_acc is not None else 0, _lib.ptr(dw),
+              _lib.ptr(part), _s())
     return dx, dw
 
 
+def _qkv(t, j, inner):
+    """The j-th inner-wide column block of a packed projection output t [rows, n * inner]."""
+    return t[:, j * inner:(j + 1) * inner]
+
+
 def attn_fwd(q, k, v, B, H, Lq, Lk, causal, mask, rel, R, drop=NO_DROP):
-    """(dropout(P) V, P): P [B, H, Lq, Lk] kept before dropout (drop = Dropout.args(site))."""
+    """(dropout(P) V, P): P [B, H, Lq, Lk] kept before dropout (drop = Dropout.args(site)).
+    q / k / v: [B*L, inner] column blocks of any row stride."""
     inner = q.shape[1]
     o = _empty(B * Lq, inner, like=q)
     P = _empty(B, H, Lq, Lk, like=q)
-    _lib.call("mpr_attn_train_fwd", _lib.ptr(q), Lq * inner, inner, _lib.ptr(k), Lk * inner,
-              inner, _lib.ptr(v), Lk * inner, inner, B, H, Lq, Lk, int(causal), _lib.ptr(mask),
-              _lib.ptr(rel), R, _lib.ptr(o), Lq * inner, inner, _lib.ptr(P), *drop, _s())
+    qs, ks, vs = q.stride(0), k.stride(0), v.stride(0)
+    _lib.call("mpr_attn_train_fwd", _lib.ptr(q), Lq * qs, qs, _lib.ptr(k), Lk * ks, ks,
+              _lib.ptr(v), Lk * vs, vs, B, H, Lq, Lk, int(causal), _lib.ptr(mask), _lib.ptr(rel),
+              R, _lib.ptr(o), Lq * inner, inner, _lib.ptr(P), *drop, _s())
     return o, P
 
 
-def attn_bwd(q, k, v, P, do, B, H, Lq, Lk, drel, R, drop=NO_DROP):
+def attn_bwd(q, k, v, P, do, B, H, Lq, Lk, drel, R, drop=NO_DROP, dq=None, dk=None, dv=None):
+    """(dq, dk, dv); given outputs (column blocks of packed buffers) are written in place."""
     inner = q.shape[1]
     dS = torch.empty_like(P)
-    dq, dk, dv = _empty(B * Lq, inner, like=q), _empty(B * Lk, inner, like=q), \
-        _empty(B * Lk, inner, like=q)
-    _lib.call("mpr_attn_train_bwd", _lib.ptr(q), Lq * inner, inner, _lib.ptr(k), Lk * inner,
-              inner, _lib.ptr(v), Lk * inner, inner, B, H, Lq, Lk, _lib.ptr(P), _lib.ptr(do),
-              Lq * inner, inner, _lib.ptr(dS), _lib.ptr(dq), Lq * inner, inner, _lib.ptr(dk),
-              Lk * inner, inner, _lib.ptr(dv), Lk * inner, inner, _lib.ptr(drel), R, *drop, _s())
+    dq = dq if dq is not None else _empty(B * Lq, inner, like=q)
+    dk = dk if dk is not None else _empty(B * Lk, inner, like=q)
+    dv = dv if dv is not None else _empty(B * Lk, inner, like=q)
+    qs, ks, vs = q.stride(0), k.stride(0), v.stride(0)
+    dqs, dks, dvs = dq.stride(0), dk.stride(0), dv.stride(0)
+    _lib.call("mpr_attn_train_bwd", _lib.ptr(q), Lq * qs, qs, _lib.ptr(k), Lk * ks, ks,
+              _lib.ptr(v), Lk * vs, vs, B, H, Lq, Lk, _lib.ptr(P), _lib.ptr(do), Lq * inner,
+              inner, _lib.ptr(dS), _lib.ptr(dq), Lq * dqs, dqs, _lib.ptr(dk), Lk * dks, dks,
+              _lib.ptr(dv), Lk * dvs, dvs, _lib.ptr(drel), R, *drop, _s())
     return dq, dk, dv
 
 
@@ -194,10 +231,21 @@ def _grouped(ids: np.ndarray):
     return uniq.astype(np.int32), offs.astype(np.int32), order.astype(np.int32)
 
 
+def _upload_i32(dev, *arrays):
+    """Host int arrays -> int32 device tensors through ONE pinned, non-blocking copy."""
+    flat = np.concatenate([np.asarray(a, dtype=np.int32).reshape(-1) for a in arrays])
+    t = _lib.to_device_async(torch.from_numpy(flat), dev)
+    out, o = [], 0
+    for a in arrays:
+        n = int(np.asarray(a).size)
+        out.append(t[o:o + n])
+        o += n
+    return out
+
+
 def embed_bwd_into(dW, ids_host: np.ndarray, dY):
     uniq, offs, pos = _grouped(ids_host)
-    dev = dY.device
-    u, o, p = (torch.from_numpy(a).to(dev) for a in (uniq, offs, pos))
+    u, o, p = _upload_i32(dY.device, uniq, offs, pos)
     _lib.call("mpr_embed_bwd", _lib.ptr(dY), dY.shape[-1], _lib.ptr(u), _lib.ptr(o), _lib.ptr(p),
               len(uniq), _lib.ptr(dW), _s())
 
@@ -210,20 +258,27 @@ def gather_rows(table, ids_dev):
     return out
 
 
+def _host_ids(ids) -> np.ndarray:
+    """Token ids as a host array (prepare_input's tokenizer output is a host tensor already; a
+    device tensor costs a wait for the GPU here)."""
+    return ids.detach().cpu().numpy() if ids.device.type != "cpu" else ids.detach().numpy()
+
+
 class EmbedFn(torch.autograd.Function):
     """``T5_model.shared(input_ids)`` (architectures/T5VisionModel.py:169) with its gradient."""
 
     @staticmethod
     def forward(ctx, weight, ids):
-        ids_dev = ids.to(weight.device, torch.int32).contiguous()
-        ctx.ids_host = ids.detach().cpu().numpy()
+        ids_dev = _lib.to_device_async(ids, weight.device, torch.int32).contiguous()
+        ctx.ids_host = _host_ids(ids) if ids.device.type == "cpu" else ids.detach()
         ctx.wshape = weight.shape
         return gather_rows(weight.detach(), ids_dev.view(-1)).view(*ids.shape, weight.shape[1])
 
     @staticmethod
     def backward(ctx, dy):
         dW = torch.zeros(ctx.wshape, device=dy.device, dtype=torch.float32)
-        embed_bwd_into(dW, ctx.ids_host, dy.contiguous().view(-1, ctx.wshape[1]))
+        ids = ctx.ids_host if isinstance(ctx.ids_host, np.ndarray) else _host_ids(ctx.ids_host)
+        embed_bwd_into(dW, ids, dy.contiguous().view(-1, ctx.wshape[1]))
         return dW, None
 
 
@@ -244,8 +299,10 @@ class T5LossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dloss):
+        # dloss stays on the device (the cross-entropy kernel reads it): no host wait
         needs = ctx.needs_input_grad
-        d_emb, grads = ctx.runner.backward(ctx.tape, float(dloss), needs[4:], needs[1])
+        dl = dloss.detach().to(torch.float32).contiguous()
+        d_emb, grads = ctx.runner.backward(ctx.tape, dl, needs[4:], needs[1])
         ctx.tape = None
         return (None, d_emb, None, None, *grads)
 
@@ -281,17 +338,24 @@ class _Runner:
         self.p = {n: t.detach().contiguous() for n, t in zip(self.names, params)}
 
     # ---- forward --------------------------------------------------------------------------------
+    def cat_w(self, names):
+        """The named [n, K] weights stacked row-wise: one GEMM computes their projections side by
+        side (q | k | v of a layer; every decoder layer's cross k | v of the encoder output)."""
+        return torch.cat([self.p[n] for n in names], 0)
+
     def forward(self, emb, mask, labels):
         c, p = self.c, self.p
         dr = c.dropout  # a Dropout in train mode, else None
         B, L, d = emb.shape
         H, inner = c.H, c.inner
         dev = emb.device
-        lab_host = labels.detach().cpu().numpy().astype(np.int64)
+        lab_host = _host_ids(labels).astype(np.int64)
         T = lab_host.shape[1]
         dec_ids = np.zeros_like(lab_host)
         dec_ids[:, 1:] = lab_host[:, :-1]
         dec_ids[dec_ids == -100] = 0  # shift_right (decoder_start_token_id 0, pad 0)
+        ids_dev, lab32 = _upload_i32(dev, dec_ids, lab_host)
+        n_valid = int((lab_host != -100).sum())
         Re, Rd = max(L, 1), max(T, 1)
         lut_e, lut_d = c.lut(Re, True, dev), c.lut(Rd, False, dev)
         rel_e = _empty(2 * Re + 1, H, like=emb)
@@ -300,7 +364,7 @@ class _Runner:
         rel_d = _empty(2 * Rd + 1, H, like=emb)
         _lib.call("mpr_rel_gather", _lib.ptr(p[self.names[2]]), _lib.ptr(lut_d), Rd, H,
                   _lib.ptr(rel_d), _s())
-        maskf = mask.to(dev, torch.float32).contiguous()
+        maskf = _lib.to_device_async(mask, dev, torch.float32).contiguous()
         tape = {"B": B, "L": L, "T": T, "Re": Re, "Rd": Rd, "lut_e": lut_e, "lut_d": lut_d,
                 "mask": maskf, "dec_ids": dec_ids, "enc": [], "dec": []}
 
@@ -318,10 +382,10 @@ class _Runner:
             pre = f"encoder.block.{i}.layer"
             t = {"x0": x}
             t["n1"], t["r1"] = rms_fwd(x, p[pre + ".0.layer_norm.weight"])
-            t["q"] = gemm(t["n1"], p[pre + ".0.SelfAttention.q.weight"])
-            t["k"] = gemm(t["n1"], p[pre + ".0.SelfAttention.k.weight"])
-            t["v"] = gemm(t["n1"], p[pre + ".0.SelfAttention.v.weight"])
-            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, L, L, False, maskf, rel_e, Re,
+            t["Wqkv"] = self.cat_w([pre + f".0.SelfAttention.{z}.weight" for z in "qkv"])
+            t["qkv"] = gemm(t["n1"], t["Wqkv"])
+            q, k, v = (_qkv(t["qkv"], j, inner) for j in range(3))
+            t["a"], t["P"] = attn_fwd(q, k, v, B, H, L, L, False, maskf, rel_e, Re,
                                       pdrop(0, i, D_SELF_P))
             t["x1"] = proj_res(t["a"], p[pre + ".0.SelfAttention.o.weight"], x,
                                dropout_site(0, i, D_SELF_OUT))
@@ -335,26 +399,29 @@ class _Runner:
         enc, tape["enc_r"] = rms_fwd(x, p["encoder.final_layer_norm.weight"])
         enc = dropout(enc, dr, dropout_site(0, 255, D_FINAL))
         tape["enc_out"] = enc
+        # every decoder layer's cross-attention k | v of the encoder output in one GEMM
+        ckv_names = [f"decoder.block.{i}.layer.1.EncDecAttention.{z}.weight"
+                     for i in range(c.n_dec) for z in "kv"]
+        tape["Wckv"] = self.cat_w(ckv_names) if c.n_dec else None
+        tape["ckv"] = gemm(enc, tape["Wckv"]) if c.n_dec else None
         # decoder
-        ids_dev = torch.from_numpy(dec_ids.astype(np.int32)).to(dev).view(-1)
         g = dropout(gather_rows(p["shared.weight"], ids_dev), dr, dropout_site(1, 255, D_IN))
         for i in range(c.n_dec):
             pre = f"decoder.block.{i}.layer"
             t = {"g0": g}
             t["n1"], t["r1"] = rms_fwd(g, p[pre + ".0.layer_norm.weight"])
-            t["q"] = gemm(t["n1"], p[pre + ".0.SelfAttention.q.weight"])
-            t["k"] = gemm(t["n1"], p[pre + ".0.SelfAttention.k.weight"])
-            t["v"] = gemm(t["n1"], p[pre + ".0.SelfAttention.v.weight"])
-            t["a"], t["P"] = attn_fwd(t["q"], t["k"], t["v"], B, H, T, T, True, None, rel_d, Rd,
+            t["Wqkv"] = self.cat_w([pre + f".0.SelfAttention.{z}.weight" for z in "qkv"])
+            t["qkv"] = gemm(t["n1"], t["Wqkv"])
+            q, k, v = (_qkv(t["qkv"], j, inner) for j in range(3))
+            t["a"], t["P"] = attn_fwd(q, k, v, B, H, T, T, True, None, rel_d, Rd,
                                       pdrop(1, i, D_SELF_P))
             t["g1"] = proj_res(t["a"], p[pre + ".0.SelfAttention.o.weight"], g,
                                dropout_site(1, i, D_SELF_OUT))
             t["n2"], t["r2"] = rms_fwd(t["g1"], p[pre + ".1.layer_norm.weight"])
             t["cq"] = gemm(t["n2"], p[pre + ".1.EncDecAttention.q.weight"])
-            t["ck"] = gemm(enc, p[pre + ".1.EncDecAttention.k.weight"])
-            t["cv"] = gemm(enc, p[pre + ".1.EncDecAttention.v.weight"])
-            t["ca"], t["cP"] = attn_fwd(t["cq"], t["ck"], t["cv"], B, H, T, L, False, maskf, None,
-                                        0, pdrop(1, i, D_CROSS_P))
+            ck, cv = _qkv(tape["ckv"], 2 * i, inner), _qkv(tape["ckv"], 2 * i + 1, inner)
+            t["ca"], t["cP"] = attn_fwd(t["cq"], ck, cv, B, H, T, L, False, maskf, None, 0,
+                                        pdrop(1, i, D_CROSS_P))
             t["g2"] = proj_res(t["ca"], p[pre + ".1.EncDecAttention.o.weight"], t["g1"],
                                dropout_site(1, i, D_CROSS_OUT))
             t["n3"], t["r3"] = rms_fwd(t["g2"], p[pre + ".2.layer_norm.weight"])
@@ -371,21 +438,20 @@ class _Runner:
         tape["hs"] = hs
         logits = gemm(hs, p["shared.weight"])
         tape["logits"] = logits
-        lab32 = torch.from_numpy(lab_host.astype(np.int32)).to(dev).view(-1)
-        n_valid = int((lab_host != -100).sum())
         tape["lab"], tape["n_valid"] = lab32, n_valid
         row_loss = _empty(B * T, like=emb)
         loss = torch.empty((), device=dev, dtype=torch.float32)
         _lib.call("mpr_ce_train", _lib.ptr(logits), B * T, c.vocab, _lib.ptr(lab32),
-                  1.0 / max(n_valid, 1) if n_valid else float("nan"), 0.0, _lib.ptr(row_loss),
-                  _lib.ptr(loss), None, 0, _s())
+                  1.0 / max(n_valid, 1) if n_valid else float("nan"), 0.0, None,
+                  _lib.ptr(row_loss), _lib.ptr(loss), None, 0, _s())
         return loss, tape
 
     # ---- backward -------------------------------------------------------------------------------
-    def backward(self, tape, dloss: float, need_params, need_emb):
+    def backward(self, tape, dloss, need_params, need_emb):
+        """dloss: the loss gradient as a device scalar."""
         c, p = self.c, self.p
         dr = c.dropout
-        B, L, T, H = tape["B"], tape["L"], tape["T"], c.H
+        B, L, T, H, inner = tape["B"], tape["L"], tape["T"], c.H, c.inner
         nm = self.names
         idx = {n: i for i, n in enumerate(nm)}
         grads = [None] * len(nm)
@@ -396,6 +462,11 @@ class _Runner:
         def put(name, g):
             if want(name):
                 grads[idx[name]] = g
+
+        def put_rows(names, dW):  # the row blocks of a stacked weight's gradient
+            n = dW.shape[0] // len(names)
+            for j, name in enumerate(names):
+                put(name, dW[j * n:(j + 1) * n])
 
         def pdrop(stack, layer, kind):
             return dr.args(dropout_site(stack, layer, kind)) if dr else NO_DROP
@@ -411,6 +482,18 @@ class _Runner:
                 wt[name] = transpose(p[name])
             return wt[name]
 
+        def self_attn_bwd(t, da, stack, i, Lx, causal_R, drel, names, x_name):
+            """The self-attention block's projections from da: dn (input of q|k|v) and the
+            stacked q|k|v weight gradient (one GEMM each over the packed dq|dk|dv)."""
+            q, k, v = (_qkv(t["qkv"], j, inner) for j in range(3))
+            dqkv = _empty(B * Lx, 3 * inner, like=da)
+            attn_bwd(q, k, v, t["P"], da, B, H, Lx, Lx, drel, causal_R, pdrop(stack, i, D_SELF_P),
+                     *(_qkv(dqkv, j, inner) for j in range(3)))
+            dn = gemm(dqkv, transpose(t["Wqkv"]))
+            if any(want(n) for n in names):
+                put_rows(names, gemm(transpose(dqkv), transpose(t[x_name])))
+            return dn
+
         # loss -> logits
         logits = tape["logits"]
         V4 = _r4(c.vocab)  # dlogits rows padded with zeros: the lm_head dx GEMM's K
@@ -419,20 +502,19 @@ class _Runner:
         scratch = torch.empty((), device=dev, dtype=torch.float32)
         nv = max(tape["n_valid"], 1)
         _lib.call("mpr_ce_train", _lib.ptr(logits), B * T, c.vocab, _lib.ptr(tape["lab"]),
-                  1.0 / nv, dloss / nv, _lib.ptr(row_loss), _lib.ptr(scratch),
+                  1.0 / nv, 1.0 / nv, _lib.ptr(dloss), _lib.ptr(row_loss), _lib.ptr(scratch),
                   _lib.ptr(dlogits), V4, _s())
         tape["logits"] = None
-        # lm_head (tied): logits = hs shared^T
-        d_shared = torch.zeros_like(p["shared.weight"])
-        dhs, dW = linear_bwd(tape["hs"], p["shared.weight"], Wt("shared.weight"), dlogits)
-        _lib.call("mpr_add", _lib.ptr(d_shared), _lib.ptr(dW), d_shared.numel(),
-                  _lib.ptr(d_shared), _s())
-        del dlogits, dW
+        # lm_head (tied): logits = hs shared^T; its weight gradient opens the tied gradient
+        dhs, d_shared = linear_bwd(tape["hs"], p["shared.weight"], Wt("shared.weight"), dlogits)
+        del dlogits
         dg, dw = rms_bwd(tape["dec_in"], p["decoder.final_layer_norm.weight"], tape["dec_r"],
                          dmask(dhs, 1, 255, D_FINAL), scale=tape["s"])
         put("decoder.final_layer_norm.weight", dw)
         drel_d = torch.zeros((2 * tape["Rd"] + 1, H), device=dev, dtype=torch.float32)
-        d_enc = None
+        # every layer's cross k | v gradient lands in one packed buffer: one GEMM each for the
+        # encoder output's gradient and the stacked weight gradient after the loop
+        dckv = _empty(B * L, 2 * c.n_dec * inner, like=tape["enc_out"]) if c.n_dec else None
         for i in reversed(range(c.n_dec)):
             pre = f"decoder.block.{i}.layer"
             t = tape["dec"][i]
@@ -455,17 +537,13 @@ class _Runner:
             dca, dW = linear_bwd(t["ca"], p[co], Wt(co), dmask(dg2, 1, i, D_CROSS_OUT),
                                  need_dw=want(co))
             put(co, dW)
-            dcq, dck, dcv = attn_bwd(t["cq"], t["ck"], t["cv"], t["cP"], dca, B, H, T, L, None,
-                                     0, pdrop(1, i, D_CROSS_P))
-            cq, ck, cv = (pre + f".1.EncDecAttention.{x}.weight" for x in "qkv")
+            ck, cv = _qkv(tape["ckv"], 2 * i, inner), _qkv(tape["ckv"], 2 * i + 1, inner)
+            dcq, _, _ = attn_bwd(t["cq"], ck, cv, t["cP"], dca, B, H, T, L, None, 0,
+                                 pdrop(1, i, D_CROSS_P), dk=_qkv(dckv, 2 * i, inner),
+                                 dv=_qkv(dckv, 2 * i + 1, inner))
+            cq = pre + ".1.EncDecAttention.q.weight"
             dn2, dW = linear_bwd(t["n2"], p[cq], Wt(cq), dcq, need_dw=want(cq))
             put(cq, dW)
-            d_enc, dW = linear_bwd(tape["enc_out"], p[ck], Wt(ck), dck, dx_acc=d_enc,
-                                   need_dw=want(ck))
-            put(ck, dW)
-            d_enc, dW = linear_bwd(tape["enc_out"], p[cv], Wt(cv), dcv, dx_acc=d_enc,
-                                   need_dw=want(cv))
-            put(cv, dW)
             ln = pre + ".1.layer_norm.weight"
             dg1, dw = rms_bwd(t["g1"], p[ln], t["r2"], dn2, dx_acc=dg2)
             put(ln, dw)
@@ -474,15 +552,8 @@ class _Runner:
             da, dW = linear_bwd(t["a"], p[so], Wt(so), dmask(dg1, 1, i, D_SELF_OUT),
                                 need_dw=want(so))
             put(so, dW)
-            dq, dk, dv = attn_bwd(t["q"], t["k"], t["v"], t["P"], da, B, H, T, T, drel_d,
-                                  tape["Rd"], pdrop(1, i, D_SELF_P))
-            sq, sk, sv = (pre + f".0.SelfAttention.{x}.weight" for x in "qkv")
-            dn1, dW = linear_bwd(t["n1"], p[sq], Wt(sq), dq, need_dw=want(sq))
-            put(sq, dW)
-            dn1, dW = linear_bwd(t["n1"], p[sk], Wt(sk), dk, dx_acc=dn1, need_dw=want(sk))
-            put(sk, dW)
-            dn1, dW = linear_bwd(t["n1"], p[sv], Wt(sv), dv, dx_acc=dn1, need_dw=want(sv))
-            put(sv, dW)
+            dn1 = self_attn_bwd(t, da, 1, i, T, tape["Rd"], drel_d,
+                                [pre + f".0.SelfAttention.{z}.weight" for z in "qkv"], "n1")
             ln = pre + ".0.layer_norm.weight"
             dg, dw = rms_bwd(t["g0"], p[ln], t["r1"], dn1, dx_acc=dg1)
             put(ln, dw)
@@ -494,6 +565,16 @@ class _Runner:
         _lib.call("mpr_rel_scatter", _lib.ptr(drel_d), _lib.ptr(tape["lut_d"]), tape["Rd"],
                   c.num_buckets, H, _lib.ptr(dtab), _s())
         put(nm[2], dtab)
+        # the cross k | v projections of every layer: the encoder output's gradient and the
+        # stacked weight gradient
+        d_enc = None
+        if c.n_dec:
+            d_enc = gemm(dckv, transpose(tape["Wckv"]))
+            ckv_names = [f"decoder.block.{i}.layer.1.EncDecAttention.{z}.weight"
+                         for i in range(c.n_dec) for z in "kv"]
+            if any(want(n) for n in ckv_names):
+                put_rows(ckv_names, gemm(transpose(dckv), transpose(tape["enc_out"])))
+            del dckv
         # encoder
         dx, dw = rms_bwd(tape["enc_in"], p["encoder.final_layer_norm.weight"], tape["enc_r"],
                          dmask(d_enc, 0, 255, D_FINAL))
@@ -519,15 +600,8 @@ class _Runner:
             da, dW = linear_bwd(t["a"], p[so], Wt(so), dmask(dx1, 0, i, D_SELF_OUT),
                                 need_dw=want(so))
             put(so, dW)
-            dq, dk, dv = attn_bwd(t["q"], t["k"], t["v"], t["P"], da, B, H, L, L, drel_e,
-                                  tape["Re"], pdrop(0, i, D_SELF_P))
-            sq, sk, sv = (pre + f".0.SelfAttention.{x}.weight" for x in "qkv")
-            dn1, dW = linear_bwd(t["n1"], p[sq], Wt(sq), dq, need_dw=want(sq))
-            put(sq, dW)
-            dn1, dW = linear_bwd(t["n1"], p[sk], Wt(sk), dk, dx_acc=dn1, need_dw=want(sk))
-            put(sk, dW)
-            dn1, dW = linear_bwd(t["n1"], p[sv], Wt(sv), dv, dx_acc=dn1, need_dw=want(sv))
-            put(sv, dW)
+            dn1 = self_attn_bwd(t, da, 0, i, L, tape["Re"], drel_e,
+                                [pre + f".0.SelfAttention.{z}.weight" for z in "qkv"], "n1")
             ln = pre + ".0.layer_norm.weight"
             dx, dw = rms_bwd(t["x0"], p[ln], t["r1"], dn1, dx_acc=dx1)
             put(ln, dw)

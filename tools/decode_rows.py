@@ -42,7 +42,4 @@ def timed(steps):
 
 full, enc = timed(20), timed(0)
 print(f"t5-{which} {rows} rows L={L}: generate {full:.3f} ms, encoder {enc:.3f} ms, decode "
-      f"{full - enc:.3f} ms = {(full - enc) / 20 * 1e3:.1f} us per step "
-      f"[MPR_DECODE_GEMM={os.environ.get('MPR_DECODE_GEMM', 'rows')} "
-      f"MPR_ROWS_FOLD={os.environ.get('MPR_ROWS_FOLD', '1')} "
-      f"MPR_ROWS_TILE={os.environ.get('MPR_ROWS_TILE', 'auto')}]", flush=True)
+      f"{full - enc:.3f} ms = {(full - enc) / 20 * 1e3:.1f} us per step", flush=True)
