@@ -328,6 +328,37 @@ int mpr_ce_train(const float* logits, int64_t n, int32_t V, const int32_t* label
                  float loss_scale, float grad_scale, const float* grad_mult, float* row_loss,
                  float* loss, float* dlogits, int64_t ld_dlogits, void* stream);
 int mpr_gemm_f32_many(int32_t n, const int64_t* desc, void* stream);
+
+/* Native T5 trainer (csrc/trainer.hip): the whole teacher-forced forward and its backward
+ * (T5ForConditionalGeneration(inputs_embeds, attention_mask, labels).loss, loss.backward() at
+ * main.py:177-186) as one call each on the kernels above.  cfg as mpr_t5_create; the bucket luts
+ * of radius lut_radius as mpr_t5_create's.  params: the 5 + 8 Le + 13 Ld fp32 device tensors in
+ * train.py t5_param_names order (shared, enc / dec relative_attention_bias, enc / dec
+ * final_layer_norm, per encoder layer ln0 q k v o ln1 wi wo, per decoder layer ln0 q k v o ln1
+ * cq ck cv co ln2 wi wo).
+ *   mpr_t5_train_forward: emb [B, L, d], mask [B, L] (1/0), dec_ids / labels [B, T] int32 (-100
+ *   ignored) on the device; loss = sum of the per-token cross-entropies * loss_scale; dropout
+ *   (thresh 0: off) as mpr_dropout, one seed per forward.  The activations go to a tape of the
+ *   trainer (*tape_out), which reads emb-derived copies only but keeps pointers to dec_ids /
+ *   labels / params: the caller keeps them alive until the backward.
+ *   mpr_t5_train_backward: dloss (device scalar) * grad_scale per token; the decoder input ids
+ *   grouped per unique id (mpr_embed_bwd) for the tied embedding's gradient; grads[i] (nullptr:
+ *   not wanted) written, not accumulated; d_emb (optional) the gradient of emb.
+ *   mpr_t5_train_release: the tape's buffers back to the trainer (after the backward, or when
+ *   the forward's graph is dropped).  One stream at a time per trainer. */
+int mpr_t5_trainer_create(const int32_t* cfg, int32_t n_cfg, const int32_t* enc_lut,
+                          const int32_t* dec_lut, int32_t lut_radius, mpr_model** out);
+int mpr_t5_train_forward(mpr_model* trainer, const float* const* params, int32_t n_params,
+                         const float* emb, const float* mask, int32_t B, int32_t L,
+                         const int32_t* dec_ids, const int32_t* labels, int32_t T,
+                         float loss_scale, uint64_t drop_seed, uint32_t drop_thresh,
+                         float drop_scale, float* loss, int32_t* tape_out, void* stream);
+int mpr_t5_train_backward(mpr_model* trainer, int32_t tape, const float* const* params,
+                          int32_t n_params, const float* dloss, float grad_scale,
+                          const int32_t* emb_uniq, const int32_t* emb_offs,
+                          const int32_t* emb_pos, int32_t n_uniq, float* const* grads,
+                          float* d_emb, void* stream);
+int mpr_t5_train_release(mpr_model* trainer, int32_t tape);
 int mpr_gemm_f32_splitk(const float* A, int64_t lda, const float* W, int64_t ldw, float* C,
                         int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr,
                         int32_t act, int32_t splits, float* partial, void* stream);

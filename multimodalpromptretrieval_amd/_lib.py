@@ -95,6 +95,15 @@ SIGNATURES = [
     ("mpr_gemm_f32", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32,
                                c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p]),
     ("mpr_gemm_f32_many", c_int32, [c_int32, c_void_p, c_void_p]),
+    ("mpr_t5_trainer_create", c_int32, [I32P, c_int32, I32P, I32P, c_int32, POINTER(c_void_p)]),
+    ("mpr_t5_train_forward", c_int32, [c_void_p, POINTER(c_void_p), c_int32, c_void_p, c_void_p,
+                                       c_int32, c_int32, c_void_p, c_void_p, c_int32, c_float,
+                                       ctypes.c_uint64, ctypes.c_uint32, c_float, c_void_p,
+                                       POINTER(c_int32), c_void_p]),
+    ("mpr_t5_train_backward", c_int32, [c_void_p, c_int32, POINTER(c_void_p), c_int32, c_void_p,
+                                        c_float, c_void_p, c_void_p, c_void_p, c_int32,
+                                        POINTER(c_void_p), c_void_p, c_void_p]),
+    ("mpr_t5_train_release", c_int32, [c_void_p, c_int32]),
     ("mpr_gemm_f32_splitk", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                       c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
                                       c_int32, c_void_p, c_void_p]),

@@ -8,7 +8,7 @@
 #include "kernels.h"
 
 struct mpr_model {
-  enum Kind { VIT = 1, CLIP_TEXT = 2, T5 = 3 };
+  enum Kind { VIT = 1, CLIP_TEXT = 2, T5 = 3, T5_TRAIN = 4 };
   explicit mpr_model(int k) : kind(k) {}
   virtual ~mpr_model() = default;
   int kind;
