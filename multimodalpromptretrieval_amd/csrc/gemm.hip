@@ -275,7 +275,8 @@ constexpr int x3_lds_floats() {
 // order of each accumulator's own terms is unchanged, results bit-identical) — neutral, unused;
 // bit 1 raises the wave's issue priority over its MFMA run (s_setprio 1 .. 0): +0-4% on the
 // 128x128 tiles (fc2 1600x768x3072 x4: 131.2 -> 126.9 us), neutral to slightly negative on 64x128.
-// KT: some K is not a multiple of BK (the loads past K are zeroed; otherwise no select touches a
+// KT: some K is not a multiple of BK, or its tile count not a multiple of D (the loads past K
+// are zeroed: the main loop runs whole groups of D tiles; otherwise no select touches a
 // loaded value, so no load is waited for early).  Rows past M / N read a clamped in-range row;
 // their results are not stored.  (Measured and dropped: W pre-split into three bf16 planes once
 // per model, copied into LDS without conversion: +8% on 64x128 tiles, -11% on 128x128 — the
@@ -614,7 +615,7 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
   gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT, V>(a, bx, by, smem);
 }
 
-// KT when some K % BK != 0
+// KT when some K % BK != 0 or cdiv(K, BK) % D != 0
 template <int BM, int BN, int WM, int WN, int BK, int D, int KW, int V = 0>
 int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW;
@@ -622,7 +623,9 @@ int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   bool kt = false;
   for (int i = 0; i < g.n; ++i) {
     tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM) * g.g[i].batch;
-    kt = kt || g.g[i].K % BK != 0;
+    // masked K tail also when the tile count is not a multiple of D: the main loop multiplies
+    // whole groups of D tiles, and an unmasked tile past K would add clamped (repeated) columns
+    kt = kt || g.g[i].K % BK != 0 || cdiv(g.g[i].K, BK) % D != 0;
   }
   if (tiles == 0) return MPR_OK;
   if (kt)

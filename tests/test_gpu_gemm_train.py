@@ -1,0 +1,67 @@
+"""The training step's GEMM forms (csrc/train.hip + gemm.hip) against a torch fp64 product of the
+same operands (relative Frobenius error 1e-6: fp32 accumulation over K):
+
+* K whose tile count is not a multiple of the pipeline depth (K = 1936 = 121 16-deep tiles, the
+  dW products over B*L = 16 x 121 rows; K = 32 on the 32-deep 128x128 tiles) — the masked-tail
+  path, which an unmasked extra tile once corrupted;
+* mpr_gemm_f32_splitk — K cut into chunks computed side by side (a strided batch of the
+  split-bf16 kernel) and summed in order; deterministic (two runs bitwise equal).
+"""
+import pytest
+import torch
+
+from multimodalpromptretrieval_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _gemm(A, W, splits=1, R=None, act=0):
+    M, K = A.shape
+    N = W.shape[0]
+    C = torch.empty(M, N, device=A.device)
+    if splits > 1:
+        part = torch.empty(splits * M * N, device=A.device)
+        _lib.call("mpr_gemm_f32_splitk", _lib.ptr(A), K, _lib.ptr(W), K, _lib.ptr(C), N, M, N, K,
+                  _lib.ptr(R), N if R is not None else 0, act, splits, _lib.ptr(part),
+                  _lib.stream_ptr())
+    else:
+        _lib.call("mpr_gemm_f32", _lib.ptr(A), K, _lib.ptr(W), K, _lib.ptr(C), N, M, N, K,
+                  _lib.ptr(R), N if R is not None else 0, act, _lib.stream_ptr())
+    torch.cuda.synchronize()
+    return C
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm())
+
+
+def _operands(M, N, K, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 1936), (512, 1536, 1936), (1536, 512, 32),
+                                   (2048, 1024, 32), (128, 512, 48), (512, 2048, 1936)])
+def test_gemm_odd_tile_counts(device, M, N, K):
+    A, W = _operands(M, N, K, M + N + K)
+    got = _gemm(A.to(device), W.to(device))
+    assert _rel(got, A.double() @ W.double().t()) < 1e-6
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(128, 512, 32104, 16), (512, 512, 1936, 4),
+                                          (64, 64, 4096, 8), (96, 160, 1000, 3)])
+def test_splitk_matches_fp64_and_is_deterministic(device, M, N, K, splits):
+    A, W = _operands(M, N, K, M * 3 + K)
+    Ad, Wd = A.to(device), W.to(device)
+    got = _gemm(Ad, Wd, splits=splits)
+    assert _rel(got, A.double() @ W.double().t()) < 1e-6
+    assert torch.equal(got, _gemm(Ad, Wd, splits=splits))
+
+
+def test_splitk_residual_and_relu(device):
+    A, W = _operands(192, 256, 2048, 5)
+    R = torch.randn(192, 256)
+    got = _gemm(A.to(device), W.to(device), splits=4, R=R.to(device), act=2)
+    ref = torch.relu(A.double() @ W.double().t()) + R.double()
+    assert _rel(got, ref) < 1e-6
