@@ -415,13 +415,14 @@ class T5VisionModel(nn.Module):
         s_main.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s_main), torch.no_grad():
             if memo is not None:
-                combined, mask = memo
+                combined, mask, lens = memo
             else:
-                combined, mask, _ = self.prepare_input(batch, _pre=pre, _handles=handles)
+                combined, mask, enc = self.prepare_input(batch, _pre=pre, _handles=handles)
+                lens = self.row_lengths(combined, enc)
             # T5_model.generate (:200-205) hands back a device tensor as GenerationMixin does;
             # the answers only need the host copy the device generate already made, so decode
             # that one (batch_decode over a device tensor pays a D2H copy + sync per row)
-            seqs = handles[1].generate(combined, mask, self.max_new_tokens)
+            seqs = handles[1].generate(combined, mask, self.max_new_tokens, lens=lens)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     # ---- lookahead for batch-after-batch callers (main.py:262-263) ---------------------------
@@ -517,8 +518,9 @@ class T5VisionModel(nn.Module):
         main.py:177-179 follows ``model(batch)`` with ``model.predict(batch)`` on the same batch
         before any optimizer step: the inputs built here (retrieval, prompts, image tokens,
         question embeddings) are kept for that predict(), which would rebuild the same values."""
-        combined, mask, _ = self.prepare_input(batch, _pre=self._take_hint(batch))
-        self._fwd_inputs = (self._forward_key(batch), combined.detach(), mask)
+        combined, mask, enc = self.prepare_input(batch, _pre=self._take_hint(batch))
+        self._fwd_inputs = (self._forward_key(batch), combined.detach(), mask,
+                            self.row_lengths(combined, enc))
         target = self.tokenizer(batch["answer"], padding="longest",
                                 max_length=self.max_target_length, truncation=True)
         labels = torch.tensor(target["input_ids"])
@@ -540,4 +542,13 @@ class T5VisionModel(nn.Module):
         key = self._forward_key(batch)
         if ent[0][0] is not key[0] or ent[0][1:] != key[1:]:
             return None
-        return ent[1], ent[2]
+        return ent[1], ent[2], ent[3]
+
+    @staticmethod
+    def row_lengths(combined, encoding):
+        """Real length of each row of prepare_input's output (host ints, no device read): the
+        image tokens plus the prompt's tokens (the tokenizer pads on the right)."""
+        am = encoding["attention_mask"]
+        am = am if isinstance(am, torch.Tensor) else torch.as_tensor(am)
+        T = combined.shape[1] - am.shape[1]
+        return (am.sum(1) + T).tolist()

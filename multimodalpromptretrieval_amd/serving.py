@@ -35,7 +35,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from .t5 import pieces_per_call
+from .t5 import length_pieces, pieces_per_call
 
 
 @dataclass(frozen=True)
@@ -109,7 +109,7 @@ class ServingLoop:
         while len(model._s_gen) < opts.depth:
             model._s_gen.append(_lib.role_stream(model.device, f"gen:{len(model._s_gen)}"))
         self.pending = deque()  # one _Call per generate call, in launch order
-        self.order = deque()    # per batch, in order: its pieces [(call, piece index), ...]
+        self.order = deque()    # per batch, in order: ([(call, piece index), ...], row order)
         self.held = []          # prepared batches waiting for the rest of their decode group
         self.ready = deque()    # (batch, prefetched handles) in order
         self.calls = 0
@@ -235,7 +235,7 @@ class ServingLoop:
         call = self._launch(self.held)
         for j in range(len(self.held)):
             call.refs += 1
-            self.order.append([(call, j)])
+            self.order.append(([(call, j)], None))
         self.held = []
 
     def _add(self, prepared) -> bool:
@@ -244,23 +244,25 @@ class ServingLoop:
         decoded as 16-row pieces, pieces_per_call() per generate call, as predict() decodes it;
         its answers come out once every piece is done.  Returns whether a generate call was
         launched."""
-        combined, mask = prepared
+        combined, mask, lens = prepared
         rows = combined.shape[0]
         if self.o.decode_group > 1 and rows <= 16:
-            self.held.append(prepared)
+            self.held.append((combined, mask))
             if len(self.held) < self.o.decode_group:
                 return False
             self._flush_held()
             return True
         self._flush_held()
-        pieces = [(combined[i:i + 16], mask[i:i + 16]) for i in range(0, max(rows, 1), 16)]
+        # rows by length, each piece trimmed to its longest row (t5.length_pieces): the answers
+        # come back in the batch's order
+        order, pieces = length_pieces(combined, mask, lens if rows > 16 else None)
         owned = []
         per = pieces_per_call()
         for g in range(0, len(pieces), per):
             call = self._launch(pieces[g:g + per])
             call.refs += 1
             owned += [(call, j) for j in range(len(pieces[g:g + per]))]
-        self.order.append(owned)
+        self.order.append((owned, order))
         return True
 
     def _hand_out(self, drain=False):
@@ -270,7 +272,7 @@ class ServingLoop:
         the tower stream without its next pass)."""
         m = self.m
         while self.order:
-            owned = self.order[0]
+            owned, order = self.order[0]
             calls = list(dict.fromkeys(c for c, _ in owned))
             if not (drain or len(self.pending) > self.o.depth + 2):
                 if any(c.items is None or not c.items[-1][1].query() for c in calls):
@@ -289,6 +291,10 @@ class ServingLoop:
                 for c, j in owned:
                     c.items[j][1].synchronize()
                 host = torch.cat([c.items[j][0] for c, j in owned])
+                if order is not None:  # length-ordered pieces: rows back in the batch's order
+                    back = torch.empty_like(host)
+                    back[torch.from_numpy(order)] = host
+                    host = back
                 yield m._finish(host, owned[-1][0].items[owned[-1][1]][1])
 
     def drain(self):
@@ -312,10 +318,10 @@ class ServingLoop:
                 m._s_prep.wait_stream(torch.cuda.current_stream(m.device))
                 with torch.cuda.stream(m._s_prep):
                     with torch.no_grad():
-                        combined, mask, _ = m.prepare_input(batch, _pre=pre,
-                                                            _handles=self._handles())
+                        combined, mask, enc = m.prepare_input(batch, _pre=pre,
+                                                              _handles=self._handles())
                 self._pump()
-                if not self._add((combined, mask)):
+                if not self._add((combined, mask, m.row_lengths(combined, enc))):
                     continue
                 yield from self._hand_out()
             self._flush_held()

@@ -13,6 +13,7 @@ import ctypes
 import math
 import os
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -26,6 +27,31 @@ def pieces_per_call() -> int:
     batch, the serving loop's large batches): MPR_GEN_PIECES, default 16 (one 256-row loop for a
     256-question batch, every decode weight streamed once per step for all rows)."""
     return max(1, min(MAX_PIECES, int(os.environ.get("MPR_GEN_PIECES", "16"))))
+
+
+def length_pieces(embeds, mask, lens=None):
+    """A batch of more than 16 rows as 16-row pieces: (order, pieces).  With the rows' real
+    lengths (``lens``, host ints: the leading ones of each right-padded mask row, e.g. the
+    tokenizer's attention_mask sums) the rows go by length (stable) and each piece keeps only its
+    own longest row's columns: the encoder then computes ~mean-length rows instead of the batch's
+    longest (config C5: 62-71 % of a 256-question batch's padded rows are real tokens).  A row's
+    result does not depend on its piece (every GEMM tile sums in the same order; columns past a
+    row's length are masked keys, which add exact zeros), so the tokens come back in the caller's
+    row order equal to the unsorted pieces'.  order None: the pieces are the rows in order."""
+    B = embeds.shape[0]
+    if lens is None or B <= 16:
+        return None, [(embeds[i:i + 16], mask[i:i + 16]) for i in range(0, max(B, 1), 16)]
+    lens = np.asarray(lens, dtype=np.int64).reshape(-1)
+    if lens.shape[0] != B:
+        raise ValueError(f"length_pieces: {lens.shape[0]} lengths for {B} rows")
+    order = np.argsort(lens, kind="stable")
+    idx = _lib.to_device_async(torch.from_numpy(order), embeds.device)
+    e, m = embeds.index_select(0, idx), mask.index_select(0, idx)
+    pieces = []
+    for i in range(0, B, 16):
+        lp = int(max(1, lens[order[i:i + 16]].max()))
+        pieces.append((e[i:i + 16, :lp], m[i:i + 16, :lp]))
+    return order, pieces
 
 
 def relative_position_bucket(rel: torch.Tensor, bidirectional: bool, num_buckets: int = 32,
@@ -194,53 +220,69 @@ class DeviceT5:
         return out
 
     def generate_padded(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
-                        eos_token_id=1, pad_token_id=0, slot: int = 0) -> torch.Tensor:
+                        eos_token_id=1, pad_token_id=0, slot: int = 0,
+                        lens=None) -> torch.Tensor:
         """All max_new_tokens greedy steps on device: int32 [B, 1+max_new] (no host sync).
         ``slot`` picks one of the model's independent workspaces (two batches of a serving
         loop decode concurrently on different slots and streams).  A batch of more than 16 rows
-        runs as 16-row chunks sharing decode loops (pieces_per_call() chunks per loop)."""
+        runs as 16-row chunks sharing decode loops (pieces_per_call() chunks per loop); with the
+        rows' real lengths (``lens``) the chunks are length-ordered and trimmed
+        (``length_pieces``)."""
         embeds, mask = self._inputs(embeds, mask)
         B, L, _ = embeds.shape
         if B > 16:
-            chunks = [(embeds[i:i + 16], mask[i:i + 16]) for i in range(0, B, 16)]
-            per = pieces_per_call()
-            groups = [chunks[g:g + per] for g in range(0, len(chunks), per)]
-            outs = []
-            if len(groups) == 1 or os.environ.get("MPR_SPLIT_SLOTS", "1") == "0":
-                for grp in groups:
-                    outs += self.generate_batches_padded(grp, max_new_tokens,
-                                                         decoder_start_token_id, eos_token_id,
-                                                         pad_token_id, slot)
-                return torch.cat(outs)
-            # more than 128 rows (config C5's 256 questions): the 128-row decode loops are
-            # latency-bound chains of launches that leave CUs idle, so consecutive loops run on
-            # two workspace slots and streams at once (each loop's rows bit-identical to a call
-            # of its own; the caller's stream waits for both)
-            cur = torch.cuda.current_stream(self.device)
-            sts = [_lib.role_stream(self.device, f"gen:{j}" if slot < self.PREDICT_SLOT
-                                    else f"pgen:{j}") for j in range(2)]
-            for st in sts:
-                st.wait_stream(cur)
-            for gi, grp in enumerate(groups):
-                st = sts[gi % 2]
-                for e, m in grp:
-                    e.record_stream(st)
-                    m.record_stream(st)
-                with torch.cuda.stream(st):
-                    o = self.generate_batches_padded(grp, max_new_tokens, decoder_start_token_id,
-                                                     eos_token_id, pad_token_id,
-                                                     slot=slot + gi % 2)
-                for t in o:
-                    t.record_stream(cur)
-                outs += o
-            for st in sts:
-                cur.wait_stream(st)
-            return torch.cat(outs)
+            order, chunks = length_pieces(embeds, mask, lens)
+            if order is not None:
+                toks = self.generate_padded_pieces(chunks, max_new_tokens, decoder_start_token_id,
+                                                   eos_token_id, pad_token_id, slot)
+                out = torch.empty_like(toks)
+                out.index_copy_(0, _lib.to_device_async(torch.from_numpy(order), self.device),
+                                toks)
+                return out
+            return self.generate_padded_pieces(chunks, max_new_tokens, decoder_start_token_id,
+                                               eos_token_id, pad_token_id, slot)
         out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
         _lib.call("mpr_t5_generate_slot", self._h, int(slot), _lib.ptr(embeds), _lib.ptr(mask),
                   B, L, int(max_new_tokens), int(decoder_start_token_id), int(eos_token_id),
                   int(pad_token_id), _lib.ptr(out), self._stream())
         return out
+
+    def generate_padded_pieces(self, chunks, max_new_tokens=20, decoder_start_token_id=0,
+                               eos_token_id=1, pad_token_id=0, slot: int = 0) -> torch.Tensor:
+        """generate_padded over 16-row pieces [(embeds, mask), ...]: their tokens stacked."""
+        per = pieces_per_call()
+        groups = [chunks[g:g + per] for g in range(0, len(chunks), per)]
+        outs = []
+        if len(groups) == 1 or os.environ.get("MPR_SPLIT_SLOTS", "1") == "0":
+            for grp in groups:
+                outs += self.generate_batches_padded(grp, max_new_tokens,
+                                                     decoder_start_token_id, eos_token_id,
+                                                     pad_token_id, slot)
+            return torch.cat(outs)
+        # more than 128 rows (config C5's 256 questions): the 128-row decode loops are
+        # latency-bound chains of launches that leave CUs idle, so consecutive loops run on
+        # two workspace slots and streams at once (each loop's rows bit-identical to a call
+        # of its own; the caller's stream waits for both)
+        cur = torch.cuda.current_stream(self.device)
+        sts = [_lib.role_stream(self.device, f"gen:{j}" if slot < self.PREDICT_SLOT
+                                else f"pgen:{j}") for j in range(2)]
+        for st in sts:
+            st.wait_stream(cur)
+        for gi, grp in enumerate(groups):
+            st = sts[gi % 2]
+            for e, m in grp:
+                e.record_stream(st)
+                m.record_stream(st)
+            with torch.cuda.stream(st):
+                o = self.generate_batches_padded(grp, max_new_tokens, decoder_start_token_id,
+                                                 eos_token_id, pad_token_id,
+                                                 slot=slot + gi % 2)
+            for t in o:
+                t.record_stream(cur)
+            outs += o
+        for st in sts:
+            cur.wait_stream(st)
+        return torch.cat(outs)
 
     def generate_batches_padded(self, batches, max_new_tokens=20, decoder_start_token_id=0,
                                 eos_token_id=1, pad_token_id=0, slot: int = 0):
@@ -325,7 +367,7 @@ class DeviceT5:
         return tok[:, :int(first.max()) + 1]
 
     def generate(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
-                 eos_token_id=1, pad_token_id=0) -> torch.Tensor:
+                 eos_token_id=1, pad_token_id=0, lens=None) -> torch.Tensor:
         """GenerationMixin.generate(do_sample=False) result (int64, host, trimmed).  Stops where
         greedy search stops: the decode runs in chunks of MPR_EOS_STOP_CHUNK steps (default 4:
         no cost measurable against one graph, tools/eos_chunk_ab.py, where 2 cost ~0.07 ms;
@@ -336,7 +378,8 @@ class DeviceT5:
         B, L, _ = embeds_.shape
         if chunk <= 0 or B > 16 or max_new_tokens <= chunk:
             toks = self.generate_padded(embeds, mask, max_new_tokens, decoder_start_token_id,
-                                        eos_token_id, pad_token_id, slot=self.PREDICT_SLOT)
+                                        eos_token_id, pad_token_id, slot=self.PREDICT_SLOT,
+                                        lens=lens)
             self.last_steps_run = int(max_new_tokens)
             return self.trim(toks, eos_token_id)
         out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)

@@ -112,3 +112,22 @@ def test_t5_small_grouped_rows_equal_alone(device):
         for r in range(alone.shape[0]):
             n = int(safe[r]) + 1  # column 0 is the start token
             assert torch.equal(alone[r, :n], gr[r, :n]), (r, n)
+
+
+@pytest.mark.parametrize("rows", [40, 130])
+def test_length_ordered_pieces_equal_unsorted(device, rows):
+    """t5.length_pieces: a batch of more than 16 rows decoded as length-ordered pieces, each
+    trimmed to its longest row, gives every row the tokens of the unsorted, untrimmed pieces
+    (t5-small at full size, right-padded masks of lengths 3 .. 60)."""
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    cfg = syn.T5Config()
+    m = DeviceT5(syn.t5_state_dict(3, cfg), device)
+    g = torch.Generator().manual_seed(rows)
+    L = 60
+    emb = (torch.randn((rows, L, cfg.d_model), generator=g) * 0.3).to(device)
+    lens = torch.randint(3, L + 1, (rows,), generator=g)
+    lens[0] = L
+    mask = (torch.arange(L)[None, :] < lens[:, None]).float().to(device)
+    plain = m.generate_padded(emb, mask, 20).cpu()
+    ordered = m.generate_padded(emb, mask, 20, lens=lens.tolist()).cpu()
+    assert torch.equal(plain, ordered)

@@ -1,5 +1,6 @@
-"""Kernel trace of config C5's end-to-end leg alone (development aid): three 256-question
-predict() calls of bench.c5_serving's model, host sleeps around them.  Run under
+"""Kernel trace of config C5's end-to-end leg alone (development aid): bench.c5_serving's model
+over 256-question batches through the serving loop (predict_many, as the bench's pipelined
+number; ``--sync``: one predict() call per batch), host sleeps around the timed window.  Run under
 ``rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c5t -- python tools/c5_trace.py``
 then ``python tools/serving_trace.py --report gpurun_out/c5t`` (busy / idle over the window, the
 longest idle gaps, kernel time by name); ``--cprofile`` adds a cProfile of one more predict()."""
@@ -27,22 +28,29 @@ m = T5VisionModel(dev, T5_version="t5-base", use_image_info=False,
                   clip_state_dict=syn.clip_state_dict(2),
                   t5_state_dict=syn.t5_state_dict(5, syn.T5_BASE),
                   tokenizer=SpmT5Tokenizer(), retrieval_function=retr).eval()
-pool = bench.make_batches(4, B, seed=500, n_images=1)
+pool = bench.make_batches(int(os.environ.get("C5_BATCHES", "5")), B, seed=500, n_images=1)
 os.environ["MPR_EOS_STOP_CHUNK"] = "0"
 with torch.no_grad():
     for b in pool:  # every source-length bucket's graphs captured before the timed calls
         m.predict(b)
+    list(m.predict_many(pool[:2], eos_stop=False))
     torch.cuda.synchronize()
     time.sleep(0.05)
     t = time.perf_counter()
-    parts = []
-    for b in pool[1:]:
-        t1 = time.perf_counter()
-        m.predict(b)
+    if "--sync" in sys.argv:
+        parts = []
+        for b in pool[1:]:
+            t1 = time.perf_counter()
+            m.predict(b)
+            torch.cuda.synchronize()
+            parts.append((time.perf_counter() - t1) * 1e3)
+        print(f"{len(pool) - 1} batches: {(time.perf_counter() - t) / (len(pool) - 1) * 1e3:.2f} "
+              f"ms per batch ({', '.join(f'{p:.1f}' for p in parts)})", flush=True)
+    else:
+        list(m.predict_many(pool[1:], eos_stop=False))
         torch.cuda.synchronize()
-        parts.append((time.perf_counter() - t1) * 1e3)
-    print(f"{len(pool) - 1} batches: {(time.perf_counter() - t) / (len(pool) - 1) * 1e3:.2f} ms per "
-          f"batch ({', '.join(f'{p:.1f}' for p in parts)})", flush=True)
+        print(f"{len(pool) - 1} batches through the serving loop: "
+              f"{(time.perf_counter() - t) / (len(pool) - 1) * 1e3:.2f} ms per batch", flush=True)
     time.sleep(0.05)
     torch.zeros(1, device=dev).add_(1)
     torch.cuda.synchronize()

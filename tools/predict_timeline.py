@@ -15,7 +15,7 @@ dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 cfg = bench.CONFIGS["c2"]
 model, _, weights = bench.build(cfg, dev, None)
-batches = bench.make_batches(4, cfg["B"], dev, seed=100)
+batches = bench.make_batches(4, cfg["B"], seed=100)
 with torch.no_grad():
     for i in range(12):
         torch.cuda.synchronize()
