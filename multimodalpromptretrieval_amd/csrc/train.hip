@@ -323,6 +323,151 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(TrainAttn a, const flo
   dk[b * dk_bs + j * dk_rs + h * 64 + lane] = gk;
 }
 
+// ---- block per (b, h) forms (Lq, Lk <= 128: the training shapes) ------------------------------
+// The wave-per-row kernels above re-read the (b, h) K / V (or dO / Q) rows from L2 once per row:
+// at L = 121 that is 121 x 62 KB per (b, h), 24-34 us per launch.  These stage them in LDS once
+// per (b, h) block (row stride 65: a lane per key reading its row is conflict-free) and run the
+// same per-row arithmetic in the same order — bit-identical results — with 8 waves taking the
+// rows in turn.
+constexpr int TB_MAXL = 128;
+constexpr int TB_LD = 65;
+constexpr int TB_WAVES = 8;
+
+__device__ __forceinline__ void tb_stage(const float* __restrict__ src, int64_t rs, int rows,
+                                         float* dst) {
+  for (int e = threadIdx.x; e < rows * 64; e += 64 * TB_WAVES)
+    dst[(e >> 6) * TB_LD + (e & 63)] = src[(int64_t)(e >> 6) * rs + (e & 63)];
+}
+
+__global__ __launch_bounds__(64 * TB_WAVES) void attn_fwd_bh_kernel(TrainAttn a,
+                                                                    float* __restrict__ o,
+                                                                    int64_t o_bs, int64_t o_rs,
+                                                                    float* __restrict__ P) {
+  __shared__ float Ks[TB_MAXL * TB_LD], Vs[TB_MAXL * TB_LD];
+  __shared__ float prow[TB_WAVES][TB_MAXL];
+  __shared__ float qs[TB_WAVES][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = blockIdx.x % a.H, b = blockIdx.x / a.H;
+  tb_stage(a.k + b * a.k_bs + h * 64, a.k_rs, a.Lk, Ks);
+  tb_stage(a.v + b * a.v_bs + h * 64, a.v_rs, a.Lk, Vs);
+  __syncthreads();
+  for (int i = wave; i < a.Lq; i += TB_WAVES) {
+    const int64_t item = ((int64_t)b * a.H + h) * a.Lq + i;
+    qs[wave][lane] = a.q[b * a.q_bs + i * a.q_rs + h * 64 + lane];
+    wave_lds_sync();
+    float mx = -INFINITY;
+    for (int j = lane; j < a.Lk; j += 64) {
+      const bool vis = (!a.causal || j <= i) && (!a.key_mask || a.key_mask[(int64_t)b * a.Lk + j] != 0.f);
+      float s = -INFINITY;
+      if (vis) {
+        const float* kr = Ks + j * TB_LD;
+        s = 0.f;
+#pragma unroll 16
+        for (int c = 0; c < 64; ++c) s += qs[wave][c] * kr[c];
+        if (a.rel) s += a.rel[(int64_t)(j - i + a.R) * a.H + h];
+      }
+      prow[wave][j] = s;
+      mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < a.Lk; j += 64) {
+      const float s = prow[wave][j];
+      const float e = s == -INFINITY ? 0.f : expf(s - mx);
+      prow[wave][j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    float* Pr = P + item * a.Lk;
+    for (int j = lane; j < a.Lk; j += 64) {
+      const float p = prow[wave][j] * inv;
+      prow[wave][j] = p * drop_factor(a.drop, (uint64_t)item * a.Lk + j);
+      Pr[j] = p;
+    }
+    wave_lds_sync();
+    float acc = 0.f;
+    for (int j = 0; j < a.Lk; ++j) acc += prow[wave][j] * Vs[j * TB_LD + lane];
+    o[b * o_bs + i * o_rs + h * 64 + lane] = acc;
+    wave_lds_sync();  // this row's qs / prow reads done before the next row's writes
+  }
+}
+
+__global__ __launch_bounds__(64 * TB_WAVES) void attn_bwd_q_bh_kernel(
+    TrainAttn a, const float* __restrict__ P, const float* __restrict__ dO, int64_t do_bs,
+    int64_t do_rs, float* __restrict__ dS, float* __restrict__ dq, int64_t dq_bs, int64_t dq_rs) {
+  __shared__ float Ks[TB_MAXL * TB_LD], Vs[TB_MAXL * TB_LD];
+  __shared__ float srow[TB_WAVES][TB_MAXL];
+  __shared__ float gs[TB_WAVES][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = blockIdx.x % a.H, b = blockIdx.x / a.H;
+  tb_stage(a.k + b * a.k_bs + h * 64, a.k_rs, a.Lk, Ks);
+  tb_stage(a.v + b * a.v_bs + h * 64, a.v_rs, a.Lk, Vs);
+  __syncthreads();
+  for (int i = wave; i < a.Lq; i += TB_WAVES) {
+    const int64_t item = ((int64_t)b * a.H + h) * a.Lq + i;
+    gs[wave][lane] = dO[b * do_bs + i * do_rs + h * 64 + lane];
+    wave_lds_sync();
+    const float* Pr = P + item * a.Lk;
+    float dsum = 0.f;
+    for (int j = lane; j < a.Lk; j += 64) {
+      const float p = Pr[j];
+      float dp = 0.f;
+      if (p != 0.f) {
+        const float* vr = Vs + j * TB_LD;
+#pragma unroll 16
+        for (int c = 0; c < 64; ++c) dp += gs[wave][c] * vr[c];
+        dp *= drop_factor(a.drop, (uint64_t)item * a.Lk + j);
+      }
+      srow[wave][j] = dp;
+      dsum += p * dp;
+    }
+    dsum = wave_sum(dsum);
+    float* dSr = dS + item * a.Lk;
+    for (int j = lane; j < a.Lk; j += 64) {
+      const float ds = Pr[j] * (srow[wave][j] - dsum);
+      srow[wave][j] = ds;
+      dSr[j] = ds;
+    }
+    wave_lds_sync();
+    float acc = 0.f;
+    for (int j = 0; j < a.Lk; ++j) acc += srow[wave][j] * Ks[j * TB_LD + lane];
+    dq[b * dq_bs + i * dq_rs + h * 64 + lane] = acc;
+    wave_lds_sync();
+  }
+}
+
+// per key row j: its column of P (times the dropout factor) and of dS staged per wave, then
+// dV_j = sum_i Pm_ij dO_i, dK_j = sum_i dS_ij Q_i in row order
+__global__ __launch_bounds__(64 * TB_WAVES) void attn_bwd_kv_bh_kernel(
+    TrainAttn a, const float* __restrict__ P, const float* __restrict__ dS,
+    const float* __restrict__ dO, int64_t do_bs, int64_t do_rs, float* __restrict__ dk,
+    int64_t dk_bs, int64_t dk_rs, float* __restrict__ dv, int64_t dv_bs, int64_t dv_rs) {
+  __shared__ float Gs[TB_MAXL * TB_LD], Qs[TB_MAXL * TB_LD];
+  __shared__ float pc[TB_WAVES][TB_MAXL], dc[TB_WAVES][TB_MAXL];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = blockIdx.x % a.H, b = blockIdx.x / a.H;
+  tb_stage(dO + b * do_bs + h * 64, do_rs, a.Lq, Gs);
+  tb_stage(a.q + b * a.q_bs + h * 64, a.q_rs, a.Lq, Qs);
+  __syncthreads();
+  const int64_t base = ((int64_t)b * a.H + h) * a.Lq;  // (b, h, i = 0) row of P / dS
+  for (int j = wave; j < a.Lk; j += TB_WAVES) {
+    for (int i = lane; i < a.Lq; i += 64) {
+      pc[wave][i] = P[(base + i) * a.Lk + j] * drop_factor(a.drop, (uint64_t)(base + i) * a.Lk + j);
+      dc[wave][i] = dS[(base + i) * a.Lk + j];
+    }
+    wave_lds_sync();
+    float gv = 0.f, gk = 0.f;
+    for (int i = 0; i < a.Lq; ++i) {
+      gv += pc[wave][i] * Gs[i * TB_LD + lane];
+      gk += dc[wave][i] * Qs[i * TB_LD + lane];
+    }
+    dv[b * dv_bs + j * dv_rs + h * 64 + lane] = gv;
+    dk[b * dk_bs + j * dk_rs + h * 64 + lane] = gk;
+    wave_lds_sync();
+  }
+}
+
 // d(rel)[off][h] += sum_{b, i} dS[b, h, i, i + off - R]: block per (off, h), fixed order
 __global__ __launch_bounds__(256) void attn_bwd_rel_kernel(const float* __restrict__ dS, int B,
                                                            int H, int Lq, int Lk, int R,
@@ -624,8 +769,12 @@ int mpr_attn_train_fwd(const float* q, int64_t q_bs, int64_t q_rs, const float* 
   TrainAttn a = make_attn(q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs, B, H, Lq, Lk, causal,
                           key_mask, rel, R);
   a.drop = Drop{drop_seed, drop_site, drop_thresh, drop_scale};
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)cdiv(items, 4)), dim3(256), 0, S(stream), a,
-                     o, o_bs, o_rs, P);
+  if (Lq <= TB_MAXL && Lk <= TB_MAXL)
+    hipLaunchKernelGGL(attn_fwd_bh_kernel, dim3((unsigned)(B * H)), dim3(64 * TB_WAVES), 0,
+                       S(stream), a, o, o_bs, o_rs, P);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)cdiv(items, 4)), dim3(256), 0, S(stream),
+                       a, o, o_bs, o_rs, P);
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -643,12 +792,22 @@ int mpr_attn_train_bwd(const float* q, int64_t q_bs, int64_t q_rs, const float* 
   TrainAttn a = make_attn(q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs, B, H, Lq, Lk, 0, nullptr,
                           nullptr, R);
   a.drop = Drop{drop_seed, drop_site, drop_thresh, drop_scale};
-  hipLaunchKernelGGL(attn_bwd_q_kernel, dim3((unsigned)cdiv((int64_t)B * H * Lq, 4)), dim3(256), 0,
-                     S(stream), a, P, dO, do_bs, do_rs, dS, dq, dq_bs, dq_rs);
-  MPR_LAUNCHED();
-  hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3((unsigned)cdiv((int64_t)B * H * Lk, 4)), dim3(256), 0,
-                     S(stream), a, P, dS, dO, do_bs, do_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs);
-  MPR_LAUNCHED();
+  if (Lq <= TB_MAXL && Lk <= TB_MAXL) {
+    hipLaunchKernelGGL(attn_bwd_q_bh_kernel, dim3((unsigned)(B * H)), dim3(64 * TB_WAVES), 0,
+                       S(stream), a, P, dO, do_bs, do_rs, dS, dq, dq_bs, dq_rs);
+    MPR_LAUNCHED();
+    hipLaunchKernelGGL(attn_bwd_kv_bh_kernel, dim3((unsigned)(B * H)), dim3(64 * TB_WAVES), 0,
+                       S(stream), a, P, dS, dO, do_bs, do_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs);
+    MPR_LAUNCHED();
+  } else {
+    hipLaunchKernelGGL(attn_bwd_q_kernel, dim3((unsigned)cdiv((int64_t)B * H * Lq, 4)), dim3(256),
+                       0, S(stream), a, P, dO, do_bs, do_rs, dS, dq, dq_bs, dq_rs);
+    MPR_LAUNCHED();
+    hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3((unsigned)cdiv((int64_t)B * H * Lk, 4)),
+                       dim3(256), 0, S(stream), a, P, dS, dO, do_bs, do_rs, dk, dk_bs, dk_rs, dv,
+                       dv_bs, dv_rs);
+    MPR_LAUNCHED();
+  }
   if (drel) {
     hipLaunchKernelGGL(attn_bwd_rel_kernel, dim3((unsigned)(2 * R + 1), (unsigned)H), dim3(256), 0,
                        S(stream), dS, B, H, Lq, Lk, R, drel);

@@ -449,15 +449,13 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
     TR_GET(dqkv, (int64_t)M * 3 * I);
     MPR_TRY(attn_bwd(ar, qkv, 3 * I, qkv + I, 3 * I, qkv + 2 * I, 3 * I, Pm, da, B, Lx, Lx, drel,
                      R, dr, st, dqkv, 3 * I, dqkv + I, 3 * I, dqkv + 2 * I, 3 * I));
+    const bool wdw = want(ids[0]) || want(ids[1]) || want(ids[2]);
     const float* WqkvT = transpose(ar, Wqkv, 3 * I, d, d);
-    MPR_REQUIRE(WqkvT, "trainer: out of device memory");
+    const float* dT = wdw ? transpose(ar, dqkv, M, 3 * I, 3 * I) : nullptr;
+    const float* xT = wdw ? transpose(ar, n1, M, d, d) : nullptr;
+    MPR_REQUIRE(WqkvT && (!wdw || (dT && xT)), "trainer: out of device memory");
     MPR_TRY(gemm(ar, dqkv, 3 * I, WqkvT, 3 * I, dn, M, d, 3 * I));
-    if (want(ids[0]) || want(ids[1]) || want(ids[2])) {
-      const float* dT = transpose(ar, dqkv, M, 3 * I, 3 * I);
-      const float* xT = transpose(ar, n1, M, d, d);
-      MPR_REQUIRE(dT && xT, "trainer: out of device memory");
-      MPR_TRY(stacked_dw(ids, I, dT, xT, d, M));
-    }
+    if (wdw) MPR_TRY(stacked_dw(ids, I, dT, xT, d, M));
     return MPR_OK;
   };
   // loss -> logits
@@ -539,10 +537,6 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
   // weight gradient
   float* d_enc = nullptr;
   if (Ld) {
-    d_enc = ar.get((int64_t)Me * d);
-    const float* WckvT = transpose(ar, tp.Wckv, ckv_ld, d, d);
-    MPR_REQUIRE(d_enc && WckvT, "trainer: out of device memory");
-    MPR_TRY(gemm(ar, dckv, ckv_ld, WckvT, ckv_ld, d_enc, Me, d, (int)ckv_ld));
     std::vector<int> ids;
     bool any = false;
     for (int l = 0; l < Ld; ++l) {
@@ -550,12 +544,13 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
       ids.push_back(dp(l, 8));
       any = any || want(dp(l, 7)) || want(dp(l, 8));
     }
-    if (any) {
-      const float* dT = transpose(ar, dckv, Me, ckv_ld, ckv_ld);
-      const float* xT = transpose(ar, tp.enc_out, Me, d, d);
-      MPR_REQUIRE(dT && xT, "trainer: out of device memory");
-      MPR_TRY(stacked_dw(ids, I, dT, xT, d, Me));
-    }
+    d_enc = ar.get((int64_t)Me * d);
+    const float* WckvT = transpose(ar, tp.Wckv, ckv_ld, d, d);
+    const float* dT = any ? transpose(ar, dckv, Me, ckv_ld, ckv_ld) : nullptr;
+    const float* xT = any ? transpose(ar, tp.enc_out, Me, d, d) : nullptr;
+    MPR_REQUIRE(d_enc && WckvT && (!any || (dT && xT)), "trainer: out of device memory");
+    MPR_TRY(gemm(ar, dckv, ckv_ld, WckvT, ckv_ld, d_enc, Me, d, (int)ckv_ld));
+    if (any) MPR_TRY(stacked_dw(ids, I, dT, xT, d, Me));
   } else {
     d_enc = ar.get((int64_t)Me * d);
     MPR_REQUIRE(d_enc, "trainer: out of device memory");

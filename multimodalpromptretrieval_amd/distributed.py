@@ -184,6 +184,58 @@ class ShardedIndex:
         ci = i_all.permute(1, 0, 2).reshape(B, self.world * k)
         return self._merge(cd.contiguous(), ci.contiguous(), k)
 
+    def search_all_many(self, queries, k: int):
+        """search_all over an iterable of query batches (the same batches on every rank) as a
+        pipeline, yielding each batch's (dist, ids) in order, each equal to its search_all: batch
+        i+1's local scan is enqueued (on the other of two streams) before batch i's all_gather is
+        waited for and merged, so the collective and the merge run behind the next scan instead
+        of after it.  Host-staged backends (gloo over device tensors) run them one by one."""
+        it = iter(queries)
+        if self._host_staged() or self.device.type != "cuda":
+            for q in it:
+                yield self.search_all(q, k)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        streams = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+
+        def start(q, j):
+            st = streams[j % 2]
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                B = q.shape[0]
+                q = q.to(self.device, torch.float32).contiguous()
+                packed = self._pack(*self._padded_search(q, k))
+                recv = torch.empty((self.world * B,) + tuple(packed.shape[1:]),
+                                   dtype=packed.dtype, device=self.device)
+                work = dist.all_gather_into_tensor(recv, packed, group=self.group,
+                                                   async_op=True)
+            return st, B, recv, work
+
+        pend = None
+        j = 0
+        for q in it:
+            nxt = start(q, j)
+            j += 1
+            if pend is not None:
+                yield self._finish_all(pend, k)
+            pend = nxt
+        if pend is not None:
+            yield self._finish_all(pend, k)
+
+    def _finish_all(self, pend, k):
+        st, B, recv, work = pend
+        with torch.cuda.stream(st):
+            work.wait()
+            d_all, i_all = self._unpack(recv.view(self.world, B, k, 2))
+            cd = d_all.permute(1, 0, 2).reshape(B, self.world * k)
+            ci = i_all.permute(1, 0, 2).reshape(B, self.world * k)
+            out = self._merge(cd.contiguous(), ci.contiguous(), k)
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(st)
+        for t in out:
+            t.record_stream(cur)
+        return out
+
     def _padded_search(self, q, k):
         kk = min(k, self.n_local)
         d_loc, i_loc = self._search(q, kk)

@@ -270,7 +270,10 @@ class T5VisionModel(nn.Module):
         """The VQARetrieval behind ``retrieval_function``: its ``__self__``, or the one a
         reference dataset patched by ``dropin`` carries (``main.py`` passes the dataset's bound
         ``retrieve_closest_qa_pairs``, main.py:123)."""
-        owner = getattr(self.retrieval_function, "__self__", None)
+        rf = self.retrieval_function
+        owner = getattr(rf, "__self__", None)
+        if owner is None and hasattr(rf, "prefetch_many"):  # a retrieval object called directly
+            owner = rf
         return getattr(owner, "__dict__", {}).get("_mpr_retrieval", owner)
 
     @staticmethod

@@ -254,8 +254,10 @@ class ServingLoop:
             return True
         self._flush_held()
         # rows by length, each piece trimmed to its longest row (t5.length_pieces): the answers
-        # come back in the batch's order
-        order, pieces = length_pieces(combined, mask, lens if rows > 16 else None)
+        # come back in the batch's order.  The row gather runs on the prep stream, after the
+        # prepare_input work that wrote its inputs (the generate streams wait on that stream)
+        with torch.cuda.stream(self.m._s_prep):
+            order, pieces = length_pieces(combined, mask, lens if rows > 16 else None)
         owned = []
         per = pieces_per_call()
         for g in range(0, len(pieces), per):

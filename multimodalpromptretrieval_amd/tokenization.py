@@ -496,6 +496,27 @@ class SpmT5Tokenizer:
 
     def batch_decode(self, sequences, skip_special_tokens: bool = False,
                      clean_up_tokenization_spaces: bool = True, **kw) -> list:
+        """decode() per row.  With skip_special_tokens the rows holding no added token (every
+        answer of a generate) go through one SentencePiece batch decode of their kept ids —
+        decode()'s own fast path, rows at once (config C5: 256 answers 8.9 -> ~3 ms)."""
+        if skip_special_tokens and isinstance(sequences, (torch.Tensor, np.ndarray)):
+            a = sequences.cpu().numpy() if isinstance(sequences, torch.Tensor) else sequences
+            if a.ndim == 2 and np.issubdtype(a.dtype, np.integer):
+                added = np.fromiter(self.added_tokens_decoder.keys(), dtype=np.int64)
+                slow = np.isin(a, added).any(1) if added.size else np.zeros(len(a), bool)
+                keep = ~np.isin(a, np.fromiter(self._special_ids, dtype=np.int64))
+                fast = [r for r in range(len(a)) if not slow[r]]
+                # one thread: the library's default pool spans every host CPU (256 on the GPU
+                # box), ~10 ms of thread start-up per call
+                texts = (self.sp.DecodeIds([a[r][keep[r]].tolist() for r in fast], num_threads=1)
+                         if fast else [])
+                out = [None] * len(a)
+                for r, t in zip(fast, texts):
+                    t = t.strip()
+                    out[r] = self.clean_up_tokenization(t) if clean_up_tokenization_spaces else t
+                for r in np.nonzero(slow)[0]:
+                    out[r] = self.decode(a[r].tolist(), True, clean_up_tokenization_spaces)
+                return out
         if hasattr(sequences, "tolist"):
             sequences = sequences.tolist()
         return [self.decode(s, skip_special_tokens, clean_up_tokenization_spaces)

@@ -110,6 +110,10 @@ def _worker_all(rank, world, port, n, d, B, k, result_q):
         q = syn.index_rows(9, B, d)   # the same batch on every rank (replicated queries)
         six = ShardedIndex(X, "cpu", searcher=cpu_searcher, merger=cpu_merger)
         out = [six.search_all(q, k)[1].tolist() for _ in range(2)]
+        # the pipelined form over three batches: each batch's search_all result
+        qs = [q, q[:3], q]
+        many = [i.tolist() for _, i in six.search_all_many(qs, k)]
+        assert many == [six.search_all(b, k)[1].tolist() for b in qs]
         result_q.put((rank, out))
     finally:
         dist.destroy_process_group()

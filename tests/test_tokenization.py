@@ -221,3 +221,21 @@ def test_t5_decode_matches_transformers(t5_pair):
                    clean_up_tokenization_spaces=True).strip()]
     # the added token decodes as itself, space-joined (4.26.1 _decode)
     assert ours.decode([3, 32100, 30, 1], skip_special_tokens=True) == "the [itk] organ"
+
+
+def test_t5_batch_decode_equals_per_row_decode():
+    """batch_decode's batched SentencePiece path (rows without added tokens) gives decode()'s
+    string for every row: random greedy-like ids with pads, eos, extra ids and the added [itk]."""
+    tok = tk.SpmT5Tokenizer()
+    tok.add_tokens(["[itk]"])
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(3, 32000, (300, 21), generator=g)
+    ids[:7, 4] = 32100          # the added token: the per-row path
+    ids[7:20, 0] = 0            # pads and eos runs
+    ids[20:40, 9:] = 1
+    ids[40:50, 2] = 32050       # an extra id (special)
+    want = [tok.decode(r.tolist(), skip_special_tokens=True) for r in ids]
+    for seq in (ids, ids.to(torch.int32), ids.numpy()):
+        assert tok.batch_decode(seq, skip_special_tokens=True) == want
+    assert tok.batch_decode(ids, skip_special_tokens=False) == \
+        [tok.decode(r.tolist()) for r in ids]

@@ -54,12 +54,16 @@ with torch.no_grad():
     time.sleep(0.05)
     torch.zeros(1, device=dev).add_(1)
     torch.cuda.synchronize()
-    if "--cprofile" in sys.argv:  # where one predict()'s host time goes
+    if "--cprofile" in sys.argv:  # where the serving loop's host time goes
         import cProfile
         import pstats
         pr = cProfile.Profile()
         pr.enable()
-        m.predict(pool[1])
+        if "--sync" in sys.argv:
+            m.predict(pool[1])
+        else:
+            list(m.predict_many(pool[1:], eos_stop=False))
         torch.cuda.synchronize()
         pr.disable()
-        pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
+        pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
+        pstats.Stats(pr).sort_stats("tottime").print_stats(25)

@@ -24,3 +24,16 @@ with torch.no_grad():
         model.predict(batches[i % 4])
         torch.cuda.synchronize()
         print(f"predict {i}: {(time.perf_counter() - t) * 1e3:.2f} ms", flush=True)
+
+if "--cprofile" in sys.argv:  # where one predict()'s host time goes
+    import cProfile
+    import pstats
+    with torch.no_grad():
+        pr = cProfile.Profile()
+        pr.enable()
+        for i in range(4):
+            model.predict(batches[i % 4])
+            torch.cuda.synchronize()
+        pr.disable()
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(20)
