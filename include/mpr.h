@@ -362,6 +362,17 @@ int mpr_t5_train_release(mpr_model* trainer, int32_t tape);
 int mpr_gemm_f32_splitk(const float* A, int64_t lda, const float* W, int64_t ldw, float* C,
                         int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr,
                         int32_t act, int32_t splits, float* partial, void* stream);
+/* Fixed weights (the CLIP towers', the T5 encoder's and its cross-attention K/V projection) are
+ * split once: mpr_pack_x3 writes W [N, K] (row stride ldw) as its three bf16 planes in the
+ * matrix-core operand order (mpr_pack_x3_bytes bytes), and a GEMM handed that image loads its W
+ * fragments from it instead of staging W through LDS.  mpr_gemm_f32_packed: mpr_gemm_f32 with
+ * the packed image of W — bit-identical results (same split, same summation order). */
+int mpr_pack_x3_bytes(int64_t N, int64_t K, int64_t* bytes);
+int mpr_pack_x3(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, int64_t out_bytes,
+                void* stream);
+int mpr_gemm_f32_packed(const float* A, int64_t lda, const float* W, int64_t ldw, const void* wp,
+                        float* C, int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R,
+                        int64_t ldr, int32_t act, void* stream);
 int mpr_gather_rows(const float* table, const int32_t* ids, int64_t n, int32_t d, float* out,
                     void* stream);
 int mpr_embed_bwd(const float* dY, int32_t d, const int32_t* uniq, const int32_t* offs,

@@ -107,6 +107,11 @@ SIGNATURES = [
     ("mpr_gemm_f32_splitk", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                       c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
                                       c_int32, c_void_p, c_void_p]),
+    ("mpr_pack_x3_bytes", c_int32, [c_int64, c_int64, I64P]),
+    ("mpr_pack_x3", c_int32, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
+    ("mpr_gemm_f32_packed", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                      c_int64, c_int32, c_int32, c_int32, c_void_p, c_int64,
+                                      c_int32, c_void_p]),
     ("mpr_transpose", c_int32, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64,
                                 c_void_p]),
     ("mpr_rmsnorm_fwd", c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_float, c_float,

@@ -239,6 +239,9 @@ int mpr_vit_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int
     MPR_TRY(upload(m->lnpost_w, tail[0], W));
     MPR_TRY(upload(m->lnpost_b, tail[1], W));
     MPR_TRY(upload_t(m->projT, tail[2], W, out_dim));
+    MPR_TRY(pack_weight(m->pk_conv, m->conv_w, W, (int64_t)3 * patch * patch));
+    MPR_TRY(pack_weight(m->pk_projT, m->projT, out_dim, W));
+    MPR_HIP(hipStreamSynchronize(nullptr));
     *out = m.release();
     return MPR_OK;
   });
@@ -335,6 +338,8 @@ int mpr_clip_text_create(const int32_t* cfg, int32_t n_cfg, const float* const* 
     MPR_TRY(upload(m->lnf_w, tail[0], W));
     MPR_TRY(upload(m->lnf_b, tail[1], W));
     MPR_TRY(upload_t(m->projT, tail[2], W, out_dim));
+    MPR_TRY(pack_weight(m->pk_projT, m->projT, out_dim, W));
+    MPR_HIP(hipStreamSynchronize(nullptr));
     *out = m.release();
     return MPR_OK;
   });
@@ -448,6 +453,18 @@ int t5_load(T5Model* m, const float* const* t, const int32_t* enc_lut, const int
   }
   MPR_TRY(pack(m->pk_lm_head, m->lm_head, m->V, d));
   MPR_TRY(pack_many(packs, s));
+  // split images of the encoder projections and the cross-attention K/V weight (tiled GEMMs)
+  auto pack3 = [&](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
+    MPR_TRY(dst.ensure((size_t)packed_x3_bytes(n, k)));
+    return pack_x3(src.as<float>(), n, k, k, dst.ptr, s);
+  };
+  for (auto& ly : m->enc) {
+    MPR_TRY(pack3(ly->xp_qkv, ly->qkv, 3 * inner, d));
+    MPR_TRY(pack3(ly->xp_o, ly->o, d, inner));
+    MPR_TRY(pack3(ly->xp_wi, ly->wi, dff, d));
+    MPR_TRY(pack3(ly->xp_wo, ly->wo, d, dff));
+  }
+  MPR_TRY(pack3(m->xp_cross_kv, m->cross_kv_w, (int64_t)Ld * 2 * inner, d));
   if (m->fold) MPR_TRY(m->build_folded(s));
   return MPR_OK;
 }

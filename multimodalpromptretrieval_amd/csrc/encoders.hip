@@ -49,9 +49,21 @@ int ClipTower::load_blocks(const float* const* t, int w, int nl) {
     MPR_TRY(upload(b->fc_b, p[9], (size_t)4 * w));
     MPR_TRY(upload(b->pj_w, p[10], (size_t)4 * w * w));
     MPR_TRY(upload(b->pj_b, p[11], w));
+    MPR_TRY(pack_weight(b->pk_in, b->in_w, 3 * w, w));
+    MPR_TRY(pack_weight(b->pk_out, b->out_w, w, w));
+    MPR_TRY(pack_weight(b->pk_fc, b->fc_w, 4 * w, w));
+    MPR_TRY(pack_weight(b->pk_pj, b->pj_w, w, 4 * w));
     blocks.push_back(std::move(b));
   }
+  MPR_HIP(hipStreamSynchronize(nullptr));
   return MPR_OK;
+}
+
+int pack_weight(DevBuf& dst, const DevBuf& w, int64_t N, int64_t K) {
+  MPR_REQUIRE(w.bytes >= (size_t)N * K * sizeof(float), "pack_weight: %lld x %lld of %zu bytes",
+              (long long)N, (long long)K, w.bytes);
+  MPR_TRY(dst.ensure((size_t)packed_x3_bytes(N, K)));
+  return pack_x3(w.as<float>(), N, K, K, dst.ptr, nullptr);
 }
 
 // n CLIP transformers with the same layer count stepped in lockstep (the retrieval ViT, the
@@ -85,15 +97,19 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       float* mp = r[i].w->mlp.as<float>();
       GemmArgs& g = gq.g[i];
       g.A = hp; g.lda = W; g.W = b.in_w.as<float>(); g.ldw = W; g.bias = b.in_b.as<float>();
+      g.wp = b.pk_in.ptr;
       g.C = qp; g.ldc = 3 * W; g.M = M; g.N = 3 * W; g.K = W;
       GemmArgs& o = go.g[i];
       o.A = ap; o.lda = W; o.W = b.out_w.as<float>(); o.ldw = W; o.bias = b.out_b.as<float>();
+      o.wp = b.pk_out.ptr;
       o.R = x; o.ldr = W; o.C = x; o.ldc = W; o.M = M; o.N = W; o.K = W;
       GemmArgs& f = gf.g[i];
       f.A = hp; f.lda = W; f.W = b.fc_w.as<float>(); f.ldw = W; f.bias = b.fc_b.as<float>();
+      f.wp = b.pk_fc.ptr;
       f.C = mp; f.ldc = 4 * W; f.M = M; f.N = 4 * W; f.K = W; f.act = ACT_QUICKGELU;
       GemmArgs& pj = gp.g[i];
       pj.A = mp; pj.lda = 4 * W; pj.W = b.pj_w.as<float>(); pj.ldw = 4 * W;
+      pj.wp = b.pk_pj.ptr;
       pj.bias = b.pj_b.as<float>(); pj.R = x; pj.ldr = W; pj.C = x; pj.ldc = W; pj.M = M;
       pj.N = W; pj.K = 4 * W;
       g.tile_m = o.tile_m = f.tile_m = pj.tile_m = TM;
@@ -241,6 +257,7 @@ int encode_towers_eager(VitModel* const* v, const int* modes, float* const* outs
     for (int i = 0; i < nv; ++i) {
       GemmArgs& g = pe.g[i];
       g.A = cols.as<float>(); g.lda = P; g.W = v[i]->conv_w.as<float>(); g.ldw = P;
+      g.wp = v[i]->pk_conv.ptr;
       g.C = v[i]->ws[slot].patches.as<float>(); g.ldc = W; g.M = B * g2; g.N = W; g.K = P;
       g.tile_m = B / ig * g2;
     }
@@ -277,6 +294,7 @@ int encode_towers_eager(VitModel* const* v, const int* modes, float* const* outs
     float* tp = m.ws[slot].tmp.as<float>();
     GemmArgs& pj = pg.g[pg.n++];
     pj.W = m.projT.as<float>(); pj.ldw = W; pj.N = m.out_dim; pj.K = W; pj.A = tp; pj.lda = W;
+    pj.wp = m.pk_projT.ptr;
     if (modes[i] == 0) {
       // ln_post on the CLS rows only (x[b*T]), then @ proj
       MPR_TRY(layernorm(xp, (int64_t)T * W, B, W, m.lnpost_w.as<float>(),
@@ -298,6 +316,7 @@ int encode_towers_eager(VitModel* const* v, const int* modes, float* const* outs
                       pp, W, s));
     GemmArgs& pj = pg.g[pg.n++];
     pj.A = pp; pj.lda = W; pj.W = tm->projT.as<float>(); pj.ldw = W; pj.M = Bt;
+    pj.wp = tm->pk_projT.ptr;
     pj.N = tm->out_dim; pj.K = W; pj.C = out_t[j]; pj.ldc = out_t_bs[j];
   }
   MPR_TRY(gemm_group(pg, s));

@@ -513,7 +513,7 @@ __device__ __forceinline__ GemmArgs select_problem(const GemmGroup& grp, int z) 
   a.ldc = MPR_SEL(ldc); a.M = MPR_SEL(M); a.N = MPR_SEL(N); a.K = MPR_SEL(K);
   a.act = MPR_SEL(act); a.c_rpb = MPR_SEL(c_rpb); a.c_bs = MPR_SEL(c_bs);
   a.batch = MPR_SEL(batch); a.a_bs = MPR_SEL(a_bs); a.w_bs = MPR_SEL(w_bs);
-  a.cb_bs = MPR_SEL(cb_bs);
+  a.cb_bs = MPR_SEL(cb_bs); a.wp = MPR_SEL(wp);
 #undef MPR_SEL
   return a;
 }
@@ -633,6 +633,270 @@ int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
                        dim3(NT), 0, s, g);
   else
     hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, false, V>), dim3((unsigned)tiles),
+                       dim3(NT), 0, s, g);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+// ---- split-bf16 GEMM with a packed W ("x3p") ------------------------------------------------
+// The tower and T5-encoder weights are fixed for the life of a model, so their split is done
+// once: pack_x3 writes W as the three bf16 planes in v_mfma_f32_32x32x16_bf16 operand order,
+// [cdiv(N, 32) column tiles][cdiv(K, 16) k steps][3 planes][64 lanes][8 bf16] (lane (li, lh):
+// column 32 t + li, k = 16 s + 8 lh .. +7; zero past N and K), and each wave loads its W
+// fragments straight into registers — 1 KiB contiguous per wave load — D k steps ahead.  Only A
+// goes through LDS.  Measured on the tower shapes with the LDS traffic of W removed from the
+// 128x128 kernel (profiles/r04_x3_lds_diag.txt): 80.6 -> 56.5 us (qkv 1600x2304x768 x2), 109.7
+// -> 77.4 (fc1): the LDS fragment traffic, not the MFMA issue, sets that kernel's pace.  Every
+// output element is accumulated in the same order with the same split terms as gemm_x3_tile
+// (W split by the same split3, per element): bit-identical results.
+__global__ __launch_bounds__(256) void pack_x3_kernel(const float* __restrict__ W, int N, int K,
+                                                      int64_t ldw, int KS, bf16x8* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one (column tile, k step, lane)
+  const int64_t total = cdiv(N, 32) * (int64_t)KS * 64;
+  if (q >= total) return;
+  const int lane = (int)(q & 63);
+  const int64_t t = q >> 6;
+  const int ks = (int)(t % KS);
+  const int n = (int)(t / KS) * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
+  f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (k0 + e < K) lo[e] = W[(int64_t)n * ldw + k0 + e];
+      if (k0 + 4 + e < K) hi[e] = W[(int64_t)n * ldw + k0 + 4 + e];
+    }
+  }
+  bf16x8 h0, h1, h2;
+  x3::split8(lo, hi, h0, h1, h2);
+  out[(t * 3 + 0) * 64 + lane] = h0;
+  out[(t * 3 + 1) * 64 + lane] = h1;
+  out[(t * 3 + 2) * 64 + lane] = h2;
+}
+
+template <int BM, int BN, int WM, int WN, int D, bool KT>
+__device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
+  constexpr int BK = 16;
+  constexpr int WAVES_N = BN / (32 * WN);
+  constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
+  constexpr int NT = 64 * WAVES_MN;
+  constexpr int LDK = BK + 8, KQ = BK / 4;
+  constexpr int LA = BM * KQ / NT;
+  constexpr int PLANE = BM * LDK;   // bf16 per plane (A rows only)
+  constexpr int STAGE = 3 * PLANE;
+  static_assert(LA >= 1 && LA * NT == BM * KQ, "loader split");
+  __bf16* smem = reinterpret_cast<__bf16*>(smem_f);
+  const int M = a.M, N = a.N, K = a.K;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wmn = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wmn / WAVES_N, wn = wmn % WAVES_N;
+  const int KS = (K + 15) / 16, NTW = (N + 31) / 32;
+  const bf16x8* wpk[WN];
+#pragma unroll
+  for (int ni = 0; ni < WN; ++ni)
+    wpk[ni] = reinterpret_cast<const bf16x8*>(a.wp) +
+              (int64_t)min(n0 / 32 + wn * WN + ni, NTW - 1) * KS * 3 * 64 + lane;
+
+  f32x4 ra[D][LA];
+  bool oka[D][LA];
+  bf16x8 bq[D][WN][3];
+  auto aload = [&](int j, int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = m0 + r;
+      if constexpr (KT) oka[j][i] = c < K;
+      ra[j][i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
+                                                 min(c, K - 4));
+    }
+  };
+  auto bload = [&](int j, int kt) {  // past the last k step: an in-range step (A is zero there)
+    const int ks = min(kt, KS - 1);
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[j][ni][p] = wpk[ni][((int64_t)ks * 3 + p) * 64];
+  };
+  auto put = [&](__bf16* base, int row, int kc, const f32x4& v) {
+    bf16x4 h0, h1, h2;
+    split3(v, h0, h1, h2);
+    __bf16* p = base + row * LDK + kc;
+    *reinterpret_cast<bf16x4*>(p) = h0;
+    *reinterpret_cast<bf16x4*>(p + PLANE) = h1;
+    *reinterpret_cast<bf16x4*>(p + 2 * PLANE) = h2;
+  };
+  auto swrite = [&](int st, int j) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    __bf16* base = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int idx = tid + i * NT;
+      if constexpr (KT) put(base, idx / KQ, (idx % KQ) * 4, oka[j][i] ? ra[j][i] : zero);
+      else put(base, idx / KQ, (idx % KQ) * 4, ra[j][i]);
+    }
+  };
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int li = lane & 31, lh = lane >> 5;
+  bf16x8 fa[WM][3], na[WM][3];
+  auto sread = [&](int st, bf16x8(&xa)[WM][3]) {
+    const __bf16* base = smem + st * STAGE;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int mi = 0; mi < WM; ++mi)
+        xa[mi][p] = *reinterpret_cast<const bf16x8*>(base + p * PLANE +
+                                                     (wm * 32 * WM + mi * 32 + li) * LDK + 8 * lh);
+  };
+  // MFMA u of the step's WM * WN * 6 (u = (mi * WN + ni) * 6 + term), terms in gemm_x3_tile's
+  // order: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
+  constexpr int NMF = WM * WN * 6;
+  auto mfmas = [&](int j, int u_lo, int u_hi) {
+#pragma unroll
+    for (int u = u_lo; u < u_hi; ++u) {
+      const int term = u % 6, t = u / 6, ni = t % WN, mi = t / WN;
+      constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+      acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PA[term]], bq[j][ni][PB[term]],
+                                                            acc[mi][ni], 0, 0, 0);
+    }
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  const int nkr = (nk + D - 1) / D * D;
+  aload(0, 0);
+  swrite(0, 0);
+  aload(0, 1);
+  swrite(1, 0);
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    aload(j, 2 + j);
+    bload(j, j);
+  }
+  __syncthreads();
+  sread(0, fa);
+  __syncthreads();
+  // Iteration t: multiply tile t (A fragments read the iteration before, W fragments loaded D
+  // iterations before), read tile t+1's A fragments from the other stage, write tile t+2's A
+  // into tile t's stage, re-arm the register slots with tile t+2+D's A and tile t+D's W.
+  constexpr int U1 = NMF / 3 > 0 ? NMF / 3 : 1;
+  for (int kt = 0; kt < nkr; kt += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int st = (kt + j) & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      mfmas(j, 0, U1);
+      __builtin_amdgcn_sched_barrier(0);
+      sread(st ^ 1, na);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(j, U1, NMF);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+      swrite(st, j);
+      aload(j, kt + j + 2 + D);
+      bload(j, kt + j + D);
+      __syncthreads();
+#pragma unroll
+      for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fa[mi][p] = na[mi][p];
+    }
+  }
+
+#pragma unroll
+  for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+      const int col = n0 + wn * 32 * WN + ni * 32 + li, colc = min(col, N - 1);
+      const int rbase = m0 + wm * 32 * WM + mi * 32 + 4 * lh;
+      const float bv = a.bias ? a.bias[colc] : 0.f;
+      float rv[16];
+      if (a.R) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          rv[r] = a.R[(int64_t)min(rbase + (r & 3) + 8 * (r >> 2), M - 1) * a.ldr + colc];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        float v = act_exact(acc[mi][ni][r] + bv, a.act);
+        if (a.R) v = rv[r] + v;
+        const int64_t coff = a.c_rpb ? (int64_t)(row / a.c_rpb) * a.c_bs +
+                                           (int64_t)(row % a.c_rpb) * a.ldc
+                                     : (int64_t)row * a.ldc;
+        if (row < M && col < N) a.C[coff + col] = v;
+      }
+    }
+}
+
+// gemm_x3_kernel's grid and tile order, the packed-W tile
+template <int BM, int BN, int WM, int WN, int D, bool KT>
+__global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm_x3p_kernel(
+    const GemmGroup grp) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * 3 * BM * (16 + 8) / 2];
+  const int total = gridDim.x, hw = blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
+  int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  int z = 0, gy = 0;
+#pragma unroll
+  for (int i = 0; i < GEMM_GROUP; ++i) {
+    if (i == z && i < grp.n) {
+      const int gyi = (int)cdiv(i == 0 ? grp.g[0].M : i == 1 ? grp.g[1].M : i == 2 ? grp.g[2].M
+                                                                                  : grp.g[3].M,
+                                BM);
+      const int gxi = (int)cdiv(i == 0 ? grp.g[0].N : i == 1 ? grp.g[1].N : i == 2 ? grp.g[2].N
+                                                                                  : grp.g[3].N,
+                                BN);
+      if (t >= gxi * gyi) {
+        t -= gxi * gyi;
+        ++z;
+      } else {
+        gy = gyi;
+      }
+    }
+  }
+  const GemmArgs a = select_problem(grp, z);
+  const int gx = (int)cdiv(a.N, BN);
+  const int run = (total + 7) >> 3;
+  int G = 1;
+  while ((G + 1) * (G + 1) <= run) ++G;
+  G = G < gy ? G : gy;
+  const int full = gy / G * G, band = G * gx;
+  int bx, by;
+  if (t < (full / G) * band) {
+    const int gb = t / band, tt = t - gb * band;
+    bx = tt / G;
+    by = gb * G + (tt - bx * G);
+  } else {
+    const int rem = gy - full, tt = t - (full / G) * band;
+    bx = tt / rem;
+    by = full + (tt - bx * rem);
+  }
+  gemm_x3p_tile<BM, BN, WM, WN, D, KT>(a, bx, by, smem);
+}
+
+template <int BM, int BN, int WM, int WN, int D>
+int launch_gemm_x3p_group(const GemmGroup& g, hipStream_t s) {
+  constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN));
+  int64_t tiles = 0;
+  bool kt = false;
+  for (int i = 0; i < g.n; ++i) {
+    tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM);
+    kt = kt || g.g[i].K % 16 != 0 || cdiv(g.g[i].K, 16) % D != 0;
+  }
+  if (tiles == 0) return MPR_OK;
+  if (kt)
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, true>), dim3((unsigned)tiles), dim3(NT),
+                       0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, false>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -1054,8 +1318,10 @@ namespace {
 // order whatever the block tile, so the tile may follow the launch (grouped or alone, one batch
 // or two concatenated: bit-identical results).
 enum GemmKind : int {
-  F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3, X3_SMALL = 4, X3_WIDE32 = 5
+  F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3, X3_SMALL = 4, X3_WIDE32 = 5,
+  X3P_WIDE = 6, X3P_SMALL = 7, X3P_SMALL3 = 8
 };
+
 
 const bool g_gemm_f32 = [] {
   const char* e = getenv("MPR_GEMM");
@@ -1088,6 +1354,9 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
       case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>(g, s);
       case X3_WIDE32: return launch_gemm_x3_group<128, 128, 2, 1, 32, 2, 1, 2>(g, s);
       case X3_SMALL: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>(g, s);
+      case X3P_WIDE: return launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s);
+      case X3P_SMALL: return launch_gemm_x3p_group<64, 64, 1, 1, 2>(g, s);
+      case X3P_SMALL3: return launch_gemm_x3p_group<64, 64, 1, 1, 3>(g, s);
       default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);
     }
   });
@@ -1143,7 +1412,8 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   GemmGroup fam;
   fam.n = 0;
   int64_t b128 = 0, b64x128 = 0;
-  bool short_k = true;
+  bool short_k = true, packed = true;
+  int max_n = 0, max_k = 0;
   for (int i = 0; i < g.n; ++i) {
     const GemmArgs& a = g.g[i];
     if (a.M == 0 || a.N == 0) continue;
@@ -1151,7 +1421,22 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
     b128 += cdiv(a.M, 128) * cdiv(a.N, 128) * a.batch;
     b64x128 += cdiv(a.M, 64) * cdiv(a.N, 128) * a.batch;
     short_k = short_k && a.K <= 512;
+    packed = packed && a.wp && a.batch == 1;
+    max_n = std::max(max_n, a.N);
+    max_k = std::max(max_k, a.K);
   }
+  // Every W of the launch packed (fixed model weights): W fragments straight from the packed
+  // image (tools/x3pbench.hip over the tower / T5-encoder shapes, bit-identical to the kernels
+  // below): 128x128 blocks of 8 waves for wide launches of > 160 of them (ViT qkv 1600x2304x768
+  // x2: 80.9 -> 73.5 us, fc1 110.7 -> 102.1, qkv at 800 rows 46.0 -> 41.4), else 64x64 blocks of
+  // 4 waves (ViT out 1600x768x768 x2: 38.7 -> 33.6, T5 qkv 1536x1536x512 27.6 -> 24.3), three
+  // k steps of W in flight at K >= 2048 (T5 wo 1536x512x2048: 44.2 -> 38.8, ViT fc2 at 800 rows
+  // 76.5 -> 77.1; fc2 1600x768x3072 x2 127.7 -> 113.0).
+  if (fam.n && packed)
+    return gemm_launch(fam, b128 > 160 && max_n >= 2048 ? X3P_WIDE
+                            : max_k >= 2048            ? X3P_SMALL3
+                                                       : X3P_SMALL,
+                       s);
   // A launch of <= 256 128x128 blocks (at most one per CU) takes 32-deep K tiles: 123 KB of LDS,
   // half the barriers per K, same k order (bit-identical).  Replayed alone equal (0.79-0.80 of
   // 157.3 either way); in the serving loop the GEMMs run 0.64 -> 0.68 (a CU holding one leaves no
@@ -1178,6 +1463,18 @@ int gemm(const GemmArgs& a, hipStream_t s) {
   g.g[0] = a;
   g.n = 1;
   return gemm_group(g, s);
+}
+
+int64_t packed_x3_bytes(int64_t N, int64_t K) { return cdiv(N, 32) * cdiv(K, 16) * 3 * 64 * 16; }
+
+int pack_x3(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, hipStream_t s) {
+  MPR_REQUIRE(N > 0 && K > 0 && ldw >= K && N < (1 << 30) && K < (1 << 30) && aligned16(out),
+              "pack_x3: bad shape N=%lld K=%lld", (long long)N, (long long)K);
+  const int64_t q = cdiv(N, 32) * cdiv(K, 16) * 64;
+  hipLaunchKernelGGL(pack_x3_kernel, dim3((unsigned)cdiv(q, 256)), dim3(256), 0, s, W, (int)N,
+                     (int)K, ldw, (int)cdiv(K, 16), reinterpret_cast<bf16x8*>(out));
+  MPR_LAUNCHED();
+  return MPR_OK;
 }
 
 int64_t packed_rows16_elems(int64_t N, int64_t K) { return cdiv(N, 16) * cdiv(K, 16) * 256; }

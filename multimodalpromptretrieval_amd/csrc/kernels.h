@@ -33,9 +33,16 @@ struct GemmArgs {
   // GEMM side by side in one launch.
   int batch = 1;
   int64_t a_bs = 0, w_bs = 0, cb_bs = 0;
+  // Optional packed split image of W (pack_x3): the split-bf16 kernel then loads its W operand
+  // fragments straight into registers instead of staging W through LDS (results identical).
+  const void* wp = nullptr;
 };
 
 int gemm(const GemmArgs& a, hipStream_t s);
+
+// The packed split image of a fixed W [N, K] for GemmArgs::wp (bytes, and the pack itself).
+int64_t packed_x3_bytes(int64_t N, int64_t K);
+int pack_x3(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, hipStream_t s);
 
 // Up to GEMM_GROUP independent problems in one launch (blockIdx.z picks the problem): the two
 // ViT-B/32 towers of a batch run their layer-l projections together, which doubles the blocks

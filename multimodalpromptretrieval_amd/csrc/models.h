@@ -33,7 +33,11 @@ namespace mpr {
 // One pre-LN residual attention block of the CLIP transformers (openai CLIP ResidualAttentionBlock).
 struct ClipBlock {
   DevBuf ln1_w, ln1_b, in_w, in_b, out_w, out_b, ln2_w, ln2_b, fc_w, fc_b, pj_w, pj_b;
+  DevBuf pk_in, pk_out, pk_fc, pk_pj;  // their pack_x3 images (the towers' weights are fixed)
 };
+
+// dst = the pack_x3 image of the fixed weight w [N, K] (legacy stream; the creating call syncs).
+int pack_weight(DevBuf& dst, const DevBuf& w, int64_t N, int64_t K);
 
 // Per-call scratch of one CLIP model (activations of its tower, patch/pooling buffers).  A model
 // holds TOWER_SLOTS of them: passes on different slots may be in flight at once (two batches'
@@ -76,6 +80,7 @@ struct VitModel : mpr_model {
   VitModel() : mpr_model(VIT) {}
   int width = 0, patch = 0, image = 0, out_dim = 0, grid = 0;
   DevBuf conv_w, cls, pos, lnpre_w, lnpre_b, lnpost_w, lnpost_b, projT;
+  DevBuf pk_conv, pk_projT;
   ClipTower tower;
   TowerWs ws[TOWER_SLOTS];
   int forward(const float* img, int B, int mode, float* out, int64_t out_bs, hipStream_t s);
@@ -85,6 +90,7 @@ struct TextModel : mpr_model {
   TextModel() : mpr_model(CLIP_TEXT) {}
   int width = 0, ctx = 0, vocab = 0, out_dim = 0;
   DevBuf tok_emb, pos, lnf_w, lnf_b, projT;
+  DevBuf pk_projT;
   ClipTower tower;
   TowerWs ws[TOWER_SLOTS];
   int forward(const int32_t* tok, int B, int L, float* out, int64_t out_bs, hipStream_t s);
@@ -118,6 +124,7 @@ struct T5Layer {
   //   W_ocq  = [[o | I_d], [cq diag(ln1) o | cq diag(ln1)]]     [d + inner, inner + d]
   //   W_cowi = [[co | I_d], [wi diag(ln2) co | wi diag(ln2)]]   [d + d_ff, inner + d]
   DevBuf pk_ocq, pk_cowi;
+  DevBuf xp_qkv, xp_o, xp_wi, xp_wo;       // encoder only: pack_x3 images (tiled GEMMs)
 };
 
 // Per-call workspace of generate(): activations, decode caches, captured graphs and the decode
@@ -200,6 +207,7 @@ struct T5Model : mpr_model {
   int build_folded(hipStream_t s);  // stream-ordered
   DevBuf rel_tmp;  // update scratch: a bias table
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
+  DevBuf xp_cross_kv;  // pack_x3 image of cross_kv_w
   DevBuf pk_lm_head;  // pack_rows16 image of lm_head (decode argmax head)
   // relative position bias by offset: tab[(key - query + lut_radius) * H + h]
   DevBuf enc_tab, dec_tab;

@@ -16,6 +16,7 @@
 // two hipGraphs (private capture stream): the encoder + cross K/V projection, replayed on the
 // caller's stream, and the decode loop (~50 launches per step), replayed on the decode stream when
 // one is set (a CU partition of its own) or else on the caller's stream.
+#include <chrono>
 #include <cstdlib>
 
 #include "models.h"
@@ -362,22 +363,23 @@ int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embe
   float* fp = ws->ff.as<float>();
   const bool merged = gemm_uniform_order();
   // one projection over rows [r0, r1) of the stacked batches
-  auto proj = [&](int64_t r0, int64_t r1, const float* A, int64_t lda, const float* W, int N,
-                  int K, const float* R, float* C, int act) {
+  auto proj = [&](int64_t r0, int64_t r1, const float* A, int64_t lda, const DevBuf& Wb,
+                  const DevBuf& Wp, int N, int K, const float* R, float* C, int act) {
     GemmArgs g;
-    g.A = A + r0 * lda; g.lda = lda; g.W = W; g.ldw = K;
+    g.A = A + r0 * lda; g.lda = lda; g.W = Wb.as<float>(); g.ldw = K; g.wp = Wp.ptr;
     g.R = R ? R + r0 * N : nullptr; g.ldr = N; g.C = C + r0 * N; g.ldc = N;
     g.M = (int)(r1 - r0); g.N = N; g.K = K; g.act = act;
     return g;
   };
-  auto run = [&](const float* A, int64_t lda, const float* W, int N, int K, const float* R,
-                 float* C, int act) -> int {
-    if (merged) return gemm(proj(0, M, A, lda, W, N, K, R, C, act), s);
+  auto run = [&](const float* A, int64_t lda, const DevBuf& W, const DevBuf& Wp, int N, int K,
+                 const float* R, float* C, int act) -> int {
+    if (merged) return gemm(proj(0, M, A, lda, W, Wp, N, K, R, C, act), s);
     for (int g0 = 0; g0 < n; g0 += GEMM_GROUP) {
       GemmGroup gg;
       gg.n = 0;
       for (int g = g0; g < std::min(n, g0 + GEMM_GROUP); ++g)
-        if (row0[g + 1] > row0[g]) gg.g[gg.n++] = proj(row0[g], row0[g + 1], A, lda, W, N, K, R, C, act);
+        if (row0[g + 1] > row0[g])
+          gg.g[gg.n++] = proj(row0[g], row0[g + 1], A, lda, W, Wp, N, K, R, C, act);
       if (gg.n) MPR_TRY(gemm_group(gg, s));
     }
     return MPR_OK;
@@ -386,7 +388,7 @@ int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embe
   for (auto& lp : enc) {
     const T5Layer& ly = *lp;
     MPR_TRY(rmsnorm(xp, d, (int)M, d, ly.ln0.as<float>(), T5_EPS, hp, d, s));
-    MPR_TRY(run(hp, d, ly.qkv.as<float>(), 3 * inner, d, nullptr, qp, ACT_NONE));
+    MPR_TRY(run(hp, d, ly.qkv, ly.xp_qkv, 3 * inner, d, nullptr, qp, ACT_NONE));
     for (int g0 = 0; g0 < n; g0 += ATTN_GROUP) {
       AttnGroup at;
       at.n = 0;
@@ -407,10 +409,10 @@ int T5Model::encode_multi(int n, const int* Bs, const int* Ls, const float* embe
       }
       if (at.n) MPR_TRY(attention_group(at, s));
     }
-    MPR_TRY(run(ap, inner, ly.o.as<float>(), d, inner, xp, xp, ACT_NONE));
+    MPR_TRY(run(ap, inner, ly.o, ly.xp_o, d, inner, xp, xp, ACT_NONE));
     MPR_TRY(rmsnorm(xp, d, (int)M, d, ly.ln1.as<float>(), T5_EPS, hp, d, s));
-    MPR_TRY(run(hp, d, ly.wi.as<float>(), dff, d, nullptr, fp, ACT_RELU));
-    MPR_TRY(run(fp, dff, ly.wo.as<float>(), d, dff, xp, xp, ACT_NONE));
+    MPR_TRY(run(hp, d, ly.wi, ly.xp_wi, dff, d, nullptr, fp, ACT_RELU));
+    MPR_TRY(run(fp, dff, ly.wo, ly.xp_wo, d, dff, xp, xp, ACT_NONE));
   }
   MPR_TRY(rmsnorm(xp, d, (int)M, d, enc_final.as<float>(), T5_EPS, out, d, s));
   return MPR_OK;
@@ -420,6 +422,7 @@ int T5Model::cross_kv_project(int B, int L, hipStream_t s) {
   const int M = B * L, N = Ld * 2 * inner;
   GemmArgs g;
   g.A = ws->enc_out.as<float>(); g.lda = d; g.W = cross_kv_w.as<float>(); g.ldw = d;
+  g.wp = xp_cross_kv.ptr;
   g.C = ws->cross_kv.as<float>(); g.ldc = N; g.M = M; g.N = N; g.K = d;
   return gemm(g, s);
 }
@@ -931,9 +934,11 @@ int T5Model::graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body) {
     if (!ws->cap_stream)
       MPR_HIP(hipStreamCreateWithFlags(&ws->cap_stream, hipStreamNonBlocking));
     hipGraph_t graph = nullptr;
+    const auto t_cap0 = std::chrono::steady_clock::now();
     MPR_HIP(hipStreamBeginCapture(ws->cap_stream, hipStreamCaptureModeThreadLocal));
     const int rc = body(ws->cap_stream);
     const hipError_t ec = hipStreamEndCapture(ws->cap_stream, &graph);
+    const auto t_cap1 = std::chrono::steady_clock::now();
     if (rc != MPR_OK) {
       if (graph) (void)hipGraphDestroy(graph);
       return rc;
@@ -943,6 +948,14 @@ int T5Model::graph_for(const GraphKey& key, hipGraphExec_t* out, F&& body) {
     const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     MPR_HIP(ei);
+    if (getenv("MPR_GRAPH_LOG")) {  // host cost of each capture
+      const auto t_ins = std::chrono::steady_clock::now();
+      fprintf(stderr, "[graph] key");
+      for (int v : key) fprintf(stderr, " %d", v);
+      fprintf(stderr, ": capture %.3f ms, instantiate %.3f ms\n",
+              std::chrono::duration<double, std::milli>(t_cap1 - t_cap0).count(),
+              std::chrono::duration<double, std::milli>(t_ins - t_cap1).count());
+    }
     it = graphs.emplace(key, T5Work::GraphEnt{exec, ws->gen}).first;
   }
   *out = it->second.exec;

@@ -644,6 +644,38 @@ int mpr_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, float
   });
 }
 
+int mpr_pack_x3_bytes(int64_t N, int64_t K, int64_t* bytes) {
+  return guarded_call([&]() -> int {
+    MPR_REQUIRE(N > 0 && K > 0 && bytes, "pack_x3_bytes: N=%lld K=%lld", (long long)N,
+                (long long)K);
+    *bytes = packed_x3_bytes(N, K);
+    return MPR_OK;
+  });
+}
+
+int mpr_pack_x3(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, int64_t out_bytes,
+                void* stream) {
+  return guarded_call([&]() -> int {
+    MPR_REQUIRE(W && out && out_bytes >= packed_x3_bytes(N, K),
+                "pack_x3: output of %lld bytes, %lld needed", (long long)out_bytes,
+                (long long)packed_x3_bytes(N, K));
+    return pack_x3(W, N, K, ldw, out, S(stream));
+  });
+}
+
+int mpr_gemm_f32_packed(const float* A, int64_t lda, const float* W, int64_t ldw, const void* wp,
+                        float* C, int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R,
+                        int64_t ldr, int32_t act, void* stream) {
+  return guarded_call([&]() -> int {
+    MPR_REQUIRE(act == ACT_NONE || act == ACT_RELU, "gemm: act %d (none or relu)", act);
+    MPR_REQUIRE(wp != nullptr, "gemm_packed: no packed image");
+    GemmArgs g;
+    g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.C = C; g.ldc = ldc; g.wp = wp;
+    g.M = M; g.N = N; g.K = K; g.R = R; g.ldr = ldr; g.act = act;
+    return gemm(g, S(stream));
+  });
+}
+
 int mpr_gemm_f32_many(int32_t n, const int64_t* desc, void* stream) {
   return guarded_call([&]() -> int {
     MPR_REQUIRE(n >= 0 && n <= 64 && (n == 0 || desc), "gemm_many: %d problems", n);

@@ -372,9 +372,10 @@ def test_coarse_scan_falls_back_on_a_dense_neighbourhood(device):
     assert 0 <= ix2.coarse_fallbacks() <= 1
 
 
-@pytest.mark.parametrize("k", [1, 3])
-def test_c2_full_size_end_to_end_vs_oracle(device, k):
-    """Config C2 (C3's k = 3 too) end to end at full size: a 6,500 x 1,024 index, two seeded
+@pytest.mark.parametrize("N,k", [(6500, 1), (6500, 3), (10000, 3)])
+def test_c2_full_size_end_to_end_vs_oracle(device, N, k):
+    """Config C2 (k = 1) and C3 (k = 3 over the combined SLAKE + VQA_RAD index, ~10,000 rows)
+    end to end at full size: a 6,500 (10,000) x 1,024 index, two seeded
     ViT-B/32 towers + CLIP text, t5-small, batches of 16 with real-algorithm tokenizers and host
     images — T5VisionModel.predict() and the retrieval prompts on the device against
     oracle/pipeline.py (torch-CPU fp32 restatement of the reference path, the CPU baseline's
@@ -383,7 +384,7 @@ def test_c2_full_size_end_to_end_vs_oracle(device, k):
     from multimodalpromptretrieval_amd.model import T5VisionModel
     from multimodalpromptretrieval_amd.tokenization import SpmT5Tokenizer, clip_tokenize
     from oracle import pipeline
-    N, D, B = 6500, 1024, 16
+    D, B = 1024, 16
     retr_sd, tok_sd, t5_sd = syn.clip_state_dict(1), syn.clip_state_dict(2), syn.t5_state_dict(3)
     X = syn.index_rows(4, N, D)
     answers = syn.answers(N, 50)

@@ -65,3 +65,36 @@ def test_splitk_residual_and_relu(device):
     got = _gemm(A.to(device), W.to(device), splits=4, R=R.to(device), act=2)
     ref = torch.relu(A.double() @ W.double().t()) + R.double()
     assert _rel(got, ref) < 1e-6
+
+
+def _packed(W):
+    N, K = W.shape
+    nb = _lib.c_int64()
+    _lib.call("mpr_pack_x3_bytes", N, K, _lib.ctypes.byref(nb))
+    img = torch.empty(nb.value, dtype=torch.uint8, device=W.device)
+    _lib.call("mpr_pack_x3", _lib.ptr(W), N, K, K, _lib.ptr(img), nb.value, _lib.stream_ptr())
+    return img
+
+
+@pytest.mark.parametrize("M,N,K,act,res", [
+    (1600, 2304, 768, 0, False),    # ViT qkv, two batches (128x128 packed tiles)
+    (1600, 768, 3072, 0, True),     # ViT fc2 + residual (64x64, three W steps in flight)
+    (1536, 1536, 512, 0, False),    # T5 encoder qkv (64x64)
+    (800, 3072, 768, 2, False),     # ViT fc1 shape, relu
+    (77, 200, 52, 0, True),         # ragged: N and K tails, K % 16 != 0
+    (1000, 1000, 1000, 2, True),    # odd tile counts
+])
+def test_packed_weight_gemm_is_bit_identical(device, M, N, K, act, res):
+    """mpr_gemm_f32_packed (W fragments from the pack_x3 image, no LDS staging of W) returns the
+    same bits as mpr_gemm_f32 on the same operands: the same split of W and the same summation
+    order of every output element."""
+    A, W = _operands(M, N, K, 7 * M + N + K)
+    Ad, Wd = A.to(device), W.to(device)
+    R = torch.randn(M, N, device=device) if res else None
+    ref = _gemm(Ad, Wd, R=R, act=act)
+    img = _packed(Wd)
+    C = torch.empty(M, N, device=device)
+    _lib.call("mpr_gemm_f32_packed", _lib.ptr(Ad), K, _lib.ptr(Wd), K, _lib.ptr(img), _lib.ptr(C),
+              N, M, N, K, _lib.ptr(R), N if R is not None else 0, act, _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(C, ref)
