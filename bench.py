@@ -870,6 +870,12 @@ def main():
                     model.predict(b)
 
     run(args.warmup, src=warm)
+    # The serving loop once more, untimed, at the timed step count over the warmup batches: the
+    # graphs of its decode-group shapes (rows x source-length bucket, one per generate slot) are
+    # captured here, as a long-running server has them after its first groups.  At W = 5 the
+    # warmup pass is one 5-batch group, so the timed run captured the 128-row and final-group
+    # decode graphs itself, ~1.3 ms of host time each (MPR_GRAPH_LOG=1).
+    run(args.steps, src=warm)
     run(args.warmup, pipelined=False, src=warm)
     run(args.warmup, pipelined=False, ahead=True, src=warm)
     run(args.warmup, main=True, src=warm)
@@ -938,9 +944,12 @@ def main():
                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
                         "traffic": traffic,
-                        "kernel": ("gemm_x3_kernel (fp32 product as 6 bf16 v_mfma_f32_32x32x16_bf16"
-                                   " partial products of a 3-way bf16 split; achieved/peak are fp32"
-                                   " algorithmic flops against the fp32 MFMA dense peak)" if x3 else
+                        "kernel": ("gemm_x3p_kernel (the towers' GEMMs: fp32 product as 6 bf16"
+                                   " v_mfma_f32_32x32x16_bf16 partial products of a 3-way bf16"
+                                   " split, the fixed weights pre-split into operand order and"
+                                   " loaded straight into registers; achieved/peak are fp32"
+                                   " algorithmic flops against the fp32 MFMA dense peak;"
+                                   " algorithmic bytes count fp32 operands)" if x3 else
                                    "gemm_f32_kernel (v_mfma_f32_32x32x2_f32 / 16x16x4)"),
                         "measured": "replay of the timed steps' launches back to back, one "
                                     "hipEvent pair around the replay",
@@ -988,7 +997,9 @@ def main():
             "pipelining": f"serving loop (predict_many): next batch's towers + scan enqueued "
                           f"ahead, {os.environ.get('MPR_DECODE_GROUP', '8')} batches per decode "
                           f"loop, {args.inflight} generate calls in flight; ramp-up and drain "
-                          f"inside the timed steps",
+                          f"inside the timed steps; warmup: {args.warmup} steps per leg plus one "
+                          f"untimed serving-loop pass of {args.steps} steps over the warmup "
+                          f"batches (decode-group graphs captured before timing)",
             "sync_ms_per_step": round(sync_ms, 3),
             "lookahead_ms_per_step": round(ahead_ms, 3),
             "main_loop_ms_per_step": round(main_ms, 3),

@@ -38,7 +38,7 @@ if [ -z "$SKIP_PROF" ]; then
   python tools/prof_summary.py --replay "$OUT/prof/run_kernel_trace.csv" "$OUT/replay_window.json" >> "$OUT/prof.log" 2>&1
   rm -f "$OUT/prof/run_kernel_trace.csv"  # summarised; the full trace of 80 steps is > 64 MiB
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_x3_kernel|gemm_f32_kernel|probe_marker_kernel" \
+    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "gemm_x3_kernel|gemm_x3p_kernel|gemm_f32_kernel|probe_marker_kernel" \
       -d "$OUT/pmc_$c" -o run --output-format csv \
       -- python bench.py --steps "$STEPS" --warmup 4 --no-cpu-baseline $LEAN > "$OUT/pmc_$c.log" 2>&1
     ok_or_stop $? pmc_$c 0

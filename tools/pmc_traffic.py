@@ -30,7 +30,7 @@ def per_dispatch(path, counter, by_class=None):
     if len(marks) < 2:
         raise SystemExit(f"{path}: no replay markers")
     lo, hi = marks[-2], marks[-1]
-    sel = [k for k in order if lo < k < hi and ("gemm_f32_kernel" in disp[k]["name"] or "gemm_x3_kernel" in disp[k]["name"])]
+    sel = [k for k in order if lo < k < hi and any(n in disp[k]["name"] for n in ("gemm_f32_kernel", "gemm_x3_kernel", "gemm_x3p_kernel"))]
     if by_class is not None:  # (kernel template, grid) -> [launches, counter sum]
         for k in sel:
             nm = disp[k]["name"]
@@ -48,7 +48,7 @@ def main():
     n = min(len(fetch), len(write))
     fk = sum(fetch) / len(fetch)
     wk = sum(write) / len(write)
-    out = {"kernel": "gemm_x3_kernel|gemm_f32_kernel", "window": "bench.py roofline replay (markers)",
+    out = {"kernel": "gemm_x3p_kernel|gemm_x3_kernel|gemm_f32_kernel", "window": "bench.py roofline replay (markers)",
            "launches": n, "fetch_size_kb_avg": round(fk, 1), "write_size_kb_avg": round(wk, 1),
            "traffic_bytes_per_launch": round((2.0 * fk + wk) * 1024.0),
            "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of 16 B/lane streaming "

@@ -18,7 +18,7 @@ def _rows(path):
     return rows
 
 
-def replay_window(rows, names=("gemm_x3_kernel", "gemm_f32_kernel"), marker="probe_marker_kernel"):
+def replay_window(rows, names=("gemm_x3_kernel", "gemm_x3p_kernel", "gemm_f32_kernel"), marker="probe_marker_kernel"):
     marks = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
     if len(marks) < 2:
         raise SystemExit("no replay markers in the trace (bench.py run without --no-probe?)")
@@ -30,7 +30,7 @@ def main():
     if sys.argv[1] == "--replay":
         rows = replay_window(_rows(sys.argv[2]))
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-        out = {"kernel": "gemm_x3_kernel|gemm_f32_kernel", "window": "bench.py roofline replay (markers)",
+        out = {"kernel": "gemm_x3p_kernel|gemm_x3_kernel|gemm_f32_kernel", "window": "bench.py roofline replay (markers)",
                "launches": len(durs), "avg_launch_us": round(sum(durs) / len(durs) / 1e3, 3),
                "total_ms": round(sum(durs) / 1e6, 4)}
         print(json.dumps(out))
