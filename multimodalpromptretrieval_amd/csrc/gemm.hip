@@ -648,7 +648,10 @@ int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
 // 128x128 kernel (profiles/r04_x3_lds_diag.txt): 80.6 -> 56.5 us (qkv 1600x2304x768 x2), 109.7
 // -> 77.4 (fc1): the LDS fragment traffic, not the MFMA issue, sets that kernel's pace.  Every
 // output element is accumulated in the same order with the same split terms as gemm_x3_tile
-// (W split by the same split3, per element): bit-identical results.
+// (W split by the same split3, per element): bit-identical results.  (Measured and dropped: W
+// kept as fp32 in the same operand order — 4 bytes per element instead of 6 — and split in
+// registers by each wave: 5-15 % slower than the planes, close to the LDS kernel again;
+// profiles/r04_x3p_f32frag_ab.txt.)
 __global__ __launch_bounds__(256) void pack_x3_kernel(const float* __restrict__ W, int N, int K,
                                                       int64_t ldw, int KS, bf16x8* __restrict__ out) {
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one (column tile, k step, lane)
@@ -1427,15 +1430,17 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   }
   // Every W of the launch packed (fixed model weights): W fragments straight from the packed
   // image (tools/x3pbench.hip over the tower / T5-encoder shapes, bit-identical to the kernels
-  // below): 128x128 blocks of 8 waves for wide launches of > 160 of them (ViT qkv 1600x2304x768
-  // x2: 80.9 -> 73.5 us, fc1 110.7 -> 102.1, qkv at 800 rows 46.0 -> 41.4), else 64x64 blocks of
-  // 4 waves (ViT out 1600x768x768 x2: 38.7 -> 33.6, T5 qkv 1536x1536x512 27.6 -> 24.3), three
-  // k steps of W in flight at K >= 2048 (T5 wo 1536x512x2048: 44.2 -> 38.8, ViT fc2 at 800 rows
-  // 76.5 -> 77.1; fc2 1600x768x3072 x2 127.7 -> 113.0).
+  // below): 128x128 blocks of 8 waves for launches of > 160 of them with a wide N or a long K
+  // (ViT qkv 1600x2304x768 x2: 80.9 -> 73.5 us, fc1 110.7 -> 102.1, qkv at 800 rows 46.0 ->
+  // 41.4, fc2 1600x768x3072 x2 127.7 -> 116.2), else 64x64 blocks of 4 waves (ViT out
+  // 1600x768x768 x2: 38.7 -> 33.6, T5 qkv 1536x1536x512 27.6 -> 24.3), three k steps of W in
+  // flight at K >= 2048 (T5 wo 1536x512x2048: 44.2 -> 38.8).  (The 64x64 tiles on the ViT fc2,
+  // 113.0 us alone, fetched 314 MB per launch from beyond L2 against ~120 MB for 128x128 tiles:
+  // r04_v2 PMC.)
   if (fam.n && packed)
-    return gemm_launch(fam, b128 > 160 && max_n >= 2048 ? X3P_WIDE
-                            : max_k >= 2048            ? X3P_SMALL3
-                                                       : X3P_SMALL,
+    return gemm_launch(fam, b128 > 160 && (max_n >= 2048 || max_k >= 2048) ? X3P_WIDE
+                            : max_k >= 2048                                 ? X3P_SMALL3
+                                                                            : X3P_SMALL,
                        s);
   // A launch of <= 256 128x128 blocks (at most one per CU) takes 32-deep K tiles: 123 KB of LDS,
   // half the barriers per K, same k order (bit-identical).  Replayed alone equal (0.79-0.80 of
