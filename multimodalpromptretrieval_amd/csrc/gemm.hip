@@ -1566,19 +1566,22 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
       // 128-row qkv ran in ~3 rounds of blocks).  Same chunk order per accumulator chain,
       // padding chunks add exact zeros: bit-identical.  C5 end to end 72.1-73.1 -> 68.4-69.3
       // ms per batch, the serving loop unchanged (3.69-3.71 ms per step either way).
-      // MPR_SKINNY_MAXC=8 (read per call) restores the 8-chunk slabs.
-      const char* mce = getenv("MPR_SKINNY_MAXC");
-      const bool c4 = !(mce && atoi(mce) == 8);
-      if (amax && tiles >= 1024 && per <= 4)
+      // Above 128 rows of a model with d >= 768 (C5's 256-row t5-base loop) the rows go in
+      // blocks of 64 (MR = 4, 2-chunk passes: 74 KB of slabs), halving the weight re-reads per
+      // step: t5-base 256 rows 1621 -> 1430 us per step, 192 rows 1490 -> 1331; at 128 rows
+      // (1055 -> 1200) and for t5-small (256 rows 514 -> 586) the 32-row blocks stay; 128-row
+      // blocks ran 2206 at 256 (tools/decode_rows.py, profiles/r04_skinny_rows_ab.txt).  Rows
+      // are independent and every chain keeps its chunk order: bit-identical.
+      if (!amax && a.M > 128 && std::min(a.N, a.K) >= 768) {
+        const unsigned g = (unsigned)cdiv(a.M, 64);
+        if (per <= 2) launch_skinny<2, 1, false, 4>(sa, F, (unsigned)tiles, s, g);
+        else launch_skinny<2, 1, true, 4>(sa, F, (unsigned)tiles, s, g);
+      } else if (amax && tiles >= 1024 && per <= 4)
         launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s, gy);
       else if (per <= 4)
         launch_skinny<4, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
-      else if (c4)
-        launch_skinny<4, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
-      else if (per <= 8)
-        launch_skinny<8, 1, false, 2>(sa, F, (unsigned)tiles, s, gy);
       else
-        launch_skinny<8, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
+        launch_skinny<4, 1, true, 2>(sa, F, (unsigned)tiles, s, gy);
     } else if (a.M > 16) {  // two row groups per weight load (2 batches of <= 16 rows)
       if (amax && tiles >= 1024 && per <= 4)
         launch_skinny<4, 2, false, 2>(sa, F, (unsigned)cdiv(tiles, 2), s);

@@ -565,19 +565,23 @@ def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
     assert torch.equal(got, want)
 
 
-def test_grouped_decode_skinny_maxc4_matches(device, t5_sd, monkeypatch):
-    """The grouped decode's 32-row GEMV blocks in 4-chunk passes (the default; t5-small's K = 2048
-    FFN-out here) sum every output in the 8-chunk kernel's order (MPR_SKINNY_MAXC=8): the greedy
-    tokens of 128 + 69 rows are equal."""
+def test_grouped_decode_row_blocks_match(device, monkeypatch):
+    """A t5-base decode loop of more than 128 rows runs its GEMVs on 64-row blocks (MR = 4,
+    2-chunk passes); the same rows decoded as loops of <= 128 rows (32-row blocks, 4-chunk
+    passes; MPR_GEN_PIECES=8) give the same greedy tokens bit for bit: rows are independent and
+    every accumulator chain keeps its chunk order."""
+    from multimodalpromptretrieval_amd import synthetic as syn
     from multimodalpromptretrieval_amd.t5 import DeviceT5
-    A = _t5_batch(t5_sd, 16, 75)
-    emb = torch.cat([A[0]] * 12 + [A[0][:5]])
-    emb = emb + 1e-3 * torch.randn(emb.shape, generator=torch.Generator().manual_seed(7))
-    fm = torch.cat([A[1]] * 12 + [A[1][:5]])
-    monkeypatch.setenv("MPR_SKINNY_MAXC", "8")
-    want = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
-    monkeypatch.delenv("MPR_SKINNY_MAXC", raising=False)
-    got = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
+    m = DeviceT5(syn.t5_state_dict(3, syn.T5_BASE), device)
+    g = torch.Generator().manual_seed(11)
+    rows, L = 200, 40
+    emb = torch.randn((rows, L, syn.T5_BASE.d_model), generator=g) * 0.3
+    mask = torch.ones((rows, L))
+    mask[1::3, 30:] = 0
+    monkeypatch.setenv("MPR_GEN_PIECES", "8")
+    want = m.generate_padded(emb.to(device), mask.to(device), 20).cpu()
+    monkeypatch.setenv("MPR_GEN_PIECES", "16")
+    got = m.generate_padded(emb.to(device), mask.to(device), 20).cpu()
     assert torch.equal(got, want)
 
 
