@@ -676,9 +676,9 @@ __global__ __launch_bounds__(256) void pack_x3_kernel(const float* __restrict__ 
   out[(t * 3 + 2) * 64 + lane] = h2;
 }
 
-template <int BM, int BN, int WM, int WN, int D, bool KT>
+template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16>
 __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
-  constexpr int BK = 16;
+  constexpr int NS = BK / 16;  // 16-deep MFMA steps per K tile
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
   constexpr int NT = 64 * WAVES_MN;
@@ -686,7 +686,7 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
   constexpr int LA = BM * KQ / NT;
   constexpr int PLANE = BM * LDK;   // bf16 per plane (A rows only)
   constexpr int STAGE = 3 * PLANE;
-  static_assert(LA >= 1 && LA * NT == BM * KQ, "loader split");
+  static_assert(LA >= 1 && LA * NT == BM * KQ && NS * 16 == BK, "loader split");
   __bf16* smem = reinterpret_cast<__bf16*>(smem_f);
   const int M = a.M, N = a.N, K = a.K;
   const int m0 = by * BM, n0 = bx * BN;
@@ -702,7 +702,7 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
 
   f32x4 ra[D][LA];
   bool oka[D][LA];
-  bf16x8 bq[D][WN][3];
+  bf16x8 bq[D][NS][WN][3];
   auto aload = [&](int j, int kt) {
     const int k0 = kt * BK;
 #pragma unroll
@@ -714,11 +714,14 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
     }
   };
   auto bload = [&](int j, int kt) {  // past the last k step: an in-range step (A is zero there)
-    const int ks = min(kt, KS - 1);
 #pragma unroll
-    for (int ni = 0; ni < WN; ++ni)
+    for (int s4 = 0; s4 < NS; ++s4) {
+      const int ks = min(kt * NS + s4, KS - 1);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bq[j][ni][p] = wpk[ni][((int64_t)ks * 3 + p) * 64];
+      for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bq[j][s4][ni][p] = wpk[ni][((int64_t)ks * 3 + p) * 64];
+    }
   };
   auto put = [&](__bf16* base, int row, int kc, const f32x4& v) {
     bf16x4 h0, h1, h2;
@@ -748,26 +751,29 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   const int li = lane & 31, lh = lane >> 5;
-  bf16x8 fa[WM][3], na[WM][3];
-  auto sread = [&](int st, bf16x8(&xa)[WM][3]) {
+  bf16x8 fa[NS][WM][3], na[NS][WM][3];
+  auto sread = [&](int st, bf16x8(&xa)[NS][WM][3]) {
     const __bf16* base = smem + st * STAGE;
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int s4 = 0; s4 < NS; ++s4)
 #pragma unroll
-      for (int mi = 0; mi < WM; ++mi)
-        xa[mi][p] = *reinterpret_cast<const bf16x8*>(base + p * PLANE +
-                                                     (wm * 32 * WM + mi * 32 + li) * LDK + 8 * lh);
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+          xa[s4][mi][p] = *reinterpret_cast<const bf16x8*>(
+              base + p * PLANE + (wm * 32 * WM + mi * 32 + li) * LDK + 16 * s4 + 8 * lh);
   };
-  // MFMA u of the step's WM * WN * 6 (u = (mi * WN + ni) * 6 + term), terms in gemm_x3_tile's
-  // order: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
-  constexpr int NMF = WM * WN * 6;
+  // MFMA u of the tile's NS * WM * WN * 6 (u = ((s4 * WM + mi) * WN + ni) * 6 + term: every
+  // accumulator takes its 16-deep steps in k order), terms in gemm_x3_tile's order: a2b0, a1b1,
+  // a0b2, a1b0, a0b1, a0b0
+  constexpr int NMF = NS * WM * WN * 6;
   auto mfmas = [&](int j, int u_lo, int u_hi) {
 #pragma unroll
     for (int u = u_lo; u < u_hi; ++u) {
-      const int term = u % 6, t = u / 6, ni = t % WN, mi = t / WN;
+      const int term = u % 6, t = u / 6, ni = t % WN, mi = (t / WN) % WM, s4 = t / (WN * WM);
       constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
-      acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PA[term]], bq[j][ni][PB[term]],
-                                                            acc[mi][ni], 0, 0, 0);
+      acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+          fa[s4][mi][PA[term]], bq[j][s4][ni][PB[term]], acc[mi][ni], 0, 0, 0);
     }
   };
 
@@ -807,9 +813,11 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
       bload(j, kt + j + D);
       __syncthreads();
 #pragma unroll
-      for (int mi = 0; mi < WM; ++mi)
+      for (int s4 = 0; s4 < NS; ++s4)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) fa[mi][p] = na[mi][p];
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) fa[s4][mi][p] = na[s4][mi][p];
     }
   }
 
@@ -840,10 +848,10 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
 }
 
 // gemm_x3_kernel's grid and tile order, the packed-W tile
-template <int BM, int BN, int WM, int WN, int D, bool KT>
+template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16>
 __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm_x3p_kernel(
     const GemmGroup grp) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * 3 * BM * (16 + 8) / 2];
+  __shared__ __attribute__((aligned(16))) float smem[2 * 3 * BM * (BK + 8) / 2];
   const int total = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
   int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
@@ -882,24 +890,24 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
     bx = tt / rem;
     by = full + (tt - bx * rem);
   }
-  gemm_x3p_tile<BM, BN, WM, WN, D, KT>(a, bx, by, smem);
+  gemm_x3p_tile<BM, BN, WM, WN, D, KT, BK>(a, bx, by, smem);
 }
 
-template <int BM, int BN, int WM, int WN, int D>
+template <int BM, int BN, int WM, int WN, int D, int BK = 16>
 int launch_gemm_x3p_group(const GemmGroup& g, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN));
   int64_t tiles = 0;
   bool kt = false;
   for (int i = 0; i < g.n; ++i) {
     tiles += cdiv(g.g[i].N, BN) * cdiv(g.g[i].M, BM);
-    kt = kt || g.g[i].K % 16 != 0 || cdiv(g.g[i].K, 16) % D != 0;
+    kt = kt || g.g[i].K % BK != 0 || cdiv(g.g[i].K, BK) % D != 0;
   }
   if (tiles == 0) return MPR_OK;
   if (kt)
-    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, true>), dim3((unsigned)tiles), dim3(NT),
-                       0, s, g);
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, true, BK>), dim3((unsigned)tiles),
+                       dim3(NT), 0, s, g);
   else
-    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, false>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, false, BK>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -1359,7 +1367,7 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
       case X3_SMALL: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>(g, s);
       case X3P_WIDE: return launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s);
       case X3P_SMALL: return launch_gemm_x3p_group<64, 64, 1, 1, 2>(g, s);
-      case X3P_SMALL3: return launch_gemm_x3p_group<64, 64, 1, 1, 3>(g, s);
+      case X3P_SMALL3: return launch_gemm_x3p_group<64, 64, 1, 1, 2, 32>(g, s);
       default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);
     }
   });
@@ -1433,8 +1441,9 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // below): 128x128 blocks of 8 waves for launches of > 160 of them with a wide N or a long K
   // (ViT qkv 1600x2304x768 x2: 80.9 -> 73.5 us, fc1 110.7 -> 102.1, qkv at 800 rows 46.0 ->
   // 41.4, fc2 1600x768x3072 x2 127.7 -> 116.2), else 64x64 blocks of 4 waves (ViT out
-  // 1600x768x768 x2: 38.7 -> 33.6, T5 qkv 1536x1536x512 27.6 -> 24.3), three k steps of W in
-  // flight at K >= 2048 (T5 wo 1536x512x2048: 44.2 -> 38.8).  (The 64x64 tiles on the ViT fc2,
+  // 1600x768x768 x2: 38.7 -> 33.6, T5 qkv 1536x1536x512 27.6 -> 24.3), 32-deep K tiles at
+  // K >= 2048 (T5 wo 1536x512x2048: 44.2 -> 36.4, ViT fc2 at 800 rows 76.5 -> 70.7; 32-deep
+  // tiles on the 128x128 blocks measured 5-15 % slower, profiles/r04_x3p_k32_ab.txt).  (The 64x64 tiles on the ViT fc2,
   // 113.0 us alone, fetched 314 MB per launch from beyond L2 against ~120 MB for 128x128 tiles:
   // r04_v2 PMC.)
   if (fam.n && packed)
