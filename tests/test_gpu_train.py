@@ -139,6 +139,15 @@ def test_adamw_steps_lower_the_loss_and_refresh_predict(device):
         assert abs(float(model(batch)) - losses[-1]) < losses[0]  # the updated weights serve
     after = model.predict(batch)
     assert isinstance(after, list) and len(after) == len(before)
+    # the in-place refresh after the optimizer steps (mpr_t5_update_async: copies, lane-order
+    # packs, folds and the encoder's split images) serves exactly what a model built from the
+    # updated weights serves
+    ref = _g2_model(device)
+    ref.load_state_dict(model.state_dict())
+    ref.eval()
+    with torch.no_grad():
+        assert float(ref(batch)) == float(model(batch))
+    assert ref.predict(batch) == after
 
 
 def test_g12_train_mode_dropout_gradients(device):
