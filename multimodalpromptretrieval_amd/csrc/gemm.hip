@@ -1579,7 +1579,8 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
       // blocks of 64 (MR = 4, 2-chunk passes: 74 KB of slabs), halving the weight re-reads per
       // step: t5-base 256 rows 1621 -> 1430 us per step, 192 rows 1490 -> 1331; at 128 rows
       // (1055 -> 1200) and for t5-small (256 rows 514 -> 586) the 32-row blocks stay; 128-row
-      // blocks ran 2206 at 256 (tools/decode_rows.py, profiles/r04_skinny_rows_ab.txt).  Rows
+      // blocks ran 2206 at 256, 48-row blocks 1712 vs 1479 (tools/decode_rows.py,
+      // profiles/r04_skinny_rows_ab.txt).  Rows
       // are independent and every chain keeps its chunk order: bit-identical.
       if (!amax && a.M > 128 && std::min(a.N, a.K) >= 768) {
         const unsigned g = (unsigned)cdiv(a.M, 64);
