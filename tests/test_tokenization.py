@@ -239,3 +239,12 @@ def test_t5_batch_decode_equals_per_row_decode():
         assert tok.batch_decode(seq, skip_special_tokens=True) == want
     assert tok.batch_decode(ids, skip_special_tokens=False) == \
         [tok.decode(r.tolist()) for r in ids]
+    # the per-id tables follow tokens added after a first batch decode (the new id takes the
+    # per-row path; unknown ids are special and dropped as decode() drops them)
+    tok.add_tokens(["[new]"])
+    new_id = max(tok.added_tokens_decoder)
+    ids[50:60, 5] = new_id
+    ids[60:70, 6] = 2
+    want = [tok.decode(r.tolist(), skip_special_tokens=True) for r in ids]
+    assert tok.batch_decode(ids, skip_special_tokens=True) == want
+    assert any("[new]" in w for w in want)
