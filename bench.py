@@ -153,15 +153,76 @@ AG_ALPHA_US = 20.0
 AG_BETA_GBS = 50.0
 
 
+def _projected_shard_class():
+    from multimodalpromptretrieval_amd.distributed import ShardedIndex
+
+    class ProjectedShard(ShardedIndex):
+        """One rank's shard of a W-rank row-sharded index, run on a world-1 RCCL group: the
+        product's ShardedIndex (local scan, pack, all_gather, merge) whose gathered candidate
+        lists are this shard's own top-k repeated for the W - 1 shards it stands in for (ids
+        offset by the shard size), so the merge reads W x k candidates per query as rank r of W
+        does.  Used by the one-GPU strong-scaling projection only."""
+
+        def __init__(self, rows, device, virtual_world: int, group=None):
+            super().__init__(rows, device, group=group, rows_are_local=True, row_offset=0)
+            self.virtual_world = int(virtual_world)
+            self._offs = None
+
+        def _candidates(self, recv, B: int, k: int):
+            cd, ci = super()._candidates(recv, B, k)
+            W = self.virtual_world
+            if W == 1:
+                return cd, ci
+            if self._offs is None or self._offs.shape[0] != W * k:
+                self._offs = (torch.arange(W, device=ci.device, dtype=torch.int64)
+                              .repeat_interleave(k) * self.n_local)
+            return cd.repeat(1, W).contiguous(), (ci.repeat(1, W) + self._offs).contiguous()
+
+    return ProjectedShard
+
+
+def _world1_group(device):
+    """A one-rank RCCL process group on this GPU (the projection's collectives are then real
+    RCCL calls).  Returns (group, created)."""
+    if dist.is_initialized():
+        return dist.group.WORLD, False
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=device)
+    return dist.group.WORLD, True
+
+
 def c5_projection(device, iters: int = 20):
     """Config C5's strong scaling, projected from one GPU: the exact per-rank
     work of W = 2, 4, 8 — the search of a 1,048,576 / W-row shard for all 256 queries (k = 5)
     and the merge of the W x 5 gathered candidates per query — timed here, plus a modelled RCCL
-    all_gather of the W x 256 x 5 packed (dist, id) float64 pairs."""
+    all_gather of the W x 256 x 5 packed (dist, id) float64 pairs.  The pipelined form runs the
+    product's ShardedIndex.search_all_many on a world-1 RCCL group (ProjectedShard: the merge
+    reads W x k candidates), timed with hipEvents on the caller's stream."""
     from multimodalpromptretrieval_amd.index import DeviceIndex, topk_merge
     n, d, B, k = C5["N"], C5["D"], C5["B"], C5["k"]
     gq = torch.Generator(device=device).manual_seed(8)
     q = torch.randn((B, d), device=device, generator=gq) * 0.3
+    group, created = _world1_group(device)
+    ProjectedShard = _projected_shard_class()
+
+    def timed_sharded(six):
+        """Per-batch time of ShardedIndex.search_all_many over `iters` batches back to back
+        (two in flight on its two streams); returns (us, ids of the last batch)."""
+        last = None
+        for rep in range(2):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for out in six.search_all_many((q for _ in range(iters if rep else 4)), k):
+                last = out
+            e1.record()
+            e1.synchronize()
+        return e0.elapsed_time(e1) / iters * 1e3, last[1]
 
     def timed(fn):
         for _ in range(3):
@@ -201,17 +262,20 @@ def c5_projection(device, iters: int = 20):
     t1 = t1_tp = None
     for W in (1, 2, 4, 8):
         rows = syn.index_rows_device(7, 0, n // W, d, device)
-        ix = DeviceIndex(rows, device)
-        del rows
-        t_search = timed(lambda: ix.search(q, k))
         if W == 1:
+            ix = DeviceIndex(rows, device)
+            del rows
+            t1 = timed(lambda: ix.search(q, k))
             t1_tp = timed_pipelined(lambda: ix.search(q, k))
             ix.close()
+            ix = None
             torch.cuda.empty_cache()
-            t1 = t_search
-            out["1"] = {"search_us": round(t_search, 1), "projected_us": round(t_search, 1),
+            out["1"] = {"search_us": round(t1, 1), "projected_us": round(t1, 1),
                         "pipelined_us": round(t1_tp, 1)}
             continue
+        six = ProjectedShard(rows, device, W, group)
+        del rows
+        ix = six._local
         dl, il = ix.search(q, k)
         cd = dl.repeat(1, W).contiguous()
         ci = (il.repeat(1, W) + torch.arange(W, device=device).repeat_interleave(k)
@@ -226,8 +290,10 @@ def c5_projection(device, iters: int = 20):
             diffs.append(timed(lambda: (ix.search(q, k), topk_merge(cd, ci, k))) - searches[-1])
         t_search = float(np.median(searches))
         t_merge = max(0.0, float(np.median(diffs)))
-        t_tp = timed_pipelined(lambda: (ix.search(q, k), topk_merge(cd, ci, k)))
-        ix.close()
+        # the product's pipelined sharded search (search_all_many on the RCCL group)
+        t_tp, ids_tp = timed_sharded(six)
+        same = bool(torch.equal(ids_tp, il))
+        six = ix = None
         torch.cuda.empty_cache()
         ag_bytes = W * B * k * 16
         t_ag = AG_ALPHA_US + ag_bytes / (AG_BETA_GBS * 1e3)
@@ -239,13 +305,80 @@ def c5_projection(device, iters: int = 20):
                        "speedup": round(t1 / tot, 2),
                        "pipelined_us": round(t_tp, 1),
                        "pipelined_projected_us": round(tot_tp, 1),
-                       "pipelined_speedup": round(t1_tp / tot_tp, 2)}
+                       "pipelined_speedup": round(t1_tp / tot_tp, 2),
+                       "pipelined_ids_equal_search": same}
+    if created:
+        dist.destroy_process_group()
     out["model"] = (f"per rank: the W-shard search (timed) + merge of W x {k} candidates (timed behind the "
                     f"search: the marginal GPU-timeline cost) + "
                     f"all_gather {AG_ALPHA_US} us + bytes / {AG_BETA_GBS} GB/s (modelled); "
-                    f"pipelined (ShardedIndex.search_all_many, two batches in flight): per batch "
-                    f"max(search + merge on two alternating streams, the all_gather model), "
-                    f"against the one-GPU search on two alternating streams")
+                    f"pipelined: ShardedIndex.search_all_many itself (two batches in flight on "
+                    f"its two streams, a real all_gather on a world-1 RCCL group, the merge of "
+                    f"W x {k} candidates per query), per batch max(that measured time, the "
+                    f"all_gather model), against the one-GPU DeviceIndex.search on two "
+                    f"alternating streams")
+    return out
+
+
+def c4_projection(device, iters: int = 50):
+    """Config C4's retrieval at W = 1, 2, 4, 8 GPUs, projected from one GPU (SURVEY.md §8(e),
+    BASELINE config 4: a 65,536 x 1,024 index row-sharded over the ranks, 16 questions per rank
+    per step, k = 5).  Per rank per step, ShardedIndex.search does: an all_gather of the ranks'
+    16-query blocks, the local scan of all 16 W queries over the 65,536 / W-row shard, an
+    all_to_all of the [16 W, 5] candidates back to their owners, and the merge of W x 5
+    candidates for its own 16 queries.  The scan and the merge are timed here on the exact
+    per-rank shapes (hipEvents, back to back); the two collectives are modelled (alpha + bytes /
+    beta each, as the C5 projection's all_gather).  Weak scaling: every rank serves its own 16
+    questions, so the aggregate rate is W x 16 / (per-rank time)."""
+    from multimodalpromptretrieval_amd.index import DeviceIndex, topk_merge
+    n, d, b, k = 65536, 1024, 16, 5
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters * 1e3  # us
+
+    out = {}
+    base = None
+    for W in (1, 2, 4, 8):
+        rows = syn.index_rows_device(11, 0, n // W, d, device)
+        ix = DeviceIndex(rows, device)
+        del rows
+        g = torch.Generator(device=device).manual_seed(12)
+        q = torch.randn((b * W, d), device=device, generator=g) * 0.3
+        t_scan = timed(lambda: ix.search(q, k))
+        ent = {"shard_rows": n // W, "queries_scanned": b * W, "search_us": round(t_scan, 1)}
+        tot = t_scan
+        if W > 1:
+            dl, il = ix.search(q[:b], k)
+            cd, ci = dl.repeat(1, W).contiguous(), il.repeat(1, W).contiguous()
+            t_both = timed(lambda: (ix.search(q, k), topk_merge(cd, ci, k)))
+            t_merge = max(0.0, t_both - t_scan)
+            ag = AG_ALPHA_US + W * (b + 1) * d * 4 / (AG_BETA_GBS * 1e3)
+            a2a = AG_ALPHA_US + W * b * k * 16 / (AG_BETA_GBS * 1e3)
+            tot = t_scan + t_merge + ag + a2a
+            ent.update({"merge_us": round(t_merge, 1), "all_gather_queries_us_model": round(ag, 1),
+                        "all_to_all_us_model": round(a2a, 1)})
+        ix.close()
+        ix = None
+        torch.cuda.empty_cache()
+        base = base or tot
+        ent.update({"per_rank_us": round(tot, 1),
+                    "retrieval_qa_pairs_per_s": round(W * b / (tot * 1e-6), 1),
+                    "aggregate_vs_1": round(W * base / tot, 2)})
+        out[str(W)] = ent
+    out["model"] = (f"per rank per step: the 65,536/W-row scan of 16 W queries + the merge of "
+                    f"W x {k} candidates (timed, the merge as its marginal GPU-timeline cost) + "
+                    f"all_gather of the query blocks + all_to_all of the candidates, each "
+                    f"{AG_ALPHA_US} us + bytes / {AG_BETA_GBS} GB/s (modelled); weak scaling "
+                    f"(16 questions per rank)")
     return out
 
 
@@ -717,11 +850,30 @@ def host_cpu():
     return model, len(cores) or None, len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(cfg, weights, batches, seconds: float, gpu_answers=None):
+def gpu_parity_outputs(model, retr, batches):
+    """Per batch, what the full-size parity check compares with the CPU oracle: predict()'s
+    answers, the retrieval prompts, the retrieved example ids (``return_info=["question_id"]``,
+    dataset/VQAFeatureDataset.py:202-210), the ``return_dists`` values (:242-245) and the device
+    query rows (to bound what the device / CPU tower difference can move)."""
+    out = []
+    with torch.no_grad():
+        for b in batches:
+            ids = [[int(s) for s in row]
+                   for row in retr.retrieve_closest_qa_pairs(b, return_info=["question_id"])]
+            dists = [d for _, d in retr.retrieve_closest_qa_pairs(b, return_dists=True)]
+            out.append({"answers": model.predict(b), "prompts": retr.retrieve_closest_qa_pairs(b),
+                        "ids": ids, "dists": dists, "query": retr.encode_queries(b).cpu()})
+    return out
+
+
+def cpu_baseline(cfg, weights, batches, seconds: float, gpu_out=None, serving_answers=None):
     """The CPU oracle pipeline (restated reference path, torch-CPU fp32) on a bounded sample of
-    the bench's own batches.  With ``gpu_answers`` (predict() on the same batches, same weights)
-    the CPU leg's prompts and answers double as a full-size C2 parity check (``parity``)."""
+    the bench's own batches.  With ``gpu_out`` (``gpu_parity_outputs`` on the same batches and
+    weights) the CPU leg doubles as a full-size C2 parity check (``parity``): retrieved ids,
+    distances, prompts and predict()'s answers; ``serving_answers`` are the answers the timed
+    serving loop itself produced for the same batches."""
     from oracle import pipeline
+    from oracle import retrieval as oret
     retr_sd, tok_sd, t5_sd, X, info = weights
     answers = syn.answers(cfg["N"], 50)
     tok = SpmT5Tokenizer()
@@ -734,10 +886,11 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_answers=None):
         while True:
             i = n % len(cpu_batches)
             b = cpu_batches[i]
+            trace = {}
             preds, prompts, _ = pipeline.predict(
                 b, retr_sd, tok_sd, t5_sd, heads, X, answers, info, cfg["k"], False,
-                clip_tokenize, tok, 20, forced_steps=True)
-            cpu_out.setdefault(i, (preds, prompts))
+                clip_tokenize, tok, 20, forced_steps=True, trace=trace)
+            cpu_out.setdefault(i, (preds, prompts, trace))
             n += 1
             el = time.perf_counter() - t0
             if el >= seconds or n >= 32:
@@ -752,20 +905,42 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_answers=None):
            "cores_note": "threads = this job's CPU share on the GPU box (OMP_NUM_THREADS, 16 per "
                          "GPU: the box's 8 GPUs' jobs share its physical cores; SURVEY.md §8(d) "
                          "asks for the available cores)"}
-    if gpu_answers is not None:
+    if gpu_out is not None:
         # forced steps keep finished rows on pad, as the device loop does: the decoded answers
         # compare as strings
-        n_pairs = n_prompt = n_ans = 0
-        for i, (preds, prompts) in cpu_out.items():
-            g_preds, g_prompts = gpu_answers[i]
+        n_pairs = n_prompt = n_ans = n_ids = n_loop = n_loop_pred = 0
+        dist_ok, margins, guards, dq = True, [], [], []
+        for i, (preds, prompts, trace) in cpu_out.items():
+            g = gpu_out[i]
             n_pairs += len(preds)
-            n_prompt += sum(a == b for a, b in zip(prompts, g_prompts))
-            n_ans += sum(a == b for a, b in zip(preds, g_preds))
-        out["parity"] = {"batches": len(cpu_out), "qa_pairs": n_pairs,
-                         "prompts_equal": n_prompt, "answers_equal": n_ans,
-                         "check": "CPU oracle vs GPU predict() on the same full-size C2 "
-                                  "batches and weights (prompts = retrieved ids, answers = "
-                                  "greedy tokens)"}
+            n_prompt += sum(a == b for a, b in zip(prompts, g["prompts"]))
+            n_ans += sum(a == b for a, b in zip(preds, g["answers"]))
+            par = oret.id_parity(g["ids"], g["dists"], g["query"], trace)
+            n_ids += par["ids_equal_rows"]
+            dist_ok &= par["dists_within_bound"]
+            margins.append(par["min_rel_margin"])
+            guards.append(par["min_margin_over_perturbation"])
+            dq.append(par["max_query_delta_rel"])
+            if serving_answers is not None and i < len(serving_answers):
+                n_loop += sum(a == b for a, b in zip(preds, serving_answers[i]))
+                n_loop_pred += sum(a == b for a, b in zip(g["answers"], serving_answers[i]))
+        out["parity"] = {
+            "batches": len(cpu_out), "qa_pairs": n_pairs,
+            "ids_equal": n_ids, "dists_within_bound": dist_ok,
+            "prompts_equal": n_prompt, "answers_equal": n_ans,
+            "serving_loop_answers_equal": n_loop if serving_answers is not None else None,
+            "serving_loop_equal_predict": n_loop_pred if serving_answers is not None else None,
+            "min_margin": min(margins), "min_margin_over_perturbation": min(guards),
+            "max_query_delta_rel": max(dq),
+            "check": "CPU oracle vs the GPU on the same full-size C2 batches and weights: "
+                     "retrieved example ids (return_info question_id) bit-exact per QA pair; "
+                     "return_dists within the cdist bound; prompts; predict()'s greedy answers; "
+                     "the answers the timed serving loop produced for these batches.  "
+                     "min_margin: smallest fp64 gap between rank k and rank k+1 squared "
+                     "distances / (|q|^2 + |x|^2) over the queries; "
+                     "min_margin_over_perturbation: that gap / twice what the device-vs-CPU "
+                     "query difference plus fp32 evaluation can move it (>= 1: equal ids are "
+                     "implied by the bound)"}
     return out
 
 
@@ -848,7 +1023,7 @@ def main():
         finally:
             retr.cache_enabled = False
 
-    def run(steps, pipelined=True, ahead=False, main=False, src=None):
+    def run(steps, pipelined=True, ahead=False, main=False, src=None, keep=None):
         # A step = one batch through encode -> retrieve -> prompt -> T5 generate.  The serving
         # loop keeps two batches in flight (T5VisionModel.predict_many): batch i+1's encoders
         # and scan run beside batch i's decode; each batch's work and answers are predict()'s.
@@ -860,10 +1035,13 @@ def main():
             if main:
                 main_loop(src[s % len(src)] for s in range(steps))
             elif pipelined:
-                # forced 20 decode steps (deterministic work per pair)
-                for _ in model.predict_many((src[s % len(src)] for s in range(steps)),
-                                            args.inflight, eos_stop=False):
-                    pass
+                # forced 20 decode steps (deterministic work per pair); `keep`
+                # holds the first batches' answers (a list append: the parity check's input)
+                for s, ans in enumerate(model.predict_many(
+                        (src[s % len(src)] for s in range(steps)), args.inflight,
+                        eos_stop=False)):
+                    if keep is not None and s < 4:
+                        keep.append(ans)
             else:
                 seq = (src[s % len(src)] for s in range(steps))
                 for b in (lookahead(seq, model) if ahead else seq):
@@ -882,7 +1060,8 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.steps)
+    timed_answers = []
+    run(args.steps, keep=timed_answers)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -971,20 +1150,19 @@ def main():
                     "avg_launch_us": round(ms_live * 1e3 / launches_live, 2)}
         barrier()
 
-    c5 = None
+    c5 = c4 = None
     if not args.no_c5:
         c5 = c5_scan(world, rank, device, group, rdev)
         if world == 1:
             c5["projection_1_to_8"] = c5_projection(device)
+            c4 = c4_projection(device)
         c5["end_to_end_t5_base"] = c5_serving(world, rank, device, group, rdev)
         barrier()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        with torch.no_grad():
-            gpu_answers = [(model.predict(b), retr.retrieve_closest_qa_pairs(b))
-                           for b in batches[:4]]
-        cpu = cpu_baseline(cfg, weights, batches[:4], args.cpu_seconds, gpu_answers)
+        gpu_out = gpu_parity_outputs(model, retr, batches[:4])
+        cpu = cpu_baseline(cfg, weights, batches[:4], args.cpu_seconds, gpu_out, timed_answers)
 
     if rank == 0:
         pairs = world * cfg["B"] * args.steps
@@ -1034,7 +1212,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "c5_scan": c5, "index_build": ib,
+            "c5_scan": c5, "c4_projection_1_to_8": c4, "index_build": ib,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(SL_NT) void select_large_kernel(const float* keys,
   uint64_t* items = sl_lds;                                 // [P]
   uint32_t* hist = reinterpret_cast<uint32_t*>(sl_lds + P);  // [256]
   __shared__ uint64_t s_prefix;
-  __shared__ uint32_t s_rem, s_count;
+  __shared__ uint32_t s_rem, s_count, s_all;
   const int q = blockIdx.x, tid = threadIdx.x;
   const float* kr = keys + (int64_t)q * n;
   const int64_t* ir = ids ? ids + (int64_t)q * n : nullptr;
@@ -187,9 +187,12 @@ __global__ __launch_bounds__(SL_NT) void select_large_kernel(const float* keys,
   if (tid == 0) {
     s_prefix = 0;
     s_rem = (uint32_t)k;
+    s_all = 0;
   }
   uint64_t mask = 0;
   for (int pass = 7; pass >= 0; --pass) {
+    __syncthreads();
+    if (s_all) break;  // fewer than k valid candidates (ids < 0 dropped): every one is kept
     for (int i = tid; i < 256; i += SL_NT) hist[i] = 0;
     __syncthreads();
     const uint64_t prefix = s_prefix;
@@ -207,8 +210,13 @@ __global__ __launch_bounds__(SL_NT) void select_large_kernel(const float* keys,
         if (cum + hist[dgt] >= rem) break;
         cum += hist[dgt];
       }
-      s_rem = rem - cum;
-      s_prefix = prefix | ((uint64_t)dgt << sh);
+      if (dgt == 256) {  // only reachable in the first pass: fewer than k valid words in all
+        s_all = 1;
+        s_prefix = ~0ull;
+      } else {
+        s_rem = rem - cum;
+        s_prefix = prefix | ((uint64_t)dgt << sh);
+      }
     }
     mask |= (uint64_t)255 << sh;
     __syncthreads();
@@ -239,10 +247,11 @@ __global__ __launch_bounds__(SL_NT) void select_large_kernel(const float* keys,
       __syncthreads();
     }
   }
-  for (int t = tid; t < k; t += SL_NT) {
+  for (int t = tid; t < k; t += SL_NT) {  // ranks past the valid candidates: NaN / -1 (as merge)
     const uint64_t w = items[t];
-    out_val[(int64_t)q * k + t] = sign * word_key(w);
-    out_id[(int64_t)q * k + t] = (int64_t)(uint32_t)w + (ir ? 0 : id_offset);
+    const bool none = w == ~0ull;
+    out_val[(int64_t)q * k + t] = none ? NAN : sign * word_key(w);
+    out_id[(int64_t)q * k + t] = none ? -1 : (int64_t)(uint32_t)w + (ir ? 0 : id_offset);
   }
 }
 

@@ -179,10 +179,16 @@ class ShardedIndex:
         recv = torch.empty((self.world * B,) + tuple(packed.shape[1:]), dtype=packed.dtype,
                            device=packed.device)
         dist.all_gather_into_tensor(recv, packed, group=self.group)
-        d_all, i_all = self._unpack(recv.to(self.device).view(self.world, B, k, 2))  # [W, B, k]
+        cd, ci = self._candidates(recv.to(self.device), B, k)
+        return self._merge(cd, ci, k)
+
+    def _candidates(self, recv, B: int, k: int):
+        """The all_gathered per-shard top-k [W * B, k, 2] as the merge's candidate lists:
+        (dist [B, W * k], ids [B, W * k]), shard-major within a query's list."""
+        d_all, i_all = self._unpack(recv.view(self.world, B, k, 2))  # [W, B, k]
         cd = d_all.permute(1, 0, 2).reshape(B, self.world * k)
         ci = i_all.permute(1, 0, 2).reshape(B, self.world * k)
-        return self._merge(cd.contiguous(), ci.contiguous(), k)
+        return cd.contiguous(), ci.contiguous()
 
     def search_all_many(self, queries, k: int):
         """search_all over an iterable of query batches (the same batches on every rank) as a
@@ -204,6 +210,9 @@ class ShardedIndex:
             with torch.cuda.stream(st):
                 B = q.shape[0]
                 q = q.to(self.device, torch.float32).contiguous()
+                # q may be the caller's own tensor (allocated on `cur`): once the caller drops
+                # it after the yield, its memory must not be reused while this scan reads it
+                q.record_stream(st)
                 packed = self._pack(*self._padded_search(q, k))
                 recv = torch.empty((self.world * B,) + tuple(packed.shape[1:]),
                                    dtype=packed.dtype, device=self.device)
@@ -226,10 +235,7 @@ class ShardedIndex:
         st, B, recv, work = pend
         with torch.cuda.stream(st):
             work.wait()
-            d_all, i_all = self._unpack(recv.view(self.world, B, k, 2))
-            cd = d_all.permute(1, 0, 2).reshape(B, self.world * k)
-            ci = i_all.permute(1, 0, 2).reshape(B, self.world * k)
-            out = self._merge(cd.contiguous(), ci.contiguous(), k)
+            out = self._merge(*self._candidates(recv, B, k), k)
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(st)
         for t in out:

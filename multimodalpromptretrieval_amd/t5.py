@@ -160,6 +160,10 @@ class DeviceT5:
             _lib.call("mpr_t5_update_async", self._h, _lib.tensor_array(host), len(host),
                       _lib.c_void_p(cur.cuda_stream))
             self._seen[cur.cuda_stream] = cur
+            # later work of this handle on any other stream waits for the refresh (_stream)
+            self._refresh = torch.cuda.Event()
+            self._refresh.record(cur)
+            self._refresh_waited = {cur.cuda_stream}
         else:
             _lib.call("mpr_t5_update", self._h, _lib.tensor_array(host), len(host), enc_lut,
                       dec_lut)
@@ -177,9 +181,14 @@ class DeviceT5:
             pass
 
     def _stream(self):
-        # streams this handle's work was enqueued on: update() orders itself after them
+        # streams this handle's work was enqueued on: update() orders itself after them, and
+        # each of them waits (once) for the newest asynchronous refresh before its next call
         st = torch.cuda.current_stream(self.device)
         self._seen[st.cuda_stream] = st
+        ev = getattr(self, "_refresh", None)
+        if ev is not None and st.cuda_stream not in self._refresh_waited:
+            st.wait_event(ev)
+            self._refresh_waited.add(st.cuda_stream)
         return _lib.c_void_p(st.cuda_stream)
 
     def set_decode_stream(self, stream=None, slot: int = 0):

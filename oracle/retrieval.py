@@ -64,6 +64,70 @@ def retrieve_closest_qa_pairs(query: torch.Tensor, index: torch.Tensor, answers:
     return prompts
 
 
+def smallest_dists(query: torch.Tensor, index: torch.Tensor, k: int) -> torch.Tensor:
+    """dataset/VQAFeatureDataset.py:242-245 — the `return_dists` values: the k smallest cdist
+    entries per row, [B, k] fp32 (the training phase does not skip the self match here)."""
+    return torch.sort(cdist(query, index), dim=1).values[:, 0:k]
+
+
+def rank_margins(query: torch.Tensor, index: torch.Tensor, k: int, skip_first: bool):
+    """SURVEY.md §7 hard part (i): per query, the fp64 squared-distance gap between the last
+    retrieved rank and the first one left out (ranks s+k-1 and s+k, s = 1 in the training
+    phase), absolute and relative to |q|^2 + |x|^2 of those rows.  A retrieved-id set can only
+    change under a perturbation of the query or of the summation order that moves a squared
+    distance by more than half that gap.  Returns (gap [B], rel_gap [B], fp64 |q - x_last| [B]);
+    inf where the index has no row past the retrieved ones."""
+    qd, xd = query.double(), index.double()
+    d2 = (qd * qd).sum(1, keepdim=True) + (xd * xd).sum(1)[None, :] - 2.0 * qd @ xd.T
+    s = 1 if skip_first else 0
+    last = s + k - 1
+    B, n = d2.shape
+    if last + 1 >= n:
+        inf = torch.full((B,), float("inf"), dtype=torch.float64)
+        return inf, inf, d2.clamp(min=0).sqrt().max(1).values
+    v, i = torch.topk(d2, last + 2, dim=1, largest=False, sorted=True)
+    gap = v[:, last + 1] - v[:, last]
+    scale = (qd * qd).sum(1) + (xd * xd).sum(1)[i[:, last]]
+    return gap, gap / scale, v[:, last].clamp(min=0).sqrt()
+
+
+def id_parity(ids, dists, query, trace: dict) -> dict:
+    """Checker for a device retrieval against ``pipeline.predict(..., trace=...)`` on the same
+    batch: ``ids`` [B, k] (the retrieved example ids, e.g. ``return_info=["question_id"]``),
+    ``dists`` [B, k] (``return_dists``), ``query`` [B, D] the device's query rows.
+
+    The device query comes from fp32-accurate device towers, the oracle's from torch-CPU fp32,
+    so the two differ by |dq| (measured here).  Squared distances then differ by at most
+    2|dq|·|q - x| + |dq|^2 plus the mm-path evaluation error 2e-6·(|q|^2 + |x|^2) (§4 of
+    DESIGN.md), and a retrieved id can differ only where the fp64 rank margin (``rank_margins``)
+    is below twice that.  Returns counts and the worst margins (plain Python values)."""
+    ids = torch.as_tensor(np.asarray(ids), dtype=torch.int64)
+    got = torch.as_tensor(np.asarray(dists), dtype=torch.float64)
+    want_ids, want = trace["ids"].to(torch.int64), trace["dists"].double()
+    qo = trace["query"].double()
+    dq = (torch.as_tensor(query).double().cpu() - qo).norm(dim=1)          # [B]
+    qn = (qo * qo).sum(1)
+    d_last = trace["d_last"]
+    gap = trace["gap"]
+    d_next = torch.where(torch.isfinite(gap), (d_last * d_last + gap).sqrt(), d_last)
+    pert = 2.0 * dq * d_next + dq * dq                  # [B]: |d2(q + dq) - d2(q)|, any kept row
+    scale = qn + (qn.sqrt() + d_next) ** 2               # >= |q|^2 + |x|^2, ranks 1 .. k+1
+    tol2 = 2e-6 * scale + pert
+    derr = (got * got - want * want).abs().amax(1)
+    rows_equal = (ids == want_ids).all(1)
+    # >= 1: the rank k / k+1 gap exceeds what both the query difference and the two sides'
+    # fp32 evaluation errors can move, so equal ids are implied, not luck
+    guard = gap / (2.0 * (pert + 2e-6 * scale))
+    return {"rows": int(ids.shape[0]), "ids_equal_rows": int(rows_equal.sum()),
+            "ids_equal": bool(rows_equal.all()),
+            "dists_within_bound": bool((derr <= tol2).all()),
+            "max_dist2_err_over_bound": float((derr / tol2).max()),
+            "max_query_delta": float(dq.max()),
+            "max_query_delta_rel": float((dq / qn.sqrt()).max()),
+            "min_rel_margin": float(trace["rel_gap"].min()),
+            "min_margin_over_perturbation": float(guard.min())}
+
+
 def cosine_similarity(x1: torch.Tensor, x2: torch.Tensor, dim: int = 1, eps: float = 1e-8):
     """utils.py:57-62."""
     w12 = torch.sum(x1 * x2, dim)

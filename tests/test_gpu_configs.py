@@ -379,11 +379,17 @@ def test_c2_full_size_end_to_end_vs_oracle(device, N, k):
     ViT-B/32 towers + CLIP text, t5-small, batches of 16 with real-algorithm tokenizers and host
     images — T5VisionModel.predict() and the retrieval prompts on the device against
     oracle/pipeline.py (torch-CPU fp32 restatement of the reference path, the CPU baseline's
-    code) on the same weights and batches: retrieved prompts and greedy answers equal."""
+    code) on the same weights and batches: the retrieved example ids (``return_info=
+    ["question_id"]``, dataset/VQAFeatureDataset.py:202-210) bit-exact, the ``return_dists``
+    values within the cdist bound, prompts and greedy answers equal — for predict() and for the
+    serving loop (predict_many, the path the headline times).  The fp64 rank-k / rank-k+1
+    margin of every query is reported against what the device / CPU query difference can move
+    (SURVEY.md §7 hard part (i))."""
     from multimodalpromptretrieval_amd.dataset import VQARetrieval
     from multimodalpromptretrieval_amd.model import T5VisionModel
     from multimodalpromptretrieval_amd.tokenization import SpmT5Tokenizer, clip_tokenize
     from oracle import pipeline
+    from oracle import retrieval as oret
     D, B = 1024, 16
     retr_sd, tok_sd, t5_sd = syn.clip_state_dict(1), syn.clip_state_dict(2), syn.t5_state_dict(3)
     X = syn.index_rows(4, N, D)
@@ -400,6 +406,7 @@ def test_c2_full_size_end_to_end_vs_oracle(device, N, k):
              "abnormal", "scan", "where", "does", "it", "appear", "brain", "chest", "liver"]
     ref_tok = SpmT5Tokenizer()
     ref_tok.add_tokens(["[itk]"])
+    batches, want = [], []
     for bi in range(2):
         batch = {"image": syn.images(900 + bi, B),
                  "question": [" ".join(rng.choice(words, size=int(rng.integers(5, 14)))) + "?"
@@ -407,11 +414,27 @@ def test_c2_full_size_end_to_end_vs_oracle(device, N, k):
                  "task": ["vqa"] * B, "answer": ["yes"] * B,
                  "question_id": [str(bi * B + j) for j in range(B)],
                  "question_type": ["open"] * B}
+        trace = {}
         with torch.no_grad():
             got = model.predict(batch)
             got_prompts = retr.retrieve_closest_qa_pairs(batch)
+            got_ids = [[int(s) for s in row]
+                       for row in retr.retrieve_closest_qa_pairs(batch, return_info=["question_id"])]
+            got_dists = [d for _, d in retr.retrieve_closest_qa_pairs(batch, return_dists=True)]
+            q_dev = retr.encode_queries(batch).cpu()
             preds, prompts, _ = pipeline.predict(
                 batch, retr_sd, tok_sd, t5_sd, 8, X, answers, info, k, False, clip_tokenize,
-                ref_tok, 20, forced_steps=True)
+                ref_tok, 20, forced_steps=True, trace=trace)
+        par = oret.id_parity(got_ids, got_dists, q_dev, trace)
+        print(f"batch {bi}: {par}")
+        assert par["ids_equal"], f"batch {bi}: retrieved ids differ: {got_ids} vs {trace['ids']}"
+        assert par["dists_within_bound"], f"batch {bi}: return_dists outside the bound: {par}"
         assert got_prompts == prompts, f"batch {bi}: retrieved prompts differ"
         assert got == preds, f"batch {bi}: greedy answers differ"
+        batches.append(batch)
+        want.append(preds)
+    # the serving loop (T5VisionModel.predict_many: grouped towers and decodes) on fresh batch
+    # objects: the same answers as the oracle's
+    fresh = [dict(b, image=b["image"].view_as(b["image"])) for b in batches]
+    with torch.no_grad():
+        assert list(model.predict_many(fresh, eos_stop=False)) == want

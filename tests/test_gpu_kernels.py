@@ -137,6 +137,29 @@ def test_topk_merge_shards(device, index_mod):
     assert torch.equal(ids.cpu(), ref_ids)
 
 
+@pytest.mark.parametrize("k", [5, 100])
+def test_topk_merge_fewer_valid_than_k(device, index_mod, k):
+    """Candidate lists whose valid entries (id >= 0) number fewer than k (tiny shards pad with
+    -1 sentinels): the valid ones come first in order, the remaining ranks are NaN / -1 — for
+    the wave merge (k <= 64) and the radix select (k > 64)."""
+    g = torch.Generator().manual_seed(3)
+    b, n = 6, 160
+    cd = torch.rand((b, n), generator=g)
+    ci = torch.arange(n, dtype=torch.int64).repeat(b, 1)
+    nvalid = [0, 1, 3, k - 1, min(k, n), n][:b]
+    for r, nv in enumerate(nvalid):
+        ci[r, nv:] = -1
+        cd[r, nv:] = float("inf")
+    d, ids = index_mod.topk_merge(cd.to(device), ci.to(device), k)
+    d, ids = d.cpu(), ids.cpu()
+    for r, nv in enumerate(nvalid):
+        m = min(nv, k)
+        order = torch.argsort(cd[r, :nv], stable=True)[:m]
+        assert torch.equal(ids[r, :m], order), r
+        assert torch.equal(d[r, :m], cd[r, order]), r
+        assert bool((ids[r, m:] == -1).all()) and bool(torch.isnan(d[r, m:]).all()), r
+
+
 @pytest.fixture(scope="module")
 def clip_sd():
     return syn.clip_state_dict(11)

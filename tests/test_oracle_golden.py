@@ -59,6 +59,33 @@ def test_g1_retrieval_oracle(case_idx):
                                rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("case_idx", [0, 5, 11])
+def test_id_parity_checker_on_g1(case_idx):
+    """The full-size id checker (oracle.retrieval.id_parity): the G1 ids / dists the reference
+    returned pass it against the oracle's trace; a swapped id, a perturbed distance fail; the
+    rank margins are the fp64 gaps at rank k / k+1."""
+    case = _g1()["cases"][case_idx]
+    N, D, k, tr = case["N"], case["D"], case["k"], case["training"]
+    X, q, _ = gi.g1_queries(N, D, case["seed"])
+    trace = {"query": q, "ids": oret.topk_ids(oret.cdist(q, X), k, tr),
+             "dists": oret.smallest_dists(q, X, k)}
+    trace["gap"], trace["rel_gap"], trace["d_last"] = oret.rank_margins(q, X, k, tr)
+    par = oret.id_parity(case["ids"], case["dists"], q, trace)
+    assert par["ids_equal"] and par["dists_within_bound"]
+    assert par["max_query_delta"] == 0.0
+    assert (trace["gap"] >= 0).all()
+    d2 = ((q.double()[:, None, :] - X.double()[None]) ** 2).sum(-1)
+    srt = d2.sort(1).values
+    s = 1 if tr else 0
+    torch.testing.assert_close(trace["gap"], srt[:, s + k] - srt[:, s + k - 1], rtol=1e-9,
+                               atol=1e-9)
+    bad = [list(r) for r in case["ids"]]
+    bad[0][0] = (bad[0][0] + 1) % N
+    assert oret.id_parity(bad, case["dists"], q, trace)["ids_equal_rows"] == len(bad) - 1
+    far = np.array(case["dists"]) * 1.01
+    assert not oret.id_parity(case["ids"], far, q, trace)["dists_within_bound"]
+
+
 def test_g1_ties_oracle():
     Xt, qt = gi.tie_index()
     ans = syn.answers(300, 5)
