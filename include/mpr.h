@@ -359,6 +359,11 @@ int mpr_t5_train_backward(mpr_model* trainer, int32_t tape, const float* const* 
                           const int32_t* emb_pos, int32_t n_uniq, float* const* grads,
                           float* d_emb, void* stream);
 int mpr_t5_train_release(mpr_model* trainer, int32_t tape);
+/* Give device memory back: after the work queued on `stream` completes, the arenas of released
+ * tapes past the first `keep_idle` are freed (and the backward's scratch when keep_idle == 0);
+ * later forwards re-grow them.  train.trim_trainers() calls it (e.g. after a large validation
+ * batch).  The trainer itself goes with mpr_model_destroy. */
+int mpr_t5_trainer_trim(mpr_model* trainer, int32_t keep_idle, void* stream);
 int mpr_gemm_f32_splitk(const float* A, int64_t lda, const float* W, int64_t ldw, float* C,
                         int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr,
                         int32_t act, int32_t splits, float* partial, void* stream);

@@ -104,6 +104,7 @@ SIGNATURES = [
                                         c_float, c_void_p, c_void_p, c_void_p, c_int32,
                                         POINTER(c_void_p), c_void_p, c_void_p]),
     ("mpr_t5_train_release", c_int32, [c_void_p, c_int32]),
+    ("mpr_t5_trainer_trim", c_int32, [c_void_p, c_int32, c_void_p]),
     ("mpr_gemm_f32_splitk", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                       c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
                                       c_int32, c_void_p, c_void_p]),

@@ -136,9 +136,37 @@ struct T5Trainer : mpr_model {
   int d = 0, dkv = 0, H = 0, dff = 0, Le = 0, Ld = 0, V = 0, nb = 0, scale_out = 1, inner = 0;
   int radius = 0;
   DevBuf enc_lut, dec_lut;  // bucket of offset r - radius, r in [0, 2 radius]
+  std::vector<int32_t> enc_lut_h, dec_lut_h;  // host copies (grown on demand, grow_luts)
   std::vector<std::unique_ptr<Tape>> tapes;
   Arena scratch;  // the backward's temporaries
   hipStream_t s = nullptr;
+
+  // Relative positions beyond the LUT radius: T5's buckets saturate past max_distance (every
+  // |offset| >= max_distance of one sign shares the last bucket of that sign,
+  // modeling_t5.py _relative_position_bucket), so the tables extend exactly by repeating their
+  // end entries (checked at create: radius >= max_distance there).  Tapes recorded before a
+  // growth stay valid: both tables stay centred on offset 0.
+  int grow_luts(int R) {
+    const int R2 = std::max(R, 2 * radius);
+    const size_t nr = 2 * (size_t)R2 + 1, pad = (size_t)(R2 - radius);
+    for (auto* h : {&enc_lut_h, &dec_lut_h}) {
+      std::vector<int32_t> g(nr);
+      for (size_t i = 0; i < nr; ++i) {
+        const size_t j = i < pad ? 0 : std::min(i - pad, h->size() - 1);
+        g[i] = (*h)[j];
+      }
+      h->swap(g);
+    }
+    MPR_HIP(hipStreamSynchronize(s));  // the old tables may be read by queued work
+    enc_lut.release();
+    dec_lut.release();
+    MPR_TRY(enc_lut.ensure(nr * 4));
+    MPR_TRY(dec_lut.ensure(nr * 4));
+    MPR_HIP(hipMemcpy(enc_lut.ptr, enc_lut_h.data(), nr * 4, hipMemcpyHostToDevice));
+    MPR_HIP(hipMemcpy(dec_lut.ptr, dec_lut_h.data(), nr * 4, hipMemcpyHostToDevice));
+    radius = R2;
+    return MPR_OK;
+  }
   int nparams() const { return 5 + 8 * Le + 13 * Ld; }
 
   // parameter order of train.py t5_param_names
@@ -270,8 +298,7 @@ int T5Trainer::forward(Tape& tp, const float* emb, const float* mask, const int3
   tp.labels = labels;
   tp.Re = std::max(L, 1);
   tp.Rd = std::max(T, 1);
-  MPR_REQUIRE(tp.Re <= radius && tp.Rd <= radius, "trainer: L=%d / T=%d beyond the lut radius %d",
-              L, T, radius);
+  if (std::max(tp.Re, tp.Rd) > radius) MPR_TRY(grow_luts(std::max(tp.Re, tp.Rd)));
   TR_GET(rel_e, (int64_t)(2 * tp.Re + 1) * H);
   TR_GET(rel_d, (int64_t)(2 * tp.Rd + 1) * H);
   MPR_TRY(mpr_rel_gather(enc_rel(), enc_lut.as<int32_t>() + (radius - tp.Re), tp.Re, H, rel_e, s));
@@ -645,6 +672,13 @@ int mpr_t5_trainer_create(const int32_t* cfg, int32_t n_cfg, const int32_t* enc_
     for (const int32_t* lut : {enc_lut, dec_lut})
       for (size_t r = 0; r < nr; ++r)
         MPR_REQUIRE(lut[r] >= 0 && lut[r] < t->nb, "trainer_create: lut bucket %d", lut[r]);
+    // the tables must have reached their saturated buckets at both ends (grow_luts extends them
+    // by repetition): true whenever radius >= max_distance
+    for (const int32_t* lut : {enc_lut, dec_lut})
+      MPR_REQUIRE(radius < 2 || (lut[0] == lut[1] && lut[nr - 1] == lut[nr - 2]),
+                  "trainer_create: the lut of radius %d does not saturate at its ends", radius);
+    t->enc_lut_h.assign(enc_lut, enc_lut + nr);
+    t->dec_lut_h.assign(dec_lut, dec_lut + nr);
     MPR_TRY(t->enc_lut.ensure(nr * 4));
     MPR_TRY(t->dec_lut.ensure(nr * 4));
     MPR_HIP(hipMemcpy(t->enc_lut.ptr, enc_lut, nr * 4, hipMemcpyHostToDevice));
@@ -716,6 +750,26 @@ int mpr_t5_train_release(mpr_model* m, int32_t tape) {
     TRAINER(m);
     MPR_REQUIRE(tape >= 0 && tape < (int)tr->tapes.size(), "train_release: tape %d", tape);
     tr->tapes[tape]->busy = false;
+    return MPR_OK;
+  });
+}
+
+int mpr_t5_trainer_trim(mpr_model* m, int32_t keep_idle, void* stream) {
+  return tr_guarded([&]() -> int {
+    TRAINER(m);
+    MPR_REQUIRE(keep_idle >= 0, "trainer_trim: keep_idle %d", keep_idle);
+    // queued forwards / backwards on `stream` may still read the arenas
+    MPR_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    int idle = 0;
+    for (auto& t : tr->tapes)
+      if (!t->busy && idle++ >= keep_idle) {  // a released tape past the first keep_idle: free
+        t->ar.chunks.clear();
+        t->ar.reset();
+      }
+    if (keep_idle == 0) {
+      tr->scratch.chunks.clear();
+      tr->scratch.reset();
+    }
     return MPR_OK;
   });
 }

@@ -299,6 +299,21 @@ class T5Config:
         return tr
 
 
+def trim_trainers(keep_idle: int = 0, destroy: bool = False):
+    """Hand the native trainers' device memory back (their tape arenas and scratch
+    live outside torch's caching allocator, at their high-water mark): free the arenas of
+    released tapes past the first ``keep_idle`` (mpr_t5_trainer_trim, after each device's
+    queued work); ``destroy`` drops the trainers themselves (rebuilt on the next forward)."""
+    for key, tr in list(_TRAINERS.items()):
+        dev = torch.device(key[2])
+        if destroy:
+            torch.cuda.synchronize(dev)
+            _lib.load().mpr_model_destroy(tr)
+            del _TRAINERS[key]
+        else:
+            _lib.call("mpr_t5_trainer_trim", tr, int(keep_idle), _lib.stream_ptr(dev))
+
+
 def t5_loss(named_params: dict, inputs_embeds, attention_mask, labels, num_heads: int,
             scale_out: bool = True, dropout_rate: float = 0.0, dropout_seed: int = None):
     """Differentiable T5ForConditionalGeneration(...).loss over ``named_params`` (transformers
