@@ -255,7 +255,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, flo
 // — six v_mfma_f32_32x32x16_bf16 per 16-deep k step, each product of two bf16 exact in fp32 and
 // accumulated in fp32.  Six bf16 MFMAs cost 12 cycles per k per SIMD against 32 for one
 // v_mfma_f32_32x32x2_f32 (bf16 runs at 16x the f32 MFMA rate): the same tile does 2.67x the
-// arithmetic per cycle.  Error vs fp64 (tools/x3bench.hip): within a factor ~1.5 of the f32 MFMA
+// arithmetic per cycle.  Error vs fp64 (round-1 lab tools/x3bench.hip, removed in round 5; git show 28e8ac6:tools/x3bench.hip): within a factor ~1.5 of the f32 MFMA
 // kernel's (both ~1e-7 of sum|a.b| at K <= 3072), orders below every parity tolerance.
 // Structure as gemm_tile: BM x BN block tile, WM x WN 32x32 accumulators per wave, BK-deep K
 // tiles staged fp32 global -> registers (D tiles in flight) -> split -> 3 bf16 planes in LDS (two
@@ -271,7 +271,7 @@ constexpr int x3_lds_floats() {
   return 2 * 3 * (BM + BN) * (BK + 8) / 2;
 }
 
-// V (variants, tools/x3bench.hip): bit 0 interleaves the accumulators' MFMAs (term-major; the
+// V (variants, the round-1 x3bench lab, git show 28e8ac6:tools/x3bench.hip): bit 0 interleaves the accumulators' MFMAs (term-major; the
 // order of each accumulator's own terms is unchanged, results bit-identical) — neutral, unused;
 // bit 1 raises the wave's issue priority over its MFMA run (s_setprio 1 .. 0): +0-4% on the
 // 128x128 tiles (fc2 1600x768x3072 x4: 131.2 -> 126.9 us), neutral to slightly negative on 64x128.
@@ -1352,7 +1352,7 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
   }
   // F32_SMALL: 32x32 blocks, or 64x32 blocks (two 32x32 tiles sharing each W slice, 8 waves)
   // once the launch has >= 2048 32x32 blocks; every 32x32 sub-tile is summed by the same 4
-  // K-slice waves in the same order in both (bit-identical, tools/gbench.hip checks).
+  // K-slice waves in the same order in both (bit-identical: the round-1 gbench lab, git show a67dcca:tools/gbench.hip).
   int64_t blocks32 = 0;
   for (int i = 0; i < g.n; ++i) blocks32 += cdiv(g.g[i].M, 32) * cdiv(g.g[i].N, 32);
   return probed(PROBE_GEMM, flops, bytes, s, [&]() {
@@ -1393,7 +1393,7 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   if (g_gemm_f32) {
     for (int i = 0; i < g.n; ++i)
       MPR_REQUIRE(g.g[i].batch == 1, "gemm: strided batches need the split-bf16 kernels");
-    // Round-1 f32 MFMA tiles, per problem (tools/gbench.hip): 64x64 tiles (4 waves of 32x32,
+    // Round-1 f32 MFMA tiles, per problem (round-1 gbench lab, a67dcca): 64x64 tiles (4 waves of 32x32,
     // BK 32) once the problem has >= 1.5 blocks per CU, else 32x32 tiles with the K tile split
     // over 4 waves.  A problem keeps its tile alone or grouped (bit-identical results).
     GemmGroup big, small;
@@ -1409,7 +1409,7 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
     if (small.n) MPR_TRY(gemm_launch(small, F32_SMALL, s));
     return MPR_OK;
   }
-  // Split-bf16 tiles (tools/x3bench.hip: the tower launches of two batches, each ViT problem plus
+  // Split-bf16 tiles (x3bench lab, 28e8ac6: the tower launches of two batches, each ViT problem plus
   // the text tower's problem of the same layer in one launch).  Every problem of a launch shares
   // one KW = 1 tile, so the choice may follow the launch: 128x128 blocks of 8 waves (2x1 32x32
   // accumulators each) once the launch has >= 160 of them — even below one block per CU they beat
@@ -1417,7 +1417,7 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // for the f32 kernel; qkv 106 vs 158, fc1 140 vs 196, fc2 137 vs 178) — else 64x128 blocks of 8
   // waves of 32x32 (one-batch fc2 800x768x3072 x2 + text: 93.7 vs 114 us f32).
   // Below that, 64x64 blocks (4 waves) when the 64x128 grid would leave half the CUs idle or
-  // every K is short (tools/x3small_bench.hip, one-batch T5 encoder at M = 1440: qkv 37.2 ->
+  // every K is short (x3small_bench lab, git show 770f90b:tools/x3small_bench.hip, one-batch T5 encoder at M = 1440: qkv 37.2 ->
   // 25.8 us, o 18.0 -> 14.6, wo 52.1 -> 43.5; the one-batch ViT out / fc2, K >= 768 with 156+
   // 64x128 blocks, stay on 64x128).  Same k order in every tile: bit-identical results.
   GemmGroup fam;
