@@ -67,6 +67,34 @@ bool gemm_uniform_order();
 int64_t packed_rows16_elems(int64_t N, int64_t K);
 int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, hipStream_t s);
 
+struct AttnArgs {
+  const float* q = nullptr;
+  int64_t q_bs = 0, q_rs = 0;
+  const float* k = nullptr;
+  int64_t k_bs = 0, k_rs = 0;
+  const float* v = nullptr;
+  int64_t v_bs = 0, v_rs = 0;
+  float* o = nullptr;
+  int64_t o_bs = 0, o_rs = 0;
+  int B = 0, H = 0, Lq = 0, Lk = 0;
+  float scale = 1.f;
+  int causal = 0;   // key j visible iff j <= i + q_pos0
+  int q_pos0 = 0;   // absolute position of query row 0
+  const float* key_mask = nullptr;  // [B, mask_bs] 1/0 (0 = padded key), optional
+  int64_t mask_bs = 0;
+  // T5 relative position bias by offset: rel_tab[(j - (i + q_pos0) + lut_radius) * H + h]
+  // (the layer-0 bias table gathered through the bucket LUT once at model load), optional.
+  const float* rel_tab = nullptr;
+  int lut_radius = 0;
+  // one-query decode only: q row b is scaled by rsqrt(sum_t q_rms_part[b * q_rms_nparts + t] /
+  // q_rms_n + eps) — the decode chain's folded RMSNorm ahead of the cross-attention query, from
+  // the per-tile partial sums of squares the producing GEMM wrote (t5.hip)
+  const float* q_rms_part = nullptr;
+  int q_rms_nparts = 0;
+  int q_rms_n = 0;
+  float q_rms_eps = 1e-6f;
+};
+
 struct SkinnyArgs {
   GemmArgs g;                    // g.W / g.ldw unused: the weights come from wpk
   const float* wpk = nullptr;    // pack_rows16 image of the [N, K] weight
@@ -88,6 +116,13 @@ struct SkinnyArgs {
   const float* rs_part = nullptr;
   int rs_nparts = 0;
   int rs_n = 0;
+  // Fused self-attention of a decode step (t5.hip, MPR_DECODE_FUSE_ATTN): this GEMV writes the
+  // step's q | k | v row (N = 3 H 64, <= 16 rows); each 16-column tile's block counts itself in
+  // attn_ctr[head] (agent-scope release / atomic add), and the last of a head's 3 x 4 tile blocks
+  // runs that head's attention for every row (decode_attn.h) into attn.o.  attn_ctr: H ints, zero
+  // between launches (the last arriver resets its head's).
+  AttnArgs attn;
+  int* attn_ctr = nullptr;
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 
@@ -126,33 +161,6 @@ int rmsnorm(const float* x, int64_t ldx, int M, int D, const float* w, float eps
 
 // Multi-head attention with head_dim 64 for short sequences.
 // q(b,i,h,:) at q + b*q_bs + i*q_rs + h*64  (same for k, v, o).
-struct AttnArgs {
-  const float* q = nullptr;
-  int64_t q_bs = 0, q_rs = 0;
-  const float* k = nullptr;
-  int64_t k_bs = 0, k_rs = 0;
-  const float* v = nullptr;
-  int64_t v_bs = 0, v_rs = 0;
-  float* o = nullptr;
-  int64_t o_bs = 0, o_rs = 0;
-  int B = 0, H = 0, Lq = 0, Lk = 0;
-  float scale = 1.f;
-  int causal = 0;   // key j visible iff j <= i + q_pos0
-  int q_pos0 = 0;   // absolute position of query row 0
-  const float* key_mask = nullptr;  // [B, mask_bs] 1/0 (0 = padded key), optional
-  int64_t mask_bs = 0;
-  // T5 relative position bias by offset: rel_tab[(j - (i + q_pos0) + lut_radius) * H + h]
-  // (the layer-0 bias table gathered through the bucket LUT once at model load), optional.
-  const float* rel_tab = nullptr;
-  int lut_radius = 0;
-  // one-query decode only: q row b is scaled by rsqrt(sum_t q_rms_part[b * q_rms_nparts + t] /
-  // q_rms_n + eps) — the decode chain's folded RMSNorm ahead of the cross-attention query, from
-  // the per-tile partial sums of squares the producing GEMM wrote (t5.hip)
-  const float* q_rms_part = nullptr;
-  int q_rms_nparts = 0;
-  int q_rms_n = 0;
-  float q_rms_eps = 1e-6f;
-};
 int attention(const AttnArgs& a, hipStream_t s);
 // The attentions of up to ATTN_GROUP towers of a lockstep pass (or batches of a T5 encoder
 // group) in one launch (when all take the

@@ -8,6 +8,7 @@
 #include <cfloat>
 #include <cstdlib>
 
+#include "decode_attn.h"
 #include "kernels.h"
 
 namespace mpr {
@@ -346,99 +347,10 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
 __global__ __launch_bounds__(256) void attention_decode_wave_kernel(AttnArgs a) {
   __shared__ float Ps[4][128];
   __shared__ __attribute__((aligned(16))) float Os[4][8][ATT_D];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pr = blockIdx.x * 4 + wave;
   if (pr >= a.B * a.H) return;  // wave-uniform; no block barrier below
-  const int b = pr / a.H, h = pr % a.H;
-  const float* qp = a.q + (int64_t)b * a.q_bs + h * ATT_D;
-  const int qpos = a.q_pos0;
-  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
-  const float* kb = a.k + (int64_t)b * a.k_bs + h * ATT_D;
-  const float* vb = a.v + (int64_t)b * a.v_bs + h * ATT_D;
-  int lk_end = a.Lk;
-  if (a.causal) lk_end = min(lk_end, qpos + 1);
-  const bool two = lk_end > 64;  // wave-uniform
-  float qscale = a.scale, qpart = 0.f;
-  if (a.q_rms_part && lane < a.q_rms_nparts) qpart = a.q_rms_part[(int64_t)b * a.q_rms_nparts + lane];
-  // scores of keys lane and 64 + lane (clamped rows / words as the block kernel's)
-  f32x4 qv[ATT_D / 4], kr[2][ATT_D / 4];
-  float mraw[2], braw[2];
-#pragma unroll
-  for (int d = 0; d < ATT_D / 4; ++d) qv[d] = *reinterpret_cast<const f32x4*>(qp + 4 * d);
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    if (hf == 1 && !two) break;
-    const int j = hf * 64 + lane;
-    const int jc = j < lk_end ? j : 0;
-    const float* kp = kb + (int64_t)jc * a.k_rs;
-#pragma unroll
-    for (int d = 0; d < ATT_D / 4; ++d) kr[hf][d] = *reinterpret_cast<const f32x4*>(kp + 4 * d);
-    const float* mp = maskb ? maskb + jc : kp;
-    const float* bp = a.rel_tab ? a.rel_tab + (int64_t)(jc - qpos + a.lut_radius) * a.H + h : kp;
-    mraw[hf] = *mp;
-    braw[hf] = *bp;
-  }
-  if (a.q_rms_part)
-    qscale = a.scale * (1.0f / sqrtf(wave_sum(qpart) / (float)a.q_rms_n + a.q_rms_eps));
-  float sc[2] = {-INFINITY, -INFINITY};
-  bool valid[2] = {false, false};
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    if (hf == 1 && !two) break;
-    const int j = hf * 64 + lane;
-    const float mk = maskb ? mraw[hf] : 1.f, rb = a.rel_tab ? braw[hf] : 0.f;
-    float s = 0.f;
-#pragma unroll
-    for (int d = 0; d < ATT_D / 4; ++d)
-      s += qv[d][0] * kr[hf][d][0] + qv[d][1] * kr[hf][d][1] + qv[d][2] * kr[hf][d][2] +
-           qv[d][3] * kr[hf][d][3];
-    valid[hf] = j < lk_end && mk != 0.f;
-    sc[hf] = valid[hf] ? s * qscale + rb : -INFINITY;
-  }
-  const float mnew = fmaxf(wave_max(sc[0]), wave_max(sc[1]));
-  float p[2];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) p[hf] = valid[hf] ? expf(sc[hf] - mnew) : 0.f;
-  // the block kernel: l = 0 * alpha + ((w0 + w1) + (w2 + w3)), waves 2-3 (and 1 when Lk <= 64)
-  // summing zeros
-  const float l = (wave_sum(p[0]) + wave_sum(p[1])) + (0.f + 0.f);
-  Ps[wave][lane] = p[0];
-  Ps[wave][64 + lane] = p[1];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // P.V: lane (dg, kq) sums dims 4 dg .. +3 over key group kq (and 4 + kq), 16 keys each, as the
-  // block kernel's thread (dg, kg) does (o starts at 0 * alpha = 0)
-  const int dg = lane & 15, kq = lane >> 4;
-  f32x4 vr[2][16];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    if (hf == 1 && !two) break;
-    const int jv0 = (hf * 4 + kq) * 16;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int jv = jv0 + u < lk_end ? jv0 + u : 0;
-      vr[hf][u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)jv * a.v_rs + 4 * dg);
-    }
-  }
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    if (hf == 1 && !two) break;
-    const int g = hf * 4 + kq;
-    f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 16; ++u) o += Ps[wave][g * 16 + u] * vr[hf][u];
-    *reinterpret_cast<f32x4*>(&Os[wave][g][4 * dg]) = o;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // the block kernel's sum over its 16 key groups in order (groups past Lk add exact zeros)
-  float acc = 0.f;
-  const int ng = two ? 8 : 4;
-  for (int g = 0; g < ng; ++g) acc += Os[wave][g][lane];
-  a.o[(int64_t)b * a.o_bs + h * ATT_D + lane] = acc / l;
+  dattn::pair(a, pr / a.H, pr % a.H, Ps[wave], Os[wave]);  // decode_attn.h
 }
 
 // ---- short-sequence attention on MFMA ----------------------------------------------------------

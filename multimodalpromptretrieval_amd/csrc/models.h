@@ -138,6 +138,7 @@ struct T5Work {
   DevBuf mask_enc, enc_tmp;  // a group's encoder mask / output when several groups share a decode
   DevBuf ax, yq, hz;  // folded decode chain rows: [a | x], [c | h | u], [h2 | z]
   DevBuf x1ss, x2ss;  // their residual rows' per-16-column sums of squares
+  DevBuf attn_ctr;    // fused qkv + self-attention arrival counters (H ints, zero between uses)
   uint64_t gen = 0;  // bumped by every buffer growth: invalidates captured graphs
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {
@@ -203,7 +204,8 @@ struct T5Model : mpr_model {
   // A decode projection: the skinny GEMV on the packed weight (gemm_skinny)
   int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
                int* amax_nparts = nullptr) const;
-  bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
+  bool tiled_head(int B) const;
+  bool fuse_attn(int B, int max_new) const;  // qkv GEMV + self-attention in one launch  // the grouped decode's argmax head on the tiled GEMM
   int build_folded(hipStream_t s);  // stream-ordered
   DevBuf rel_tmp;  // update scratch: a bias table
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
