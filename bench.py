@@ -158,25 +158,33 @@ def _projected_shard_class():
 
     class ProjectedShard(ShardedIndex):
         """One rank's shard of a W-rank row-sharded index, run on a world-1 RCCL group: the
-        product's ShardedIndex (local scan, pack, all_gather, merge) whose gathered candidate
-        lists are this shard's own top-k repeated for the W - 1 shards it stands in for (ids
-        offset by the shard size), so the merge reads W x k candidates per query as rank r of W
-        does.  Used by the one-GPU strong-scaling projection only."""
+        product's ShardedIndex (local scan, pack, all_gather, merge) whose all_gather fills
+        block 0 of a [W, B, k] receive buffer whose other W - 1 blocks hold this shard's first
+        top-k again with ids offset by the shard size (written once, untimed), so the merge
+        reads W x k candidates per query as rank r of W does.  Two receive buffers alternate (two
+        batches are in flight).  Used by the one-GPU strong-scaling projection only."""
 
         def __init__(self, rows, device, virtual_world: int, group=None):
             super().__init__(rows, device, group=group, rows_are_local=True, row_offset=0)
             self.virtual_world = int(virtual_world)
-            self._offs = None
+            self._recv = []
+            self._calls = 0
 
-        def _candidates(self, recv, B: int, k: int):
-            cd, ci = super()._candidates(recv, B, k)
-            W = self.virtual_world
+        def _gather(self, packed, async_op: bool = False):
+            W, B = self.virtual_world, packed.shape[0]
             if W == 1:
-                return cd, ci
-            if self._offs is None or self._offs.shape[0] != W * k:
-                self._offs = (torch.arange(W, device=ci.device, dtype=torch.int64)
-                              .repeat_interleave(k) * self.n_local)
-            return cd.repeat(1, W).contiguous(), (ci.repeat(1, W) + self._offs).contiguous()
+                return super()._gather(packed, async_op)
+            if not self._recv or self._recv[0].shape[0] != W * B:
+                rest = packed.repeat(W, 1, 1)
+                offs = (torch.arange(W, device=packed.device, dtype=torch.float64)
+                        .repeat_interleave(B) * self.n_local)
+                rest[..., 1] += offs[:, None]
+                self._recv = [rest, rest.clone()]
+            recv = self._recv[self._calls % 2]
+            self._calls += 1
+            work = dist.all_gather_into_tensor(recv[:B], packed, group=self.group,
+                                               async_op=async_op)
+            return recv, work
 
     return ProjectedShard
 

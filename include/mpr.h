@@ -79,6 +79,17 @@ int mpr_index_scores(mpr_index* index, const float* q_dev, int32_t b, float* out
 int mpr_topk_merge(const float* cand_dist_dev, const int64_t* cand_ids_dev, int32_t b,
                    int32_t n_cand, int32_t k, int32_t metric, float* out_dist_dev,
                    int64_t* out_ids_dev, void* stream);
+/* The sharded search's candidate exchange without host-side reshaping (distributed.py):
+ * mpr_topk_pack writes n (dist, id) pairs as float64 [n][2] (ids < 2^53 and fp32 values are
+ * exact), the tensor the RCCL all_gather / all_to_all moves; mpr_topk_merge_packed merges what
+ * arrives, packed [W shards][Bp query slots][kc][2], for query slots 0 .. b-1 (each query's
+ * candidates shard-major): the same outputs as mpr_topk_merge over the unpacked [b, W kc] lists.
+ * k <= 64, W kc <= 512. */
+int mpr_topk_pack(const float* dist_dev, const int64_t* ids_dev, int64_t n, double* packed_dev,
+                  void* stream);
+int mpr_topk_merge_packed(const double* packed_dev, int32_t W, int32_t Bp, int32_t b, int32_t kc,
+                          int32_t k, int32_t metric, float* out_dist_dev, int64_t* out_ids_dev,
+                          void* stream);
 /* Row-wise cosine similarity (utils.py:57-62 with aligned rows): out[i] =
  * sum(x1[i]*x2[i]) / max(|x1[i]|*|x2[i]|, eps), x1/x2 [m, d]. */
 int mpr_cosine_rows(const float* x1_dev, const float* x2_dev, int64_t m, int32_t d, float eps,

@@ -202,6 +202,23 @@ int mpr_topk_merge(const float* cand_dist, const int64_t* cand_ids, int32_t b, i
   });
 }
 
+int mpr_topk_pack(const float* dist, const int64_t* ids, int64_t n, double* packed, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(n >= 0 && (n == 0 || (dist && ids && packed)), "topk_pack: null buffer");
+    return topk_pack(dist, ids, n, packed, S(stream));
+  });
+}
+
+int mpr_topk_merge_packed(const double* packed, int32_t W, int32_t Bp, int32_t b, int32_t kc,
+                          int32_t k, int32_t metric, float* out_dist, int64_t* out_ids,
+                          void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(metric == 0 || metric == 1, "merge_packed: metric %d", metric);
+    MPR_REQUIRE(b == 0 || (packed && out_dist && out_ids), "merge_packed: null buffer");
+    return merge_packed(packed, W, Bp, b, kc, k, metric, out_dist, out_ids, S(stream));
+  });
+}
+
 int mpr_cosine_rows(const float* x1, const float* x2, int64_t m, int32_t d, float eps, float* out,
                     void* stream) {
   return guarded([&]() -> int {

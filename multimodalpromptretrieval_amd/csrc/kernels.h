@@ -213,6 +213,11 @@ int scale_inplace(float* p, int64_t n, float scale, hipStream_t s);
 int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
                 const int* gate);
+// the sharded search's exchange (select.hip): (dist, id) -> float64 pairs; merge of packed
+// [W][Bp][kc][2] candidate lists for query slots < b (keys are values)
+int topk_pack(const float* d, const int64_t* ids, int64_t n, double* out, hipStream_t s);
+int merge_packed(const double* packed, int W, int Bp, int b, int kc, int k, int metric,
+                 float* od, int64_t* oi, hipStream_t s);
 // k > 64: per row the k smallest (sign * key, id) of n (ids null: id = column + id_offset),
 // ascending, ties to the lowest id; values written as given (sign undone).
 constexpr int SELECT_MAX_K = 16384;

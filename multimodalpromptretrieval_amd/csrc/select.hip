@@ -104,23 +104,39 @@ __global__ __launch_bounds__(NT) void merge_kernel(const float* cand_key, const 
 // queries per block, so the k rounds are wave shuffles with no block barrier (the block kernel
 // above spends a barrier per round).  Same (key, id) order, same outputs.
 constexpr int MW_MAX = 512;
-template <int K>
+// PK: the candidates are a sharded search's all_gathered per-shard top-k as they arrive, packed
+// (dist, id) float64 pairs [W shards][Bp query slots][kc][2] (distributed.py); query q's list is
+// shard-major, candidate c = (shard c / kc, rank c % kc) — the order of the unpacked [b, W kc]
+// lists, so the outputs are the unpacked merge's.
+template <int K, bool PK = false>
 __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
                                                          const int64_t* cand_id, int64_t n_cand,
                                                          int b, int k, int keys_are_values,
                                                          int metric, float* out_val,
-                                                         int64_t* out_id, const int* gate) {
+                                                         int64_t* out_id, const int* gate,
+                                                         const double* packed = nullptr,
+                                                         int Bp = 0, int kc = 1) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (q >= b || (gate && gate[q] == 0)) return;  // wave-uniform
-  const float* ck = cand_key + (int64_t)q * n_cand;
-  const int64_t* ci = cand_id + (int64_t)q * n_cand;
+  const float* ck = PK ? nullptr : cand_key + (int64_t)q * n_cand;
+  const int64_t* ci = PK ? nullptr : cand_id + (int64_t)q * n_cand;
   const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
   uint64_t w[K];
 #pragma unroll
   for (int t = 0; t < K; ++t) w[t] = ~0ull;
   for (int64_t c = lane; c < n_cand; c += 64) {
-    const float kk = sign * ck[c];
-    uint64_t v = head_word(kk, kk == kk ? ci[c] : -1);  // NaN keys never rank (as key_less)
+    float key;
+    int64_t id;
+    if constexpr (PK) {
+      const double* e = packed + (((c / kc) * (int64_t)Bp + q) * kc + c % kc) * 2;
+      key = (float)e[0];
+      id = (int64_t)e[1];
+    } else {
+      key = ck[c];
+      id = ci[c];
+    }
+    const float kk = sign * key;
+    uint64_t v = head_word(kk, kk == kk ? id : -1);  // NaN keys never rank (as key_less)
 #pragma unroll
     for (int t = 0; t < K; ++t) {  // sorted insert (words are unique per valid candidate)
       const uint64_t lo = v < w[t] ? v : w[t], hi = v < w[t] ? w[t] : v;
@@ -274,7 +290,53 @@ int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int 
   return MPR_OK;
 }
 
+__global__ __launch_bounds__(256) void topk_pack_kernel(const float* __restrict__ d,
+                                                        const int64_t* __restrict__ ids, int64_t n,
+                                                        double2* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = make_double2((double)d[i], (double)ids[i]);
+}
+
+template <int K>
+int launch_merge_packed(const double* packed, int W, int Bp, int b, int kc, int k, int metric,
+                        float* od, int64_t* oi, hipStream_t s) {
+  hipLaunchKernelGGL((merge_wave_kernel<K, true>), dim3((unsigned)((b + 3) / 4)), dim3(256), 0, s,
+                     nullptr, nullptr, (int64_t)W * kc, b, k, /*keys_are_values=*/1, metric, od,
+                     oi, nullptr, packed, Bp, kc);
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
 }  // namespace
+
+// (dist fp32, id int64) [n] -> float64 pairs [n][2] (ids < 2^53 and fp32 values are exact)
+int topk_pack(const float* d, const int64_t* ids, int64_t n, double* out, hipStream_t s) {
+  if (n == 0) return MPR_OK;
+  hipLaunchKernelGGL(topk_pack_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, d, ids, n,
+                     reinterpret_cast<double2*>(out));
+  MPR_LAUNCHED();
+  return MPR_OK;
+}
+
+int merge_packed(const double* packed, int W, int Bp, int b, int kc, int k, int metric,
+                 float* od, int64_t* oi, hipStream_t s) {
+  MPR_REQUIRE(W >= 1 && Bp >= b && b >= 0 && kc >= 1 && k >= 1 && k <= 64 && k <= W * kc &&
+                  (int64_t)W * kc <= MW_MAX,
+              "merge_packed: W=%d Bp=%d b=%d kc=%d k=%d (k <= 64, W kc <= %d)", W, Bp, b, kc, k,
+              MW_MAX);
+  if (b == 0) return MPR_OK;
+  int c = 1;
+  while (c < k) c <<= 1;
+  switch (c) {
+    case 1: return launch_merge_packed<1>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+    case 2: return launch_merge_packed<2>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+    case 4: return launch_merge_packed<4>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+    case 8: return launch_merge_packed<8>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+    case 16: return launch_merge_packed<32>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+    case 32: return launch_merge_packed<32>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+    default: return launch_merge_packed<64>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+  }
+}
 
 int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,

@@ -38,6 +38,7 @@ import contextlib
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from .index import L2, DeviceIndex, topk_merge
 
 
@@ -74,6 +75,9 @@ class ShardedIndex:
         else:
             self._search = lambda q, k: searcher(local, lo, q, k)
         self._merge = merger or (lambda d, i, k: topk_merge(d, i, k, metric))
+        # device kernels for the exchange's pack / merge (mpr_topk_pack / _merge_packed: no host
+        # reshaping between the collective and the merge); the CPU tests inject both instead
+        self._native = searcher is None and merger is None and self.device.type == "cuda"
 
     def _host_staged(self) -> bool:
         # gloo (CPU tests, or a one-GPU rehearsal of N ranks) moves host tensors only
@@ -158,11 +162,8 @@ class ShardedIndex:
                 return None, True
             return (torch.empty((0, k), device=self.device, dtype=torch.float32),
                     torch.empty((0, k), device=self.device, dtype=torch.int64)), True
-        d_recv, i_recv = self._unpack(recv.to(self.device))
-        # [W(src shard), bmax, k] -> this rank's b real queries: [b, W*k]
-        cd = d_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
-        ci = i_recv.view(self.world, bmax, k)[:, :b].permute(1, 0, 2).reshape(b, self.world * k)
-        return self._merge(cd.contiguous(), ci.contiguous(), k), True
+        # [W(src shard), bmax, k] -> this rank's b real queries
+        return self._merge_recv(recv.to(self.device), bmax, b, k), True
 
     def search_all(self, q: torch.Tensor, k: int):
         """q: the SAME [B, d] query batch on every rank (replicated).  Returns (dist, ids)
@@ -176,19 +177,22 @@ class ShardedIndex:
         stage = self._host_staged()
         if stage:
             packed = packed.cpu()
-        recv = torch.empty((self.world * B,) + tuple(packed.shape[1:]), dtype=packed.dtype,
-                           device=packed.device)
-        dist.all_gather_into_tensor(recv, packed, group=self.group)
-        cd, ci = self._candidates(recv.to(self.device), B, k)
-        return self._merge(cd, ci, k)
+        recv, _ = self._gather(packed)
+        return self._merge_recv(recv.to(self.device), B, B, k)
 
-    def _candidates(self, recv, B: int, k: int):
-        """The all_gathered per-shard top-k [W * B, k, 2] as the merge's candidate lists:
-        (dist [B, W * k], ids [B, W * k]), shard-major within a query's list."""
-        d_all, i_all = self._unpack(recv.view(self.world, B, k, 2))  # [W, B, k]
-        cd = d_all.permute(1, 0, 2).reshape(B, self.world * k)
-        ci = i_all.permute(1, 0, 2).reshape(B, self.world * k)
-        return cd.contiguous(), ci.contiguous()
+    def _merge_recv(self, recv, Bp: int, b: int, k: int):
+        """Merge the exchanged per-shard top-k, packed [W, Bp, k, 2] float64 (shard w's list
+        for query slot j at [w, j]), for query slots 0 .. b-1: (dist, ids) [b, k]."""
+        if self._native and k <= 64 and self.world * k <= 512:
+            od = torch.empty((b, k), device=self.device, dtype=torch.float32)
+            oi = torch.empty((b, k), device=self.device, dtype=torch.int64)
+            _lib.call("mpr_topk_merge_packed", _lib.ptr(recv), self.world, Bp, b, k, k,
+                      self.metric, _lib.ptr(od), _lib.ptr(oi), _lib.stream_ptr(self.device))
+            return od, oi
+        d_all, i_all = self._unpack(recv.view(self.world, Bp, k, 2)[:, :b])  # [W, b, k]
+        cd = d_all.permute(1, 0, 2).reshape(b, self.world * k)
+        ci = i_all.permute(1, 0, 2).reshape(b, self.world * k)
+        return self._merge(cd.contiguous(), ci.contiguous(), k)
 
     def search_all_many(self, queries, k: int):
         """search_all over an iterable of query batches (the same batches on every rank) as a
@@ -214,10 +218,7 @@ class ShardedIndex:
                 # it after the yield, its memory must not be reused while this scan reads it
                 q.record_stream(st)
                 packed = self._pack(*self._padded_search(q, k))
-                recv = torch.empty((self.world * B,) + tuple(packed.shape[1:]),
-                                   dtype=packed.dtype, device=self.device)
-                work = dist.all_gather_into_tensor(recv, packed, group=self.group,
-                                                   async_op=True)
+                recv, work = self._gather(packed, async_op=True)
             return st, B, recv, work
 
         pend = None
@@ -235,7 +236,7 @@ class ShardedIndex:
         st, B, recv, work = pend
         with torch.cuda.stream(st):
             work.wait()
-            out = self._merge(*self._candidates(recv, B, k), k)
+            out = self._merge_recv(recv, B, B, k)
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(st)
         for t in out:
@@ -254,8 +255,21 @@ class ShardedIndex:
                                                  device=i_loc.device)], 1)
         return d_loc, i_loc
 
-    @staticmethod
-    def _pack(d, i):
+    def _gather(self, packed, async_op: bool = False):
+        """The all_gather of the per-shard top-k, packed [B, k, 2] -> [W B, k, 2] (every rank's
+        block, rank-major).  Returns (recv, work or None)."""
+        recv = torch.empty((self.world * packed.shape[0],) + tuple(packed.shape[1:]),
+                           dtype=packed.dtype, device=packed.device)
+        work = dist.all_gather_into_tensor(recv, packed, group=self.group, async_op=async_op)
+        return recv, work
+
+    def _pack(self, d, i):
+        """(dist, ids) [b, k] -> float64 pairs [b, k, 2] (ids < 2^53, fp32 values exact)."""
+        if self._native and d.is_cuda:
+            out = torch.empty(tuple(d.shape) + (2,), device=d.device, dtype=torch.float64)
+            _lib.call("mpr_topk_pack", _lib.ptr(d.contiguous()), _lib.ptr(i.contiguous()),
+                      d.numel(), _lib.ptr(out), _lib.stream_ptr(d.device))
+            return out
         return torch.stack([d.to(torch.float64), i.to(torch.float64)], -1).contiguous()
 
     @staticmethod

@@ -160,6 +160,35 @@ def test_topk_merge_fewer_valid_than_k(device, index_mod, k):
         assert bool((ids[r, m:] == -1).all()) and bool(torch.isnan(d[r, m:]).all()), r
 
 
+@pytest.mark.parametrize("W,Bp,b,kc,k,metric", [(8, 256, 256, 5, 5, 0), (3, 20, 16, 4, 4, 0),
+                                                 (2, 17, 5, 15, 15, 1), (8, 16, 16, 64, 64, 0)])
+def test_topk_merge_packed_equals_unpacked(device, index_mod, W, Bp, b, kc, k, metric):
+    """mpr_topk_pack + mpr_topk_merge_packed (the sharded search's exchange, merged as it
+    arrives: [W][Bp][kc][2] float64) give topk_merge's outputs over the unpacked [b, W kc]
+    lists, exact ties (duplicated keys across shards) and -1 / NaN empty slots included."""
+    from multimodalpromptretrieval_amd import _lib
+    g = torch.Generator().manual_seed(W * 100 + kc)
+    d = torch.rand((W, Bp, kc), generator=g)
+    d[1 % W, :, 0] = d[0, :, 0]                      # exact ties across shards
+    ids = torch.randint(0, 1 << 30, (W, Bp, kc), generator=g)
+    ids[0, 0, -1] = -1                               # an empty slot (tiny shard)
+    d[0, 0, -1] = float("nan")
+    dd, ii = d.to(device).contiguous(), ids.to(device).contiguous()
+    packed = torch.empty((W, Bp, kc, 2), device=device, dtype=torch.float64)
+    _lib.call("mpr_topk_pack", _lib.ptr(dd), _lib.ptr(ii), dd.numel(), _lib.ptr(packed),
+              _lib.stream_ptr(device))
+    assert torch.equal(packed[..., 0].cpu(), d.double())
+    od = torch.empty((b, k), device=device)
+    oi = torch.empty((b, k), device=device, dtype=torch.int64)
+    _lib.call("mpr_topk_merge_packed", _lib.ptr(packed), W, Bp, b, kc, k, metric, _lib.ptr(od),
+              _lib.ptr(oi), _lib.stream_ptr(device))
+    cd = dd[:, :b].permute(1, 0, 2).reshape(b, W * kc).contiguous()
+    ci = ii[:, :b].permute(1, 0, 2).reshape(b, W * kc).contiguous()
+    rd, ri = index_mod.topk_merge(cd, ci, k, metric)
+    assert torch.equal(oi.cpu(), ri.cpu())
+    assert torch.equal(od.cpu().nan_to_num(-7.0), rd.cpu().nan_to_num(-7.0))
+
+
 @pytest.fixture(scope="module")
 def clip_sd():
     return syn.clip_state_dict(11)
