@@ -23,7 +23,9 @@ the answers a ``ServingLoop`` over the same batches computed (towers two batches
 groups of up to 8 batches), and the four analytics calls per batch reuse that batch's search.
 Batches, their order and every result are unchanged.  ``MPR_MAIN_PIPELINE=lookahead`` iterates
 one batch ahead instead (``serving.lookahead``: the next batch's towers and scan beside this
-batch's decode), ``=off`` not at all.
+batch's decode), ``=off`` not at all.  Training loaders (the model in train mode, main.py:170)
+are iterated one batch ahead (``serving.lookahead``): the next batch's retrieval towers, scan
+and image tokens run beside this step's T5 forward, backward and optimizer step.
 
 The prediction-head variants (``main.py:132-139``; SURVEY.md §2 "OUT") keep the reference's own
 class: their modules are imported (binding the original base class) before the swap.
@@ -110,6 +112,15 @@ def _eval_model():
     return None
 
 
+def _train_model():
+    """The newest live device T5VisionModel in training mode, or None."""
+    from .model import LIVE_MODELS
+    for m in reversed(list(LIVE_MODELS.values())):
+        if m.training:
+            return m
+    return None
+
+
 def patch_dataloader() -> None:
     """Iterate DataLoaders over a patched reference dataset through the serving loop
     (``serving.pipelined``; MPR_MAIN_PIPELINE=lookahead: one batch ahead, ``serving.lookahead``;
@@ -123,11 +134,16 @@ def patch_dataloader() -> None:
     def __iter__(self):
         it = orig(self)
         if getattr(type(self.dataset), "_mpr_patched", False):
-            m = _eval_model()
             mode = os.environ.get("MPR_MAIN_PIPELINE", "serving")
-            if m is not None and mode != "off":
-                from .serving import lookahead, pipelined
+            if mode == "off":
+                return it
+            from .serving import lookahead, pipelined
+            m = _eval_model()
+            if m is not None:
                 return lookahead(it, m) if mode == "lookahead" else pipelined(it, m)
+            m = _train_model()  # main.py:170-188: the next batch's retrieval beside this step
+            if m is not None:
+                return lookahead(it, m)
         return it
 
     DataLoader._mpr_orig_iter = orig

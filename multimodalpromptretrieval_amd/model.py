@@ -438,11 +438,12 @@ class T5VisionModel(nn.Module):
         index scan and the top-k copy to host (``_prefetch``) — is enqueued now on the retrieval
         stream, so it runs on the GPU beside the current ``predict()``'s T5 encoder and greedy
         decode, which leave most of the chip idle; the hinted ``predict()`` then only waits for
-        it.  Same launches, same results as an unhinted call.  Returns whether anything was
-        enqueued: nothing in training mode, without a ``VQARetrieval`` with an index on this
-        device, or for a batch already hinted."""
-        if self.training:
-            return False
+        it.  Same launches, same results as an unhinted call.  In training mode the hinted
+        ``forward(batch)`` picks it up the same way (main.py:177-178: the towers are frozen and
+        the index fixed while the T5 trains, so the next batch's retrieval and image tokens run
+        beside this step's T5 forward / backward).  Returns whether anything was enqueued:
+        nothing without a ``VQARetrieval`` with an index on this device, or for a batch already
+        hinted."""
         if not hasattr(self, "_hints"):
             self._hints = {}
         key = id(batch["image"])

@@ -150,7 +150,7 @@ def test_pipelined_hands_out_batches_in_order_with_the_loops_answers(monkeypatch
     assert pipe.answers_for({"image": object()}) is None  # never fed: predict() runs as usual
 
 
-def test_dataloader_patch_wraps_only_patched_datasets_in_eval_mode(monkeypatch):
+def test_dataloader_patch_wraps_only_patched_datasets(monkeypatch):
     from torch.utils.data import DataLoader
     monkeypatch.setenv("MPR_MAIN_PIPELINE", "lookahead")
 
@@ -185,9 +185,13 @@ def test_dataloader_patch_wraps_only_patched_datasets_in_eval_mode(monkeypatch):
         assert [int(b) for b in DataLoader(VQADataset(), batch_size=1)] == [0, 1, 2]
         assert hints == [0, 1, 2]
         assert [int(b) for b in DataLoader(Other(), batch_size=1)] == [0, 1, 2]
-        fake.training = True  # a training loop is never hinted
+        fake.training = True  # a training loop: one batch ahead whatever MPR_MAIN_PIPELINE
+        monkeypatch.setenv("MPR_MAIN_PIPELINE", "serving")
         assert [int(b) for b in DataLoader(VQADataset(), batch_size=1)] == [0, 1, 2]
-        assert hints == [0, 1, 2]
+        assert hints == [0, 1, 2, 0, 1, 2]
+        monkeypatch.setenv("MPR_MAIN_PIPELINE", "off")
+        assert [int(b) for b in DataLoader(VQADataset(), batch_size=1)] == [0, 1, 2]
+        assert hints == [0, 1, 2, 0, 1, 2]
     finally:
         LIVE_MODELS.pop(id(fake), None)
         DataLoader.__iter__ = saved

@@ -184,8 +184,15 @@ def test_g2_predict_many_matches_predict(device):
         assert got == want
     model.hint_next(batches[2])  # a hinted batch predicted out of order, another never
     assert model.predict(batches[1]) == want[1] and model.predict(batches[2]) == want[2]
+    # training mode (main.py:170-178 under the dropin launcher's lookahead): a hinted batch's
+    # forward inputs are the unhinted ones
     model.train()
-    assert model.hint_next(batches[0]) is False  # no hints in training mode
+    assert model.hint_next(batches[0]) is True
+    pre = model._take_hint(batches[0])
+    with torch.no_grad():
+        hinted = model.prepare_input(batches[0], _pre=pre)
+        plain = model.prepare_input(batches[0])
+    assert torch.equal(hinted[0], plain[0]) and torch.equal(hinted[1], plain[1])
     model.eval()
 
 
