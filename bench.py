@@ -170,10 +170,8 @@ def _projected_shard_class():
             self._recv = []
             self._calls = 0
 
-        def _gather(self, packed, async_op: bool = False):
+        def _buffers(self, packed):
             W, B = self.virtual_world, packed.shape[0]
-            if W == 1:
-                return super()._gather(packed, async_op)
             if not self._recv or self._recv[0].shape[0] != W * B:
                 rest = packed.repeat(W, 1, 1)
                 offs = (torch.arange(W, device=packed.device, dtype=torch.float64)
@@ -182,7 +180,21 @@ def _projected_shard_class():
                 self._recv = [rest, rest.clone()]
             recv = self._recv[self._calls % 2]
             self._calls += 1
-            work = dist.all_gather_into_tensor(recv[:B], packed, group=self.group,
+            return recv
+
+        def _recv_blocks(self, q, B: int, k: int):  # the native path (mpr_sharded_search_all)
+            if self.virtual_world == 1:
+                return super()._recv_blocks(q, B, k)
+            if not self._recv:
+                self._buffers(self._pack(*self._local.search(q, k)))
+                self._calls = 0
+            return self._buffers(self._recv[0][:B]), self.virtual_world
+
+        def _gather(self, packed, async_op: bool = False):  # the Python path
+            if self.virtual_world == 1:
+                return super()._gather(packed, async_op)
+            recv = self._buffers(packed)
+            work = dist.all_gather_into_tensor(recv[:packed.shape[0]], packed, group=self.group,
                                                async_op=async_op)
             return recv, work
 

@@ -90,6 +90,20 @@ int mpr_topk_pack(const float* dist_dev, const int64_t* ids_dev, int64_t n, doub
 int mpr_topk_merge_packed(const double* packed_dev, int32_t W, int32_t Bp, int32_t b, int32_t kc,
                           int32_t k, int32_t metric, float* out_dist_dev, int64_t* out_ids_dev,
                           void* stream);
+/* One search of a row-sharded index with the query batch replicated on every rank (config C5;
+ * north_star's "RCCL all-gather over xGMI of per-shard local top-k"), in one call on `stream`:
+ * this rank's local search (index rows carry their global ids through row_offset), its top-k
+ * packed into block `rank` of recv ((NaN, -1) past a tiny shard's rows), ncclAllGather in place
+ * on `comm` (an RCCL communicator of `world` ranks: PyTorch's, ProcessGroupNCCL._comm_ptr(); the
+ * RCCL library already loaded in the process is used), then the merge of recv's n_blocks >= world
+ * blocks [n_blocks][b][k][2] (blocks past world: candidates the caller placed there) into
+ * out_dist / out_ids [b, k].  Replaces dataset/VQAFeatureDataset.py:192-197 over a sharded index;
+ * the same results as mpr_index_search over the whole index up to fp32 rounding ties (exact ties
+ * to the lowest global id).  k <= 64, n_blocks * k <= 512. */
+int mpr_sharded_search_all(mpr_index* index, void* comm, int32_t world, int32_t rank,
+                           const float* q_dev, int32_t b, int32_t k, double* recv_dev,
+                           int32_t n_blocks, float* out_dist_dev, int64_t* out_ids_dev,
+                           void* stream);
 /* Row-wise cosine similarity (utils.py:57-62 with aligned rows): out[i] =
  * sum(x1[i]*x2[i]) / max(|x1[i]|*|x2[i]|, eps), x1/x2 [m, d]. */
 int mpr_cosine_rows(const float* x1_dev, const float* x2_dev, int64_t m, int32_t d, float eps,

@@ -39,6 +39,9 @@ SIGNATURES = [
     ("mpr_topk_pack", c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("mpr_topk_merge_packed", c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                         c_int32, c_void_p, c_void_p, c_void_p]),
+    ("mpr_sharded_search_all", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p,
+                                         c_int32, c_int32, c_void_p, c_int32, c_void_p, c_void_p,
+                                         c_void_p]),
     ("mpr_cosine_rows", c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p,
                                   c_void_p]),
     ("mpr_vit_create", c_int32, [I32P, c_int32, POINTER(c_void_p), c_int32, POINTER(c_void_p)]),

@@ -1,4 +1,7 @@
 // api.hip — the extern "C" boundary of libmpr.so (declared in include/mpr.h).
+#include <dlfcn.h>
+
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -205,7 +208,52 @@ int mpr_topk_merge(const float* cand_dist, const int64_t* cand_ids, int32_t b, i
 int mpr_topk_pack(const float* dist, const int64_t* ids, int64_t n, double* packed, void* stream) {
   return guarded([&]() -> int {
     MPR_REQUIRE(n >= 0 && (n == 0 || (dist && ids && packed)), "topk_pack: null buffer");
-    return topk_pack(dist, ids, n, packed, S(stream));
+    return topk_pack(dist, ids, n, packed, S(stream), 1, 1);
+  });
+}
+
+// ---- the sharded search in one call: local scan -> pack -> RCCL all_gather -> merge ----------
+// ncclAllGather is taken from the RCCL library already loaded in the process (PyTorch's, whose
+// communicator the caller passes: ProcessGroupNCCL._comm_ptr()), found by its soname without
+// loading another copy; libmpr.so itself does not link RCCL.
+namespace {
+using AllGatherFn = int (*)(const void*, void*, size_t, int, void*, hipStream_t);
+AllGatherFn rccl_allgather() {
+  static AllGatherFn fn = [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    return h ? reinterpret_cast<AllGatherFn>(dlsym(h, "ncclAllGather")) : nullptr;
+  }();
+  return fn;
+}
+constexpr int NCCL_FLOAT64 = 8;  // ncclFloat64 (rccl.h)
+}  // namespace
+
+int mpr_sharded_search_all(mpr_index* ix, void* comm, int32_t world, int32_t rank,
+                           const float* q, int32_t b, int32_t k, double* recv, int32_t n_blocks,
+                           float* out_dist, int64_t* out_ids, void* stream) {
+  return guarded([&]() -> int {
+    MPR_REQUIRE(ix != nullptr && comm != nullptr && recv != nullptr, "sharded_search: null argument");
+    MPR_REQUIRE(world >= 1 && rank >= 0 && rank < world && n_blocks >= world,
+                "sharded_search: world %d rank %d n_blocks %d", world, rank, n_blocks);
+    MPR_REQUIRE(k >= 1 && k <= 64 && (int64_t)n_blocks * k <= 512,
+                "sharded_search: k=%d (<= 64, n_blocks * k <= 512)", k);
+    if (b == 0) return MPR_OK;
+    MPR_REQUIRE(q && out_dist && out_ids, "sharded_search: null buffer");
+    AllGatherFn ag = rccl_allgather();
+    MPR_REQUIRE(ag != nullptr, "sharded_search: RCCL (librccl.so.1) is not loaded in this process");
+    const int kk = (int)std::min<int64_t>(k, ix->n);
+    auto& slot = ix->xch[stream];
+    if (!slot) slot = std::make_unique<DevBuf>();
+    MPR_TRY(slot->ensure((size_t)b * kk * 12 + 256));
+    float* ld = slot->as<float>();
+    int64_t* li = reinterpret_cast<int64_t*>(ld + ((size_t)b * kk + 63) / 64 * 64);
+    MPR_TRY(mpr_index_search(ix, q, b, kk, li, ld, stream));
+    const size_t count = (size_t)b * k * 2;  // this rank's block, float64 words
+    double* mine = recv + (size_t)rank * count;
+    MPR_TRY(topk_pack(ld, li, (int64_t)b * k, mine, S(stream), kk, k));
+    const int rc = ag(mine, recv, count, NCCL_FLOAT64, comm, S(stream));  // in place
+    MPR_REQUIRE(rc == 0, "sharded_search: ncclAllGather returned %d", rc);
+    return merge_packed(recv, n_blocks, b, b, k, k, ix->metric, out_dist, out_ids, S(stream));
   });
 }
 

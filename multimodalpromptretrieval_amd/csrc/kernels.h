@@ -215,7 +215,9 @@ int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k
                 const int* gate);
 // the sharded search's exchange (select.hip): (dist, id) -> float64 pairs; merge of packed
 // [W][Bp][kc][2] candidate lists for query slots < b (keys are values)
-int topk_pack(const float* d, const int64_t* ids, int64_t n, double* out, hipStream_t s);
+// (rows of kk pairs padded to k with (NaN, -1) when kk < k; n = rows * k)
+int topk_pack(const float* d, const int64_t* ids, int64_t n, double* out, hipStream_t s,
+              int kk = 1, int k = 1);
 int merge_packed(const double* packed, int W, int Bp, int b, int kc, int k, int metric,
                  float* od, int64_t* oi, hipStream_t s);
 // k > 64: per row the k smallest (sign * key, id) of n (ids null: id = column + id_offset),

@@ -22,6 +22,8 @@ struct mpr_index {
   // the tower stream beside an analytics search on the caller's) never share candidate buffers
   std::map<void*, std::unique_ptr<mpr::DevBuf>> ws;
   std::map<void*, int> last_coarse_b;  // batch of the last coarse search per stream (0: none)
+  // mpr_sharded_search_all: the local top-k per stream before it is packed for the exchange
+  std::map<void*, std::unique_ptr<mpr::DevBuf>> xch;
   int64_t n = 0;
   int d = 0;
   int metric = 0;

@@ -290,11 +290,17 @@ int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int 
   return MPR_OK;
 }
 
+// rows of kk (dist, id) -> rows of k >= kk float64 pairs, ranks past kk empty (NaN, -1): a
+// shard holding fewer than k rows
 __global__ __launch_bounds__(256) void topk_pack_kernel(const float* __restrict__ d,
                                                         const int64_t* __restrict__ ids, int64_t n,
-                                                        double2* __restrict__ out) {
+                                                        int kk, int k, double2* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] = make_double2((double)d[i], (double)ids[i]);
+  if (i >= n) return;
+  const int64_t r = i / k;
+  const int j = (int)(i - r * k);
+  out[i] = j < kk ? make_double2((double)d[r * kk + j], (double)ids[r * kk + j])
+                  : make_double2((double)NAN, -1.0);
 }
 
 template <int K>
@@ -310,10 +316,13 @@ int launch_merge_packed(const double* packed, int W, int Bp, int b, int kc, int 
 }  // namespace
 
 // (dist fp32, id int64) [n] -> float64 pairs [n][2] (ids < 2^53 and fp32 values are exact)
-int topk_pack(const float* d, const int64_t* ids, int64_t n, double* out, hipStream_t s) {
+int topk_pack(const float* d, const int64_t* ids, int64_t n, double* out, hipStream_t s, int kk,
+              int k) {
   if (n == 0) return MPR_OK;
+  MPR_REQUIRE(kk >= 1 && k >= kk && n % k == 0, "topk_pack: kk=%d k=%d n=%lld", kk, k,
+              (long long)n);
   hipLaunchKernelGGL(topk_pack_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, d, ids, n,
-                     reinterpret_cast<double2*>(out));
+                     kk, k, reinterpret_cast<double2*>(out));
   MPR_LAUNCHED();
   return MPR_OK;
 }

@@ -34,6 +34,7 @@ searcher/merger so the sharding logic is exercised without a GPU).
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -172,6 +173,8 @@ class ShardedIndex:
         scan of all B queries, one all_gather of the per-shard top-k, the merge."""
         B = q.shape[0]
         q = q.to(self.device, torch.float32).contiguous()
+        if self._rccl_ok(k):  # one native call: scan, pack, RCCL all_gather, merge
+            return self._native_search_all(q, k)
         d_loc, i_loc = self._padded_search(q, k)                # [B, k]
         packed = self._pack(d_loc, i_loc)                        # [B, k, 2]
         stage = self._host_staged()
@@ -179,6 +182,45 @@ class ShardedIndex:
             packed = packed.cpu()
         recv, _ = self._gather(packed)
         return self._merge_recv(recv.to(self.device), B, B, k)
+
+    def _comm(self):
+        """This group's RCCL communicator (ProcessGroupNCCL._comm_ptr()) for the native sharded
+        search, or 0 when there is none (gloo, CPU, an older PyTorch).  The first call makes sure
+        the communicator exists (a one-element all_gather)."""
+        if not hasattr(self, "_comm_cache"):
+            ptr = 0
+            try:
+                if self._native and dist.get_backend(self.group) == "nccl":
+                    x = torch.zeros(1, device=self.device)
+                    dist.all_gather_into_tensor(torch.empty(self.world, device=self.device), x,
+                                                group=self.group)
+                    pg = self.group if self.group is not None else dist.group.WORLD
+                    ptr = int(pg._get_backend(self.device)._comm_ptr())
+            except (AttributeError, RuntimeError, TypeError):
+                ptr = 0
+            self._comm_cache = ptr
+        return self._comm_cache
+
+    def _rccl_ok(self, k: int) -> bool:
+        return (self._native and k <= 64 and self.world * k <= 512
+                and os.environ.get("MPR_SHARDED_NATIVE", "1") != "0" and self._comm() != 0)
+
+    def _recv_blocks(self, q, B: int, k: int):
+        """The native search's receive buffer [n_blocks * B, k, 2] float64 and n_blocks (the
+        all_gather fills blocks 0 .. world-1)."""
+        return torch.empty((self.world * B, k, 2), device=self.device,
+                           dtype=torch.float64), self.world
+
+    def _native_search_all(self, q, k: int):
+        """mpr_sharded_search_all on the current stream (q: contiguous fp32 on this device)."""
+        B = q.shape[0]
+        recv, nb = self._recv_blocks(q, B, k)
+        od = torch.empty((B, k), device=self.device, dtype=torch.float32)
+        oi = torch.empty((B, k), device=self.device, dtype=torch.int64)
+        _lib.call("mpr_sharded_search_all", self._local._h, _lib.c_void_p(self._comm()),
+                  self.world, self.rank, _lib.ptr(q), B, int(k), _lib.ptr(recv), nb,
+                  _lib.ptr(od), _lib.ptr(oi), _lib.stream_ptr(self.device))
+        return od, oi
 
     def _merge_recv(self, recv, Bp: int, b: int, k: int):
         """Merge the exchanged per-shard top-k, packed [W, Bp, k, 2] float64 (shard w's list
@@ -206,7 +248,10 @@ class ShardedIndex:
                 yield self.search_all(q, k)
             return
         cur = torch.cuda.current_stream(self.device)
-        streams = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+        if not hasattr(self, "_streams2"):
+            self._streams2 = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+        streams = self._streams2
+        native = self._rccl_ok(k)
 
         def start(q, j):
             st = streams[j % 2]
@@ -217,6 +262,8 @@ class ShardedIndex:
                 # q may be the caller's own tensor (allocated on `cur`): once the caller drops
                 # it after the yield, its memory must not be reused while this scan reads it
                 q.record_stream(st)
+                if native:  # the whole search (RCCL included) enqueued on st in one call
+                    return st, B, self._native_search_all(q, k), None
                 packed = self._pack(*self._padded_search(q, k))
                 recv, work = self._gather(packed, async_op=True)
             return st, B, recv, work
@@ -234,9 +281,12 @@ class ShardedIndex:
 
     def _finish_all(self, pend, k):
         st, B, recv, work = pend
-        with torch.cuda.stream(st):
-            work.wait()
-            out = self._merge_recv(recv, B, B, k)
+        if work is None:  # native: recv already holds the merged (dist, ids)
+            out = recv
+        else:
+            with torch.cuda.stream(st):
+                work.wait()
+                out = self._merge_recv(recv, B, B, k)
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(st)
         for t in out:

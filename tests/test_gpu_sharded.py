@@ -110,9 +110,23 @@ def test_search_all_many_pipelined_on_rccl(device):
     try:
         X = syn.index_rows(81, 40000, D)
         six = ShardedIndex(X, device)
+        assert six._rccl_ok(5), "the native RCCL path (mpr_sharded_search_all) is not available"
         sizes = [96, 16, 256, 96, 16, 256]
         qs = [syn.index_rows(90 + j, b, D) for j, b in enumerate(sizes)]
         want = [tuple(t.cpu() for t in six.search_all(q.to(device), 5)) for q in qs]
+        # the native call equals the Python exchange (pack, torch all_gather, packed merge) and
+        # the single-index search
+        from multimodalpromptretrieval_amd.index import DeviceIndex
+        ix = DeviceIndex(X, device)
+        os.environ["MPR_SHARDED_NATIVE"] = "0"
+        try:
+            py = [tuple(t.cpu() for t in six.search_all(q.to(device), 5)) for q in qs]
+        finally:
+            os.environ.pop("MPR_SHARDED_NATIVE", None)
+        for (dw, iw), (dp, ip), q in zip(want, py, qs):
+            assert torch.equal(iw, ip) and torch.equal(dw, dp)
+            d1, i1 = ix.search(q.to(device), 5)
+            assert torch.equal(iw, i1.cpu()) and torch.equal(dw, d1.cpu())
 
         def fresh():  # each batch a new device tensor, unreferenced by the caller after yield
             for q in qs:
