@@ -923,15 +923,32 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_out=None, serving_an
             if el >= seconds or n >= 32:
                 break
     pairs = n * cfg["B"]
+    # one batch on ONE thread: the per-core rate, so the whole host's rate is bounded by
+    # physical cores x that (the box's share for this GPU is 16 threads: more would take other
+    # jobs' cores, so the 128-core figure is an upper bound, not a run)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        with torch.no_grad():
+            t1 = time.perf_counter()
+            pipeline.predict(cpu_batches[0], retr_sd, tok_sd, t5_sd, heads, X, answers, info,
+                             cfg["k"], False, clip_tokenize, tok, 20, forced_steps=True)
+            one = cfg["B"] / (time.perf_counter() - t1)
+    finally:
+        torch.set_num_threads(nt)
     model, phys, avail = host_cpu()
     out = {"value": pairs / el, "unit": "QA pairs/s", "cores": torch.get_num_threads(),
            "kind": "port",
            "sample": f"{n} batches x {cfg['B']} QA pairs of the same workload ({el:.1f} s), "
                      f"oracle/pipeline.py (torch-CPU fp32, KV-cached greedy, 20 forced steps)",
            "cpu_model": model, "host_physical_cores": phys, "host_cpus_available": avail,
+           "one_thread_value": round(one, 2),
+           "whole_host_bound": round(one * phys, 1) if phys else None,
            "cores_note": "threads = this job's CPU share on the GPU box (OMP_NUM_THREADS, 16 per "
-                         "GPU: the box's 8 GPUs' jobs share its physical cores; SURVEY.md §8(d) "
-                         "asks for the available cores)"}
+                         "GPU: the box's 8 GPUs' jobs share its physical cores, so the run stays "
+                         "inside that share; SURVEY.md §8(d) asks for os.cpu_count()); "
+                         "whole_host_bound = one_thread_value x physical cores, a perfect-scaling "
+                         "upper bound on the whole host's CPU rate"}
     if gpu_out is not None:
         # forced steps keep finished rows on pad, as the device loop does: the decoded answers
         # compare as strings
