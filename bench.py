@@ -160,8 +160,9 @@ def _projected_shard_class():
         """One rank's shard of a W-rank row-sharded index, run on a world-1 RCCL group: the
         product's ShardedIndex (local scan, pack, all_gather, merge) whose all_gather fills
         block 0 of a [W, B, k] receive buffer whose other W - 1 blocks hold this shard's first
-        top-k again with ids offset by the shard size (written once, untimed), so the merge
-        reads W x k candidates per query as rank r of W does.  Two receive buffers alternate (two
+        top-k again with ids offset by the shard size and distances set to +inf (written once,
+        untimed), so the merge reads and orders W x k candidates per query as rank r of W does
+        and returns this shard's own top-k.  Two receive buffers alternate (two
         batches are in flight).  Used by the one-GPU strong-scaling projection only."""
 
         def __init__(self, rows, device, virtual_world: int, group=None):
@@ -177,7 +178,12 @@ def _projected_shard_class():
                 offs = (torch.arange(W, device=packed.device, dtype=torch.float64)
                         .repeat_interleave(B) * self.n_local)
                 rest[..., 1] += offs[:, None]
+                # the stand-in shards' candidates rank behind this shard's (+inf distances):
+                # the merge still reads and orders all W x k of them, and its result is this
+                # shard's own top-k (copies at equal distances would win ties by fill order)
+                rest[B:, :, 0] = float("inf")
                 self._recv = [rest, rest.clone()]
+                torch.cuda.current_stream(packed.device).synchronize()
             recv = self._recv[self._calls % 2]
             self._calls += 1
             return recv

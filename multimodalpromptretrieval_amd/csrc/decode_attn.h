@@ -1,7 +1,9 @@
 // decode_attn.h — one-query decode attention of one (batch, head) pair by one wave, with few keys
-// (Lk <= 128): the body of layers.hip's attention_decode_wave_kernel, shared with the fused
-// qkv-GEMV + self-attention of the decode chain (gemm.hip, SKF_ATTN).  One definition, so both
-// give the same bits (and those of attention_decode_kernel: see layers.hip).
+// (Lk <= 128): the body of layers.hip's attention_decode_wave_kernel (bit-identical to
+// attention_decode_kernel: see layers.hip), as a device function a kernel can call per pair.
+// (Round 5 used it for a q|k|v GEMV with the step's self-attention fused in by the last-arriving
+// tile block of each head: bit-identical tokens, but 225 -> 298 us per 16-row t5-small step and
+// 631 -> 824 for t5-base, profiles/r05_decode_fuse_ab.txt; removed, git show fe367d2.)
 #pragma once
 
 #include "kernels.h"

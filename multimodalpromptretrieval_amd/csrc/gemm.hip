@@ -17,7 +17,6 @@
 #include <algorithm>
 #include <cstring>
 
-#include "decode_attn.h"
 #include "kernels.h"
 #include "x3.h"
 
@@ -960,7 +959,7 @@ __global__ __launch_bounds__(256) void pack_rows16_kernel(const float* __restric
 // per-row scale of SKF_RSCALE); SKF_RSCALE: the epilogue scales row m by rsqrt(mean(src_m^2) +
 // eps) of an external row (the decode chain's folded RMSNorm, t5.hip).
 enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8, SKF_RELU_IN = 16,
-             SKF_RSCALE = 32, SKF_SSQ = 64, SKF_ATTN = 128 };
+             SKF_RSCALE = 32, SKF_SSQ = 64 };
 
 // NT 16-column tiles per block share the activation slab (NT > 1 for the 32k-column lm_head,
 // which needs more bytes in flight per wave); two accumulator chains per tile halve the
@@ -972,9 +971,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   constexpr bool RMS = (F & SKF_RMS) != 0, RES = (F & SKF_RES) != 0,
                  RELU = (F & SKF_RELU) != 0, AMAX = (F & SKF_AMAX) != 0,
                  RELU_IN = (F & SKF_RELU_IN) != 0, RSCALE = (F & SKF_RSCALE) != 0,
-                 SSQ = (F & SKF_SSQ) != 0, ATTN = (F & SKF_ATTN) != 0;
+                 SSQ = (F & SKF_SSQ) != 0;
   static_assert(!(RMS && RSCALE), "one row-scale source");
-  static_assert(!ATTN || (NT == 1 && MR == 1), "fused attention: one tile, <= 16 rows per block");
   constexpr int MROWS = 16 * MR;      // activation rows: MR 16-row groups share each weight load
   const GemmArgs& a = sa.g;
   constexpr int XLD = MAXC * 16 + 4;  // slab row stride (floats): conflict-free fragment reads
@@ -1182,37 +1180,6 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
           sa.ssq_out[(int64_t)(row0 + m) * (sa.ssq_cols / 16) + tile] = q;
       }
     }
-  }
-  if constexpr (ATTN) {
-    // Hand-off to the head's last tile block (MI355X_MICROARCH.md "Valid forms"): every storing
-    // wave drains its stores, the block barrier, ONE lane's agent release + drain + agent-scope
-    // add; the add that returns count - 1 is the last arrival: agent acquire + drain + barrier,
-    // then plain loads of the q | k | v row the other blocks wrote.
-    __shared__ int s_head;
-    const int inner = sa.attn.H * dattn::D;
-    const int hh = ((int)blockIdx.x * 16 % inner) / dattn::D;
-    if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int old = __hip_atomic_fetch_add(sa.attn_ctr + hh, 1, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = old == 3 * (dattn::D / 16) - 1;
-      if (last) {
-        __hip_atomic_store(sa.attn_ctr + hh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      s_head = last ? hh : -1;
-    }
-    __syncthreads();
-    const int hl = s_head;
-    if (hl < 0) return;
-    // wave w: rows w, w + 8 of head hl; Ps (128) and Os (8 x 64) in the wave's own slab
-    float* Ps = smem + wave * MROWS * XLD;
-    float(*Os)[dattn::D] = reinterpret_cast<float(*)[dattn::D]>(Ps + 128);
-    for (int b = wave; b < M; b += SK_WAVES) dattn::pair(sa.attn, b, hl, Ps, Os);
   }
 }
 
@@ -1553,10 +1520,6 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, un
       MPR_SK(SKF_RELU_IN | SKF_RSCALE | SKF_RES) MPR_SK(SKF_SSQ)
       default: break;
     }
-    if constexpr (MR == 1) switch (F) {
-      MPR_SK(SKF_RMS | SKF_ATTN)
-      default: break;
-    }
   }
 #undef MPR_SK
 }
@@ -1589,12 +1552,7 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const int F = (sa.rms_w ? SKF_RMS : 0) | (a.R ? SKF_RES : 0) |
                 (a.act == ACT_RELU ? SKF_RELU : 0) | (amax ? SKF_AMAX : 0) |
                 (sa.relu_in ? SKF_RELU_IN : 0) | (sa.rs_part ? SKF_RSCALE : 0) |
-                (sa.ssq_out ? SKF_SSQ : 0) | (sa.attn_ctr ? SKF_ATTN : 0);
-  MPR_REQUIRE(!(F & SKF_ATTN) ||
-                  (F == (SKF_RMS | SKF_ATTN) && a.M <= 16 && a.N == 3 * sa.attn.H * 64 &&
-                   sa.attn.B == a.M && sa.attn.Lk <= 128 && cdiv(cdiv(a.K, 16), SK_WAVES) <= 8),
-              "gemm_skinny: fused attention only on a <= 16-row q|k|v GEMV with RMSNorm, <= 128 "
-              "keys");
+                (sa.ssq_out ? SKF_SSQ : 0);
   MPR_REQUIRE(!(F & (SKF_RELU_IN | SKF_RSCALE)) || F == (SKF_RELU_IN | SKF_RSCALE | SKF_RES),
               "gemm_skinny: relu_in / row scale only as the folded FFN-out (relu_in + scale + "
               "residual)");

@@ -116,13 +116,6 @@ struct SkinnyArgs {
   const float* rs_part = nullptr;
   int rs_nparts = 0;
   int rs_n = 0;
-  // Fused self-attention of a decode step (t5.hip, MPR_DECODE_FUSE_ATTN): this GEMV writes the
-  // step's q | k | v row (N = 3 H 64, <= 16 rows); each 16-column tile's block counts itself in
-  // attn_ctr[head] (agent-scope release / atomic add), and the last of a head's 3 x 4 tile blocks
-  // runs that head's attention for every row (decode_attn.h) into attn.o.  attn_ctr: H ints, zero
-  // between launches (the last arriver resets its head's).
-  AttnArgs attn;
-  int* attn_ctr = nullptr;
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 

@@ -227,16 +227,6 @@ bool T5Model::tiled_head(int B) const {
   return on && B > 32 && !fold_rows(B);
 }
 
-// MPR_DECODE_FUSE_ATTN=1: the folded chain's q | k | v GEMV also runs the step's self-attention
-// (gemm.hip SKF_ATTN: the last of each head's 12 tile blocks, after an agent-scope hand-off, runs
-// that head for every row with attention_decode_wave_kernel's arithmetic): 6 -> 5 launches per
-// layer, bit-identical tokens.  Read per call (a captured decode graph keeps the form it was
-// captured with).
-bool T5Model::fuse_attn(int B, int max_new) const {
-  const char* e = getenv("MPR_DECODE_FUSE_ATTN");
-  return e && e[0] == '1' && fold_rows(B) && B <= 16 && max_new <= 128 && dkv == 64;
-}
-
 int T5Model::build_folded(hipStream_t s) {
   const int K = inner + d;
   MPR_REQUIRE(d % 16 == 0 && inner % 16 == 0 && dff % 16 == 0, "fold: d=%d inner=%d dff=%d", d,
@@ -585,7 +575,6 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
   const float* ckv = ws->cross_kv.as<float>();
   const int64_t ckv_ld = (int64_t)Ld * 2 * inner;
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
-  const bool fuse = fuse_attn(B, max_new);
   for (int t = t0; t < t1; ++t) {
     for (int l = 0; l < Ld; ++l) {
       const T5Layer& ly = *dec[l];
@@ -602,12 +591,8 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       sq.g.A = xp; sq.g.lda = ldA;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      if (fuse) {  // the self-attention below runs inside this launch
-        sq.attn = at;
-        sq.attn_ctr = ws->attn_ctr.as<int>();
-      }
       MPR_TRY(dec_gemm(sq, ly.pk_qkv, s));
-      if (!fuse) MPR_TRY(attention(at, s));
+      MPR_TRY(attention(at, s));
       SkinnyArgs so;  // [x1 | u] = [a | x] W_ocq^T
       so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
       so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
@@ -748,12 +733,6 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
     MPR_TRY(grow(ws->hz, (size_t)B * (d + dff) * 4));
     MPR_TRY(grow(ws->x1ss, (size_t)B * (d / 16) * 4));
     MPR_TRY(grow(ws->x2ss, (size_t)B * (d / 16) * 4));
-    if (fuse_attn(B, max_new)) {
-      const void* before = ws->attn_ctr.ptr;
-      MPR_TRY(grow(ws->attn_ctr, (size_t)H * 4));
-      if (ws->attn_ctr.ptr != before)
-        MPR_HIP(hipMemsetAsync(ws->attn_ctr.ptr, 0, (size_t)H * 4, s));
-    }
   }
   MPR_TRY(grow(ws->part_val, (size_t)nparts * 16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->part_idx, (size_t)nparts * 16 * MAX_GROUPS * 4));

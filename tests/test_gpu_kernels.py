@@ -177,7 +177,8 @@ def test_topk_merge_packed_equals_unpacked(device, index_mod, W, Bp, b, kc, k, m
     packed = torch.empty((W, Bp, kc, 2), device=device, dtype=torch.float64)
     _lib.call("mpr_topk_pack", _lib.ptr(dd), _lib.ptr(ii), dd.numel(), _lib.ptr(packed),
               _lib.stream_ptr(device))
-    assert torch.equal(packed[..., 0].cpu(), d.double())
+    assert torch.equal(packed[..., 0].cpu().nan_to_num(-7.0), d.double().nan_to_num(-7.0))
+    assert torch.equal(packed[..., 1].cpu(), ids.double())
     od = torch.empty((b, k), device=device)
     oi = torch.empty((b, k), device=device, dtype=torch.int64)
     _lib.call("mpr_topk_merge_packed", _lib.ptr(packed), W, Bp, b, kc, k, metric, _lib.ptr(od),
