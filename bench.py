@@ -338,10 +338,11 @@ def c5_projection(device, iters: int = 20):
     out["model"] = (f"per rank: the W-shard search (timed) + merge of W x {k} candidates (timed behind the "
                     f"search: the marginal GPU-timeline cost) + "
                     f"all_gather {AG_ALPHA_US} us + bytes / {AG_BETA_GBS} GB/s (modelled); "
-                    f"pipelined: ShardedIndex.search_all_many itself (two batches in flight on "
-                    f"its two streams, a real all_gather on a world-1 RCCL group, the merge of "
-                    f"W x {k} candidates per query), per batch max(that measured time, the "
-                    f"all_gather model), against the one-GPU DeviceIndex.search on two "
+                    f"pipelined: ShardedIndex.search_all_many itself on a world-1 RCCL group "
+                    f"(two batches in flight on its two streams, each one mpr_sharded_search_all "
+                    f"call: local scan, pack, the merge of W x {k} candidates per query; at one "
+                    f"rank there is no collective to make), per batch max(that measured time, "
+                    f"the all_gather model), against the one-GPU DeviceIndex.search on two "
                     f"alternating streams")
     return out
 

@@ -95,7 +95,8 @@ int mpr_topk_merge_packed(const double* packed_dev, int32_t W, int32_t Bp, int32
  * this rank's local search (index rows carry their global ids through row_offset), its top-k
  * packed into block `rank` of recv ((NaN, -1) past a tiny shard's rows), ncclAllGather in place
  * on `comm` (an RCCL communicator of `world` ranks: PyTorch's, ProcessGroupNCCL._comm_ptr(); the
- * RCCL library already loaded in the process is used), then the merge of recv's n_blocks >= world
+ * RCCL library already loaded in the process is used; none at world 1), then the merge of recv's
+ * n_blocks >= world
  * blocks [n_blocks][b][k][2] (blocks past world: candidates the caller placed there) into
  * out_dist / out_ids [b, k].  Replaces dataset/VQAFeatureDataset.py:192-197 over a sharded index;
  * the same results as mpr_index_search over the whole index up to fp32 rounding ties (exact ties

@@ -251,8 +251,10 @@ int mpr_sharded_search_all(mpr_index* ix, void* comm, int32_t world, int32_t ran
     const size_t count = (size_t)b * k * 2;  // this rank's block, float64 words
     double* mine = recv + (size_t)rank * count;
     MPR_TRY(topk_pack(ld, li, (int64_t)b * k, mine, S(stream), kk, k));
-    const int rc = ag(mine, recv, count, NCCL_FLOAT64, comm, S(stream));  // in place
-    MPR_REQUIRE(rc == 0, "sharded_search: ncclAllGather returned %d", rc);
+    if (world > 1) {  // (one rank: its block is the whole exchange)
+      const int rc = ag(mine, recv, count, NCCL_FLOAT64, comm, S(stream));  // in place
+      MPR_REQUIRE(rc == 0, "sharded_search: ncclAllGather returned %d", rc);
+    }
     return merge_packed(recv, n_blocks, b, b, k, k, ix->metric, out_dist, out_ids, S(stream));
   });
 }
