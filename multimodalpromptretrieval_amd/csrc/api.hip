@@ -251,7 +251,10 @@ int mpr_sharded_search_all(mpr_index* ix, void* comm, int32_t world, int32_t ran
     const size_t count = (size_t)b * k * 2;  // this rank's block, float64 words
     double* mine = recv + (size_t)rank * count;
     MPR_TRY(topk_pack(ld, li, (int64_t)b * k, mine, S(stream), kk, k));
-    if (world > 1) {  // (one rank: its block is the whole exchange)
+    // (one rank: its block is the whole exchange; MPR_SHARDED_FORCE_COLLECTIVE=1 keeps the call,
+    // so a one-GPU test exercises the RCCL path)
+    const bool force = getenv("MPR_SHARDED_FORCE_COLLECTIVE") != nullptr;
+    if (world > 1 || force) {
       const int rc = ag(mine, recv, count, NCCL_FLOAT64, comm, S(stream));  // in place
       MPR_REQUIRE(rc == 0, "sharded_search: ncclAllGather returned %d", rc);
     }

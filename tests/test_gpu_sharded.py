@@ -105,6 +105,9 @@ def test_search_all_many_pipelined_on_rccl(device):
     from multimodalpromptretrieval_amd.distributed import ShardedIndex
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
+    # keep the in-place ncclAllGather at world 1 (libmpr reads it per call): the RCCL
+    # call itself (dlsym'd ncclAllGather on PyTorch's communicator) runs here
+    os.environ["MPR_SHARDED_FORCE_COLLECTIVE"] = "1"
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0,
                             world_size=1, device_id=device)
     try:
@@ -143,4 +146,5 @@ def test_search_all_many_pipelined_on_rccl(device):
         for d, i in outs:
             assert torch.equal(i, i1) and torch.equal(d, d1)
     finally:
+        os.environ.pop("MPR_SHARDED_FORCE_COLLECTIVE", None)
         dist.destroy_process_group()
