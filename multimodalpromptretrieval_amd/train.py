@@ -263,6 +263,10 @@ class T5LossFn(torch.autograd.Function):
 
 
 _TRAINERS = {}
+# The native trainer's initial relative-position LUT radius (t5.LUT_RADIUS when None); its LUTs
+# grow past it on demand (trainer.hip grow_luts).  The attention kernels take sequences of up to
+# 1024 keys (max_source_length 512 + 50 image tokens is 562).
+LUT_RADIUS_INIT = None
 
 
 class T5Config:
@@ -284,17 +288,18 @@ class T5Config:
         and scratch are reused step to step)."""
         cfg = (self.d, self.inner // self.H, self.H, self.d_ff, self.n_enc, self.n_dec,
                self.vocab, self.num_buckets, 1 if self.scale_out else 0)
-        key = (cfg, self.max_distance, str(device))
+        from .t5 import LUT_RADIUS
+        radius = int(LUT_RADIUS_INIT or LUT_RADIUS)
+        key = (cfg, self.max_distance, str(device), radius)
         tr = _TRAINERS.get(key)
         if tr is None:
-            from .t5 import LUT_RADIUS
-            rel = torch.arange(-LUT_RADIUS, LUT_RADIUS + 1, dtype=torch.long)
+            rel = torch.arange(-radius, radius + 1, dtype=torch.long)
             luts = [relative_position_bucket(rel, bi, self.num_buckets, self.max_distance)
                     for bi in (True, False)]
             tr = _lib.ctypes.c_void_p()
             _lib.call("mpr_t5_trainer_create", _lib.int_array(cfg), len(cfg),
                       _lib.int_array(luts[0].tolist()), _lib.int_array(luts[1].tolist()),
-                      LUT_RADIUS, _lib.ctypes.byref(tr))
+                      radius, _lib.ctypes.byref(tr))
             _TRAINERS[key] = tr
         return tr
 

@@ -120,23 +120,27 @@ def test_g11_t5_small_gradients(device):
     _check_grads(params, z, full=False, tol=G11_TOL)
 
 
-def test_long_source_beyond_lut_radius(device):
-    """An encoder source longer than the trainer's bucket LUT radius (1024; ADVICE r04: the
-    trainer used to refuse it, HF T5 has no limit): the LUTs grow by repeating their saturated
-    end buckets, and the loss and every gradient match the oracle (torch-CPU autograd through
-    oracle/t5.py, whose buckets are computed per offset) at G2 size.  trim_trainers then hands
-    the arenas back and the next step re-grows them."""
+def test_long_source_beyond_lut_radius(device, monkeypatch):
+    """An encoder source longer than the trainer's bucket LUT radius (the trainer
+    refused L or T past its radius; HF T5 has no such limit): the LUTs grow by repeating their
+    saturated end buckets, and the loss and every gradient match the oracle (torch-CPU autograd
+    through oracle/t5.py, whose buckets are computed per offset) at G2 size.  The trainer here
+    starts at radius 256 with L = 600 (the attention kernels' own bound is 1024 keys: a longer
+    source is refused with an error, not run wrong).  trim_trainers then hands the arenas back
+    and the next step re-grows them."""
+    from multimodalpromptretrieval_amd import train
     from multimodalpromptretrieval_amd.train import t5_loss, trim_trainers
     from oracle import t5 as ot5
+    monkeypatch.setattr(train, "LUT_RADIUS_INIT", 256)
     t5cfg = gi.g2_models()[4]
     sd = syn.t5_state_dict(gi.G2["seeds"]["t5"], t5cfg)
     keep = [n for n in sd if n not in ("lm_head.weight", "encoder.embed_tokens.weight",
                                        "decoder.embed_tokens.weight")]
     g = torch.Generator().manual_seed(5)
-    B, L, T = 2, 1100, 4
+    B, L, T = 2, 600, 4
     emb = torch.randn((B, L, t5cfg.d_model), generator=g) * 0.5
     mask = torch.ones((B, L))
-    mask[1, 1000:] = 0
+    mask[1, 500:] = 0
     labels = torch.randint(2, t5cfg.vocab_size - 1, (B, T), generator=g)
     for rep in range(2):
         params = {n: torch.nn.Parameter(sd[n].clone().to(device)) for n in keep}
@@ -155,6 +159,10 @@ def test_long_source_beyond_lut_radius(device):
     bad = [(n, _rel(params[n].grad, ref[n].grad)) for n in keep
            if _rel(params[n].grad, ref[n].grad) > GRAD_TOL]
     assert not bad, bad
+    long_emb = torch.randn((1, 1100, t5cfg.d_model), generator=g).to(device)
+    with pytest.raises(RuntimeError, match="Lk=1100"):
+        t5_loss(params, long_emb, torch.ones((1, 1100), device=device), labels[:1].to(device),
+                num_heads=t5cfg.num_heads)
 
 
 def test_adamw_steps_lower_the_loss_and_refresh_predict(device):
