@@ -138,9 +138,10 @@ int mpr_index_destroy(mpr_index* index) {
 
 int64_t mpr_index_rows(const mpr_index* index) { return index ? index->n : -1; }
 
-int mpr_index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_t* ids,
-                     float* dist, void* stream) {
-  return guarded([&]() -> int {
+namespace {
+int index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_t* ids, float* dist,
+                 void* stream, double* pack_out = nullptr, bool* packed = nullptr) {
+  {
     MPR_REQUIRE(ix != nullptr, "search: null index");
     MPR_REQUIRE(b == 0 || (q && ids && dist), "search: null buffer");
     if (b == 0) return MPR_OK;
@@ -171,8 +172,14 @@ int mpr_index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_
     ix->last_coarse_b[stream] = xb ? b : 0;
     return scan_topk(ix->rows.as<float>(), ix->norms.as<float>(), ix->n, ix->d, ix->row_offset,
                      ix->metric, q, b, k, slot->as<float>(), slot->bytes, dist, ids, S(stream),
-                     xb, xmax);
-  });
+                     xb, xmax, pack_out, packed);
+  }
+}
+}  // namespace
+
+int mpr_index_search(mpr_index* ix, const float* q, int32_t b, int32_t k, int64_t* ids,
+                     float* dist, void* stream) {
+  return guarded([&]() -> int { return index_search(ix, q, b, k, ids, dist, stream); });
 }
 
 int mpr_index_coarse_fallbacks(mpr_index* ix, void* stream, int32_t* count) {
@@ -247,10 +254,11 @@ int mpr_sharded_search_all(mpr_index* ix, void* comm, int32_t world, int32_t ran
     MPR_TRY(slot->ensure((size_t)b * kk * 12 + 256));
     float* ld = slot->as<float>();
     int64_t* li = reinterpret_cast<int64_t*>(ld + ((size_t)b * kk + 63) / 64 * 64);
-    MPR_TRY(mpr_index_search(ix, q, b, kk, li, ld, stream));
     const size_t count = (size_t)b * k * 2;  // this rank's block, float64 words
     double* mine = recv + (size_t)rank * count;
-    MPR_TRY(topk_pack(ld, li, (int64_t)b * k, mine, S(stream), kk, k));
+    bool packed = false;  // the coarse path packs on the way (its gated merge)
+    MPR_TRY(index_search(ix, q, b, kk, li, ld, stream, kk == k ? mine : nullptr, &packed));
+    if (!packed) MPR_TRY(topk_pack(ld, li, (int64_t)b * k, mine, S(stream), kk, k));
     // (one rank: its block is the whole exchange; MPR_SHARDED_FORCE_COLLECTIVE=1 keeps the call,
     // so a one-GPU test exercises the RCCL path)
     const bool force = getenv("MPR_SHARDED_FORCE_COLLECTIVE") != nullptr;

@@ -205,7 +205,7 @@ int scale_inplace(float* p, int64_t n, float scale, hipStream_t s);
 // gate (optional, per query): 0 skips the query.
 int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
-                const int* gate);
+                const int* gate, double* pack_out = nullptr);
 // the sharded search's exchange (select.hip): (dist, id) -> float64 pairs; merge of packed
 // [W][Bp][kc][2] candidate lists for query slots < b (keys are values)
 // (rows of kk pairs padded to k with (NaN, -1) when kk < k; n = rows * k)
@@ -218,10 +218,12 @@ int merge_packed(const double* packed, int W, int Bp, int b, int kc, int k, int 
 constexpr int SELECT_MAX_K = 16384;
 int select_large(const float* keys, const int64_t* ids, int b, int64_t n, int k, float sign,
                  int64_t id_offset, float* od, int64_t* oi, hipStream_t s);
+// pack_out (optional): the results also as float64 (dist, id) pairs [b][k][2] when the search
+// can write them on the way (the coarse path's gated merge); *packed tells whether it did
 int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
               int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
               float* out_dist, int64_t* out_ids, hipStream_t s, const void* Xb = nullptr,
-              const float* xmax = nullptr);
+              const float* xmax = nullptr, double* pack_out = nullptr, bool* packed = nullptr);
 size_t scan_topk_workspace(int64_t n, int b, int k);
 bool scan_coarse_eligible(int64_t n, int d, int b, int k, int metric);
 // queries of the last coarse search on workspace `ws` that needed the exact fallback (host sync)

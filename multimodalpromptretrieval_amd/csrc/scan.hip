@@ -1118,8 +1118,8 @@ int launch_scan(const float* X, const float* xnorm, int64_t n, int d, int64_t ro
 
 int merge_dispatch(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                    int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
-                   const int* gate = nullptr) {
-  return merge_lists(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate);
+                   const int* gate = nullptr, double* pack_out = nullptr) {
+  return merge_lists(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate, pack_out);
 }
 
 }  // namespace
@@ -1135,12 +1135,21 @@ int scan_mm_rowblocks(int64_t n, int b) {
   const int64_t rb = std::max<int64_t>(1, 512 / nqt);  // ~2 blocks per CU
   return (int)std::min(rb, ntile);
 }
+// As the coarse path's gated fallback the scan runs on few row blocks (8 per query tile): when no
+// query is flagged (the common case) its blocks exit at once, and a grid of 32 exits in ~2 us
+// where 512 blocks of this LDS-heavy kernel took ~5 us and, beside another stream's coarse scan,
+// waited for CUs (profiles/r05_proj_w8_kernel_stats.csv); a flagged query tile scans with 8
+// blocks instead of ~128 (rare: rows within the coarse error bound overflowing the candidate
+// list).  Any row blocking gives the same keys and the same exact top k.
+int scan_mm_rb(int64_t n, int b, bool gated) {
+  return gated ? std::min(scan_mm_rowblocks(n, b), 8) : scan_mm_rowblocks(n, b);
+}
 
 template <int K>
 int launch_scan_mm(const float* X, int64_t n, int d, int64_t row_offset, int metric,
                    const float* Q, float* qn, int b, float* ck, int64_t* ci, hipStream_t s,
                    const int* gate, const float* qn_pre) {
-  const int nqt = (int)cdiv(b, SM_B), RB = scan_mm_rowblocks(n, b);
+  const int nqt = (int)cdiv(b, SM_B), RB = scan_mm_rb(n, b, gate != nullptr);
   if (qn_pre)
     qn = const_cast<float*>(qn_pre);
   else
@@ -1265,7 +1274,8 @@ size_t scan_topk_workspace(int64_t n, int b, int k) {
 int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_offset,
               int metric, const float* Q, int b, int k, float* ws, size_t ws_bytes,
               float* out_dist, int64_t* out_ids, hipStream_t s, const void* Xb,
-              const float* xmax) {
+              const float* xmax, double* pack_out, bool* packed) {
+  if (packed) *packed = false;
   MPR_REQUIRE(k >= 1 && k <= SELECT_MAX_K, "search: k=%d must be in [1, %d]", k, SELECT_MAX_K);
   MPR_REQUIRE(k <= n, "search: k=%d exceeds index rows %lld", k, (long long)n);
   MPR_REQUIRE(d % 16 == 0 && d <= 8192, "search: d=%d must be a multiple of 16", d);
@@ -1315,7 +1325,7 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     gate = w.gate;
   }
   if (use_scan_mm(n, d, b, k) && !getenv("MPR_SCAN_MM_OFF")) {
-    const int RB = scan_mm_rowblocks(n, b);
+    const int RB = scan_mm_rb(n, b, gate != nullptr);
     int64_t* ci = reinterpret_cast<int64_t*>(ws);
     float* ck = reinterpret_cast<float*>(ci + (size_t)b * RB * K);
     float* qn = ck + (size_t)b * RB * K;
@@ -1328,8 +1338,12 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
 #undef MPR_SM
     }
     if (rc != MPR_OK) return rc;
+    // the coarse path's gated merge also writes every query's packed pair when asked (the wave
+    // merge: <= 512 candidates, k <= 8)
+    double* po = (gate && pack_out && (int64_t)RB * K <= 512 && k <= 8) ? pack_out : nullptr;
+    if (po && packed) *packed = true;
     return merge_dispatch(ck, ci, b, (int64_t)RB * K, k, /*keys_are_values=*/0, metric, out_dist,
-                          out_ids, s, gate);
+                          out_ids, s, gate, po);
   }
   MPR_REQUIRE(gate == nullptr, "search: coarse path without its exact fallback");
   const bool small = use_scan_small(n, d, b);

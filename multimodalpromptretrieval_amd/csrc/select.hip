@@ -108,6 +108,9 @@ constexpr int MW_MAX = 512;
 // (dist, id) float64 pairs [W shards][Bp query slots][kc][2] (distributed.py); query q's list is
 // shard-major, candidate c = (shard c / kc, rank c % kc) — the order of the unpacked [b, W kc]
 // lists, so the outputs are the unpacked merge's.
+// pack_out (gated merges only): every query's final (dist, id) also as float64 pairs
+// [b][k][2] — a query the gate skips copies the re-rank's result already in out_val / out_id —
+// so the sharded search's exchange needs no separate pack launch (mpr_sharded_search_all).
 template <int K, bool PK = false>
 __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
                                                          const int64_t* cand_id, int64_t n_cand,
@@ -115,9 +118,16 @@ __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
                                                          int metric, float* out_val,
                                                          int64_t* out_id, const int* gate,
                                                          const double* packed = nullptr,
-                                                         int Bp = 0, int kc = 1) {
+                                                         int Bp = 0, int kc = 1,
+                                                         double2* pack_out = nullptr) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (q >= b || (gate && gate[q] == 0)) return;  // wave-uniform
+  if (q >= b) return;  // wave-uniform
+  if (gate && gate[q] == 0) {
+    if (pack_out && lane < k)
+      pack_out[(int64_t)q * k + lane] =
+          make_double2((double)out_val[(int64_t)q * k + lane], (double)out_id[(int64_t)q * k + lane]);
+    return;
+  }
   const float* ck = PK ? nullptr : cand_key + (int64_t)q * n_cand;
   const int64_t* ci = PK ? nullptr : cand_id + (int64_t)q * n_cand;
   const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
@@ -159,8 +169,11 @@ __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
     if (lane == 0) {
       const bool none = m == ~0ull;
       const float kk = word_key(m);
-      out_val[(int64_t)q * k + r] = none ? NAN : (metric == 1 ? -kk : kk);
-      out_id[(int64_t)q * k + r] = none ? -1 : (int64_t)(uint32_t)m;
+      const float v = none ? NAN : (metric == 1 ? -kk : kk);
+      const int64_t id = none ? -1 : (int64_t)(uint32_t)m;
+      out_val[(int64_t)q * k + r] = v;
+      out_id[(int64_t)q * k + r] = id;
+      if (pack_out) pack_out[(int64_t)q * k + r] = make_double2((double)v, (double)id);
     }
   }
 }
@@ -274,15 +287,18 @@ __global__ __launch_bounds__(SL_NT) void select_large_kernel(const float* keys,
 template <int K>
 int launch_merge(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                  int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
-                 const int* gate) {
+                 const int* gate, double* pack_out) {
   if constexpr (K <= 8) {
     if (n_cand <= MW_MAX && !getenv("MPR_MERGE_BLOCK")) {
       hipLaunchKernelGGL((merge_wave_kernel<K>), dim3((unsigned)((b + 3) / 4)), dim3(256), 0, s,
-                         ck, ci, n_cand, b, k, keys_are_values, metric, od, oi, gate);
+                         ck, ci, n_cand, b, k, keys_are_values, metric, od, oi, gate, nullptr, 0,
+                         1, reinterpret_cast<double2*>(pack_out));
       MPR_LAUNCHED();
       return MPR_OK;
     }
   }
+  MPR_REQUIRE(!pack_out, "merge: packed output on the wave merge only (k <= 8, <= %d lists)",
+              MW_MAX);
   constexpr int NT = K >= 32 ? 128 : 256;
   hipLaunchKernelGGL((merge_kernel<K, NT>), dim3(b), dim3(NT), 0, s, ck, ci, n_cand, k,
                      keys_are_values, metric, od, oi, gate);
@@ -349,12 +365,14 @@ int merge_packed(const double* packed, int W, int Bp, int b, int kc, int k, int 
 
 int merge_lists(const float* ck, const int64_t* ci, int b, int64_t n_cand, int k,
                 int keys_are_values, int metric, float* od, int64_t* oi, hipStream_t s,
-                const int* gate) {
+                const int* gate, double* pack_out) {
+  MPR_REQUIRE(!pack_out || gate, "merge: packed output only on a gated merge");
   int c = 1;
   while (c < k) c <<= 1;
   if (c == 16) c = 32;  // merge_kernel<16, *> hangs hipcc 7.2's backend (every other K compiles)
 #define MPR_MG(K) \
-  case K: return launch_merge<K>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate);
+  case K: return launch_merge<K>(ck, ci, b, n_cand, k, keys_are_values, metric, od, oi, s, gate, \
+                                 pack_out);
   switch (c) {
     MPR_MG(1) MPR_MG(2) MPR_MG(4) MPR_MG(8) MPR_MG(32) MPR_MG(64)
   }
