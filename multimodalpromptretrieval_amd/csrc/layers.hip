@@ -353,6 +353,85 @@ __global__ __launch_bounds__(256) void attention_decode_wave_kernel(AttnArgs a) 
   dattn::pair(a, pr / a.H, pr % a.H, Ps[wave], Os[wave]);  // decode_attn.h
 }
 
+// attention_decode_wave_kernel's pairs with 65..128 keys (a grouped decode's cross-attention over
+// its encoder rows) as two waves per pair, one per 64-key half, so twice the loads of a pair are
+// in flight per CU.  The halves' maxima, sums and P.V groups meet in LDS and combine in the same
+// expressions and order as the one-wave form (fmaxf(max0, max1), (sum0 + sum1) + (0 + 0), the
+// groups 0..7 summed in order): bit-identical outputs.  4 pairs per block, 8 waves.
+__global__ __launch_bounds__(512) void attention_decode_wave2_kernel(AttnArgs a) {
+  using dattn::D;
+  __shared__ float Ps[4][128];
+  __shared__ __attribute__((aligned(16))) float Os[4][8][D];
+  __shared__ float mx[4][2], sm[4][2];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ps = wave >> 1, hf = wave & 1;  // pair slot, key half
+  const int pr = blockIdx.x * 4 + ps;
+  const bool live = pr < a.B * a.H;  // wave-uniform; dead waves still meet the barriers
+  const int b = live ? pr / a.H : 0, h = live ? pr % a.H : 0;
+  const float* qp = a.q + (int64_t)b * a.q_bs + h * D;
+  const int qpos = a.q_pos0;
+  const float* maskb = a.key_mask ? a.key_mask + (int64_t)b * a.mask_bs : nullptr;
+  const float* kb = a.k + (int64_t)b * a.k_bs + h * D;
+  const float* vb = a.v + (int64_t)b * a.v_bs + h * D;
+  int lk_end = a.Lk;
+  if (a.causal) lk_end = min(lk_end, qpos + 1);
+  float qscale = a.scale, qpart = 0.f;
+  if (a.q_rms_part && lane < a.q_rms_nparts) qpart = a.q_rms_part[(int64_t)b * a.q_rms_nparts + lane];
+  f32x4 qv[D / 4], kr[D / 4];
+#pragma unroll
+  for (int d = 0; d < D / 4; ++d) qv[d] = *reinterpret_cast<const f32x4*>(qp + 4 * d);
+  const int j = hf * 64 + lane;
+  const int jc = j < lk_end ? j : 0;
+  const float* kp = kb + (int64_t)jc * a.k_rs;
+#pragma unroll
+  for (int d = 0; d < D / 4; ++d) kr[d] = *reinterpret_cast<const f32x4*>(kp + 4 * d);
+  const float* mp = maskb ? maskb + jc : kp;
+  const float* bp = a.rel_tab ? a.rel_tab + (int64_t)(jc - qpos + a.lut_radius) * a.H + h : kp;
+  const float mraw = *mp, braw = *bp;
+  // this half's P.V operands, issued with the key loads
+  const int dg = lane & 15, kq = lane >> 4;
+  f32x4 vr[16];
+  {
+    const int jv0 = (hf * 4 + kq) * 16;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int jv = jv0 + u < lk_end ? jv0 + u : 0;
+      vr[u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)jv * a.v_rs + 4 * dg);
+    }
+  }
+  if (a.q_rms_part)
+    qscale = a.scale * (1.0f / sqrtf(dattn::wsum(qpart) / (float)a.q_rms_n + a.q_rms_eps));
+  const float mk = maskb ? mraw : 1.f, rb = a.rel_tab ? braw : 0.f;
+  float sd = 0.f;
+#pragma unroll
+  for (int d = 0; d < D / 4; ++d)
+    sd += qv[d][0] * kr[d][0] + qv[d][1] * kr[d][1] + qv[d][2] * kr[d][2] + qv[d][3] * kr[d][3];
+  const bool valid = j < lk_end && mk != 0.f;
+  const float sc = valid ? sd * qscale + rb : -INFINITY;
+  const float hmax = dattn::wmax(sc);
+  if (lane == 0) mx[ps][hf] = hmax;
+  __syncthreads();
+  const float mnew = fmaxf(mx[ps][0], mx[ps][1]);
+  const float p = valid ? expf(sc - mnew) : 0.f;
+  const float hsum = dattn::wsum(p);
+  if (lane == 0) sm[ps][hf] = hsum;
+  Ps[ps][hf * 64 + lane] = p;
+  __syncthreads();
+  const float l = (sm[ps][0] + sm[ps][1]) + (0.f + 0.f);
+  const int g = hf * 4 + kq;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 16; ++u) o += Ps[ps][g * 16 + u] * vr[u];
+  *reinterpret_cast<f32x4*>(&Os[ps][g][4 * dg]) = o;
+  __syncthreads();
+  if (hf == 0 && live) {
+    float acc = 0.f;
+    for (int gg = 0; gg < 8; ++gg) acc += Os[ps][gg][lane];
+    a.o[(int64_t)b * a.o_bs + h * D + lane] = acc / l;
+  }
+}
+
 // ---- short-sequence attention on MFMA ----------------------------------------------------------
 // Block = one (batch, head) and up to 64 queries (4 waves x 16-query tiles), Lk <= ATT_MFMA_MAXK,
 // head dim 64, on v_mfma_f32_16x16x4_f32 (exact f32 products, 4-deep k steps).  The block stages
@@ -831,8 +910,13 @@ int attention(const AttnArgs& a, hipStream_t s) {
     const bool wave_ok = !(we && we[0] == '0');
     const int lk_end = a.causal ? std::min(a.Lk, a.q_pos0 + 1) : a.Lk;
     if (wave_ok && lk_end <= 128 && (int64_t)a.B * a.H >= 512) {
-      hipLaunchKernelGGL(attention_decode_wave_kernel,
-                         dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(256), 0, s, a);
+      const char* w2 = getenv("MPR_ATT_WAVE2");  // read per call (as MPR_ATT_WAVE)
+      if (lk_end > 64 && !(w2 && w2[0] == '0'))  // two 64-key halves: a wave each
+        hipLaunchKernelGGL(attention_decode_wave2_kernel,
+                           dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL(attention_decode_wave_kernel,
+                           dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(256), 0, s, a);
       MPR_LAUNCHED();
       return MPR_OK;
     }

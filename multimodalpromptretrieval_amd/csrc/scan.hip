@@ -830,7 +830,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
 // Sufficient when nothing was cut off: every list's bound > T and the gather did not overflow
 // (a row missing from every list has a key >= its lane's bound).  Same outputs as the select +
 // rerank_block pair whenever both are exact.
-template <int K>
+template <int K, int DIAG = 0>  // DIAG > 0: timing-only early exits (MPR_RERANK_DIAG; garbage out)
 __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
     const float* __restrict__ cand_key, const int64_t* __restrict__ cand_id, int n_lists,
     const float* __restrict__ X, const float* __restrict__ xnorm, int d, int64_t row_offset,
@@ -883,6 +883,11 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
 #pragma unroll
   for (int j = 0; j < 2; ++j) qv[j] = tid + 256 * j < d ? qp[tid + 256 * j] : 0.f;
   const float xm0 = xmax[0], xm1 = xmax[1];
+  if constexpr (DIAG == 1) {  // loads only
+    if (tid == 0) gate[qi] = (lk[0][0] == 12345.f && lid[0][0] == 7 && lb == 3.f && qv[0] == 2.f &&
+                              xm0 == xm1) ? 1 : 0;
+    return;
+  }
   // 1. the wave's k smallest keys: k rounds of "minimum head, its owner advances"
   {
     int h0 = 0, h1 = 0;  // heads of the thread's two lists
@@ -959,6 +964,10 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   }
   __syncthreads();
   const float T = s_T, Tcut = T * (1.0f + 1.5258789e-5f);
+  if constexpr (DIAG == 2) {  // loads, the k-th coarse key, T
+    if (tid == 0) gate[qi] = T == 12345.f ? 1 : 0;
+    return;
+  }
   // 3. gather every entry <= Tcut (from the kept copy of the lists: step 1 consumed lk)
   int cnt[LPT], mycnt = 0;
 #pragma unroll
@@ -997,6 +1006,10 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   }
   __syncthreads();
   const int need = min(total, CB_C);
+  if constexpr (DIAG == 3) {  // ... and the gather of the candidates within T
+    if (tid == 0) gate[qi] = need == 12345 ? 1 : 0;
+    return;
+  }
   // 4. exact keys (rerank_block's summation: 64 lanes over the row), 8 candidates per wave with
   // their rows and norms loaded together: one memory round trip for up to 32 candidates
   constexpr int G = 8;
@@ -1319,8 +1332,18 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     MPR_LAUNCHED();
     // threshold gather over the sorted per-block lists (no full selection) + exact re-rank
     MPR_REQUIRE(RB <= 512, "search: %d coarse row blocks", RB);
-    hipLaunchKernelGGL(coarse_rerank2_kernel<16>, dim3((unsigned)b), dim3(256), 0, s, w.ck, w.ci,
-                       RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids, w.gate);
+    static const int diag = [] {
+      const char* e = getenv("MPR_RERANK_DIAG");
+      return e ? atoi(e) : 0;
+    }();
+#define MPR_RR(DG)                                                                            \
+  hipLaunchKernelGGL((coarse_rerank2_kernel<16, DG>), dim3((unsigned)b), dim3(256), 0, s, w.ck, \
+                     w.ci, RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids, w.gate)
+    if (diag == 1) MPR_RR(1);
+    else if (diag == 2) MPR_RR(2);
+    else if (diag == 3) MPR_RR(3);
+    else MPR_RR(0);
+#undef MPR_RR
     MPR_LAUNCHED();
     gate = w.gate;
   }

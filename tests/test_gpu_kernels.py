@@ -605,7 +605,9 @@ def test_t5_grouped_decode_head_vs_oracle(device, t5_sd, grouped_40, monkeypatch
 def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
     """Decodes over >= 64 rows (>= 512 batch x head pairs) run the decode attention one wave per
     pair (attention_decode_wave_kernel), whose outputs are bit-identical to the block kernel's
-    (MPR_ATT_WAVE=0): the greedy tokens of 128 + 69 rows are equal."""
+    (MPR_ATT_WAVE=0), and pairs with 65..128 keys (this cross-attention over 73 source rows) two
+    waves per pair (attention_decode_wave2_kernel; MPR_ATT_WAVE2=0 keeps one): the greedy tokens
+    of 128 + 69 rows are equal in all three forms."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     A = _t5_batch(t5_sd, 16, 73)
     emb = torch.cat([A[0]] * 12 + [A[0][:5]])
@@ -616,6 +618,9 @@ def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
     monkeypatch.setenv("MPR_ATT_WAVE", "1")
     got = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
     assert torch.equal(got, want)
+    monkeypatch.setenv("MPR_ATT_WAVE2", "0")
+    one_wave = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
+    assert torch.equal(one_wave, want)
 
 
 def test_grouped_decode_row_blocks_match(device, monkeypatch):

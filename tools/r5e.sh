@@ -6,3 +6,7 @@ rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 200 python -u tools/proj_trace.py 8 40 > $OUT/proj.txt 2>&1; echo "proj rc=$?"
 timeout -k 10 200 python -u tools/proj_trace.py 1 20 > $OUT/proj1.txt 2>&1; echo "proj1 rc=$?"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python -u tools/proj_trace.py 8 40 > $OUT/prof.log 2>&1; echo "prof rc=$?"
+for dg in 1 2 3; do
+  MPR_RERANK_DIAG=$dg timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/diag$dg -o run --output-format csv -- python -u tools/proj_trace.py 8 20 > $OUT/diag$dg.log 2>&1; echo "diag$dg rc=$?"
+done
+timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_gpu_kernels.py -k "wave_form" > $OUT/pytest_wave2.log 2>&1; echo "wave2 test rc=$?"
