@@ -352,9 +352,10 @@ __global__ __launch_bounds__(256) void scan_mm_kernel(const float* __restrict__ 
     rb = t / nqt;
   }
   if (gate) {  // the coarse path's exact fallback: only query tiles holding a flagged query run
-    int any = 0;
-    for (int i = 0; i < SM_B && qt * SM_B + i < b; ++i) any |= gate[qt * SM_B + i];
-    if (!any) return;
+    // (one vector load of the tile's 64 flags per wave and a ballot: a scalar loop over them
+    // waited on 64 dependent loads, ~5 us for a grid that does nothing)
+    const int qf = qt * SM_B + (int)(threadIdx.x & 63);
+    if (__ballot(qf < b && gate[qf] != 0) == 0) return;
   }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -830,12 +831,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
 // Sufficient when nothing was cut off: every list's bound > T and the gather did not overflow
 // (a row missing from every list has a key >= its lane's bound).  Same outputs as the select +
 // rerank_block pair whenever both are exact.
-template <int K, int DIAG = 0>  // DIAG > 0: timing-only early exits (MPR_RERANK_DIAG; garbage out)
+// D = d (256 or 512, scan_coarse_eligible): the exact keys' row loads are straight-line code.
+// pack_out: the (dist, id) float64 pairs of every query too (the sharded search's exchange block;
+// the gated fallback merge rewrites a flagged query's).
+template <int K, int D>
 __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
     const float* __restrict__ cand_key, const int64_t* __restrict__ cand_id, int n_lists,
     const float* __restrict__ X, const float* __restrict__ xnorm, int d, int64_t row_offset,
     const float* __restrict__ Q, const float* __restrict__ lane_bound, int k, const float* xmax,
-    float* out_dist, int64_t* out_id, int* gate) {
+    float* out_dist, int64_t* out_id, int* gate, double2* pack_out) {
   constexpr int LPT = 2;  // lists per thread (n_lists <= 512)
   __shared__ float qs[512];
   __shared__ float wk[4][K];
@@ -883,11 +887,6 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
 #pragma unroll
   for (int j = 0; j < 2; ++j) qv[j] = tid + 256 * j < d ? qp[tid + 256 * j] : 0.f;
   const float xm0 = xmax[0], xm1 = xmax[1];
-  if constexpr (DIAG == 1) {  // loads only
-    if (tid == 0) gate[qi] = (lk[0][0] == 12345.f && lid[0][0] == 7 && lb == 3.f && qv[0] == 2.f &&
-                              xm0 == xm1) ? 1 : 0;
-    return;
-  }
   // 1. the wave's k smallest keys: k rounds of "minimum head, its owner advances"
   {
     int h0 = 0, h1 = 0;  // heads of the thread's two lists
@@ -964,10 +963,6 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   }
   __syncthreads();
   const float T = s_T, Tcut = T * (1.0f + 1.5258789e-5f);
-  if constexpr (DIAG == 2) {  // loads, the k-th coarse key, T
-    if (tid == 0) gate[qi] = T == 12345.f ? 1 : 0;
-    return;
-  }
   // 3. gather every entry <= Tcut (from the kept copy of the lists: step 1 consumed lk)
   int cnt[LPT], mycnt = 0;
 #pragma unroll
@@ -1006,61 +1001,76 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   }
   __syncthreads();
   const int need = min(total, CB_C);
-  if constexpr (DIAG == 3) {  // ... and the gather of the candidates within T
-    if (tid == 0) gate[qi] = need == 12345 ? 1 : 0;
-    return;
-  }
-  // 4. exact keys (rerank_block's summation: 64 lanes over the row), 8 candidates per wave with
-  // their rows and norms loaded together: one memory round trip for up to 32 candidates
-  constexpr int G = 8;
-  for (int c0 = wave * G; c0 < need; c0 += 4 * G) {
-    float xv[G][8], xn[G];
+  // 4. exact keys (rerank_block's summation: 64 lanes over the row, lane l summing elements
+  // l + 64 j in j order, then the xor butterfly).  Each wave takes CB_C / 4 candidates and loads
+  // all their rows and norms before the first product (branch-free: past `need` it re-loads the
+  // last candidate and discards it), so the block waits on memory once; the 16 butterflies
+  // interleave.
+  static_assert(CB_C == 64, "one candidate per lane in the final rank");
+  constexpr int J = D / 64, G = CB_C / 4;
+  const int c0 = wave * G;
+  if (c0 < need) {  // wave-uniform
+    float qr[J], xv[G][J], xn[G], dot[G];
+#pragma unroll
+    for (int j = 0; j < J; ++j) qr[j] = qs[lane + 64 * j];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      if (c0 + g >= need) break;  // wave-uniform
-      const int64_t id = ids[c0 + g];
+      const int64_t id = ids[min(c0 + g, need - 1)];
       const int64_t r = id >= 0 ? id - row_offset : 0;
-      const float* xp = X + r * (int64_t)d;
+      const float* xp = X + r * (int64_t)D;
       xn[g] = xnorm[r];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int e = lane + 64 * j;
-        xv[g][j] = e < d ? xp[e] : 0.f;
-      }
+      for (int j = 0; j < J; ++j) xv[g][j] = xp[lane + 64 * j];
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int c = c0 + g;
-      if (c >= need) break;  // wave-uniform
-      const int64_t id = ids[c];
-      float dot = 0.f;
+      dot[g] = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < J; ++j) {
         const int e = lane + 64 * j;
-        dot += e < d ? qs[e] * xv[g][j] : 0.f;
+        dot[g] += e < d ? qr[j] * xv[g][j] : 0.f;
       }
+    }
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) dot += __shfl_xor(dot, off, 64);
-      if (lane == 0) {
-        keys[c] = id >= 0 ? sqrtf(fmaxf(qn + xn[g] - 2.0f * dot, 0.0f)) : INFINITY;
-        if (id < 0) ids[c] = INT64_MAX;
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+      for (int g = 0; g < G; ++g) dot[g] += __shfl_xor(dot[g], off, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int c = c0 + g;
+        if (c < need) {
+          const int64_t id = ids[c];
+          keys[c] = id >= 0 ? sqrtf(fmaxf(qn + xn[g] - 2.0f * dot[g], 0.0f)) : INFINITY;
+          if (id < 0) ids[c] = INT64_MAX;
+        }
       }
     }
   }
   __syncthreads();
-  if (tid == 0) {
+  // 5. the best k by (key, id): one wave, lane c holding candidate c, ranks by lane reads (the
+  // placeholders past `need`, (+inf, INT64_MAX), never rank below a candidate)
+  if (wave != 0) return;
+  if (lane == 0) {
     const float lists_bound = fminf(fminf(red[2][0], red[2][1]), fminf(red[2][2], red[2][3]));
     gate[qi] = (total <= CB_C && lists_bound > T) ? 0 : 1;
   }
-  if (tid < CB_C) {
-    const float a = keys[tid];
-    const int64_t ia = ids[tid];
-    int rank = 0;
-    for (int c = 0; c < CB_C; ++c) rank += key_less(keys[c], ids[c], a, ia) ? 1 : 0;
-    if (rank < k) {
-      out_dist[(int64_t)qi * k + rank] = ia == INT64_MAX ? NAN : a;
-      out_id[(int64_t)qi * k + rank] = ia == INT64_MAX ? -1 : ia;
-    }
+  const float a = keys[lane];
+  const int64_t ia = ids[lane];
+  const int alo = (int)(uint32_t)(uint64_t)ia, ahi = (int)(uint32_t)((uint64_t)ia >> 32);
+  int rank = 0;
+  for (int c = 0; c < need; ++c) {
+    const float kc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), c));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(alo, c);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(ahi, c);
+    rank += key_less(kc, (int64_t)(((uint64_t)hi << 32) | lo), a, ia) ? 1 : 0;
+  }
+  if (rank < k) {
+    const float v = ia == INT64_MAX ? NAN : a;
+    const int64_t id = ia == INT64_MAX ? -1 : ia;
+    out_dist[(int64_t)qi * k + rank] = v;
+    out_id[(int64_t)qi * k + rank] = id;
+    if (pack_out) pack_out[(int64_t)qi * k + rank] = make_double2((double)v, (double)id);
   }
 }
 
@@ -1156,6 +1166,11 @@ int scan_mm_rowblocks(int64_t n, int b) {
 // list).  Any row blocking gives the same keys and the same exact top k.
 int scan_mm_rb(int64_t n, int b, bool gated) {
   return gated ? std::min(scan_mm_rowblocks(n, b), 8) : scan_mm_rowblocks(n, b);
+}
+// whether the coarse path's gated merge is the wave merge writing packed pairs (<= 512
+// candidates, k <= 8) — and so the re-rank writes them for every query
+bool coarse_packs(int64_t n, int b, int k) {
+  return (int64_t)scan_mm_rb(n, b, true) * list_cap(k) <= 512 && k <= 8;
 }
 
 template <int K>
@@ -1332,17 +1347,15 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     MPR_LAUNCHED();
     // threshold gather over the sorted per-block lists (no full selection) + exact re-rank
     MPR_REQUIRE(RB <= 512, "search: %d coarse row blocks", RB);
-    static const int diag = [] {
-      const char* e = getenv("MPR_RERANK_DIAG");
-      return e ? atoi(e) : 0;
-    }();
-#define MPR_RR(DG)                                                                            \
-  hipLaunchKernelGGL((coarse_rerank2_kernel<16, DG>), dim3((unsigned)b), dim3(256), 0, s, w.ck, \
-                     w.ci, RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids, w.gate)
-    if (diag == 1) MPR_RR(1);
-    else if (diag == 2) MPR_RR(2);
-    else if (diag == 3) MPR_RR(3);
-    else MPR_RR(0);
+    // the re-rank writes every query's packed pair when the gated merge below would (it rewrites
+    // only the flagged queries')
+    double2* rr_pack = (pack_out && coarse_packs(n, b, k)) ? reinterpret_cast<double2*>(pack_out)
+                                                           : nullptr;
+#define MPR_RR(D_)                                                                            \
+  hipLaunchKernelGGL((coarse_rerank2_kernel<16, D_>), dim3((unsigned)b), dim3(256), 0, s, w.ck, \
+                     w.ci, RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids, w.gate, \
+                     rr_pack)
+    if (d == 512) MPR_RR(512); else MPR_RR(256);
 #undef MPR_RR
     MPR_LAUNCHED();
     gate = w.gate;
@@ -1363,7 +1376,7 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     if (rc != MPR_OK) return rc;
     // the coarse path's gated merge also writes every query's packed pair when asked (the wave
     // merge: <= 512 candidates, k <= 8)
-    double* po = (gate && pack_out && (int64_t)RB * K <= 512 && k <= 8) ? pack_out : nullptr;
+    double* po = (gate && pack_out && coarse_packs(n, b, k)) ? pack_out : nullptr;
     if (po && packed) *packed = true;
     return merge_dispatch(ck, ci, b, (int64_t)RB * K, k, /*keys_are_values=*/0, metric, out_dist,
                           out_ids, s, gate, po);

@@ -108,9 +108,9 @@ constexpr int MW_MAX = 512;
 // (dist, id) float64 pairs [W shards][Bp query slots][kc][2] (distributed.py); query q's list is
 // shard-major, candidate c = (shard c / kc, rank c % kc) — the order of the unpacked [b, W kc]
 // lists, so the outputs are the unpacked merge's.
-// pack_out (gated merges only): every query's final (dist, id) also as float64 pairs
-// [b][k][2] — a query the gate skips copies the re-rank's result already in out_val / out_id —
-// so the sharded search's exchange needs no separate pack launch (mpr_sharded_search_all).
+// pack_out (gated merges only): the merged queries' final (dist, id) also as float64 pairs
+// [b][k][2]; the coarse re-rank wrote every query's, so the sharded search's exchange needs no
+// separate pack launch (mpr_sharded_search_all).
 template <int K, bool PK = false>
 __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
                                                          const int64_t* cand_id, int64_t n_cand,
@@ -122,12 +122,7 @@ __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
                                                          double2* pack_out = nullptr) {
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (q >= b) return;  // wave-uniform
-  if (gate && gate[q] == 0) {
-    if (pack_out && lane < k)
-      pack_out[(int64_t)q * k + lane] =
-          make_double2((double)out_val[(int64_t)q * k + lane], (double)out_id[(int64_t)q * k + lane]);
-    return;
-  }
+  if (gate && gate[q] == 0) return;  // the re-rank's result stands (its packed pair too)
   const float* ck = PK ? nullptr : cand_key + (int64_t)q * n_cand;
   const int64_t* ci = PK ? nullptr : cand_id + (int64_t)q * n_cand;
   const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
