@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "topk_wave.h"
 
 namespace mpr {
 namespace {
@@ -38,6 +39,25 @@ constexpr float COS_EPS = 1e-8f;
 __device__ __forceinline__ bool key_less(float ka, int64_t ia, float kb, int64_t ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
+
+// Wave minimum by DPP row operations (a few cycles each, where a __shfl_xor butterfly waits on
+// six LDS-unit permutes): quad xor 1 and xor 2, half-row and row mirrors leave each row's minimum
+// in all its lanes; row_bcast15 / row_bcast31 fold rows 0-2 into row 3, whose lane 63 is read
+// out (wave-uniform result).  The whole wave must be active.  Min is order-free, so this equals
+// the butterfly's result (for the non-negative or infinite keys it is used on).
+#define MPR_DPP_MIN(v, CTRL, ROWS)                                                               \
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), \
+                                                          CTRL, ROWS, 0xF, false)))
+__device__ __forceinline__ float wave_min(float v) {
+  MPR_DPP_MIN(v, 0xB1, 0xF);   // quad_perm [1, 0, 3, 2]
+  MPR_DPP_MIN(v, 0x4E, 0xF);   // quad_perm [2, 3, 0, 1]
+  MPR_DPP_MIN(v, 0x141, 0xF);  // row_half_mirror
+  MPR_DPP_MIN(v, 0x140, 0xF);  // row_mirror
+  MPR_DPP_MIN(v, 0x142, 0xA);  // row_bcast15 -> rows 1, 3
+  MPR_DPP_MIN(v, 0x143, 0xC);  // row_bcast31 -> rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+#undef MPR_DPP_MIN
 
 __device__ __forceinline__ float score_key(int metric, float dot, float qn, float xn) {
   if (metric == 0) return sqrtf(fmaxf(qn + xn - 2.0f * dot, 0.0f));
@@ -340,7 +360,11 @@ __global__ __launch_bounds__(256) void scan_mm_kernel(const float* __restrict__ 
                                                       const float* __restrict__ Q,
                                                       const float* __restrict__ qnorm, int b,
                                                       int nqt, int RB, float* cand_key,
-                                                      int64_t* cand_id, const int* gate) {
+                                                      int64_t* cand_id, const int* gate,
+                                                      int* tile_cnt = nullptr, int k = 0,
+                                                      float* out_dist = nullptr,
+                                                      int64_t* out_id = nullptr,
+                                                      double2* pack_out = nullptr) {
   __shared__ __attribute__((aligned(16))) float smem[2 * SM_STAGE];
   constexpr int KQ = SM_BK / 4, LA = SM_B * KQ / 256;  // float4 per thread and operand: 2
   int qt, rb;
@@ -523,6 +547,31 @@ __global__ __launch_bounds__(256) void scan_mm_kernel(const float* __restrict__ 
       oi[t] = bidx == INT_MAX ? -1 : (int64_t)bidx + row_offset;
     }
   }
+  if (!tile_cnt) return;
+  // The gated fallback's merge, folded in: the tile's last block to finish (agent-scope release
+  // of every block's lists, counter, acquire) merges its flagged queries' RB x K candidates, one
+  // wave per query (select.hip's wave merge).  Only flagged tiles get here, so the fences cost
+  // nothing on the common path, which makes no merge launch at all.
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(tile_cnt + qt, 1) == RB - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const int64_t nc = (int64_t)RB * K;
+  for (int ql = wave; ql < SM_B; ql += 4) {
+    const int q = q0 + ql;
+    if (q >= b || gate[q] == 0) continue;  // wave-uniform
+    const float* ck = cand_key + (int64_t)q * nc;
+    const int64_t* ci = cand_id + (int64_t)q * nc;
+    tkw::merge_query<K>(
+        [&](int64_t c, float& key, int64_t& id) {
+          key = ck[c];
+          id = ci[c];
+        },
+        nc, k, metric, q, out_dist, out_id, pack_out);
+  }
 }
 
 __global__ void qnorm_kernel(const float* Q, int b, int d, float* out) {
@@ -643,6 +692,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
   constexpr int LDK = BK + 8;                       // LDS row stride (bf16): conflict-free
   constexpr int STAGE = CB2_RT * LDK;
   static_assert(LPS >= 1 && SPT % D == 0, "stage slots repeat per row tile");
+  static_assert(SPT % 2 == 0, "a tile's first stage lands in LDS buffer 0");
   __shared__ __attribute__((aligned(16))) __bf16 xs[2][STAGE];
   __shared__ float xn_s[2][CB2_RT];
   int qt, rb;
@@ -839,7 +889,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
     const float* __restrict__ cand_key, const int64_t* __restrict__ cand_id, int n_lists,
     const float* __restrict__ X, const float* __restrict__ xnorm, int d, int64_t row_offset,
     const float* __restrict__ Q, const float* __restrict__ lane_bound, int k, const float* xmax,
-    float* out_dist, int64_t* out_id, int* gate, double2* pack_out) {
+    float* out_dist, int64_t* out_id, int* gate, double2* pack_out, int* tile_cnt) {
   constexpr int LPT = 2;  // lists per thread (n_lists <= 512)
   __shared__ float qs[512];
   __shared__ float wk[4][K];
@@ -894,9 +944,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
       float a = h0 < CB_L ? lk[0][0] : INFINITY, b2 = h1 < CB_L ? lk[1][0] : INFINITY;
       // (static indexing: the head value is rotated to slot 0 as a list advances, below)
       const float mine = fminf(a, b2);
-      float m = mine;
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
+      const float m = wave_min(mine);
       // the lowest lane holding the minimum advances one list
       const uint64_t bal = __ballot(mine == m);
       const int win = __ffsll((unsigned long long)bal) - 1;
@@ -947,9 +995,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
     float v = lane < 4 * k ? wk[lane / k][lane % k] : INFINITY;
     float kth = INFINITY;
     for (int r = 0; r < k; ++r) {
-      float m = v;
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off, 64));
+      const float m = wave_min(v);
       kth = m;
       const uint64_t bal = __ballot(v == m);
       if (lane == __ffsll((unsigned long long)bal) - 1) v = INFINITY;
@@ -1051,6 +1097,7 @@ __global__ __launch_bounds__(256) void coarse_rerank2_kernel(
   // 5. the best k by (key, id): one wave, lane c holding candidate c, ranks by lane reads (the
   // placeholders past `need`, (+inf, INT64_MAX), never rank below a candidate)
   if (wave != 0) return;
+  if (lane == 0 && qi % SM_B == 0) tile_cnt[qi / SM_B] = 0;  // arm the gated fallback's merge
   if (lane == 0) {
     const float lists_bound = fminf(fminf(red[2][0], red[2][1]), fminf(red[2][2], red[2][3]));
     gate[qi] = (total <= CB_C && lists_bound > T) ? 0 : 1;
@@ -1176,14 +1223,16 @@ bool coarse_packs(int64_t n, int b, int k) {
 template <int K>
 int launch_scan_mm(const float* X, int64_t n, int d, int64_t row_offset, int metric,
                    const float* Q, float* qn, int b, float* ck, int64_t* ci, hipStream_t s,
-                   const int* gate, const float* qn_pre) {
+                   const int* gate, const float* qn_pre, int* tile_cnt = nullptr, int k = 0,
+                   float* od = nullptr, int64_t* oi = nullptr, double* pack_out = nullptr) {
   const int nqt = (int)cdiv(b, SM_B), RB = scan_mm_rb(n, b, gate != nullptr);
   if (qn_pre)
     qn = const_cast<float*>(qn_pre);
   else
     hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(b, 4)), dim3(256), 0, s, Q, b, d, qn);
   hipLaunchKernelGGL((scan_mm_kernel<K>), dim3((unsigned)(nqt * RB)), dim3(256), 0, s, X, n, d,
-                     row_offset, metric, Q, qn, b, nqt, RB, ck, ci, gate);
+                     row_offset, metric, Q, qn, b, nqt, RB, ck, ci, gate, tile_cnt, k, od, oi,
+                     reinterpret_cast<double2*>(pack_out));
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -1240,6 +1289,7 @@ struct CoarseWs {
   int64_t *ci, *si;
   __bf16* qb;
   int* gate;
+  int* cnt;  // per exact-scan query tile: fallback blocks done (zeroed by the re-rank)
   size_t bytes;
 };
 CoarseWs coarse_ws(void* base, int64_t n, int d, int b) {
@@ -1255,6 +1305,7 @@ CoarseWs coarse_ws(void* base, int64_t n, int d, int b) {
   w.qn = reinterpret_cast<float*>(p); p += ((size_t)b * 4 + 15) / 16 * 16;
   w.qb = reinterpret_cast<__bf16*>(p); p += ((size_t)b * d * 2 + 15) / 16 * 16;
   w.gate = reinterpret_cast<int*>(p); p += ((size_t)b * 4 + 15) / 16 * 16;
+  w.cnt = reinterpret_cast<int*>(p); p += ((size_t)cdiv(b, SM_B) * 4 + 15) / 16 * 16;
   w.bytes = (size_t)(p - reinterpret_cast<char*>(base));
   return w;
 }
@@ -1319,9 +1370,11 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
   }
   const int K = list_cap(k);
   const int* gate = nullptr;
+  void* ws_coarse = nullptr;      // the coarse path's buffers (its fallback's tile counters)
   const float* qn_pre = nullptr;  // |q|^2 already computed by the coarse path
   if (Xb && xmax && scan_coarse_eligible(n, d, b, k, metric)) {
     // coarse bf16 scan -> top CB_C per query -> exact re-rank (+ the gated exact fallback below)
+    ws_coarse = ws;
     CoarseWs w = coarse_ws(ws, n, d, b);
     ws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + (w.bytes + 255) / 256 * 256);
     const int RB = coarse_rowblocks(n, b);
@@ -1333,13 +1386,17 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     const __bf16* xb = reinterpret_cast<const __bf16*>(Xb);
     const int NW = coarse_waves(b), nqt = (int)cdiv(b, NW * 32);
     const dim3 grid((unsigned)(nqt * RB)), blk((unsigned)(NW * 64));
-    // prefetch depth: 4 stages (4 KiB per thread-slot at 8 waves); 2 at 4 waves, where each
-    // stage is two 16-byte loads per thread (the 256-VGPR budget of 2 blocks per CU)
+    // prefetch: 16-byte loads per thread in flight = D x LPS = 4 at 8 waves (d = 512: one
+    // 256-deep stage, 4 loads; d = 256: 4 64-deep stages), 4 at 4 waves (2 stages of 2 loads:
+    // the 256-VGPR budget of 2 blocks per CU)
 #define MPR_BF2(KS_, NW_, D_, BK_)                                                          \
   hipLaunchKernelGGL((scan_bf2_kernel<KS_, NW_, D_, BK_>), grid, blk, 0, s, xb, xnorm, n,     \
                      row_offset, w.qb, b, w.qn, nqt, RB, w.ck, w.ci, w.lb)
     if (d == 512) {
-      if (NW == 8) MPR_BF2(32, 8, 4, 64); else MPR_BF2(32, 4, 2, 64);
+      // 8 waves: 256-deep stages, one in flight (two barriers per 64-row tile instead of 8 at
+      // 64-deep x 4 in flight, the same 32 KiB of loads in flight per CU): C5 search 0.389 ->
+      // 0.357 ms, 1/8 shard 72 -> 70 us (tools/scan_c5.py)
+      if (NW == 8) MPR_BF2(32, 8, 1, 256); else MPR_BF2(32, 4, 2, 64);
     } else {
       if (NW == 8) MPR_BF2(16, 8, 4, 64); else MPR_BF2(16, 4, 2, 64);
     }
@@ -1354,7 +1411,7 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
 #define MPR_RR(D_)                                                                            \
   hipLaunchKernelGGL((coarse_rerank2_kernel<16, D_>), dim3((unsigned)b), dim3(256), 0, s, w.ck, \
                      w.ci, RB, X, xnorm, d, row_offset, Q, w.lb, k, xmax, out_dist, out_ids, w.gate, \
-                     rr_pack)
+                     rr_pack, w.cnt)
     if (d == 512) MPR_RR(512); else MPR_RR(256);
 #undef MPR_RR
     MPR_LAUNCHED();
@@ -1365,19 +1422,23 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     int64_t* ci = reinterpret_cast<int64_t*>(ws);
     float* ck = reinterpret_cast<float*>(ci + (size_t)b * RB * K);
     float* qn = ck + (size_t)b * RB * K;
+    // the coarse path's gated merge also writes the flagged queries' packed pairs when asked (the
+    // wave merge: <= 512 candidates, k <= 8; the re-rank wrote every query's); with K <= 8 it is
+    // folded into the fallback scan's last block per query tile (coarse_packs: RB * K <= 512)
+    double* po = (gate && pack_out && coarse_packs(n, b, k)) ? pack_out : nullptr;
+    if (po && packed) *packed = true;
+    const bool fold = gate && K <= 8 && !getenv("MPR_MERGE_BLOCK");
+    int* cnt = fold ? coarse_ws(ws_coarse, n, d, b).cnt : nullptr;
     int rc = MPR_EUNSUP;
     switch (K) {
 #define MPR_SM(KK) \
-  case KK: rc = launch_scan_mm<KK>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s, gate, qn_pre); \
+  case KK: rc = launch_scan_mm<KK>(X, n, d, row_offset, metric, Q, qn, b, ck, ci, s, gate, qn_pre, \
+                                   cnt, k, out_dist, out_ids, po); \
     break;
       MPR_SM(1) MPR_SM(2) MPR_SM(4) MPR_SM(8) MPR_SM(16)
 #undef MPR_SM
     }
-    if (rc != MPR_OK) return rc;
-    // the coarse path's gated merge also writes every query's packed pair when asked (the wave
-    // merge: <= 512 candidates, k <= 8)
-    double* po = (gate && pack_out && coarse_packs(n, b, k)) ? pack_out : nullptr;
-    if (po && packed) *packed = true;
+    if (rc != MPR_OK || fold) return rc;
     return merge_dispatch(ck, ci, b, (int64_t)RB * K, k, /*keys_are_values=*/0, metric, out_dist,
                           out_ids, s, gate, po);
   }

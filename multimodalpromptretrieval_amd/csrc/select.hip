@@ -8,6 +8,7 @@
 #include <cstdlib>
 
 #include "kernels.h"
+#include "topk_wave.h"
 
 namespace mpr {
 namespace {
@@ -120,56 +121,27 @@ __global__ __launch_bounds__(256) void merge_wave_kernel(const float* cand_key,
                                                          const double* packed = nullptr,
                                                          int Bp = 0, int kc = 1,
                                                          double2* pack_out = nullptr) {
-  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= b) return;  // wave-uniform
   if (gate && gate[q] == 0) return;  // the re-rank's result stands (its packed pair too)
-  const float* ck = PK ? nullptr : cand_key + (int64_t)q * n_cand;
-  const int64_t* ci = PK ? nullptr : cand_id + (int64_t)q * n_cand;
   const float sign = (keys_are_values && metric == 1) ? -1.f : 1.f;
-  uint64_t w[K];
-#pragma unroll
-  for (int t = 0; t < K; ++t) w[t] = ~0ull;
-  for (int64_t c = lane; c < n_cand; c += 64) {
-    float key;
-    int64_t id;
-    if constexpr (PK) {
-      const double* e = packed + (((c / kc) * (int64_t)Bp + q) * kc + c % kc) * 2;
-      key = (float)e[0];
-      id = (int64_t)e[1];
-    } else {
-      key = ck[c];
-      id = ci[c];
-    }
-    const float kk = sign * key;
-    uint64_t v = head_word(kk, kk == kk ? id : -1);  // NaN keys never rank (as key_less)
-#pragma unroll
-    for (int t = 0; t < K; ++t) {  // sorted insert (words are unique per valid candidate)
-      const uint64_t lo = v < w[t] ? v : w[t], hi = v < w[t] ? w[t] : v;
-      w[t] = lo;
-      v = hi;
-    }
-  }
-  for (int r = 0; r < k; ++r) {
-    uint64_t m = w[0];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const uint64_t o = __shfl_xor(m, off, 64);
-      m = o < m ? o : m;
-    }
-    if (m != ~0ull && w[0] == m) {
-#pragma unroll
-      for (int t = 0; t < K - 1; ++t) w[t] = w[t + 1];
-      w[K - 1] = ~0ull;
-    }
-    if (lane == 0) {
-      const bool none = m == ~0ull;
-      const float kk = word_key(m);
-      const float v = none ? NAN : (metric == 1 ? -kk : kk);
-      const int64_t id = none ? -1 : (int64_t)(uint32_t)m;
-      out_val[(int64_t)q * k + r] = v;
-      out_id[(int64_t)q * k + r] = id;
-      if (pack_out) pack_out[(int64_t)q * k + r] = make_double2((double)v, (double)id);
-    }
+  if constexpr (PK) {
+    tkw::merge_query<K>(
+        [&](int64_t c, float& key, int64_t& id) {
+          const double* e = packed + (((c / kc) * (int64_t)Bp + q) * kc + c % kc) * 2;
+          key = sign * (float)e[0];
+          id = (int64_t)e[1];
+        },
+        n_cand, k, metric, q, out_val, out_id, pack_out);
+  } else {
+    const float* ck = cand_key + (int64_t)q * n_cand;
+    const int64_t* ci = cand_id + (int64_t)q * n_cand;
+    tkw::merge_query<K>(
+        [&](int64_t c, float& key, int64_t& id) {
+          key = sign * ck[c];
+          id = ci[c];
+        },
+        n_cand, k, metric, q, out_val, out_id, pack_out);
   }
 }
 
