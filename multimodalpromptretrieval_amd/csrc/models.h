@@ -127,6 +127,8 @@ struct T5Layer {
   //   W_cowi = [[co | I_d], [wi diag(ln2) co | wi diag(ln2)]]   [d + d_ff, inner + d]
   DevBuf pk_ocq, pk_cowi;
   DevBuf xp_qkv, xp_o, xp_wi, xp_wo;       // encoder only: pack_x3 images (tiled GEMMs)
+  // decoder only, > 128-row decodes (T5Model::x3_rows): pack_x3 images of qkv, o, cq, co, wi, wo
+  DevBuf xd_qkv, xd_o, xd_cq, xd_co, xd_wi, xd_wo;
 };
 
 // Per-call workspace of generate(): activations, decode caches, captured graphs and the decode
@@ -205,8 +207,14 @@ struct T5Model : mpr_model {
   // A decode projection: the skinny GEMV on the packed weight (gemm_skinny)
   int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
                int* amax_nparts = nullptr) const;
-  bool tiled_head(int B) const;
-  bool fuse_attn(int B, int max_new) const;  // qkv GEMV + self-attention in one launch  // the grouped decode's argmax head on the tiled GEMM
+  bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
+  // Decodes of more than 128 rows (C5's 256-question batches): the projections on the packed-W
+  // split-bf16 tiles (gemm_rows_x3p: compute-bound there, where the skinny GEMV's f32 MFMAs are
+  // not), from the decoder's pack_x3 images made on first use (dec_x3) and kept in step with
+  // every weight refresh.  MPR_DECODE_X3_ROWS overrides the 128.
+  bool x3_rows(int B) const;
+  bool dec_x3 = false;
+  int ensure_dec_x3(hipStream_t s);
   int build_folded(hipStream_t s);  // stream-ordered
   DevBuf rel_tmp;  // update scratch: a bias table
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;
