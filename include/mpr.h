@@ -404,15 +404,6 @@ int mpr_pack_x3(const float* W, int64_t N, int64_t K, int64_t ldw, void* out, in
 int mpr_gemm_f32_packed(const float* A, int64_t lda, const float* W, int64_t ldw, const void* wp,
                         float* C, int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R,
                         int64_t ldr, int32_t act, void* stream);
-/* mpr_gemm_rows_x3p: a projection of a grouped decode step of more than 128 rows (C5's t5-base
- * loop; replaces the skinny GEMV there, T5ForConditionalGeneration's decoder projections,
- * transformers modeling_t5.py T5LayerFF / T5Attention): C = act(rms(A) W^T) + R from W's pack_x3
- * image alone; rms_w non-null fuses T5's RMSNorm of the A rows (operand rms_w[k] A[m, k], the
- * row scaled by 1 / sqrt(mean A[m]^2 + rms_eps)).  Rows are independent: any M gives every row
- * the same bits. */
-int mpr_gemm_rows_x3p(const float* A, int64_t lda, const void* wp, float* C, int64_t ldc,
-                      int32_t M, int32_t N, int32_t K, const float* rms_w, float rms_eps,
-                      const float* R, int64_t ldr, int32_t act, void* stream);
 int mpr_gather_rows(const float* table, const int32_t* ids, int64_t n, int32_t d, float* out,
                     void* stream);
 int mpr_embed_bwd(const float* dY, int32_t d, const int32_t* uniq, const int32_t* offs,

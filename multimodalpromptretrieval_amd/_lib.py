@@ -119,9 +119,6 @@ SIGNATURES = [
     ("mpr_gemm_f32_packed", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                       c_int64, c_int32, c_int32, c_int32, c_void_p, c_int64,
                                       c_int32, c_void_p]),
-    ("mpr_gemm_rows_x3p", c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32,
-                                    c_int32, c_int32, c_void_p, c_float, c_void_p, c_int64,
-                                    c_int32, c_void_p]),
     ("mpr_transpose", c_int32, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64,
                                 c_void_p]),
     ("mpr_rmsnorm_fwd", c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_float, c_float,

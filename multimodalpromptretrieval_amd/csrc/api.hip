@@ -543,10 +543,6 @@ int t5_load(T5Model* m, const float* const* t, const int32_t* enc_lut, const int
     MPR_TRY(pack3(ly->xp_wo, ly->wo, d, dff));
   }
   MPR_TRY(pack3(m->xp_cross_kv, m->cross_kv_w, (int64_t)Ld * 2 * inner, d));
-  if (m->dec_x3) {  // the > 128-row decode's images, once made, follow every refresh
-    m->dec_x3 = false;
-    MPR_TRY(m->ensure_dec_x3(s));
-  }
   if (m->fold) MPR_TRY(m->build_folded(s));
   return MPR_OK;
 }

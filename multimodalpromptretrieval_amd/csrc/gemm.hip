@@ -513,8 +513,7 @@ __device__ __forceinline__ GemmArgs select_problem(const GemmGroup& grp, int z) 
   a.ldc = MPR_SEL(ldc); a.M = MPR_SEL(M); a.N = MPR_SEL(N); a.K = MPR_SEL(K);
   a.act = MPR_SEL(act); a.c_rpb = MPR_SEL(c_rpb); a.c_bs = MPR_SEL(c_bs);
   a.batch = MPR_SEL(batch); a.a_bs = MPR_SEL(a_bs); a.w_bs = MPR_SEL(w_bs);
-  a.cb_bs = MPR_SEL(cb_bs); a.wp = MPR_SEL(wp); a.rms_w = MPR_SEL(rms_w);
-  a.rms_eps = MPR_SEL(rms_eps);
+  a.cb_bs = MPR_SEL(cb_bs); a.wp = MPR_SEL(wp);
 #undef MPR_SEL
   return a;
 }
@@ -677,13 +676,8 @@ __global__ __launch_bounds__(256) void pack_x3_kernel(const float* __restrict__ 
   out[(t * 3 + 2) * 64 + lane] = h2;
 }
 
-// RMS: the fused RMSNorm of gemm_rows_x3p (16-deep k tiles only): each A element staged as
-// rms_w[k] A[m, k], the row's squares summed by its KQ loader threads (each over its own columns,
-// k tiles in order, then a quad butterfly) and the accumulator scaled by the row's
-// 1 / sqrt(mean + eps) in the epilogue; rs_s = BM floats of LDS.
-template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16, bool RMS = false>
-__device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by, float* smem_f,
-                                              float* rs_s = nullptr) {
+template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16>
+__device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
   constexpr int NS = BK / 16;  // 16-deep MFMA steps per K tile
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
@@ -706,12 +700,8 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
     wpk[ni] = reinterpret_cast<const bf16x8*>(a.wp) +
               (int64_t)min(n0 / 32 + wn * WN + ni, NTW - 1) * KS * 3 * 64 + lane;
 
-  static_assert(!RMS || BK == 16, "the fused RMSNorm's square sums follow 16-deep k tiles");
-  f32x4 ra[D][LA], rg[RMS ? D : 1][LA];
+  f32x4 ra[D][LA];
   bool oka[D][LA];
-  float ssq[LA];
-#pragma unroll
-  for (int i = 0; i < LA; ++i) ssq[i] = 0.f;
   bf16x8 bq[D][NS][WN][3];
   auto aload = [&](int j, int kt) {
     const int k0 = kt * BK;
@@ -721,7 +711,6 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
       if constexpr (KT) oka[j][i] = c < K;
       ra[j][i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
                                                  min(c, K - 4));
-      if constexpr (RMS) rg[j][i] = *reinterpret_cast<const f32x4*>(a.rms_w + min(c, K - 4));
     }
   };
   auto bload = [&](int j, int kt) {  // past the last k step: an in-range step (A is zero there)
@@ -742,21 +731,14 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
     *reinterpret_cast<bf16x4*>(p + PLANE) = h1;
     *reinterpret_cast<bf16x4*>(p + 2 * PLANE) = h2;
   };
-  const int nk = (K + BK - 1) / BK;
-  // kt: the k tile being staged (RMS: its squares count while kt < nk; tiles past K are zero)
-  auto swrite = [&](int st, int j, int kt) {
+  auto swrite = [&](int st, int j) {
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     __bf16* base = smem + st * STAGE;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT;
-      f32x4 v = ra[j][i];
-      if constexpr (KT) v = oka[j][i] ? v : zero;
-      if constexpr (RMS) {
-        if (kt < nk) ssq[i] += ((v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]));
-        v = rg[j][i] * v;
-      }
-      put(base, idx / KQ, (idx % KQ) * 4, v);
+      if constexpr (KT) put(base, idx / KQ, (idx % KQ) * 4, oka[j][i] ? ra[j][i] : zero);
+      else put(base, idx / KQ, (idx % KQ) * 4, ra[j][i]);
     }
   };
 
@@ -795,11 +777,12 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
     }
   };
 
+  const int nk = (K + BK - 1) / BK;
   const int nkr = (nk + D - 1) / D * D;
   aload(0, 0);
-  swrite(0, 0, 0);
+  swrite(0, 0);
   aload(0, 1);
-  swrite(1, 0, 1);
+  swrite(1, 0);
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     aload(j, 2 + j);
@@ -825,7 +808,7 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
       mfmas(j, U1, NMF);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(0);
-      swrite(st, j, kt + j + 2);
+      swrite(st, j);
       aload(j, kt + j + 2 + D);
       bload(j, kt + j + D);
       __syncthreads();
@@ -838,23 +821,12 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
     }
   }
 
-  if constexpr (RMS) {  // the rows' sums of squares: the KQ loader lanes of a row, then LDS
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      float v = ssq[i];
-#pragma unroll
-      for (int off = 1; off < KQ; off <<= 1) v += __shfl_xor(v, off, 64);
-      const int idx = tid + i * NT;
-      if (idx % KQ == 0) rs_s[idx / KQ] = v;
-    }
-    __syncthreads();
-  }
 #pragma unroll
   for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
     for (int ni = 0; ni < WN; ++ni) {
       const int col = n0 + wn * 32 * WN + ni * 32 + li, colc = min(col, N - 1);
-      const int rl = wm * 32 * WM + mi * 32 + 4 * lh, rbase = m0 + rl;
+      const int rbase = m0 + wm * 32 * WM + mi * 32 + 4 * lh;
       const float bv = a.bias ? a.bias[colc] : 0.f;
       float rv[16];
       if (a.R) {
@@ -865,10 +837,7 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = rbase + (r & 3) + 8 * (r >> 2);
-        float x = acc[mi][ni][r];
-        if constexpr (RMS)
-          x *= 1.0f / sqrtf(rs_s[rl + (r & 3) + 8 * (r >> 2)] / (float)K + a.rms_eps);
-        float v = act_exact(x + bv, a.act);
+        float v = act_exact(acc[mi][ni][r] + bv, a.act);
         if (a.R) v = rv[r] + v;
         const int64_t coff = a.c_rpb ? (int64_t)(row / a.c_rpb) * a.c_bs +
                                            (int64_t)(row % a.c_rpb) * a.ldc
@@ -879,11 +848,10 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
 }
 
 // gemm_x3_kernel's grid and tile order, the packed-W tile
-template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16, bool RMS = false>
+template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16>
 __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm_x3p_kernel(
     const GemmGroup grp) {
   __shared__ __attribute__((aligned(16))) float smem[2 * 3 * BM * (BK + 8) / 2];
-  __shared__ float rs_s[RMS ? BM : 1];
   const int total = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
   int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
@@ -922,10 +890,10 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
     bx = tt / rem;
     by = full + (tt - bx * rem);
   }
-  gemm_x3p_tile<BM, BN, WM, WN, D, KT, BK, RMS>(a, bx, by, smem, rs_s);
+  gemm_x3p_tile<BM, BN, WM, WN, D, KT, BK>(a, bx, by, smem);
 }
 
-template <int BM, int BN, int WM, int WN, int D, int BK = 16, bool RMS = false>
+template <int BM, int BN, int WM, int WN, int D, int BK = 16>
 int launch_gemm_x3p_group(const GemmGroup& g, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN));
   int64_t tiles = 0;
@@ -936,10 +904,10 @@ int launch_gemm_x3p_group(const GemmGroup& g, hipStream_t s) {
   }
   if (tiles == 0) return MPR_OK;
   if (kt)
-    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, true, BK, RMS>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, true, BK>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   else
-    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, false, BK, RMS>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, false, BK>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -1511,28 +1479,6 @@ int gemm(const GemmArgs& a, hipStream_t s) {
   g.g[0] = a;
   g.n = 1;
   return gemm_group(g, s);
-}
-
-int gemm_rows_x3p(const GemmArgs& a, hipStream_t s) {
-  MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0 && a.batch == 1 && !a.c_rpb,
-              "gemm_rows_x3p: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
-  if (a.M == 0 || a.N == 0) return MPR_OK;
-  MPR_REQUIRE(a.wp && aligned16(a.wp) && a.K % 4 == 0 && a.lda % 4 == 0 && aligned16(a.A) &&
-                  (!a.rms_w || aligned16(a.rms_w)),
-              "gemm_rows_x3p: needs the pack_x3 image, K and lda multiples of 4, 16-byte operands");
-  GemmGroup g;
-  g.g[0] = a;
-  g.n = 1;
-  // 64x64 blocks (4 waves) while they give >= 160 blocks, else 32x64 (2 waves): t5-base at 256
-  // rows, qkv / wi on 64x64, the d-wide projections on 32x64 (96 blocks)
-  const bool big = cdiv(a.M, 64) * cdiv(a.N, 64) >= 160;
-  return probed(PROBE_GEMM, 2.0 * a.M * a.N * a.K, gemm_bytes(a), s, [&]() {
-    if (a.rms_w)
-      return big ? launch_gemm_x3p_group<64, 64, 1, 1, 2, 16, true>(g, s)
-                 : launch_gemm_x3p_group<32, 64, 1, 1, 2, 16, true>(g, s);
-    return big ? launch_gemm_x3p_group<64, 64, 1, 1, 2>(g, s)
-               : launch_gemm_x3p_group<32, 64, 1, 1, 2>(g, s);
-  });
 }
 
 int64_t packed_x3_bytes(int64_t N, int64_t K) { return cdiv(N, 32) * cdiv(K, 16) * 3 * 64 * 16; }

@@ -36,19 +36,9 @@ struct GemmArgs {
   // Optional packed split image of W (pack_x3): the split-bf16 kernel then loads its W operand
   // fragments straight into registers instead of staging W through LDS (results identical).
   const void* wp = nullptr;
-  // Optional fused RMSNorm of the A rows (gemm_rows_x3p only): the operand is rms_w[k] A[m, k]
-  // and row m's accumulator is scaled by 1 / sqrt(mean_k A[m, k]^2 + rms_eps) before the
-  // activation (T5's RMSNorm ahead of a projection, in one launch).
-  const float* rms_w = nullptr;
-  float rms_eps = 0.f;
 };
 
 int gemm(const GemmArgs& a, hipStream_t s);
-// One projection of a grouped decode step (> 128 rows) on the packed-W split-bf16 tiles: W from
-// its pack_x3 image (a.wp), optional fused RMSNorm (a.rms_w), residual (a.R), relu; the tile
-// follows the shape (64x64 or 32x64 blocks, 16-deep k steps: every element summed in the same
-// order whatever the tile, so rows are independent and any row count gives the same row).
-int gemm_rows_x3p(const GemmArgs& a, hipStream_t s);
 
 // The packed split image of a fixed W [N, K] for GemmArgs::wp (bytes, and the pack itself).
 int64_t packed_x3_bytes(int64_t N, int64_t K);

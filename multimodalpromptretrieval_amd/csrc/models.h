@@ -127,8 +127,6 @@ struct T5Layer {
   //   W_cowi = [[co | I_d], [wi diag(ln2) co | wi diag(ln2)]]   [d + d_ff, inner + d]
   DevBuf pk_ocq, pk_cowi;
   DevBuf xp_qkv, xp_o, xp_wi, xp_wo;       // encoder only: pack_x3 images (tiled GEMMs)
-  // decoder only, > 128-row decodes (T5Model::x3_rows): pack_x3 images of qkv, o, cq, co, wi, wo
-  DevBuf xd_qkv, xd_o, xd_cq, xd_co, xd_wi, xd_wo;
 };
 
 // Per-call workspace of generate(): activations, decode caches, captured graphs and the decode
@@ -208,13 +206,10 @@ struct T5Model : mpr_model {
   int dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
                int* amax_nparts = nullptr) const;
   bool tiled_head(int B) const;  // the grouped decode's argmax head on the tiled GEMM
-  // Decodes of more than 128 rows (C5's 256-question batches): the projections on the packed-W
-  // split-bf16 tiles (gemm_rows_x3p: compute-bound there, where the skinny GEMV's f32 MFMAs are
-  // not), from the decoder's pack_x3 images made on first use (dec_x3) and kept in step with
-  // every weight refresh.  MPR_DECODE_X3_ROWS overrides the 128.
-  bool x3_rows(int B) const;
-  bool dec_x3 = false;
-  int ensure_dec_x3(hipStream_t s);
+  // (Measured and dropped: decodes of > 128 rows with their projections on the packed-W
+  // split-bf16 tiles, RMSNorm fused, git show e050f85: each tile's serial K loop made the
+  // 256-row t5-base projections 27-41 us against 14-21 for the skinny GEMVs' K split over 8
+  // waves; C5 end to end 45 -> 56-64 ms per batch, profiles/r05_decode_x3_ab.txt.)
   int build_folded(hipStream_t s);  // stream-ordered
   DevBuf rel_tmp;  // update scratch: a bias table
   DevBuf shared, enc_final, dec_final, lm_head, cross_kv_w;

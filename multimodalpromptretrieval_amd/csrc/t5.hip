@@ -227,31 +227,6 @@ bool T5Model::tiled_head(int B) const {
   return on && B > 32 && !fold_rows(B);
 }
 
-// (MPR_DECODE_X3_ROWS read per call; a captured decode graph keeps the path it was captured with)
-bool T5Model::x3_rows(int B) const {
-  const char* e = getenv("MPR_DECODE_X3_ROWS");
-  return B > (e ? atoi(e) : 128) && !fold_rows(B);
-}
-
-int T5Model::ensure_dec_x3(hipStream_t s) {
-  if (dec_x3) return MPR_OK;
-  auto pack3 = [&](DevBuf& dst, const DevBuf& src, int64_t n, int64_t k) -> int {
-    MPR_TRY(dst.ensure((size_t)packed_x3_bytes(n, k)));
-    return pack_x3(src.as<float>(), n, k, k, dst.ptr, s);
-  };
-  for (auto& lp : dec) {
-    T5Layer& ly = *lp;
-    MPR_TRY(pack3(ly.xd_qkv, ly.qkv, 3 * inner, d));
-    MPR_TRY(pack3(ly.xd_o, ly.o, d, inner));
-    MPR_TRY(pack3(ly.xd_cq, ly.cq, inner, d));
-    MPR_TRY(pack3(ly.xd_co, ly.co, d, inner));
-    MPR_TRY(pack3(ly.xd_wi, ly.wi, dff, d));
-    MPR_TRY(pack3(ly.xd_wo, ly.wo, d, dff));
-  }
-  dec_x3 = true;
-  return MPR_OK;
-}
-
 int T5Model::build_folded(hipStream_t s) {
   const int K = inner + d;
   MPR_REQUIRE(d % 16 == 0 && inner % 16 == 0 && dff % 16 == 0, "fold: d=%d inner=%d dff=%d", d,
@@ -496,57 +471,10 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
 
   const float out_scale = scale_out ? 1.0f / sqrtf((float)d) : 1.0f;
   if (fold_rows(B)) return decode_body_folded(B, L, max_new, eos, pad, s, t0, t1);
-  const bool x3 = x3_rows(B);
-  const char* wo_env = getenv("MPR_DECODE_X3_WO");
-  const bool x3_wo = !wo_env || wo_env[0] != '0';
-  // a projection of the > 128-row decode: out = [rms(A) ln] W^T (+ R), relu
-  auto rows = [&](const float* A, int64_t lda, const DevBuf& Wp, int N, int K, const float* ln,
-                  const float* R, float* C, int64_t ldc, int act) {
-    GemmArgs g;
-    g.A = A; g.lda = lda; g.wp = Wp.ptr; g.R = R; g.ldr = R ? ldc : 0; g.C = C; g.ldc = ldc;
-    g.M = B; g.N = N; g.K = K; g.act = act; g.rms_w = ln; g.rms_eps = T5_EPS;
-    return gemm_rows_x3p(g, s);
-  };
   for (int t = t0; t < t1; ++t) {
     for (int l = 0; l < Ld; ++l) {
       const T5Layer& ly = *dec[l];
       float* cl = ws->cache.as<float>() + l * cache_layer;
-      if (x3) {
-        float* qkv_t = cl + (int64_t)t * 3 * inner;
-        MPR_TRY(rows(xp, d, ly.xd_qkv, 3 * inner, d, ly.ln0.as<float>(), nullptr, qkv_t,
-                     (int64_t)Tc * 3 * inner, ACT_NONE));
-        AttnArgs at;
-        at.q = qkv_t; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
-        at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
-        at.v = cl + 2 * inner; at.v_bs = at.q_bs; at.v_rs = 3 * inner;
-        at.o = ap; at.o_bs = inner; at.o_rs = inner;
-        at.B = B; at.H = H; at.Lq = 1; at.Lk = t + 1; at.scale = 1.f; at.causal = 1;
-        at.q_pos0 = t;
-        at.rel_tab = dec_tab.as<float>();
-        at.lut_radius = lut_radius;
-        MPR_TRY(attention(at, s));
-        MPR_TRY(rows(ap, inner, ly.xd_o, d, inner, nullptr, xp, xp, d, ACT_NONE));
-        MPR_TRY(rows(xp, d, ly.xd_cq, inner, d, ly.ln1.as<float>(), nullptr, qp, inner, ACT_NONE));
-        AttnArgs ca;
-        ca.q = qp; ca.q_bs = inner; ca.q_rs = inner;
-        ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
-        ca.v = ckv + (int64_t)l * 2 * inner + inner; ca.v_bs = ca.k_bs; ca.v_rs = ckv_ld;
-        ca.o = ap; ca.o_bs = inner; ca.o_rs = inner;
-        ca.B = B; ca.H = H; ca.Lq = 1; ca.Lk = L; ca.scale = 1.f;
-        ca.key_mask = maskp; ca.mask_bs = L;
-        MPR_TRY(attention(ca, s));
-        MPR_TRY(rows(ap, inner, ly.xd_co, d, inner, nullptr, xp, xp, d, ACT_NONE));
-        MPR_TRY(rows(xp, d, ly.xd_wi, dff, d, ly.ln2.as<float>(), nullptr, fp, dff, ACT_RELU));
-        if (x3_wo) {
-          MPR_TRY(rows(fp, dff, ly.xd_wo, d, dff, nullptr, xp, xp, d, ACT_NONE));
-        } else {
-          SkinnyArgs fo;
-          fo.g.A = fp; fo.g.lda = dff; fo.g.R = xp;
-          fo.g.ldr = d; fo.g.C = xp; fo.g.ldc = d; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
-          MPR_TRY(dec_gemm(fo, ly.pk_wo, s));
-        }
-        continue;
-      }
       SkinnyArgs sq;
       sq.g.A = xp; sq.g.lda = d;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
@@ -786,7 +714,6 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t M = (int64_t)B * L, Mx = std::max(M, Mg);
   const int nparts = (int)cdiv(V, 16);
-  if (x3_rows(B)) MPR_TRY(ensure_dec_x3(s));  // (before any capture: packs the decoder once)
   // Every buffer the bodies touch is sized before capture (no allocation inside a graph).
   MPR_TRY(grow(ws->enc_in, (size_t)Mx * d * 4));
   MPR_TRY(grow(ws->mask_in, (size_t)M * 4));

@@ -676,18 +676,6 @@ int mpr_gemm_f32_packed(const float* A, int64_t lda, const float* W, int64_t ldw
   });
 }
 
-int mpr_gemm_rows_x3p(const float* A, int64_t lda, const void* wp, float* C, int64_t ldc,
-                      int32_t M, int32_t N, int32_t K, const float* rms_w, float rms_eps,
-                      const float* R, int64_t ldr, int32_t act, void* stream) {
-  return guarded_call([&]() -> int {
-    MPR_REQUIRE(act == ACT_NONE || act == ACT_RELU, "gemm_rows_x3p: act %d (none or relu)", act);
-    GemmArgs g;
-    g.A = A; g.lda = lda; g.wp = wp; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
-    g.R = R; g.ldr = ldr; g.act = act; g.rms_w = rms_w; g.rms_eps = rms_eps;
-    return gemm_rows_x3p(g, S(stream));
-  });
-}
-
 int mpr_gemm_f32_many(int32_t n, const int64_t* desc, void* stream) {
   return guarded_call([&]() -> int {
     MPR_REQUIRE(n >= 0 && n <= 64 && (n == 0 || desc), "gemm_many: %d problems", n);

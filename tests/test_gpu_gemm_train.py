@@ -98,54 +98,3 @@ def test_packed_weight_gemm_is_bit_identical(device, M, N, K, act, res):
               N, M, N, K, _lib.ptr(R), N if R is not None else 0, act, _lib.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(C, ref)
-
-
-def _rows_x3p(A, img, N, rms_w=None, R=None, act=0, eps=1e-6):
-    M, K = A.shape
-    C = torch.empty(M, N, device=A.device)
-    _lib.call("mpr_gemm_rows_x3p", _lib.ptr(A), K, _lib.ptr(img), _lib.ptr(C), N, M, N, K,
-              _lib.ptr(rms_w), eps, _lib.ptr(R), N if R is not None else 0, act,
-              _lib.stream_ptr())
-    torch.cuda.synchronize()
-    return C
-
-
-@pytest.mark.parametrize("M,N,K,rms,act,res", [
-    (256, 2304, 768, True, 0, False),   # t5-base decode qkv at 256 rows
-    (256, 768, 768, True, 0, False),    # cross-attention q
-    (256, 3072, 768, True, 2, False),   # wi + relu (64x64 tiles; 32x64 at 136 rows)
-    (256, 768, 768, False, 0, True),    # o / co + residual
-    (256, 768, 3072, False, 0, True),   # wo + residual
-    (200, 1000, 520, True, 2, True),    # ragged rows, columns and K (masked K tail)
-])
-def test_rows_x3p_decode_projection(device, M, N, K, rms, act, res):
-    """mpr_gemm_rows_x3p, the > 128-row decode's projection: against fp64 torch of the same
-    formula (T5's RMSNorm of the rows, relu, residual) within fp32 accuracy; without the norm
-    bit-identical to mpr_gemm_f32_packed (same split, same summation order); and rows are
-    independent: the first 136 rows alone (the other tile shape) give the same bits."""
-    A, W = _operands(M, N, K, 11 * M + N + K)
-    Ad, Wd = A.to(device), W.to(device)
-    g = torch.rand(K, generator=torch.Generator().manual_seed(K)) + 0.5
-    gd = g.to(device) if rms else None
-    R = torch.randn(M, N, device=device) if res else None
-    img = _packed(Wd)
-    got = _rows_x3p(Ad, img, N, gd, R, act)
-    x = A.double()
-    if rms:
-        x = x / torch.sqrt((x * x).mean(1, keepdim=True) + 1e-6) * g.double()
-    want = x @ W.double().t()
-    if act == 2:
-        want = want.clamp_min(0)
-    if res:
-        want = want + R.double().cpu()
-    assert _rel(got, want) < 2e-6
-    if not rms:
-        C = torch.empty(M, N, device=device)
-        _lib.call("mpr_gemm_f32_packed", _lib.ptr(Ad), K, _lib.ptr(Wd), K, _lib.ptr(img),
-                  _lib.ptr(C), N, M, N, K, _lib.ptr(R), N if R is not None else 0, act,
-                  _lib.stream_ptr())
-        torch.cuda.synchronize()
-        assert torch.equal(got, C)
-    part = _rows_x3p(Ad[:136].contiguous(), img, N, gd,
-                     R[:136].contiguous() if res else None, act)
-    assert torch.equal(part, got[:136])
