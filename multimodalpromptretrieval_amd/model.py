@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import os
 import weakref
+from collections import deque
 
 import torch
 from torch import nn
@@ -425,7 +426,8 @@ class T5VisionModel(nn.Module):
             # T5_model.generate (:200-205) hands back a device tensor as GenerationMixin does;
             # the answers only need the host copy the device generate already made, so decode
             # that one (batch_decode over a device tensor pays a D2H copy + sync per row)
-            seqs = handles[1].generate(combined, mask, self.max_new_tokens, lens=lens)
+            seqs = handles[1].generate(combined, mask, self.max_new_tokens, lens=lens,
+                                       while_running=self._flush_hints)
         return self.tokenizer.batch_decode(seqs, skip_special_tokens=True)
 
     # ---- lookahead for batch-after-batch callers (main.py:262-263) ---------------------------
@@ -435,30 +437,66 @@ class T5VisionModel(nn.Module):
         """Announce a batch the caller will ``predict()`` soon (``serving.lookahead`` does this
         one batch ahead; ``dropin`` wraps main.py's evaluation loaders with it).  The batch's
         device-side retrieval work — the query towers paired with the token-feature ViT, the
-        index scan and the top-k copy to host (``_prefetch``) — is enqueued now on the retrieval
-        stream, so it runs on the GPU beside the current ``predict()``'s T5 encoder and greedy
-        decode, which leave most of the chip idle; the hinted ``predict()`` then only waits for
-        it.  Same launches, same results as an unhinted call.  In training mode the hinted
-        ``forward(batch)`` picks it up the same way (main.py:177-178: the towers are frozen and
-        the index fixed while the T5 trains, so the next batch's retrieval and image tokens run
-        beside this step's T5 forward / backward).  Returns whether anything was enqueued:
-        nothing without a ``VQARetrieval`` with an index on this device, or for a batch already
-        hinted."""
+        index scan and the top-k copy to host (``_prefetch``) — runs on the retrieval stream
+        beside the current ``predict()``'s T5 encoder and greedy decode, which leave most of the
+        chip idle; the hinted ``predict()`` then only waits for it.  Same launches, same results
+        as an unhinted call.  In training mode the hinted ``forward(batch)`` picks it up the same
+        way (main.py:177-178: the towers are frozen and the index fixed while the T5 trains, so
+        the next batch's retrieval and image tokens run beside this step's T5 forward /
+        backward).
+
+        The work is queued here and enqueued at the model's next long stretch of GPU work — a
+        training forward's T5 launch, a ``predict()``'s decode (``_flush_hints``) — or when the
+        batch itself is needed: a loop calls this right after the previous step's host sync,
+        with the GPU idle, and staging the batch's pageable images into pinned memory (~1 ms of
+        host copy) in front of the GPU work left the GPU waiting for it.  The queued work is
+        ordered after what the caller's stream held at this call (an event), not after the T5
+        work enqueued since.  Returns whether the batch was queued: not without a
+        ``VQARetrieval`` with an index on this device, nor for a batch already hinted."""
         if not hasattr(self, "_hints"):
             self._hints = {}
+            self._pending_hints = deque()
         key = id(batch["image"])
-        if key in self._hints:
+        if key in self._hints or any(b["image"] is batch["image"]
+                                     for b, _ in self._pending_hints):
             return False
-        pre = self._prefetch([batch], int(os.environ.get("MPR_AHEAD_SLOT", "0")))[0]
-        if pre is None:
+        retr = self._retrieval_obj()
+        if (getattr(retr, "prefetch_many", None) is None or getattr(retr, "index", None) is None
+                or self.device.type != "cuda"):
             return False
-        while len(self._hints) >= self.MAX_HINTS:  # announced but never predicted: drop oldest
-            self._hints.pop(next(iter(self._hints)))
-        # the entry holds the batch's image tensor, so its id() is not reused while it lives
-        self._hints[key] = (batch["image"], tuple(batch["question"]), pre)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._pending_hints.append((batch, ev))
+        while len(self._pending_hints) > self.MAX_HINTS:  # announced, never used: drop oldest
+            self._pending_hints.popleft()
         return True
 
+    def _flush_hints(self, upto=None):
+        """Enqueue the queued hints' retrieval work (all of them, or up to and including the
+        batch ``upto``) on the hint stream, each after the event its ``hint_next`` recorded."""
+        pend = getattr(self, "_pending_hints", None)
+        if not pend:
+            return
+        if not hasattr(self, "_s_hint"):
+            self._s_hint = torch.cuda.Stream(self.device)
+        slot = int(os.environ.get("MPR_AHEAD_SLOT", "0"))
+        while pend:
+            batch, ev = pend.popleft()
+            self._s_hint.wait_event(ev)
+            with torch.cuda.stream(self._s_hint):
+                pre = self._prefetch([batch], slot)[0]
+            if pre is not None:
+                while len(self._hints) >= self.MAX_HINTS:  # never predicted: drop oldest
+                    self._hints.pop(next(iter(self._hints)))
+                # the entry holds the batch's image tensor: its id() is not reused while it lives
+                self._hints[id(batch["image"])] = (batch["image"], tuple(batch["question"]), pre)
+            if upto is not None and batch["image"] is upto["image"]:
+                break
+
     def _take_hint(self, batch):
+        pend = getattr(self, "_pending_hints", None)
+        if pend and any(b["image"] is batch["image"] for b, _ in pend):
+            self._flush_hints(upto=batch)
         hints = getattr(self, "_hints", None)
         if not hints:
             return None
@@ -530,7 +568,9 @@ class T5VisionModel(nn.Module):
                                 max_length=self.max_target_length, truncation=True)
         labels = torch.tensor(target["input_ids"])
         labels[labels == self.tokenizer.pad_token_id] = -100
-        return self.T5_model(inputs_embeds=combined, attention_mask=mask, labels=labels).loss
+        loss = self.T5_model(inputs_embeds=combined, attention_mask=mask, labels=labels).loss
+        self._flush_hints()  # the next batch's retrieval, beside this T5 forward (hint_next)
+        return loss
 
     def _forward_key(self, batch):
         # what prepare_input's result depends on besides the batch: the tied embedding's values

@@ -376,21 +376,37 @@ class DeviceT5:
         return tok[:, :int(first.max()) + 1]
 
     def generate(self, embeds, mask, max_new_tokens=20, decoder_start_token_id=0,
-                 eos_token_id=1, pad_token_id=0, lens=None) -> torch.Tensor:
+                 eos_token_id=1, pad_token_id=0, lens=None, while_running=None) -> torch.Tensor:
         """GenerationMixin.generate(do_sample=False) result (int64, host, trimmed).  Stops where
         greedy search stops: the decode runs in chunks of MPR_EOS_STOP_CHUNK steps (default 4:
         no cost measurable against one graph, tools/eos_chunk_ab.py, where 2 cost ~0.07 ms;
         0 = one graph of all steps) and no chunk is launched once every row has emitted eos
-        (mpr_t5_generate_stop; the skipped columns are pad, as the full loop writes)."""
+        (mpr_t5_generate_stop; the skipped columns are pad, as the full loop writes).
+        ``while_running``: a host callable run once the encoder and the first decode chunks are
+        enqueued, before the host waits on them (generate_begin + generate_poll: the same
+        launches as mpr_t5_generate_stop)."""
         chunk = int(os.environ.get("MPR_EOS_STOP_CHUNK", "4"))
         embeds_, mask_ = self._inputs(embeds, mask)
         B, L, _ = embeds_.shape
         if chunk <= 0 or B > 16 or max_new_tokens <= chunk:
+            if while_running is not None:
+                while_running()
             toks = self.generate_padded(embeds, mask, max_new_tokens, decoder_start_token_id,
                                         eos_token_id, pad_token_id, slot=self.PREDICT_SLOT,
                                         lens=lens)
             self.last_steps_run = int(max_new_tokens)
             return self.trim(toks, eos_token_id)
+        if while_running is not None:
+            out = self.generate_begin([(embeds_, mask_)], max_new_tokens, slot=self.PREDICT_SLOT,
+                                      stop_chunk=chunk, ahead=2,
+                                      decoder_start_token_id=decoder_start_token_id,
+                                      eos_token_id=eos_token_id, pad_token_id=pad_token_id)[0]
+            try:
+                while_running()
+            finally:
+                _, steps = self.generate_poll(self.PREDICT_SLOT, wait=True)
+            self.last_steps_run = steps
+            return self.trim(out, eos_token_id)
         out = torch.empty((B, max_new_tokens + 1), device=self.device, dtype=torch.int32)
         steps = ctypes.c_int32(0)
         _lib.call("mpr_t5_generate_stop", self._h, self.PREDICT_SLOT, _lib.ptr(embeds_),
