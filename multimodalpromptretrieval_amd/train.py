@@ -28,6 +28,8 @@ device.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -182,9 +184,12 @@ class _Tape:
 
     def __init__(self, trainer, tid: int):
         self.trainer, self.tid = trainer, tid
+        self.done = None  # a speculative backward's completion event (T5LossFn.forward)
 
     def release(self):
         if self.tid is not None and _lib._lib is not None:
+            if self.done is not None:  # the arena's next user comes after that backward
+                torch.cuda.current_stream().wait_event(self.done)
             _lib.call("mpr_t5_train_release", self.trainer, self.tid)
         self.tid = None
 
@@ -218,6 +223,7 @@ class T5LossFn(torch.autograd.Function):
         dr = cfg.dropout
         seed, thresh, scale = (dr.seed, dr.thresh, dr.scale) if dr is not None else (0, 0, 1.0)
         tr = cfg.trainer(dev)
+        _after_spec(tr, dev)
         tid = _lib.ctypes.c_int32()
         _lib.call("mpr_t5_train_forward", tr, parr, len(ps), _lib.ptr(emb), _lib.ptr(maskf), B, L,
                   _lib.ptr(ids_dev), _lib.ptr(lab32), T,
@@ -227,15 +233,51 @@ class T5LossFn(torch.autograd.Function):
         # the tape points into these: alive until the backward
         ctx.keep = (emb, maskf, ids_dev, lab32, ps, parr)
         ctx.dec_ids, ctx.n_valid, ctx.shape = dec_ids, n_valid, (B, L, d)
+        ctx.spec = None
+        if speculative_backward() and any(ctx.needs_input_grad) and dev.type == "cuda":
+            # main.py:177-186 runs model(batch), then predict(batch), then loss.backward(): the
+            # backward for a loss gradient of 1 is enqueued now on a side stream ordered after
+            # this forward, so it runs on the GPU beside predict()'s decode (which the host
+            # waits for) instead of after it; backward() then scales these gradients by the
+            # real loss gradient (x 1.0 when it is loss.backward(): the same bits).
+            cur = torch.cuda.current_stream(dev)
+            side = _spec_stream(dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                out = T5LossFn._native_backward(ctx, torch.ones((), device=dev))
+                done = torch.cuda.Event()
+                done.record(side)
+            ctx.spec = (out, done)
+            ctx.tape.done = done
+            _LAST_SPEC[tr.value] = done
         return loss
 
     @staticmethod
     def backward(ctx, dloss):
         # dloss stays on the device (the cross-entropy kernel reads it): no host wait
+        dl = dloss.detach().to(torch.float32).contiguous()
+        if ctx.spec is not None:
+            (d_emb, grads, flat), done = ctx.spec
+            cur = torch.cuda.current_stream(dl.device)
+            cur.wait_event(done)
+            for t in (flat, d_emb):
+                if t is not None:
+                    t.record_stream(cur)
+                    t.mul_(dl)
+            ctx.spec = None
+        else:
+            d_emb, grads, _ = T5LossFn._native_backward(ctx, dl)
+        ctx.tape.release()
+        ctx.keep = None
+        return (None, d_emb, None, None, *grads)
+
+    @staticmethod
+    def _native_backward(ctx, dl):
+        """mpr_t5_train_backward of the tape for loss gradient ``dl`` (device scalar) on the
+        current stream: (d_emb or None, per-parameter gradients, their flat buffer)."""
         needs = ctx.needs_input_grad
         emb, maskf, ids_dev, lab32, ps, parr = ctx.keep
         dev = emb.device
-        dl = dloss.detach().to(torch.float32).contiguous()
         # every gradient in one flat buffer (views): a stacked weight's gradient (q | k | v of a
         # layer) lands with one GEMM when its parts are adjacent
         sizes = [p.numel() for p in ps]
@@ -257,9 +299,31 @@ class T5LossFn(torch.autograd.Function):
         _lib.call("mpr_t5_train_backward", tr, ctx.tape.tid, parr, len(ps), _lib.ptr(dl),
                   1.0 / max(ctx.n_valid, 1), _lib.ptr(u), _lib.ptr(o), _lib.ptr(q), len(uniq),
                   gptr, _lib.ptr(d_emb), _s())
-        ctx.tape.release()
-        ctx.keep = None
-        return (None, d_emb, None, None, *grads)
+        return d_emb, grads, flat
+
+
+def speculative_backward() -> bool:
+    """T5LossFn's backward enqueued with its forward (MPR_SPEC_BACKWARD=0: at backward())."""
+    return os.environ.get("MPR_SPEC_BACKWARD", "1") != "0"
+
+
+_SPEC_STREAMS = {}
+_LAST_SPEC = {}  # trainer -> its latest speculative backward's completion event
+
+
+def _after_spec(tr, dev):
+    """Order the current stream after the trainer's latest speculative backward: the trainer's
+    scratch is shared by its calls, which must not overlap."""
+    ev = _LAST_SPEC.get(tr.value)
+    if ev is not None and dev.type == "cuda":
+        torch.cuda.current_stream(dev).wait_event(ev)
+
+
+def _spec_stream(dev):
+    st = _SPEC_STREAMS.get(str(dev))
+    if st is None:
+        st = _SPEC_STREAMS[str(dev)] = torch.cuda.Stream(dev)
+    return st
 
 
 _TRAINERS = {}
@@ -315,7 +379,9 @@ def trim_trainers(keep_idle: int = 0, destroy: bool = False):
             torch.cuda.synchronize(dev)
             _lib.load().mpr_model_destroy(tr)
             del _TRAINERS[key]
+            _LAST_SPEC.pop(tr.value, None)
         else:
+            _after_spec(tr, dev)
             _lib.call("mpr_t5_trainer_trim", tr, int(keep_idle), _lib.stream_ptr(dev))
 
 
