@@ -677,6 +677,91 @@ __global__ __launch_bounds__(1024) void max_kernel(const float* __restrict__ x, 
 constexpr int CB2_RT = 64;             // index rows per tile (2 x 32-row MFMA tiles)
 constexpr int CB2_BK = 64;             // k per LDS stage (4 x 16-deep MFMA steps)
 
+__device__ __forceinline__ void bf2_insert(float (&bk)[CB_L], int (&bi)[CB_L], float ck, int ci) {
+#pragma unroll
+  for (int t = 0; t < CB_L; ++t) {
+    const bool sw = ck < bk[t];
+    const float tk = sw ? bk[t] : ck;
+    const int ti = sw ? bi[t] : ci;
+    bk[t] = sw ? ck : bk[t];
+    bi[t] = sw ? ci : bi[t];
+    ck = tk;
+    ci = ti;
+  }
+}
+
+// The keys of one 64-row tile (the two 32x32 accumulators, zeroed here) into the lane's sorted
+// list: each key quantised with its row in the low 6 bits, the best three of the tile by integer
+// min / max, the best two inserted, the third bounding what was dropped (`drop`).
+__device__ __forceinline__ void bf2_tile_keys(f32x16 (&acc)[2], const float* xn, float qn_l, int lh,
+                                              int row0, float (&bk)[CB_L], int (&bi)[CB_L],
+                                              float& drop) {
+  uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const float key = fmaxf(fmaf(-2.0f, acc[mi][r], xn[rr]) + qn_l, 0.0f);
+      acc[mi][r] = 0.f;
+      const uint32_t v = (__float_as_uint(key) & ~63u) | (uint32_t)rr;
+      v3 = min(v3, max(v2, v));
+      v2 = min(v2, max(v1, v));
+      v1 = min(v1, v);
+    }
+  drop = fminf(drop, __uint_as_float(v3 & ~63u));
+  const float k1 = __uint_as_float(v1 & ~63u), k2 = __uint_as_float(v2 & ~63u);
+  if (k1 < bk[CB_L - 1]) bf2_insert(bk, bi, k1, row0 + (int)(v1 & 63u));
+  if (k2 < bk[CB_L - 1]) bf2_insert(bk, bi, k2, row0 + (int)(v2 & 63u));
+}
+
+// One list per (query, block): lane li takes lane li + 32's list (the same query's other rows)
+// and keeps the best CB_L of the 16.  Every row the merged list lacks has a key >= the new bound
+// min(both lanes' bounds, the smallest key pushed out here), so the re-rank's test is unchanged
+// and the select reads half the candidates.
+__device__ __forceinline__ void bf2_finish(float (&bk)[CB_L], int (&bi)[CB_L], float drop, int q,
+                                           bool qok, int lh, int rb, int RB, int64_t row_offset,
+                                           float* cand_key, int64_t* cand_id, float* lane_bound) {
+  float bound = fminf(bk[CB_L - 1], drop);
+  {
+    float ok[CB_L];
+    int oi[CB_L];
+#pragma unroll
+    for (int t = 0; t < CB_L; ++t) {
+      ok[t] = __shfl_xor(bk[t], 32, 64);
+      oi[t] = __shfl_xor(bi[t], 32, 64);
+    }
+    bound = fminf(bound, __shfl_xor(bound, 32, 64));
+    float pushed = INFINITY;
+#pragma unroll
+    for (int s = 0; s < CB_L; ++s) {
+      float ck = ok[s];
+      int ci = oi[s];
+#pragma unroll
+      for (int t = 0; t < CB_L; ++t) {
+        const bool sw = ck < bk[t];
+        const float tk = sw ? bk[t] : ck;
+        const int ti = sw ? bi[t] : ci;
+        bk[t] = sw ? ck : bk[t];
+        bi[t] = sw ? ci : bi[t];
+        ck = tk;
+        ci = ti;
+      }
+      pushed = fminf(pushed, ck);
+    }
+    bound = fminf(bound, pushed);
+  }
+  if (!qok || lh) return;
+  float* okp = cand_key + ((int64_t)q * RB + rb) * CB_L;
+  int64_t* oip = cand_id + ((int64_t)q * RB + rb) * CB_L;
+#pragma unroll
+  for (int t = 0; t < CB_L; ++t) {
+    okp[t] = bk[t];
+    oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
+  }
+  lane_bound[(int64_t)q * RB + rb] = bound;
+}
+
 template <int KS, int NW, int D, int BK = CB2_BK>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16* __restrict__ Xb,
                                                               const float* __restrict__ xnorm,
@@ -792,81 +877,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void scan_bf2_kernel(const __bf16*
       gload(j1, tt + (ks + 1 + D) / SPT, (ks + 1 + D) % SPT);
       __syncthreads();
     }
-    {  // keys of this row tile (6-bit row tag)
-      uint32_t v1 = 0xFFFFFFFFu, v2 = 0xFFFFFFFFu, v3 = 0xFFFFFFFFu;
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rr = mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const float key = fmaxf(fmaf(-2.0f, acc[mi][r], xn_s[tt & 1][rr]) + qn_l, 0.0f);
-          acc[mi][r] = 0.f;
-          const uint32_t v = (__float_as_uint(key) & ~63u) | (uint32_t)rr;
-          v3 = min(v3, max(v2, v));
-          v2 = min(v2, max(v1, v));
-          v1 = min(v1, v);
-        }
-      drop = fminf(drop, __uint_as_float(v3 & ~63u));
-      auto insert = [&](float ck, int ci) {
-#pragma unroll
-        for (int t = 0; t < CB_L; ++t) {
-          const bool sw = ck < bk[t];
-          const float tk = sw ? bk[t] : ck;
-          const int ti = sw ? bi[t] : ci;
-          bk[t] = sw ? ck : bk[t];
-          bi[t] = sw ? ci : bi[t];
-          ck = tk;
-          ci = ti;
-        }
-      };
-      const int row0 = (rb + tt * RB) * CB2_RT;  // n < 2^31 (checked by the launcher)
-      const float k1 = __uint_as_float(v1 & ~63u), k2 = __uint_as_float(v2 & ~63u);
-      if (k1 < bk[CB_L - 1]) insert(k1, row0 + (int)(v1 & 63u));
-      if (k2 < bk[CB_L - 1]) insert(k2, row0 + (int)(v2 & 63u));
-    }
+    // keys of this row tile (n < 2^31: checked by the launcher)
+    bf2_tile_keys(acc, xn_s[tt & 1], qn_l, lh, (rb + tt * RB) * CB2_RT, bk, bi, drop);
   }
-  // One list per (query, block): lane li takes lane li + 32's list (the same query's other rows)
-  // and keeps the best CB_L of the 16.  Every row the merged list lacks has a key >= the new bound
-  // min(both lanes' bounds, the smallest key pushed out here), so the re-rank's test is unchanged
-  // and the select reads half the candidates.
-  float bound = fminf(bk[CB_L - 1], drop);
-  {
-    float ok[CB_L];
-    int oi[CB_L];
-#pragma unroll
-    for (int t = 0; t < CB_L; ++t) {
-      ok[t] = __shfl_xor(bk[t], 32, 64);
-      oi[t] = __shfl_xor(bi[t], 32, 64);
-    }
-    bound = fminf(bound, __shfl_xor(bound, 32, 64));
-    float pushed = INFINITY;
-#pragma unroll
-    for (int s = 0; s < CB_L; ++s) {
-      float ck = ok[s];
-      int ci = oi[s];
-#pragma unroll
-      for (int t = 0; t < CB_L; ++t) {
-        const bool sw = ck < bk[t];
-        const float tk = sw ? bk[t] : ck;
-        const int ti = sw ? bi[t] : ci;
-        bk[t] = sw ? ck : bk[t];
-        bi[t] = sw ? ci : bi[t];
-        ck = tk;
-        ci = ti;
-      }
-      pushed = fminf(pushed, ck);
-    }
-    bound = fminf(bound, pushed);
-  }
-  if (!qok || lh) return;
-  float* okp = cand_key + ((int64_t)q * RB + rb) * CB_L;
-  int64_t* oip = cand_id + ((int64_t)q * RB + rb) * CB_L;
-#pragma unroll
-  for (int t = 0; t < CB_L; ++t) {
-    okp[t] = bk[t];
-    oip[t] = bi[t] == INT_MAX ? -1 : (int64_t)bi[t] + row_offset;
-  }
-  lane_bound[(int64_t)q * RB + rb] = bound;
+  bf2_finish(bk, bi, drop, q, qok, lh, rb, RB, row_offset, cand_key, cand_id, lane_bound);
 }
 
 // Select + re-rank without a full selection (block per query, the one-list-per-block layout of
@@ -1396,6 +1410,10 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
       // 8 waves: 256-deep stages, one in flight (two barriers per 64-row tile instead of 8 at
       // 64-deep x 4 in flight, the same 32 KiB of loads in flight per CU): C5 search 0.389 ->
       // 0.357 ms, 1/8 shard 72 -> 70 us (tools/scan_c5.py)
+      // (Measured and dropped: the index tile staged by LDS-DMA, global_load_lds_dwordx4 into a
+      // 3-buffer ring with 2 stages of 32 KiB in flight, counted vmcnt + raw s_barrier, XOR-
+      // swizzled by source address: bit-identical, C5 search 0.382-0.392 vs 0.361-0.374 ms, the
+      // 1/8 shard 70 vs 66 us; not bound by HBM bytes in flight, profiles/r05_scan_glds_ab.txt.)
       if (NW == 8) MPR_BF2(32, 8, 1, 256); else MPR_BF2(32, 4, 2, 64);
     } else {
       if (NW == 8) MPR_BF2(16, 8, 4, 64); else MPR_BF2(16, 4, 2, 64);
