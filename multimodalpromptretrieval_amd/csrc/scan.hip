@@ -1410,7 +1410,10 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
       // 8 waves: 256-deep stages, one in flight (two barriers per 64-row tile instead of 8 at
       // 64-deep x 4 in flight, the same 32 KiB of loads in flight per CU): C5 search 0.389 ->
       // 0.357 ms, 1/8 shard 72 -> 70 us (tools/scan_c5.py)
-      // (Measured and dropped: the index tile staged by LDS-DMA, global_load_lds_dwordx4 into a
+      // (Measured and dropped: four waves of 64 queries each (two 32-query groups per wave, one
+      // wave per SIMD, every A fragment read feeding two MFMAs): 256 VGPRs + 256 AGPRs and still
+      // 96-192 B of spills, C5 search 0.49-0.56 vs 0.37 ms, profiles/r05_scan_qg2_ab.txt.
+      // The index tile staged by LDS-DMA, global_load_lds_dwordx4 into a
       // 3-buffer ring with 2 stages of 32 KiB in flight, counted vmcnt + raw s_barrier, XOR-
       // swizzled by source address: bit-identical, C5 search 0.382-0.392 vs 0.361-0.374 ms, the
       // 1/8 shard 70 vs 66 us; not bound by HBM bytes in flight, profiles/r05_scan_glds_ab.txt.)
