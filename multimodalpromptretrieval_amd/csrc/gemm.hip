@@ -1571,7 +1571,9 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
       const unsigned gy = (unsigned)cdiv(a.M, 32);
       // (Four 16-column tiles per block sharing each staged 32-row slab — the slab is staged
       // once per 16 columns — measured slower: C5's t5-base 128-row decodes 84.0 -> 96.3 ms
-      // per batch, the serving loop 3.77-3.79 -> 3.86-3.88 ms per step.)
+      // per batch, the serving loop 3.77-3.79 -> 3.86-3.88 ms per step.  Two tiles per 64-row
+      // block above 128 rows, halving the rows' L2 reads: 146-164 VGPRs, one block per CU, C5
+      // end to end 46.3-46.7 -> 50.5 ms per batch, round 5.)
       // 4-chunk passes above 4 chunks per wave, so the block's slabs take 70 KB of LDS instead
       // of 136 KB and two blocks fit per CU (the 8-chunk slab holds one: t5-base's 576-block
       // 128-row qkv ran in ~3 rounds of blocks).  Same chunk order per accumulator chain,
