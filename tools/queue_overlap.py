@@ -37,3 +37,22 @@ for t, d in ev:
     cur += d
     last = t
 print(f"busy {busy / 1e6:.2f} ms, >= 2 kernels at once {multi / 1e6:.2f} ms")
+# how the queues interleave: runs of consecutive kernels (start order) from one queue
+runs = []
+for s, e, q, st, n in win:
+    if runs and runs[-1][0] == q:
+        runs[-1][1] += 1
+        runs[-1][3] = e
+    else:
+        runs.append([q, 1, s, e])
+per_q = {}
+for q, c, s, e in runs:
+    per_q.setdefault(q, []).append((c, e - s))
+for q, lst in sorted(per_q.items()):
+    cs = sorted(c for c, _ in lst)
+    print(f"queue {q}: {len(lst)} runs, kernels per run median {cs[len(cs) // 2]} max {cs[-1]}, "
+          f"longest run {max(d for _, d in lst) / 1e6:.2f} ms")
+if len(sys.argv) > 2:  # the run sequence: queue, kernels, start (ms into the window), duration
+    t0 = win[0][0]
+    for q, c, s, e in runs[:int(sys.argv[2])]:
+        print(f"  q{q} {c:5d} kernels at +{(s - t0) / 1e6:7.2f} ms for {(e - s) / 1e6:6.2f} ms")

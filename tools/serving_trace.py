@@ -55,8 +55,9 @@ cfg = bench.CONFIGS["c2"]
 model, _, _ = bench.build(cfg, dev, None)
 batches = bench.make_batches(4, cfg["B"], seed=100)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+warm = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 with torch.no_grad():
-    for _ in model.predict_many((batches[i % 4] for i in range(8)), eos_stop=False):
+    for _ in model.predict_many((batches[i % 4] for i in range(warm)), eos_stop=False):
         pass
     torch.cuda.synchronize()
     time.sleep(0.05)
