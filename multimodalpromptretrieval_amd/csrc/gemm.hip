@@ -676,8 +676,13 @@ __global__ __launch_bounds__(256) void pack_x3_kernel(const float* __restrict__ 
   out[(t * 3 + 2) * 64 + lane] = h2;
 }
 
-template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16>
+// SB = 2: four A stages and a block barrier every second K tile (tile t + 3 is written while
+// tile t + 1 is read; each stage is rewritten two iterations after its last read, with a barrier
+// in between), half the barriers of SB = 1 (two stages, one barrier per K tile).
+template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16, int SB = 1>
 __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
+  static_assert(SB == 1 || (SB == 2 && D % 2 == 0), "SB = 2 needs an even D");
+  constexpr int NSTG = 2 * SB, AHEAD = SB + 1;  // A stages; tile written at iteration t: t + AHEAD
   constexpr int NS = BK / 16;  // 16-deep MFMA steps per K tile
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
@@ -779,39 +784,41 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
 
   const int nk = (K + BK - 1) / BK;
   const int nkr = (nk + D - 1) / D * D;
-  aload(0, 0);
-  swrite(0, 0);
-  aload(0, 1);
-  swrite(1, 0);
+#pragma unroll
+  for (int t0 = 0; t0 < AHEAD; ++t0) {
+    aload(0, t0);
+    swrite(t0, 0);
+  }
 #pragma unroll
   for (int j = 0; j < D; ++j) {
-    aload(j, 2 + j);
+    aload(j, AHEAD + j);
     bload(j, j);
   }
   __syncthreads();
   sread(0, fa);
   __syncthreads();
   // Iteration t: multiply tile t (A fragments read the iteration before, W fragments loaded D
-  // iterations before), read tile t+1's A fragments from the other stage, write tile t+2's A
-  // into tile t's stage, re-arm the register slots with tile t+2+D's A and tile t+D's W.
+  // iterations before), read tile t+1's A fragments from its stage, write tile t+AHEAD's A into
+  // the stage of tile t+AHEAD-NSTG (read by every wave before the last barrier), re-arm the
+  // register slots with tile t+AHEAD+D's A and tile t+D's W.
   constexpr int U1 = NMF / 3 > 0 ? NMF / 3 : 1;
   for (int kt = 0; kt < nkr; kt += D) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-      const int st = (kt + j) & 1;
+      const int t = kt + j;
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
       mfmas(j, 0, U1);
       __builtin_amdgcn_sched_barrier(0);
-      sread(st ^ 1, na);
+      sread((t + 1) % NSTG, na);
       __builtin_amdgcn_sched_barrier(0);
       mfmas(j, U1, NMF);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(0);
-      swrite(st, j);
-      aload(j, kt + j + 2 + D);
-      bload(j, kt + j + D);
-      __syncthreads();
+      swrite((t + AHEAD) % NSTG, j);
+      aload(j, t + AHEAD + D);
+      bload(j, t + D);
+      if (SB == 1 || (j & 1)) __syncthreads();
 #pragma unroll
       for (int s4 = 0; s4 < NS; ++s4)
 #pragma unroll
@@ -848,10 +855,10 @@ __device__ __forceinline__ void gemm_x3p_tile(const GemmArgs& a, int bx, int by,
 }
 
 // gemm_x3_kernel's grid and tile order, the packed-W tile
-template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16>
+template <int BM, int BN, int WM, int WN, int D, bool KT, int BK = 16, int SB = 1>
 __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm_x3p_kernel(
     const GemmGroup grp) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * 3 * BM * (BK + 8) / 2];
+  __shared__ __attribute__((aligned(16))) float smem[2 * SB * 3 * BM * (BK + 8) / 2];
   const int total = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
   int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
@@ -890,10 +897,10 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN))) void gemm
     bx = tt / rem;
     by = full + (tt - bx * rem);
   }
-  gemm_x3p_tile<BM, BN, WM, WN, D, KT, BK>(a, bx, by, smem);
+  gemm_x3p_tile<BM, BN, WM, WN, D, KT, BK, SB>(a, bx, by, smem);
 }
 
-template <int BM, int BN, int WM, int WN, int D, int BK = 16>
+template <int BM, int BN, int WM, int WN, int D, int BK = 16, int SB = 1>
 int launch_gemm_x3p_group(const GemmGroup& g, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN));
   int64_t tiles = 0;
@@ -904,10 +911,10 @@ int launch_gemm_x3p_group(const GemmGroup& g, hipStream_t s) {
   }
   if (tiles == 0) return MPR_OK;
   if (kt)
-    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, true, BK>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, true, BK, SB>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   else
-    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, false, BK>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3p_kernel<BM, BN, WM, WN, D, false, BK, SB>), dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -1341,6 +1348,11 @@ const bool g_gemm_f32 = [] {
   return e && strcmp(e, "f32") == 0;
 }();
 
+const bool g_x3p_sb1 = [] {
+  const char* e = getenv("MPR_X3P_SB");
+  return e && e[0] == '1';
+}();
+
 int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
   double flops = 0, bytes = 0;
   for (int i = 0; i < g.n; ++i) {
@@ -1367,7 +1379,9 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
       case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>(g, s);
       case X3_WIDE32: return launch_gemm_x3_group<128, 128, 2, 1, 32, 2, 1, 2>(g, s);
       case X3_SMALL: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>(g, s);
-      case X3P_WIDE: return launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s);
+      case X3P_WIDE:  // four A stages, a barrier every second K tile (MPR_X3P_SB=1: every tile)
+        return g_x3p_sb1 ? launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s)
+                         : launch_gemm_x3p_group<128, 128, 2, 1, 2, 16, 2>(g, s);
       case X3P_SMALL: return launch_gemm_x3p_group<64, 64, 1, 1, 2>(g, s);
       case X3P_SMALL3: return launch_gemm_x3p_group<64, 64, 1, 1, 2, 32>(g, s);
       default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);

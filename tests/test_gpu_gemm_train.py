@@ -83,6 +83,7 @@ def _packed(W):
     (800, 3072, 768, 2, False),     # ViT fc1 shape, relu
     (77, 200, 52, 0, True),         # ragged: N and K tails, K % 16 != 0
     (1000, 1000, 1000, 2, True),    # odd tile counts
+    (1300, 2100, 772, 0, True),     # 128x128 tiles (four A stages) with a K tail, odd K tiles
 ])
 def test_packed_weight_gemm_is_bit_identical(device, M, N, K, act, res):
     """mpr_gemm_f32_packed (W fragments from the pack_x3 image, no LDS staging of W) returns the

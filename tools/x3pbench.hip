@@ -82,10 +82,11 @@ int main() {
       {"x3p 128x128 4x1 D3", launch_gemm_x3p_group<128, 128, 4, 1, 3>, true},
       {"x3p 128x128 2x1 D2 (8w)", launch_gemm_x3p_group<128, 128, 2, 1, 2>, true},
       {"x3p 128x128 2x1 D3 (8w)", launch_gemm_x3p_group<128, 128, 2, 1, 3>, true},
-      {"x3p 256x128 4x1 D2 (8w)", launch_gemm_x3p_group<256, 128, 4, 1, 2>, true},
-      {"x3p 256x128 4x1 D1 (8w)", launch_gemm_x3p_group<256, 128, 4, 1, 1>, true},
-      {"x3p 128x256 2x2 D2 (8w)", launch_gemm_x3p_group<128, 256, 2, 2, 2>, true},
-      {"x3p 128x128 2x2 D2 (4w)", launch_gemm_x3p_group<128, 128, 2, 2, 2>, true},
+      {"x3p 128x128 2x1 D2 SB2", launch_gemm_x3p_group<128, 128, 2, 1, 2, 16, 2>, true},
+      {"x3p 128x128 2x1 D4 SB2", launch_gemm_x3p_group<128, 128, 2, 1, 4, 16, 2>, true},
+      {"x3p 64x64 1x1 D2 SB2", launch_gemm_x3p_group<64, 64, 1, 1, 2, 16, 2>, true},
+      {"x3p 64x64 1x1 D2 k32", launch_gemm_x3p_group<64, 64, 1, 1, 2, 32>, true},
+      {"x3p 64x64 1x1 D2 k32 SB2", launch_gemm_x3p_group<64, 64, 1, 1, 2, 32, 2>, true},
       {"x3p 64x128 1x2 D2", launch_gemm_x3p_group<64, 128, 1, 2, 2>, true},
       {"x3p 64x128 1x2 D3", launch_gemm_x3p_group<64, 128, 1, 2, 3>, true},
       {"x3p 128x64 1x1 D2 (8w)", launch_gemm_x3p_group<128, 64, 1, 1, 2>, true},
