@@ -705,8 +705,13 @@ def train_leg(cfg, weights, retr, device, batches, steps: int = 10):
         return v
 
     try:
-        for i in range(3):
-            step(batches[i % len(batches)])
+        # warmup through the same lookahead path as the timed steps (its hint stream, prefetch
+        # slot and decode graphs are first used there; a plain-step warmup left those one-time
+        # costs inside the timed window: 27-30 vs 16 ms per step)
+        warm = (dict(b, image=b["image"].view_as(b["image"]))
+                for b in (batches[i % len(batches)] for i in range(4)))
+        for b in lookahead(warm, m):
+            step(b)
         torch.cuda.synchronize()
         # main.py's training loop under the dropin launcher: the loader iterated one batch ahead
         # (serving.lookahead -> model.hint_next: the next batch's retrieval towers, scan and image

@@ -264,11 +264,11 @@ using x3::bf16x4;
 using x3::bf16x8;
 using x3::split3;
 
-template <int BM, int BN, int BK>
+template <int BM, int BN, int BK, int SB = 1>
 constexpr int x3_lds_floats() {
   // per stage: 3 planes x (BM + BN) rows x (BK + 8) bf16 (16-byte row pad: conflict-free
-  // ds_read_b128 of 32 rows), two stages, in floats
-  return 2 * 3 * (BM + BN) * (BK + 8) / 2;
+  // ds_read_b128 of 32 rows), 2 SB stages, in floats
+  return 2 * SB * 3 * (BM + BN) * (BK + 8) / 2;
 }
 
 // V (variants, the round-1 x3bench lab, git show 28e8ac6:tools/x3bench.hip): bit 0 interleaves the accumulators' MFMAs (term-major; the
@@ -281,8 +281,11 @@ constexpr int x3_lds_floats() {
 // their results are not stored.  (Measured and dropped: W pre-split into three bf16 planes once
 // per model, copied into LDS without conversion: +8% on 64x128 tiles, -11% on 128x128 — the
 // planes' 32-byte row segments per k-tile coalesce worse than the 64-byte fp32 ones.)
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0>
+// SB = 2: four stages and a block barrier every second K tile, as gemm_x3p_tile's SB.
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0, int SB = 1>
 __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
+  static_assert(SB == 1 || (SB == 2 && D % 2 == 0), "SB = 2 needs an even D");
+  constexpr int NSTG = 2 * SB, AHEAD = SB + 1;
   constexpr int WAVES_N = BN / (32 * WN);
   constexpr int WAVES_MN = (BM / (32 * WM)) * WAVES_N;
   constexpr int NT = 64 * WAVES_MN * KW;
@@ -410,35 +413,36 @@ __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, 
 
   const int nk = (K + BK - 1) / BK;
   const int nkr = (nk + D - 1) / D * D;
-  gload(0, 0);
-  swrite(0, 0);
-  gload(0, BK);
-  swrite(1, 0);
 #pragma unroll
-  for (int j = 0; j < D; ++j) gload(j, (2 + j) * BK);
+  for (int t0 = 0; t0 < AHEAD; ++t0) {
+    gload(0, t0 * BK);
+    swrite(t0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) gload(j, (AHEAD + j) * BK);
   __syncthreads();
   sread(0, fa, fb);
   __syncthreads();  // every wave's tile-0 reads land before iteration 0 rewrites stage 0
-  // Iteration t (one barrier): multiply tile t (fragments in registers), read tile t+1's
-  // fragments from the other stage under the first MFMAs, write tile t+2 into tile t's stage
-  // (read by every wave before the previous barrier) and re-arm the register slot.
+  // Iteration t: multiply tile t (fragments in registers), read tile t+1's fragments from its
+  // stage under the first MFMAs, write tile t+AHEAD into the stage of tile t+AHEAD-NSTG (read by
+  // every wave before the last barrier) and re-arm the register slot; a barrier every SB tiles.
   constexpr int U1 = NMF / 3 > 0 ? NMF / 3 : 1;
   for (int kt = 0; kt < nkr; kt += D) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-      const int st = (kt + j) & 1;
+      const int t = kt + j;
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((V & 2) != 0) __builtin_amdgcn_s_setprio(1);
       mfmas(0, U1);
       __builtin_amdgcn_sched_barrier(0);
-      sread(st ^ 1, na, nb);
+      sread((t + 1) % NSTG, na, nb);
       __builtin_amdgcn_sched_barrier(0);
       mfmas(U1, NMF);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((V & 2) != 0) __builtin_amdgcn_s_setprio(0);
-      swrite(st, j);
-      gload(j, (kt + j + 2 + D) * BK);
-      __syncthreads();
+      swrite((t + AHEAD) % NSTG, j);
+      gload(j, (t + AHEAD + D) * BK);
+      if (SB == 1 || (j & 1)) __syncthreads();
       advance();
     }
   }
@@ -555,10 +559,10 @@ int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
 // by the largest problem instead (blockIdx.z per problem) leaves the small problems' slices
 // mostly empty, and the remap then gives whole XCDs nothing to do (the tower launches' text
 // problems: fc2 231 -> see DESIGN §3).
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0, int SB = 1>
 __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_x3_kernel(
     const GemmGroup grp) {
-  __shared__ __attribute__((aligned(16))) float smem[x3_lds_floats<BM, BN, BK>()];
+  __shared__ __attribute__((aligned(16))) float smem[x3_lds_floats<BM, BN, BK, SB>()];
   const int total = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, q = total >> 3, r = total & 7;
   int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
@@ -612,11 +616,11 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
     bx = tt / rem;
     by = full + (tt - bx * rem);
   }
-  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT, V>(a, bx, by, smem);
+  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT, V, SB>(a, bx, by, smem);
 }
 
 // KT when some K % BK != 0 or cdiv(K, BK) % D != 0
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, int V = 0>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, int V = 0, int SB = 1>
 int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   constexpr int NT = 64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW;
   int64_t tiles = 0;
@@ -629,10 +633,11 @@ int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
   }
   if (tiles == 0) return MPR_OK;
   if (kt)
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, true, V>), dim3((unsigned)tiles),
-                       dim3(NT), 0, s, g);
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, true, V, SB>),
+                       dim3((unsigned)tiles), dim3(NT), 0, s, g);
   else
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, false, V>), dim3((unsigned)tiles),
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, false, V, SB>),
+                       dim3((unsigned)tiles),
                        dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
@@ -1339,7 +1344,7 @@ namespace {
 // or two concatenated: bit-identical results).
 enum GemmKind : int {
   F32_BIG = 0, F32_SMALL = 1, X3_WIDE = 2, X3_TALL = 3, X3_SMALL = 4, X3_WIDE32 = 5,
-  X3P_WIDE = 6, X3P_SMALL = 7, X3P_SMALL3 = 8
+  X3P_WIDE = 6, X3P_SMALL = 7, X3P_SMALL3 = 8, X3_WIDE_SB2 = 9, X3_SMALL_SB2 = 10
 };
 
 
@@ -1348,6 +1353,10 @@ const bool g_gemm_f32 = [] {
   return e && strcmp(e, "f32") == 0;
 }();
 
+const bool g_x3_sb1 = [] {
+  const char* e = getenv("MPR_X3_SB");
+  return e && e[0] == '1';
+}();
 const bool g_x3p_sb1 = [] {
   const char* e = getenv("MPR_X3P_SB");
   return e && e[0] == '1';
@@ -1379,6 +1388,8 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
       case X3_WIDE: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>(g, s);
       case X3_WIDE32: return launch_gemm_x3_group<128, 128, 2, 1, 32, 2, 1, 2>(g, s);
       case X3_SMALL: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>(g, s);
+      case X3_WIDE_SB2: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2, 2>(g, s);
+      case X3_SMALL_SB2: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1, 0, 2>(g, s);
       case X3P_WIDE:  // four A stages, a barrier every second K tile (MPR_X3P_SB=1: every tile)
         return g_x3p_sb1 ? launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s)
                          : launch_gemm_x3p_group<128, 128, 2, 1, 2, 16, 2>(g, s);
@@ -1473,13 +1484,20 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // LDS for decode blocks) and the loop 4157-4165 -> 4212-4309 QA pairs/s at 40 steps.  Every
   // 128x128 launch on 32-deep tiles halves the blocks per CU of the > 256-block launches
   // (4073-4127, r02); 16-deep only is slower in the loop.
-  if (fam.n)
-    MPR_TRY(gemm_launch(fam, b128 >= 160 && b128 <= 256
-                                 ? X3_WIDE32
-                             : b128 >= 160                     ? X3_WIDE
-                             : (b64x128 < 128 || short_k) ? X3_SMALL
-                                                          : X3_TALL,
-                        s));
+  // K >= 1536 (the trainer's FFN-out and weight-gradient GEMMs): the 16-deep tiles take four
+  // stages and one barrier per two K tiles (x3pbench, profiles/r05_x3_sb2.txt: T5 wo 1536x512x2048
+  // 43.9 -> 40.4 us on 64x64, weight gradients 2048x512x1600 37.9 -> 35.1; shorter K loses, so
+  // it stays on one barrier per tile).  Bit-identical either way.
+  const bool sb2 = max_k >= 1536 && !g_x3_sb1;
+  if (fam.n) {
+    int kind = b128 >= 160 && b128 <= 256      ? X3_WIDE32
+               : b128 >= 160                   ? X3_WIDE
+               : (b64x128 < 128 || short_k)    ? X3_SMALL
+                                               : X3_TALL;
+    if (sb2 && kind == X3_WIDE) kind = X3_WIDE_SB2;
+    if (sb2 && kind == X3_SMALL) kind = X3_SMALL_SB2;
+    MPR_TRY(gemm_launch(fam, kind, s));
+  }
   return MPR_OK;
 }
 

@@ -72,6 +72,8 @@ int main() {
       {"vit qkv 800x2304x768", 800, 2304, 768, 2},   {"vit fc2 800x768x3072", 800, 768, 3072, 2},
       {"t5 qkv 1536x1536x512", 1536, 1536, 512, 1},  {"t5 wo 1536x512x2048", 1536, 512, 2048, 1},
       {"odd 1000x1000x1000", 1000, 1000, 1000, 1},   {"odd 77x200x52", 77, 200, 52, 1},
+      {"train dW ff 2048x512x1600", 2048, 512, 1600, 1}, {"train dW qkv 1536x512x1600", 1536, 512, 1600, 1},
+      {"train qkv 1600x1536x512", 1600, 1536, 512, 1},
   };
   using L = std::function<int(const GemmGroup&, hipStream_t)>;
   struct Var { const char* name; L fn; bool packed; };
@@ -79,6 +81,8 @@ int main() {
       {"x3  128x128 2x1 k16 prio", launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2>, false},
       {"x3  64x128 k32", launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>, false},
       {"x3  64x64 k16", launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>, false},
+      {"x3  128x128 2x1 k16 prio SB2", launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2, 2>, false},
+      {"x3  64x64 k16 SB2", launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1, 0, 2>, false},
       {"x3p 128x128 4x1 D3", launch_gemm_x3p_group<128, 128, 4, 1, 3>, true},
       {"x3p 128x128 2x1 D2 (8w)", launch_gemm_x3p_group<128, 128, 2, 1, 2>, true},
       {"x3p 128x128 2x1 D3 (8w)", launch_gemm_x3p_group<128, 128, 2, 1, 3>, true},
