@@ -10,7 +10,8 @@ if [ -d "$src" ]; then
   [ -f "$src/prof/run_kernel_stats.csv" ] && cp "$src/prof/run_kernel_stats.csv" "profiles/${TAG}_kernel_stats.csv"
   [ -f "$src/replay_window.json" ] && cp "$src/replay_window.json" "profiles/${TAG}_replay_window.json"
   [ -f "$src/pmc_gemm.json" ] && cp "$src/pmc_gemm.json" "profiles/${TAG}_pmc_gemm.json"
-  [ -f "$src/serving_trace.txt" ] && cp "$src/serving_trace.txt" "profiles/${TAG}_serving_trace.txt"
+  [ -f "$src/loop_events.txt" ] && grep -v amdgpu.ids "$src/loop_events.txt" > "profiles/${TAG}_loop_events.txt"
+  [ -f "$src/predict_events.txt" ] && grep -v amdgpu.ids "$src/predict_events.txt" > "profiles/${TAG}_predict_events.txt"
 fi
 if [ -n "$SCAN" ] && [ -d "gpurun_out/$SCAN" ]; then
   s=gpurun_out/$SCAN

@@ -47,11 +47,12 @@ if [ -z "$SKIP_PROF" ]; then
     "$OUT/pmc_WRITE_SIZE/run_counter_collection.csv" "$OUT/pmc_gemm.json" >> "$OUT/prof.log" 2>&1
   rm -f "$OUT"/pmc_*/run_counter_collection.csv
 fi
-if [ -z "$SKIP_PROF" ]; then  # where the serving loop's GPU time goes (kernel classes, idle gaps)
-  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/st" \
-    -- python tools/serving_trace.py 20 > "$OUT/serving_trace.txt" 2>&1
-  ok_or_stop $? serving_trace 0
-  python tools/serving_trace.py --report "$OUT/st" >> "$OUT/serving_trace.txt" 2>&1
-  rm -rf "$OUT/st"
+if [ -z "$SKIP_PROF" ]; then
+  # the serving loop's and one predict()'s stream timelines from hipEvents, unprofiled (a
+  # rocprofv3 kernel trace blocks the host in every graph launch: profiles/r05_profiler_block.txt)
+  timeout -k 10 300 python tools/loop_events.py 40 > "$OUT/loop_events.txt" 2>&1
+  ok_or_stop $? loop_events 0
+  timeout -k 10 300 python tools/predict_events.py 12 > "$OUT/predict_events.txt" 2>&1
+  ok_or_stop $? predict_events 0
 fi
 echo done >> "$OUT/steps.log"
