@@ -27,6 +27,7 @@ pipeline (torch-CPU fp32, KV-cached greedy decode) on a bounded sample of the sa
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -660,7 +661,8 @@ def eos_leg(cfg, weights, retr, device, batches, steps: int):
             key = "eos_stop" if stop else "forced_20"
             out[key] = {"qa_pairs_per_s": round(steps * cfg["B"] / el, 1),
                         "steps_run_per_call": loops[0].steps_run}
-    m = None
+    m = loops = None
+    gc.collect()  # the eos model's device handles (held by reference cycles) go before the next leg
     torch.cuda.empty_cache()
     return out
 
@@ -1147,7 +1149,7 @@ def main():
 
     host_ms, flop_per_pair = pipeline_work(model, retr, batches, cfg)
     eos = eos_leg(cfg, weights, retr, device, batches, args.steps) if not args.no_eos_leg else None
-    train = (train_leg(cfg, weights, retr, device, batches)
+    train = (train_leg(cfg, weights, retr, device, batches, steps=20)
              if rank == 0 and world == 1 and not args.no_train_leg else None)
 
     roofline = None

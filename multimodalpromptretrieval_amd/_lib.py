@@ -275,12 +275,16 @@ def separate_decode_stream(idx: int) -> bool:
     return bool(decode_cus(idx))
 
 
+PIPELINE_ROLES = ("encode:towers", "gen:0", "gen:1", "train:spec")
+
+
 def role_stream(device, role: str):
     """A process-lifetime stream for one role of the serving pipeline: ``"decode"`` (the T5
     greedy loop, CU partition only), ``"gen:<slot>"`` (a batch's T5 generate in the serving loop)
     or ``"encode:<tag>"`` (retrieval towers).  With a CU partition
     (decode_cus() > 0) the decode stream is restricted to the first n CUs (mask bits [0, n)) and
-    the encoder streams to the rest; otherwise plain non-blocking streams with
+    the encoder streams to the rest; ``"train:spec"`` is the trainer's speculative backward
+    (encoder priority); otherwise plain non-blocking streams with
     stream_priorities().  Returned as torch.cuda.ExternalStream so torch work can be enqueued on
     it as well."""
     import torch
@@ -304,8 +308,8 @@ def role_stream(device, role: str):
             call("mpr_stream_create", 0, mask, words, ctypes.byref(h))
         else:
             pe, pg = stream_priorities()
-            call("mpr_stream_create", pe if role.startswith("encode") else pg, None, 0,
-                 ctypes.byref(h))
+            call("mpr_stream_create", pe if role.startswith(("encode", "train")) else pg, None,
+                 0, ctypes.byref(h))
     st = torch.cuda.ExternalStream(h.value, device=dev)
     _role_streams[key] = st
     return st
@@ -321,6 +325,13 @@ def ensure_device(device) -> None:
     if idx not in _inited:
         call("mpr_init", c_int32(idx))
         _inited.add(idx)
+        # the pipeline's streams, created once in a fixed order right after init: a stream's
+        # hardware queue (4 per process) is fixed at its creation, and creating these on first
+        # use left their queue sharing to whatever ran before (a training step after another
+        # model's serving loop measured 24 ms against 13.5, profiles/r05_train_streams.txt)
+        if os.environ.get("MPR_EAGER_STREAMS", "1") != "0":
+            for role in PIPELINE_ROLES:
+                role_stream(torch.device("cuda", idx), role)
 
 
 def tensor_array(tensors) -> ctypes.Array:

@@ -393,9 +393,11 @@ class T5VisionModel(nn.Module):
                 return ans
         memo = self._take_forward_inputs(batch)
         pre = self._take_hint(batch) if memo is None else None
-        if pre is not None:
-            # the retrieval stream may already hold the NEXT hinted batch's towers: the T5 part
-            # runs on a stream of its own (the serving loop's first generate stream)
+        if pre is not None or memo is not None:
+            # the retrieval stream may already hold the NEXT hinted batch's towers (and, after a
+            # training forward, its speculative backward runs beside): the T5 part runs on a
+            # stream of its own (the serving loop's first generate stream) instead of queueing
+            # behind them (main.py:177-179's predict after forward: profiles/r05_train_streams.txt)
             which = os.environ.get("MPR_AHEAD_T5_STREAM", "gen:0")
             if which == "private":
                 if not hasattr(self, "_s_main"):

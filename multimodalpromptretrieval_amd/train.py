@@ -320,9 +320,14 @@ def _after_spec(tr, dev):
 
 
 def _spec_stream(dev):
+    # a library role stream (created once, low priority: the backward is off the critical path
+    # until backward(), while predict()'s decode is on it), not a torch pool stream, whose
+    # hardware queue depends on how many pool streams the process handed out before
     st = _SPEC_STREAMS.get(str(dev))
     if st is None:
-        st = _SPEC_STREAMS[str(dev)] = torch.cuda.Stream(dev)
+        st = _SPEC_STREAMS[str(dev)] = (torch.cuda.Stream(dev)
+                                        if os.environ.get("MPR_SPEC_STREAM") == "pool"
+                                        else _lib.role_stream(dev, "train:spec"))
     return st
 
 
