@@ -967,7 +967,7 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_out=None, serving_an
         # forced steps keep finished rows on pad, as the device loop does: the decoded answers
         # compare as strings
         n_pairs = n_prompt = n_ans = n_ids = n_loop = n_loop_pred = 0
-        dist_ok, margins, guards, dq = True, [], [], []
+        dist_ok, margins, guards, dq, mism = True, [], [], [], []
         for i, (preds, prompts, trace) in cpu_out.items():
             g = gpu_out[i]
             n_pairs += len(preds)
@@ -982,6 +982,9 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_out=None, serving_an
             if serving_answers is not None and i < len(serving_answers):
                 n_loop += sum(a == b for a, b in zip(preds, serving_answers[i]))
                 n_loop_pred += sum(a == b for a, b in zip(g["answers"], serving_answers[i]))
+                for r, (a, b, c) in enumerate(zip(preds, g["answers"], serving_answers[i])):
+                    if not a == b == c and len(mism) < 8:
+                        mism.append({"batch": i, "row": r, "oracle": a, "predict": b, "loop": c})
         out["parity"] = {
             "batches": len(cpu_out), "qa_pairs": n_pairs,
             "ids_equal": n_ids, "dists_within_bound": dist_ok,
@@ -990,6 +993,7 @@ def cpu_baseline(cfg, weights, batches, seconds: float, gpu_out=None, serving_an
             "serving_loop_equal_predict": n_loop_pred if serving_answers is not None else None,
             "min_margin": min(margins), "min_margin_over_perturbation": min(guards),
             "max_query_delta_rel": max(dq),
+            "mismatches": mism,
             "check": "CPU oracle vs the GPU on the same full-size C2 batches and weights: "
                      "retrieved example ids (return_info question_id) bit-exact per QA pair; "
                      "return_dists within the cdist bound; prompts; predict()'s greedy answers; "
@@ -1148,9 +1152,11 @@ def main():
     decode = decode_chain(model, batches[0])
 
     host_ms, flop_per_pair = pipeline_work(model, retr, batches, cfg)
-    eos = eos_leg(cfg, weights, retr, device, batches, args.steps) if not args.no_eos_leg else None
+    # the train leg before the eos leg: a model built after another model's serving loops gets
+    # its streams' hardware queues by creation order (profiles/r05_train_streams.txt)
     train = (train_leg(cfg, weights, retr, device, batches, steps=20)
              if rank == 0 and world == 1 and not args.no_train_leg else None)
+    eos = eos_leg(cfg, weights, retr, device, batches, args.steps) if not args.no_eos_leg else None
 
     roofline = None
     if not args.no_probe:
