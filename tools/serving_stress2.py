@@ -189,3 +189,29 @@ with torch.no_grad():
             torch.cuda.synchronize()
             res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
         print(f"generate over {k} pieces beside towers: pieces differing {res}", flush=True)
+    # one piece's generate beside other workloads on the tower stream
+    def enc_big():
+        with torch.cuda.stream(s_img):
+            for _ in range(3):
+                t5h.encode(eall, mall)
+
+    big = torch.randn(4096, 4096, device=dev)
+
+    def mm_big():
+        with torch.cuda.stream(s_img):
+            for _ in range(6):
+                torch.mm(big, big)
+
+    sub = ins1[:1]
+    with torch.cuda.stream(g1):
+        ref = [x.clone() for x in _gbp(t5h, sub, 20, slot=1)]
+    torch.cuda.synchronize()
+    for name, fn in (("T5 encoder x3", enc_big), ("torch mm 4096^3 x6", mm_big), ("towers", towers)):
+        res = []
+        for r in range(int(os.environ.get("STRESS_N", "12"))):
+            with torch.cuda.stream(g1):
+                o = _gbp(t5h, sub, 20, slot=1)
+            fn()
+            torch.cuda.synchronize()
+            res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
+        print(f"1-piece generate beside {name}: differing {sum(res)} of {len(res)}", flush=True)
