@@ -215,3 +215,29 @@ with torch.no_grad():
             torch.cuda.synchronize()
             res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
         print(f"1-piece generate beside {name}: differing {sum(res)} of {len(res)}", flush=True)
+    # the 8-piece generate beside one tower at a time
+    tok_all = torch.cat(toks)
+
+    def vit_only():
+        with torch.cuda.stream(s_img):
+            vit.forward(imgs, TOKENS)
+            retr.image_encoder.forward(imgs, CLS)
+
+    def text_only():
+        with torch.cuda.stream(s_img):
+            for _ in range(3):
+                retr.text_encoder.forward(tok_all)
+
+    with torch.cuda.stream(g1):
+        ref = [x.clone() for x in _gbp(t5h, ins1, 20, slot=1)]
+    torch.cuda.synchronize()
+    for name, fn in (("ViTs", vit_only), ("text tower", text_only), ("towers", towers)):
+        res = []
+        for r in range(int(os.environ.get("STRESS_N", "12"))):
+            with torch.cuda.stream(g1):
+                o = _gbp(t5h, ins1, 20, slot=1)
+            fn()
+            torch.cuda.synchronize()
+            res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
+        print(f"8-piece generate beside {name}: differing {sum(res)} pieces over {len(res)} runs",
+              flush=True)
