@@ -241,3 +241,19 @@ with torch.no_grad():
             res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
         print(f"8-piece generate beside {name}: differing {sum(res)} pieces over {len(res)} runs",
               flush=True)
+    # the grouped generate's pieces through the T5 encoder alone, and the teacher-forced logits,
+    # beside the text tower
+    with torch.cuda.stream(g1):
+        eref = t5h.encode(eall, mall).clone()
+        lref2 = t5h.logits(eall, mall, dec_ids).clone()
+    torch.cuda.synchronize()
+    re, rl = [], []
+    for r in range(int(os.environ.get("STRESS_N", "12"))):
+        with torch.cuda.stream(g1):
+            e_ = t5h.encode(eall, mall)
+            l_ = t5h.logits(eall, mall, dec_ids)
+        text_only()
+        torch.cuda.synchronize()
+        re.append(bool((e_ != eref).any()))
+        rl.append(bool((l_ != lref2).any()))
+    print(f"beside the text tower: encoder outputs differing {sum(re)} / {len(re)}, logits {sum(rl)} / {len(rl)}", flush=True)
