@@ -1,2 +1,2 @@
 set -o pipefail
-STRESS_N=30 timeout -k 10 500 python tools/serving_stress2.py 24 2 2>&1 | grep -E "beside the text tower:|8-piece generate beside text|Error"
+STRESS_N=20 timeout -k 10 500 python tools/serving_stress2.py 24 2 2>&1 | grep -E "beside packed|beside text|Error|error"

@@ -257,3 +257,39 @@ with torch.no_grad():
         re.append(bool((e_ != eref).any()))
         rl.append(bool((l_ != lref2).any()))
     print(f"beside the text tower: encoder outputs differing {sum(re)} / {len(re)}, logits {sum(rl)} / {len(rl)}", flush=True)
+    # the 8-piece generate beside the T5 encoder's own split-bf16 launches (3 passes of 128 rows)
+    res = []
+    for r in range(int(os.environ.get("STRESS_N", "12"))):
+        with torch.cuda.stream(g1):
+            o = _gbp(t5h, ins1, 20, slot=1)
+        enc_big()
+        torch.cuda.synchronize()
+        res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
+    print(f"8-piece generate beside the T5 encoder: differing {sum(res)} pieces over {len(res)} runs", flush=True)
+    # the 8-piece generate beside raw packed-W GEMM launches of given shapes (mpr_gemm_f32_packed)
+    def packed_gemm_fn(M, N, K):
+        A = torch.randn(M, K, device=dev)
+        W = torch.randn(N, K, device=dev) * 0.05
+        nbytes = _lib.c_int64()
+        _lib.call("mpr_pack_x3_bytes", N, K, _lib.ctypes.byref(nbytes))
+        img = torch.empty(nbytes.value, dtype=torch.uint8, device=dev)
+        _lib.call("mpr_pack_x3", _lib.ptr(W), N, K, K, _lib.ptr(img), nbytes.value, _lib.stream_ptr())
+        C = torch.empty(M, N, device=dev)
+
+        def fn():
+            with torch.cuda.stream(s_img):
+                for _ in range(12):
+                    _lib.call("mpr_gemm_f32_packed", _lib.ptr(A), K, _lib.ptr(W), K, _lib.ptr(img),
+                              _lib.ptr(C), N, M, N, K, None, 0, 0, _lib.stream_ptr(dev))
+        return fn
+
+    for shape in ((2464, 512, 2048), (2464, 1536, 512), (800, 2304, 768)):
+        fn = packed_gemm_fn(*shape)
+        res = []
+        for r in range(int(os.environ.get("STRESS_N", "12"))):
+            with torch.cuda.stream(g1):
+                o = _gbp(t5h, ins1, 20, slot=1)
+            fn()
+            torch.cuda.synchronize()
+            res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
+        print(f"8-piece generate beside packed GEMM {shape}: differing {sum(res)} pieces over {len(res)} runs", flush=True)
