@@ -267,7 +267,7 @@ with torch.no_grad():
         res.append(sum(bool((a != b).any()) for a, b in zip(ref, o)))
     print(f"8-piece generate beside the T5 encoder: differing {sum(res)} pieces over {len(res)} runs", flush=True)
     # the 8-piece generate beside raw packed-W GEMM launches of given shapes (mpr_gemm_f32_packed)
-    def packed_gemm_fn(M, N, K):
+    def packed_gemm_fn(M, N, K, act=0):
         A = torch.randn(M, K, device=dev)
         W = torch.randn(N, K, device=dev) * 0.05
         nbytes = _lib.c_int64()
@@ -280,10 +280,11 @@ with torch.no_grad():
             with torch.cuda.stream(s_img):
                 for _ in range(12):
                     _lib.call("mpr_gemm_f32_packed", _lib.ptr(A), K, _lib.ptr(W), K, _lib.ptr(img),
-                              _lib.ptr(C), N, M, N, K, None, 0, 0, _lib.stream_ptr(dev))
+                              _lib.ptr(C), N, M, N, K, None, 0, act, _lib.stream_ptr(dev))
         return fn
 
-    for shape in ((2464, 512, 2048), (2464, 1536, 512), (800, 2304, 768)):
+    shapes = ((2464, 512, 2048, 0), (2464, 1536, 512, 0), (800, 2304, 768, 0))
+    for shape in shapes:
         fn = packed_gemm_fn(*shape)
         res = []
         for r in range(int(os.environ.get("STRESS_N", "12"))):
