@@ -441,6 +441,29 @@ int mpr_probe_replay(int32_t iters, void* stream, double* total_ms, int64_t* lau
                      double* flops, double* bytes);
 int mpr_probe_clear(void);
 
+/* ---- debug detectors (no reference counterpart; off unless switched on before the library
+ * loads: MPR_DEBUG_GUARD=1, MPR_DEBUG_LDS_POISON=1, MPR_DECODE_TRACE=1) --------------------------
+ * mpr_debug_flags: bit 0 guard bands, bit 1 LDS poison, bit 2 decode trace.
+ * mpr_debug_check_guards: after a device sync, counts the library buffers whose 64 KiB guard
+ * bands (0xFF on both sides of every allocation) were written and describes up to a few in report.
+ * mpr_debug_hash_buffers: after a device sync, a 64-bit FNV-1a hash of every live library buffer
+ * (with its device address and size, in address order); *n = the number of buffers.
+ * mpr_debug_t5_workspace: the addresses and sizes of one generate workspace slot's buffers (the
+ * order of T5Work's fields; tools/decode_race.py names them).
+ * mpr_debug_t5_trace: the decode trace of the slot's last generate (every decode-chain kernel's
+ * output, MPR_DECODE_TRACE=1): copies its *n_floats floats to dst (device, cap_floats at least)
+ * on stream and its segments {kind, step, layer, rows, cols, float offset} into segs (host,
+ * 6 int64 each). */
+int mpr_debug_flags(int32_t* flags);
+int mpr_debug_check_guards(int32_t* n_bad, char* report, int32_t report_len);
+int mpr_debug_hash_buffers(uint64_t* hashes, uint64_t* ptrs, int64_t* sizes, int32_t cap,
+                           int32_t* n);
+int mpr_debug_t5_workspace(mpr_model* m, int32_t slot, uint64_t* ptrs, int64_t* sizes,
+                           int32_t cap, int32_t* n);
+int mpr_debug_t5_trace(mpr_model* m, int32_t slot, float* dst, int64_t cap_floats,
+                       int64_t* n_floats, int64_t* segs, int32_t seg_cap, int32_t* n_segs,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

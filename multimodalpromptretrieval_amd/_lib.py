@@ -98,6 +98,14 @@ SIGNATURES = [
     ("mpr_probe_replay", c_int32, [c_int32, c_void_p, POINTER(ctypes.c_double), I64P,
                                    POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
     ("mpr_probe_clear", c_int32, []),
+    ("mpr_debug_flags", c_int32, [I32P]),
+    ("mpr_debug_check_guards", c_int32, [I32P, ctypes.c_char_p, c_int32]),
+    ("mpr_debug_hash_buffers", c_int32, [POINTER(ctypes.c_uint64), POINTER(ctypes.c_uint64),
+                                         I64P, c_int32, I32P]),
+    ("mpr_debug_t5_workspace", c_int32, [c_void_p, c_int32, POINTER(ctypes.c_uint64), I64P,
+                                         c_int32, I32P]),
+    ("mpr_debug_t5_trace", c_int32, [c_void_p, c_int32, c_void_p, c_int64, I64P, I64P, c_int32,
+                                     I32P, c_void_p]),
     ("mpr_gemm_f32", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32,
                                c_int32, c_int32, c_void_p, c_int64, c_int32, c_void_p]),
     ("mpr_gemm_f32_many", c_int32, [c_int32, c_void_p, c_void_p]),

@@ -1001,6 +1001,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   };
   float(*ssq_s)[MROWS] = reinterpret_cast<float(*)[MROWS]>(smem + XS);
   const int tid = threadIdx.x, lane = tid & 63;
+  if (sa.poison) {  // debug: a read of LDS this block never wrote yields NaN
+    for (int i = tid; i < (int)(sizeof(smem) / sizeof(float)); i += 512) smem[i] = __builtin_nanf("");
+    __syncthreads();
+  }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   // blockIdx.y = a block of MROWS rows (a grouped decode's rows split over blocks); rows are
   // independent, so each row's sums keep their order whatever the split
@@ -1591,6 +1595,11 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(!(F & SKF_SSQ) || F == SKF_SSQ, "gemm_skinny: ssq only on a plain projection");
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
+  if (debug_lds_poison() && !sa.poison) {
+    SkinnyArgs p = sa;
+    p.poison = 1;
+    return gemm_skinny(p, s);
+  }
   // Above 32 rows (grouped decodes on the skinny path: MPR_DECODE_GEMM=skinny) the rows split
   // over blocks of 32 (serving loop, 20 steps: 3783-3831 with one block column of up to 8 row
   // groups -> 3893-3908 QA pairs/s; 16-row blocks within 1 %).

@@ -93,6 +93,7 @@ struct AttnArgs {
   int q_rms_nparts = 0;
   int q_rms_n = 0;
   float q_rms_eps = 1e-6f;
+  int poison = 0;  // MPR_DEBUG_LDS_POISON: LDS filled with NaN at kernel entry (set by attention())
 };
 
 struct SkinnyArgs {
@@ -116,6 +117,7 @@ struct SkinnyArgs {
   const float* rs_part = nullptr;
   int rs_nparts = 0;
   int rs_n = 0;
+  int poison = 0;  // MPR_DEBUG_LDS_POISON: LDS filled with NaN at kernel entry (set by gemm_skinny)
 };
 int gemm_skinny(const SkinnyArgs& a, hipStream_t s);
 

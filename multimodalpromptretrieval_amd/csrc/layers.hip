@@ -257,10 +257,21 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 // issued up front, so a pass costs one memory round trip; max / sum / P go through LDS.
 constexpr int DEC_KC = 256;
 
+// debug (MPR_DEBUG_LDS_POISON): NaN into n floats of LDS, then a block barrier
+__device__ __forceinline__ void poison_lds(float* p, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = __builtin_nanf("");
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
   __shared__ float red[2][4];
   __shared__ float Ps[DEC_KC];
   __shared__ __attribute__((aligned(16))) float Os[16][ATT_D];
+  if (a.poison) {
+    poison_lds(&red[0][0], 8);
+    poison_lds(Ps, DEC_KC);
+    poison_lds(&Os[0][0], 16 * ATT_D);
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
@@ -347,6 +358,10 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
 __global__ __launch_bounds__(256) void attention_decode_wave_kernel(AttnArgs a) {
   __shared__ float Ps[4][128];
   __shared__ __attribute__((aligned(16))) float Os[4][8][ATT_D];
+  if (a.poison) {
+    poison_lds(&Ps[0][0], 4 * 128);
+    poison_lds(&Os[0][0][0], 4 * 8 * ATT_D);
+  }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pr = blockIdx.x * 4 + wave;
   if (pr >= a.B * a.H) return;  // wave-uniform; no block barrier below
@@ -363,6 +378,12 @@ __global__ __launch_bounds__(512) void attention_decode_wave2_kernel(AttnArgs a)
   __shared__ float Ps[4][128];
   __shared__ __attribute__((aligned(16))) float Os[4][8][D];
   __shared__ float mx[4][2], sm[4][2];
+  if (a.poison) {
+    poison_lds(&Ps[0][0], 4 * 128);
+    poison_lds(&Os[0][0][0], 4 * 8 * D);
+    poison_lds(&mx[0][0], 8);
+    poison_lds(&sm[0][0], 8);
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ps = wave >> 1, hf = wave & 1;  // pair slot, key half
@@ -703,7 +724,7 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(const float* part_val,
                                                           int32_t* unfinished, int32_t* tokens,
                                                           int64_t tok_ld, int col, int eos,
                                                           int pad, const float* table, int D,
-                                                          float* x, int64_t x_ld) {
+                                                          float* x, int64_t x_ld, int poison) {
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int unf = unfinished[row];  // issued with the partial loads, not after the argmax
@@ -742,6 +763,10 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(const float* part_val,
   }
   __shared__ float wb[4];
   __shared__ int wi[4];
+  if (poison) {
+    poison_lds(wb, 4);
+    poison_lds(reinterpret_cast<float*>(wi), 4);
+  }
   if (lane == 0) {
     wb[wave] = best;
     wi[wave] = bi;
@@ -902,6 +927,11 @@ int attention(const AttnArgs& a, hipStream_t s) {
   MPR_REQUIRE(!a.q_rms_part || (a.Lq == 1 && a.q_rms_n > 0 && a.q_rms_nparts > 0 &&
                                 a.q_rms_nparts <= 64),
               "attention: a query row scale only on the one-query decode path");
+  if (a.Lq == 1 && debug_lds_poison() && !a.poison) {
+    AttnArgs p = a;
+    p.poison = 1;
+    return attention(p, s);
+  }
   if (a.Lq == 1) {
     // Few pairs (one batch's decode): the block kernel (a wave-per-(b, h) form measured slower at
     // 16 rows: 4.4 / 5.3 us self / cross against 3.8 / 4.1, a quarter of the loads in flight per
@@ -1093,7 +1123,7 @@ int greedy_step(const float* part_val, const int32_t* part_idx, int nparts, int 
   MPR_REQUIRE(M <= 256, "greedy_step: %d rows > 256", M);
   hipLaunchKernelGGL(greedy_step_kernel, dim3(M), dim3(256), 0, s, part_val, part_idx, nparts,
                      unfinished, tokens, tok_ld, col, eos, pad, table, D, x,
-                     x_ld < 0 ? (int64_t)D : x_ld);
+                     x_ld < 0 ? (int64_t)D : x_ld, debug_lds_poison() ? 1 : 0);
   MPR_LAUNCHED();
   return MPR_OK;
 }

@@ -1,6 +1,7 @@
 // models.h — device-resident model handles behind the opaque mpr_model of the C ABI.
 #pragma once
 
+#include <array>
 #include <map>
 #include <memory>
 #include <tuple>
@@ -140,6 +141,11 @@ struct T5Work {
   DevBuf mask_enc, enc_tmp;  // a group's encoder mask / output when several groups share a decode
   DevBuf ax, yq, hz;  // folded decode chain rows: [a | x], [c | h | u], [h2 | z]
   DevBuf x1ss, x2ss;  // their residual rows' per-16-column sums of squares
+  // MPR_DECODE_TRACE=1: every decode-chain kernel's output of the last generate, back to back;
+  // segs[i] = {kind, step, layer, rows, cols, float offset} (T5Model::trace, TraceKind)
+  DevBuf trace;
+  std::vector<std::array<int64_t, 6>> segs;
+  int64_t trace_off = 0;
   uint64_t gen = 0;  // bumped by every buffer growth: invalidates captured graphs
   hipStream_t cap_stream = nullptr;
   struct GraphEnt {
@@ -258,6 +264,15 @@ struct T5Model : mpr_model {
   // Stream for the greedy decode loop of generate() in a slot (null: the caller's stream).
   int set_decode_stream(int slot, hipStream_t ds);
   int use_slot(int slot);
+  // MPR_DECODE_TRACE: copy rows x cols floats (row stride ld) of a kernel's output into the slot's
+  // trace as one segment (debug.hip); a no-op otherwise
+  enum TraceKind : int {
+    TR_ENC_OUT = 0, TR_CROSS_KV, TR_QKV, TR_SELF_ATT, TR_O, TR_CQ, TR_CROSS_ATT, TR_CO, TR_WI,
+    TR_WO, TR_HEAD_VAL, TR_HEAD_IDX, TR_TOKEN, TR_X_NEXT, TR_OCQ, TR_X1SS, TR_COWI, TR_X2SS,
+    TR_FO, TR_HEAD_RMS, TR_LOGITS
+  };
+  int trace(int kind, int t, int l, const void* p, int64_t rows, int64_t cols, int64_t ld,
+            hipStream_t s);
 
  private:
   using GraphKey = T5Work::GraphKey;

@@ -441,6 +441,13 @@ int T5Model::encode_body(int B, int L, int max_new, int start, hipStream_t s) {
 int T5Model::init_body(int B, int L, int max_new, int start, hipStream_t s) {
   const int T1 = max_new + 1;
   MPR_TRY(cross_kv_project(B, L, s));
+  if (debug_decode_trace()) {  // a new trace: the decode's inputs first
+    ws->trace_off = 0;
+    ws->segs.clear();
+    MPR_TRY(trace(TR_ENC_OUT, -1, -1, ws->enc_out.ptr, (int64_t)B * L, d, d, s));
+    MPR_TRY(trace(TR_CROSS_KV, -1, -1, ws->cross_kv.ptr, (int64_t)B * L, (int64_t)Ld * 2 * inner,
+                  (int64_t)Ld * 2 * inner, s));
+  }
   MPR_TRY(fill_i32(ws->unfinished.as<int32_t>(), 1, B, s));
   MPR_TRY(fill_i32(ws->cur_tok.as<int32_t>(), start, B, s));
   MPR_TRY(fill_i32(ws->tok_buf.as<int32_t>(), start, (int64_t)B * T1, s));  // column 0 = start
@@ -480,6 +487,7 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
       MPR_TRY(dec_gemm(sq, ly.pk_qkv, s));
+      MPR_TRY(trace(TR_QKV, t, l, sq.g.C, B, 3 * inner, sq.g.ldc, s));
       AttnArgs at;
       at.q = cl + (int64_t)t * 3 * inner; at.q_bs = (int64_t)Tc * 3 * inner; at.q_rs = 3 * inner;
       at.k = cl + inner; at.k_bs = at.q_bs; at.k_rs = 3 * inner;
@@ -489,15 +497,18 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       at.rel_tab = dec_tab.as<float>();
       at.lut_radius = lut_radius;
       MPR_TRY(attention(at, s));
+      MPR_TRY(trace(TR_SELF_ATT, t, l, ap, B, inner, inner, s));
       SkinnyArgs so;
       so.g.A = ap; so.g.lda = inner; so.g.R = xp;
       so.g.ldr = d; so.g.C = xp; so.g.ldc = d; so.g.M = B; so.g.N = d; so.g.K = inner;
       MPR_TRY(dec_gemm(so, ly.pk_o, s));
+      MPR_TRY(trace(TR_O, t, l, xp, B, d, d, s));
       SkinnyArgs cq;
       cq.g.A = xp; cq.g.lda = d; cq.g.C = qp;
       cq.g.ldc = inner; cq.g.M = B; cq.g.N = inner; cq.g.K = d; cq.rms_w = ly.ln1.as<float>();
       cq.rms_eps = T5_EPS;
       MPR_TRY(dec_gemm(cq, ly.pk_cq, s));
+      MPR_TRY(trace(TR_CQ, t, l, qp, B, inner, inner, s));
       AttnArgs ca;
       ca.q = qp; ca.q_bs = inner; ca.q_rs = inner;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -506,19 +517,23 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       ca.B = B; ca.H = H; ca.Lq = 1; ca.Lk = L; ca.scale = 1.f;
       ca.key_mask = maskp; ca.mask_bs = L;
       MPR_TRY(attention(ca, s));
+      MPR_TRY(trace(TR_CROSS_ATT, t, l, ap, B, inner, inner, s));
       SkinnyArgs co;
       co.g.A = ap; co.g.lda = inner; co.g.R = xp;
       co.g.ldr = d; co.g.C = xp; co.g.ldc = d; co.g.M = B; co.g.N = d; co.g.K = inner;
       MPR_TRY(dec_gemm(co, ly.pk_co, s));
+      MPR_TRY(trace(TR_CO, t, l, xp, B, d, d, s));
       SkinnyArgs fi;
       fi.g.A = xp; fi.g.lda = d; fi.g.C = fp;
       fi.g.ldc = dff; fi.g.M = B; fi.g.N = dff; fi.g.K = d; fi.g.act = ACT_RELU;
       fi.rms_w = ly.ln2.as<float>(); fi.rms_eps = T5_EPS;
       MPR_TRY(dec_gemm(fi, ly.pk_wi, s));
+      MPR_TRY(trace(TR_WI, t, l, fp, B, dff, dff, s));
       SkinnyArgs fo;
       fo.g.A = fp; fo.g.lda = dff; fo.g.R = xp;
       fo.g.ldr = d; fo.g.C = xp; fo.g.ldc = d; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
       MPR_TRY(dec_gemm(fo, ly.pk_wo, s));
+      MPR_TRY(trace(TR_WO, t, l, xp, B, d, d, s));
     }
     if (tiled_head(B)) {
       // logits = rms(x) . lm_head^T on the tiled GEMM, then the row argmax in 16 parts per row
@@ -527,15 +542,21 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
       float* hb = ws->h.as<float>();
       float* lg = ws->logits.as<float>();
       MPR_TRY(rmsnorm(xp, d, B, d, dec_final.as<float>(), T5_EPS, hb, d, s));
+      MPR_TRY(trace(TR_HEAD_RMS, t, -1, hb, B, d, d, s));
       GemmArgs g;
       g.A = hb; g.lda = d; g.W = lm_head.as<float>(); g.ldw = d;
       g.C = lg; g.ldc = V; g.M = B; g.N = V; g.K = d;
       MPR_TRY(gemm(g, s));
+      MPR_TRY(trace(TR_LOGITS, t, -1, lg, B, V, V, s));
       MPR_TRY(argmax_parts(lg, V, B, V, HP, ws->part_val.as<float>(), ws->part_idx.as<int32_t>(),
                            s));
+      MPR_TRY(trace(TR_HEAD_VAL, t, -1, ws->part_val.ptr, B, HP, HP, s));
+      MPR_TRY(trace(TR_HEAD_IDX, t, -1, ws->part_idx.ptr, B, HP, HP, s));
       MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), HP, B, unf, toks,
                           T1, t + 1, eos, pad, shared.as<float>(), d,
                           t + 1 < max_new ? xp : nullptr, s));
+      MPR_TRY(trace(TR_TOKEN, t, -1, toks + t + 1, B, 1, T1, s));
+      if (t + 1 < max_new) MPR_TRY(trace(TR_X_NEXT, t, -1, xp, B, d, d, s));
       continue;
     }
     // The argmax head, one launch for all rows (gemm_skinny splits more than 32 rows over blocks
@@ -547,9 +568,13 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
     hd.amax_idx = ws->part_idx.as<int32_t>();
     int np = 0;
     MPR_TRY(dec_gemm(hd, pk_lm_head, s, &np));
+    MPR_TRY(trace(TR_HEAD_VAL, t, -1, ws->part_val.ptr, B, np, np, s));
+    MPR_TRY(trace(TR_HEAD_IDX, t, -1, ws->part_idx.ptr, B, np, np, s));
     MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks, T1,
                         t + 1, eos, pad, shared.as<float>(), d, t + 1 < max_new ? xp : nullptr,
                         s));
+    MPR_TRY(trace(TR_TOKEN, t, -1, toks + t + 1, B, 1, T1, s));
+    if (t + 1 < max_new) MPR_TRY(trace(TR_X_NEXT, t, -1, xp, B, d, d, s));
   }
   return MPR_OK;
 }
@@ -592,12 +617,16 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
       MPR_TRY(dec_gemm(sq, ly.pk_qkv, s));
+      MPR_TRY(trace(TR_QKV, t, l, sq.g.C, B, 3 * inner, sq.g.ldc, s));
       MPR_TRY(attention(at, s));
+      MPR_TRY(trace(TR_SELF_ATT, t, l, ax, B, inner, ldA, s));
       SkinnyArgs so;  // [x1 | u] = [a | x] W_ocq^T
       so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
       so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
       so.ssq_out = x1ss; so.ssq_cols = d;  // x1's per-tile sums of squares (its RMS)
       MPR_TRY(dec_gemm(so, ly.pk_ocq, s));
+      MPR_TRY(trace(TR_OCQ, t, l, yq + inner, B, d + inner, ldY, s));
+      MPR_TRY(trace(TR_X1SS, t, l, x1ss, B, d / 16, d / 16, s));
       AttnArgs ca;  // c = attention(u / rms_scale(x1), K_enc, V_enc)
       ca.q = yq + inner + d; ca.q_bs = ldY; ca.q_rs = ldY;
       ca.k = ckv + (int64_t)l * 2 * inner; ca.k_bs = (int64_t)L * ckv_ld; ca.k_rs = ckv_ld;
@@ -607,17 +636,21 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       ca.key_mask = maskp; ca.mask_bs = L;
       ca.q_rms_part = x1ss; ca.q_rms_nparts = d / 16; ca.q_rms_n = d; ca.q_rms_eps = T5_EPS;
       MPR_TRY(attention(ca, s));
+      MPR_TRY(trace(TR_CROSS_ATT, t, l, yq, B, inner, ldY, s));
       SkinnyArgs cw;  // [x2 | z] = [c | x1] W_cowi^T
       cw.g.A = yq; cw.g.lda = ldY; cw.g.C = hz; cw.g.ldc = ldZ;
       cw.g.M = B; cw.g.N = d + dff; cw.g.K = inner + d;
       cw.ssq_out = x2ss; cw.ssq_cols = d;
       MPR_TRY(dec_gemm(cw, ly.pk_cowi, s));
+      MPR_TRY(trace(TR_COWI, t, l, hz, B, d + dff, ldZ, s));
+      MPR_TRY(trace(TR_X2SS, t, l, x2ss, B, d / 16, d / 16, s));
       SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
       fo.g.A = hz + d; fo.g.lda = ldZ; fo.g.R = hz; fo.g.ldr = ldZ;
       fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
       fo.relu_in = true; fo.rs_part = x2ss; fo.rs_nparts = d / 16; fo.rs_n = d;
       fo.rms_eps = T5_EPS;
       MPR_TRY(dec_gemm(fo, ly.pk_wo, s));
+      MPR_TRY(trace(TR_FO, t, l, xp, B, d, ldA, s));
     }
     SkinnyArgs hd;
     hd.g.A = xp; hd.g.lda = ldA; hd.g.C = nullptr; hd.g.M = B; hd.g.N = V; hd.g.K = d;
@@ -626,9 +659,13 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
     hd.amax_idx = ws->part_idx.as<int32_t>();
     int np = 0;
     MPR_TRY(dec_gemm(hd, pk_lm_head, s, &np));
+    MPR_TRY(trace(TR_HEAD_VAL, t, -1, ws->part_val.ptr, B, np, np, s));
+    MPR_TRY(trace(TR_HEAD_IDX, t, -1, ws->part_idx.ptr, B, np, np, s));
     MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks,
                         T1, t + 1, eos, pad, shared.as<float>(), d,
                         t + 1 < max_new ? xp : nullptr, s, ldA));
+    MPR_TRY(trace(TR_TOKEN, t, -1, toks + t + 1, B, 1, T1, s));
+    if (t + 1 < max_new) MPR_TRY(trace(TR_X_NEXT, t, -1, xp, B, d, ldA, s));
   }
   return MPR_OK;
 }
@@ -740,6 +777,11 @@ int T5Model::gen_begin(int ng, const float* const* embeds, const float* const* m
   MPR_TRY(grow(ws->cur_tok, (size_t)16 * MAX_GROUPS * 4));
   MPR_TRY(grow(ws->tok_buf, (size_t)B * T1 * 4));
   if (tiled_head(B)) MPR_TRY(grow(ws->logits, (size_t)B * V * 4));
+  if (debug_decode_trace()) {  // every traced output of the call (T5Model::trace)
+    const int64_t per_step = (int64_t)B * ((int64_t)Ld * (6 * inner + 6 * d + 2 * dff + d / 8) +
+                                           2 * nparts + (tiled_head(B) ? V : 0) + 2 * d + 40);
+    MPR_TRY(grow(ws->trace, (size_t)(M * d + M * Ld * 2 * inner + Tc * per_step) * 4));
+  }
   if (n > 1) {
     MPR_TRY(grow(ws->mask_enc, (size_t)Mg * 4));
     MPR_TRY(grow(ws->enc_tmp, (size_t)Mg * d * 4));
