@@ -1152,8 +1152,6 @@ def main():
     decode = decode_chain(model, batches[0])
 
     host_ms, flop_per_pair = pipeline_work(model, retr, batches, cfg)
-    # the train leg before the eos leg: a model built after another model's serving loops gets
-    # its streams' hardware queues by creation order (profiles/r05_train_streams.txt)
     train = (train_leg(cfg, weights, retr, device, batches, steps=20)
              if rank == 0 and world == 1 and not args.no_train_leg else None)
     eos = eos_leg(cfg, weights, retr, device, batches, args.steps) if not args.no_eos_leg else None
@@ -1282,6 +1280,12 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    par = (cpu or {}).get("parity") or {}
+    if par and (par["serving_loop_answers_equal"] != par["qa_pairs"] or
+                par["answers_equal"] != par["qa_pairs"] or par["ids_equal"] != par["qa_pairs"]):
+        # the timed loop's answers must be the reference path's (the CPU oracle's) on every
+        # checked pair: a throughput from a loop that answers differently is not a result
+        raise SystemExit(f"parity failure: {json.dumps(par['mismatches'])}")
 
 
 if __name__ == "__main__":

@@ -333,14 +333,14 @@ def ensure_device(device) -> None:
     if idx not in _inited:
         call("mpr_init", c_int32(idx))
         _inited.add(idx)
-        # MPR_EAGER_STREAMS=1: the pipeline's streams created once in a fixed order right after
-        # init.  A stream's hardware queue (4 per process) is fixed at its creation; created on
-        # first use, their queue sharing depends on what ran before (a training step after
-        # another model's serving loop: 24 ms against 13.5, profiles/r05_train_streams.txt).
-        # Opt-in: with it, 2 of 3 bench runs gave one serving-loop answer (of 64) different from
-        # predict()'s and the oracle's — an ordering hazard this queue mapping exposes, not yet
-        # found; with the default mapping every run so far matched 64/64.
-        if os.environ.get("MPR_EAGER_STREAMS", "0") == "1":
+        # The pipeline's role streams are created once, in a fixed order, right after init
+        # (MPR_EAGER_STREAMS=0: on first use instead).  A stream's hardware queue (4 per process)
+        # is fixed at its creation; created on first use, their queue sharing depended on what
+        # ran before (a training step after another model's serving loop: 24 ms against 13.5,
+        # profiles/r05_train_streams.txt).  (Round 5 kept this opt-in because with it the serving
+        # loop's answers changed more often; the cause was packed-FP32 results corrupted beside
+        # other kernels' MFMA waves, fixed by building without packed FP32 ops)
+        if os.environ.get("MPR_EAGER_STREAMS", "1") == "1":
             for role in PIPELINE_ROLES:
                 role_stream(torch.device("cuda", idx), role)
 

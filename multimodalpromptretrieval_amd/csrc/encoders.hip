@@ -27,6 +27,16 @@ bool pool_last() {
   }();
   return on;
 }
+// Debug bisection (tools/decode_race.py): MPR_DEBUG_TOWER_SKIP = a bit mask of launch kinds a
+// tower pass leaves out (its outputs are then wrong): 1 LayerNorms, 2 q|k|v GEMMs, 4 attentions,
+// 8 out-projection GEMMs, 16 c_fc GEMMs, 32 c_proj GEMMs, 64 embedding / EOT gathers.
+int tower_skip() {
+  static const int m = [] {
+    const char* e = getenv("MPR_DEBUG_TOWER_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
 }
 
 int ClipTower::load_blocks(const float* const* t, int w, int nl) {
@@ -152,10 +162,11 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
       at.scale = 0.125f;  // 64 ** -0.5, exact power of two
       at.causal = r[i].causal ? 1 : 0;
     }
-    MPR_TRY(layernorm_group(n1, CLIP_LN_EPS, s));
-    MPR_TRY(gemm_group(gq, s));
-    MPR_TRY(attention_group(ag, s));
-    for (int i = 0; l == nl - 1 && i < n; ++i)
+    const int skip = tower_skip();
+    if (!(skip & 1)) MPR_TRY(layernorm_group(n1, CLIP_LN_EPS, s));
+    if (!(skip & 2)) MPR_TRY(gemm_group(gq, s));
+    if (!(skip & 4)) MPR_TRY(attention_group(ag, s));
+    for (int i = 0; l == nl - 1 && i < n && !(skip & 64); ++i)
       if (r[i].pool == POOL_EOT) {  // the EOT rows of the residual stream and of attention
         const int W = r[i].t->width;
         MPR_TRY(eot_gather(r[i].x, r[i].tok, r[i].B, r[i].L, r[i].ctx, W,
@@ -163,10 +174,10 @@ int ClipTower::run_group(const TowerRun* r, int n, hipStream_t s) {
         MPR_TRY(eot_gather(r[i].w->ao.as<float>(), r[i].tok, r[i].B, r[i].L, r[i].ctx, W,
                            r[i].w->h.as<float>(), s));
       }
-    MPR_TRY(gemm_group(go, s));
-    MPR_TRY(layernorm_group(n2, CLIP_LN_EPS, s));
-    MPR_TRY(gemm_group(gf, s));
-    MPR_TRY(gemm_group(gp, s));
+    if (!(skip & 8)) MPR_TRY(gemm_group(go, s));
+    if (!(skip & 1)) MPR_TRY(layernorm_group(n2, CLIP_LN_EPS, s));
+    if (!(skip & 16)) MPR_TRY(gemm_group(gf, s));
+    if (!(skip & 32)) MPR_TRY(gemm_group(gp, s));
   }
   return MPR_OK;
 }
@@ -279,8 +290,9 @@ int encode_towers_eager(VitModel* const* v, const int* modes, float* const* outs
     TowerWs& w = tm->ws[tslot[j]];
     MPR_TRY(w.x.ensure((size_t)Bt * Lt * W * 4));
     MPR_TRY(w.pooled.ensure((size_t)Bt * W * 4));
-    MPR_TRY(embed_gather(tm->tok_emb.as<float>(), tok[j], tm->ctx, Bt, Lt, W,
-                         tm->pos.as<float>(), w.x.as<float>(), (int64_t)Lt * W, 0, s));
+    if (!(tower_skip() & 64))
+      MPR_TRY(embed_gather(tm->tok_emb.as<float>(), tok[j], tm->ctx, Bt, Lt, W,
+                           tm->pos.as<float>(), w.x.as<float>(), (int64_t)Lt * W, 0, s));
     runs[nr++] = TowerRun{&tm->tower, &w, w.x.as<float>(), Bt, Lt, true, 1,
                           pool_last() ? POOL_EOT : POOL_NONE, tok[j], tm->ctx};
   }

@@ -100,6 +100,26 @@ def explain_cross_att(ref, cur, segs, seg, ins, d_inner, dev):
     print(f"  row {b} head {h}: differing dims {dims}; ref vs fp64 max err "
           f"{float((out_r[b, h * D:(h + 1) * D].double() - o64).abs().max()):.2e}, delta max "
           f"{float(dlt.abs().max()):.3e}", flush=True)
+    # hypothesis: one v_pk_fma_f32 of the P.V sum used the wrong broadcast element of its P pair
+    # for the low half (even components): key k's term took P[k ^ 1] instead of P[k], in every
+    # lane that ran the instruction (16 lanes of one key group, all 16 dg -> dims 4 dg + e)
+    es = sorted(set(dd % 4 for dd in dims))
+    if len(es) == 1 and len(dims) == 16:
+        e = es[0]
+        dd = torch.tensor([4 * g + e for g in range(16)], device=dev)
+        best = []
+        for k in range(L):
+            for kk in (k ^ 1,):
+                if kk >= L:
+                    continue
+                pred = (p[kk] - p[k]) * V[k, dd]
+                res = float((pred - dlt[dd]).abs().max())
+                best.append((res, k, kk))
+        best.sort()
+        print(f"  component {e}: best single-term fits (residual, key, key used instead): "
+              f"{[(f'{r:.2e}', k, kk) for r, k, kk in best[:3]]}; |delta| {float(dlt[dd].abs().max()):.2e}",
+              flush=True)
+        return
     ch = sorted(set(dd // 16 for dd in dims))
     for c in ch:
         sl = slice(16 * c, 16 * c + 16)
