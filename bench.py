@@ -1022,6 +1022,8 @@ def main():
                          "§8(e): C2/C3 replicas, C4's 268 MB sharded; C5's scan always sharded)")
     ap.add_argument("--no-train-leg", action="store_true",
                     help="skip the training-step line (main.py:177-188)")
+    ap.add_argument("--train-leg-last", action="store_true",
+                    help="time the training step after the eos-stop leg (stream-placement A/B)")
     ap.add_argument("--no-eos-leg", action="store_true",
                     help="skip the eos-stop serving line (an eos-early T5)")
     ap.add_argument("--no-index-build", action="store_true",
@@ -1152,9 +1154,14 @@ def main():
     decode = decode_chain(model, batches[0])
 
     host_ms, flop_per_pair = pipeline_work(model, retr, batches, cfg)
-    train = (train_leg(cfg, weights, retr, device, batches, steps=20)
-             if rank == 0 and world == 1 and not args.no_train_leg else None)
+    def train_now():
+        return (train_leg(cfg, weights, retr, device, batches, steps=20)
+                if rank == 0 and world == 1 and not args.no_train_leg else None)
+
+    train = None if args.train_leg_last else train_now()
     eos = eos_leg(cfg, weights, retr, device, batches, args.steps) if not args.no_eos_leg else None
+    if args.train_leg_last:  # (A/B of the stream placement: the same step after the eos leg's loops)
+        train = train_now()
 
     roofline = None
     if not args.no_probe:

@@ -101,6 +101,10 @@ int mpr_topk_merge_packed(const double* packed_dev, int32_t W, int32_t Bp, int32
  * out_dist / out_ids [b, k].  Replaces dataset/VQAFeatureDataset.py:192-197 over a sharded index;
  * the same results as mpr_index_search over the whole index up to fp32 rounding ties (exact ties
  * to the lowest global id).  k <= 64, n_blocks * k <= 512. */
+/* 1 in *ok when the process has RCCL loaded with ncclAllGather and ncclCommGetAsyncError (the
+ * symbols mpr_sharded_search_all calls; the Python host falls back to torch.distributed's
+ * all_gather otherwise). */
+int mpr_rccl_available(int32_t* ok);
 int mpr_sharded_search_all(mpr_index* index, void* comm, int32_t world, int32_t rank,
                            const float* q_dev, int32_t b, int32_t k, double* recv_dev,
                            int32_t n_blocks, float* out_dist_dev, int64_t* out_ids_dev,

@@ -98,6 +98,7 @@ SIGNATURES = [
     ("mpr_probe_replay", c_int32, [c_int32, c_void_p, POINTER(ctypes.c_double), I64P,
                                    POINTER(ctypes.c_double), POINTER(ctypes.c_double)]),
     ("mpr_probe_clear", c_int32, []),
+    ("mpr_rccl_available", c_int32, [I32P]),
     ("mpr_debug_flags", c_int32, [I32P]),
     ("mpr_debug_check_guards", c_int32, [I32P, ctypes.c_char_p, c_int32]),
     ("mpr_debug_hash_buffers", c_int32, [POINTER(ctypes.c_uint64), POINTER(ctypes.c_uint64),

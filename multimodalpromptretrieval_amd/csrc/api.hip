@@ -223,17 +223,37 @@ int mpr_topk_pack(const float* dist, const int64_t* ids, int64_t n, double* pack
 // ncclAllGather is taken from the RCCL library already loaded in the process (PyTorch's, whose
 // communicator the caller passes: ProcessGroupNCCL._comm_ptr()), found by its soname without
 // loading another copy; libmpr.so itself does not link RCCL.
+// The collective is issued outside ProcessGroupNCCL, so the process group's watchdog and error
+// handling do not cover it: a failed or hung all_gather surfaces here (an error code) or at the
+// next synchronisation, not as a PG timeout.
 namespace {
 using AllGatherFn = int (*)(const void*, void*, size_t, int, void*, hipStream_t);
+using AsyncErrFn = int (*)(void*, int*);
+void* rccl_handle() {
+  static void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  return h;
+}
 AllGatherFn rccl_allgather() {
-  static AllGatherFn fn = [] {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    return h ? reinterpret_cast<AllGatherFn>(dlsym(h, "ncclAllGather")) : nullptr;
-  }();
+  static AllGatherFn fn = rccl_handle() ? reinterpret_cast<AllGatherFn>(
+                                              dlsym(rccl_handle(), "ncclAllGather"))
+                                        : nullptr;
   return fn;
 }
-constexpr int NCCL_FLOAT64 = 8;  // ncclFloat64 (rccl.h)
+AsyncErrFn rccl_async_error() {
+  static AsyncErrFn fn = rccl_handle() ? reinterpret_cast<AsyncErrFn>(
+                                             dlsym(rccl_handle(), "ncclCommGetAsyncError"))
+                                       : nullptr;
+  return fn;
+}
+constexpr int NCCL_FLOAT64 = 8;      // ncclFloat64 (rccl.h)
+constexpr int NCCL_IN_PROGRESS = 7;  // ncclInProgress: a nonblocking communicator's enqueue
 }  // namespace
+
+int mpr_rccl_available(int32_t* ok) {
+  MPR_REQUIRE(ok != nullptr, "rccl_available: null");
+  *ok = rccl_allgather() != nullptr && rccl_async_error() != nullptr;
+  return MPR_OK;
+}
 
 int mpr_sharded_search_all(mpr_index* ix, void* comm, int32_t world, int32_t rank,
                            const float* q, int32_t b, int32_t k, double* recv, int32_t n_blocks,
@@ -263,7 +283,17 @@ int mpr_sharded_search_all(mpr_index* ix, void* comm, int32_t world, int32_t ran
     // so a one-GPU test exercises the RCCL path)
     const bool force = getenv("MPR_SHARDED_FORCE_COLLECTIVE") != nullptr;
     if (world > 1 || force) {
-      const int rc = ag(mine, recv, count, NCCL_FLOAT64, comm, S(stream));  // in place
+      int rc = ag(mine, recv, count, NCCL_FLOAT64, comm, S(stream));  // in place
+      if (rc == NCCL_IN_PROGRESS) {  // a nonblocking communicator: wait for the enqueue
+        AsyncErrFn ae = rccl_async_error();
+        MPR_REQUIRE(ae != nullptr, "sharded_search: nonblocking communicator without "
+                                   "ncclCommGetAsyncError");
+        for (long spin = 0; rc == NCCL_IN_PROGRESS && spin < 100000000L; ++spin) {
+          int st = 0;
+          const int e = ae(comm, &st);
+          rc = e != 0 ? e : st;
+        }
+      }
       MPR_REQUIRE(rc == 0, "sharded_search: ncclAllGather returned %d", rc);
     }
     return merge_packed(recv, n_blocks, b, b, k, k, ix->metric, out_dist, out_ids, S(stream));

@@ -1446,9 +1446,11 @@ int scan_topk(const float* X, const float* xnorm, int64_t n, int d, int64_t row_
     // the coarse path's gated merge also writes the flagged queries' packed pairs when asked (the
     // wave merge: <= 512 candidates, k <= 8; the re-rank wrote every query's); with K <= 8 it is
     // folded into the fallback scan's last block per query tile (coarse_packs: RB * K <= 512)
-    double* po = (gate && pack_out && coarse_packs(n, b, k)) ? pack_out : nullptr;
+    // (MPR_MERGE_BLOCK: the block merge, which writes no packed pairs: topk_pack runs instead)
+    const bool block_merge = getenv("MPR_MERGE_BLOCK") != nullptr;
+    double* po = (gate && pack_out && coarse_packs(n, b, k) && !block_merge) ? pack_out : nullptr;
     if (po && packed) *packed = true;
-    const bool fold = gate && K <= 8 && !getenv("MPR_MERGE_BLOCK");
+    const bool fold = gate && K <= 8 && !block_merge;
     int* cnt = fold ? coarse_ws(ws_coarse, n, d, b).cnt : nullptr;
     int rc = MPR_EUNSUP;
     switch (K) {

@@ -317,16 +317,15 @@ int merge_packed(const double* packed, int W, int Bp, int b, int kc, int k, int 
               "merge_packed: W=%d Bp=%d b=%d kc=%d k=%d (k <= 64, W kc <= %d)", W, Bp, b, kc, k,
               MW_MAX);
   if (b == 0) return MPR_OK;
+  // a lane's sorted list never needs more than the candidates it sees: W kc <= 512 over 64 lanes
+  // is <= 8 each, so lists of min(next_pow2(k), 8) give the same result at any k
   int c = 1;
-  while (c < k) c <<= 1;
+  while (c < k && c < 8) c <<= 1;
   switch (c) {
     case 1: return launch_merge_packed<1>(packed, W, Bp, b, kc, k, metric, od, oi, s);
     case 2: return launch_merge_packed<2>(packed, W, Bp, b, kc, k, metric, od, oi, s);
     case 4: return launch_merge_packed<4>(packed, W, Bp, b, kc, k, metric, od, oi, s);
-    case 8: return launch_merge_packed<8>(packed, W, Bp, b, kc, k, metric, od, oi, s);
-    case 16: return launch_merge_packed<32>(packed, W, Bp, b, kc, k, metric, od, oi, s);
-    case 32: return launch_merge_packed<32>(packed, W, Bp, b, kc, k, metric, od, oi, s);
-    default: return launch_merge_packed<64>(packed, W, Bp, b, kc, k, metric, od, oi, s);
+    default: return launch_merge_packed<8>(packed, W, Bp, b, kc, k, metric, od, oi, s);
   }
 }
 

@@ -202,8 +202,16 @@ class ShardedIndex:
         return self._comm_cache
 
     def _rccl_ok(self, k: int) -> bool:
-        return (self._native and k <= 64 and self.world * k <= 512
-                and os.environ.get("MPR_SHARDED_NATIVE", "1") != "0" and self._comm() != 0)
+        """The native exchange applies: RCCL's symbols are loaded (another soname or an RCCL
+        without them takes the torch.distributed all_gather instead) and a communicator exists."""
+        if not (self._native and k <= 64 and self.world * k <= 512
+                and os.environ.get("MPR_SHARDED_NATIVE", "1") != "0"):
+            return False
+        if not hasattr(self, "_rccl_syms"):
+            ok = _lib.ctypes.c_int32(0)
+            _lib.call("mpr_rccl_available", _lib.ctypes.byref(ok))
+            self._rccl_syms = bool(ok.value)
+        return self._rccl_syms and self._comm() != 0
 
     def _recv_blocks(self, q, B: int, k: int):
         """The native search's receive buffer [n_blocks * B, k, 2] float64 and n_blocks (the

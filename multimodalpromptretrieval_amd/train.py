@@ -234,7 +234,10 @@ class T5LossFn(torch.autograd.Function):
         ctx.keep = (emb, maskf, ids_dev, lab32, ps, parr)
         ctx.dec_ids, ctx.n_valid, ctx.shape = dec_ids, n_valid, (B, L, d)
         ctx.spec = None
-        if speculative_backward() and any(ctx.needs_input_grad) and dev.type == "cuda":
+        # needs_input_grad reflects requires_grad, not grad mode: a forward under no_grad (a
+        # train-mode forward whose loss is only read) is never backwarded, so it enqueues none
+        if (speculative_backward() and cfg.grad_enabled and any(ctx.needs_input_grad) and
+                dev.type == "cuda"):
             # main.py:177-186 runs model(batch), then predict(batch), then loss.backward(): the
             # backward for a loss gradient of 1 is enqueued now on a side stream ordered after
             # this forward, so it runs on the GPU beside predict()'s decode (which the host
@@ -243,6 +246,10 @@ class T5LossFn(torch.autograd.Function):
             cur = torch.cuda.current_stream(dev)
             side = _spec_stream(dev)
             side.wait_stream(cur)
+            # the tape's inputs were allocated on `cur`: if the graph is dropped without a
+            # backward they are freed while the side stream may still read them
+            for t in (emb, maskf, ids_dev, lab32, *ps):
+                t.record_stream(side)
             with torch.cuda.stream(side):
                 out = T5LossFn._native_backward(ctx, torch.ones((), device=dev))
                 done = torch.cuda.Event()
@@ -351,6 +358,7 @@ class T5Config:
         self.max_distance = max_distance
         self.scale_out = scale_out
         self.dropout = None  # Dropout in train mode
+        self.grad_enabled = True  # torch.is_grad_enabled() where the loss was built (t5_loss)
 
     def trainer(self, device):
         """The native trainer of this configuration on ``device`` (one per process; its tapes
@@ -405,5 +413,6 @@ def t5_loss(named_params: dict, inputs_embeds, attention_mask, labels, num_heads
         if dropout_seed is None:
             dropout_seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64))
         cfg.dropout = Dropout(dropout_rate, dropout_seed)
+    cfg.grad_enabled = torch.is_grad_enabled()  # (off inside Function.forward)
     return T5LossFn.apply(cfg, inputs_embeds, attention_mask, labels,
                           *[named_params[n] for n in order])

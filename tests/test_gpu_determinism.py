@@ -63,8 +63,9 @@ def test_grouped_generate_bit_identical_beside_tower_passes(device):
             return t5h.generate_batches_padded(ins, 20, slot=1)
 
     with torch.no_grad():
-        ref = [o.clone() for o in generate()]
-        torch.cuda.synchronize()
+        ref = generate()
+        torch.cuda.synchronize()  # (the tokens are written on the generate stream)
+        ref = [o.clone() for o in ref]
         differing = []
         for r in range(24):
             out = generate()

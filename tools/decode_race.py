@@ -187,8 +187,9 @@ def main():
             return gbp0(t5h, ins, 20, slot=1)
 
     with torch.no_grad():
-        o_ref = [x.clone() for x in generate()]
-        torch.cuda.synchronize()
+        o_ref = generate()
+        torch.cuda.synchronize()  # (the tokens are written on the generate stream)
+        o_ref = [x.clone() for x in o_ref]
         ref, segs = trace(t5h, 1, dev)
         print(f"trace: {ref.numel() / 2**20:.1f} M floats in {len(segs)} segments", flush=True)
         n_layers = max(sg[2] for sg in segs) + 1
