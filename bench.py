@@ -614,8 +614,11 @@ def decode_chain(model, batch, steps: int = 20, iters: int = 10):
     enc = min(timed(0) for _ in range(3))
     dec_ms = full - enc
     rows = int(emb.shape[0])
-    fold = (os.environ.get("MPR_DECODE_FOLD", "1") != "0"
-            and rows <= int(os.environ.get("MPR_DECODE_FOLD_ROWS", "16")))
+    # t5.hip fold_rows: the folded chain below d = 768 at every row count (the env switches are
+    # the A/B overrides)
+    fe = os.environ.get("MPR_DECODE_FOLD")
+    fold = ((fe != "0") if fe is not None else dev.d_model < 768) and \
+        rows <= int(os.environ.get("MPR_DECODE_FOLD_ROWS", str(1 << 30)))
     launches = dev.n_dec * (6 if fold else 8) + 2
     d, inner, dff, V = dev.d_model, dev.inner, dev.d_ff, dev.vocab
     per_step = 4.0 * (dev.n_dec * (6 * d * inner + 2 * d * dff) + V * d)

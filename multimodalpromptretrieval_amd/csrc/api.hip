@@ -602,8 +602,10 @@ int mpr_t5_create(const int32_t* cfg, int32_t n_cfg, const float* const* t, int3
     const int expect = 2 + 8 * Le + 1 + 1 + 13 * Ld + 2;
     MPR_REQUIRE(nt == expect, "t5_create: expected %d tensors, got %d", expect, nt);
     {
+      // the folded decode chain for models below d = 768 (T5Model::fold_rows); MPR_DECODE_FOLD
+      // = 0 / 1 forces it off / on
       const char* e = getenv("MPR_DECODE_FOLD");
-      m->fold = !(e && e[0] == '0');
+      m->fold = e ? e[0] != '0' : d < 768;
     }
     MPR_TRY(t5_load(m.get(), t, enc_lut, dec_lut, /*fresh=*/true, nullptr));
     MPR_HIP(hipDeviceSynchronize());

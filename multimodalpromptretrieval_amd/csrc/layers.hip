@@ -368,6 +368,18 @@ __global__ __launch_bounds__(256) void attention_decode_wave_kernel(AttnArgs a) 
   dattn::pair(a, pr / a.H, pr % a.H, Ps[wave], Os[wave]);  // decode_attn.h
 }
 
+// The same pair per 64-thread block (one wave): the few-pair decodes (a 16-row batch: 128 pairs)
+// get a block per pair, spread over 128 CUs, instead of 32 four-pair blocks.
+__global__ __launch_bounds__(64) void attention_decode_wave1_kernel(AttnArgs a) {
+  __shared__ float Ps[128];
+  __shared__ __attribute__((aligned(16))) float Os[8][ATT_D];
+  if (a.poison) {
+    poison_lds(Ps, 128);
+    poison_lds(&Os[0][0], 8 * ATT_D);
+  }
+  dattn::pair(a, blockIdx.x / a.H, blockIdx.x % a.H, Ps, Os);  // decode_attn.h
+}
+
 // attention_decode_wave_kernel's pairs with 65..128 keys (a grouped decode's cross-attention over
 // its encoder rows) as two waves per pair, one per 64-key half, so twice the loads of a pair are
 // in flight per CU.  The halves' maxima, sums and P.V groups meet in LDS and combine in the same
@@ -947,6 +959,19 @@ int attention(const AttnArgs& a, hipStream_t s) {
       else
         hipLaunchKernelGGL(attention_decode_wave_kernel,
                            dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(256), 0, s, a);
+      MPR_LAUNCHED();
+      return MPR_OK;
+    }
+    // few pairs: MPR_ATT_SMALL=wave1 runs them one wave per block (A/B; read per call, a
+    // captured graph keeps its form), wave2 two waves per pair (65..128 keys)
+    const char* sm = getenv("MPR_ATT_SMALL");
+    if (sm && lk_end <= 128 && sm[0] == 'w') {
+      if (sm[4] == '2' && lk_end > 64)
+        hipLaunchKernelGGL(attention_decode_wave2_kernel,
+                           dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL(attention_decode_wave1_kernel, dim3((unsigned)((int64_t)a.B * a.H)),
+                           dim3(64), 0, s, a);
       MPR_LAUNCHED();
       return MPR_OK;
     }

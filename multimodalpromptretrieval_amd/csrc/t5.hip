@@ -197,15 +197,23 @@ __global__ __launch_bounds__(256) void fold_product_kernel(const FoldJobs jobs, 
 // projections, the cross-attention applies its query's scale from the x1 row it reads, and the
 // FFN-out GEMM applies relu on load and the x2 scale in its epilogue.  8 -> 6 dependent launches
 // per layer, at a different fp32 rounding order than the reference's.
-// The folded chain trades launches for MACs (its two merged GEMMs read 50 % more weight per
-// layer): it wins for the latency-bound decodes of one batch and loses for the grouped
-// 128-row decodes of a serving loop, where the launches overlap other work (measured).
+//
+// One decode chain per model at every row count, so a batch decoded alone (predict(), <= 16 rows)
+// and inside a serving loop's grouped decode (128 rows) gets the same bits: rows are independent
+// in every kernel of a chain, whatever the row blocking.  t5-small (d < 768) takes the folded
+// chain with the skinny argmax head at every row count (its 128-row groups cost nothing
+// measurable folded: 3,934 against 3,938 QA pairs/s, profiles/r06_chain_ab.txt); d >= 768
+// (t5-base) takes the 8-launch chain with the tiled argmax head at every row count (folded, two of
+// a layer's three GEMV pairs read twice the weights, which C5's 256-row decodes pay for; the
+// skinny head stages the rows once per 16 columns: 201 against 55 us for 128 rows).
+// MPR_DECODE_FOLD_ROWS (fold only up to that many rows) / MPR_TILED_HEAD are A/B switches: a
+// chain that changes with the row count no longer matches predict() bit for bit.
 bool T5Model::fold_rows(int B) const {
   static const int max_rows = [] {
     const char* e = getenv("MPR_DECODE_FOLD_ROWS");
-    return e ? atoi(e) : 16;
+    return e ? atoi(e) : -1;
   }();
-  return fold && B <= max_rows;
+  return fold && (max_rows < 0 || B <= max_rows);
 }
 
 int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
@@ -216,15 +224,15 @@ int T5Model::dec_gemm(const SkinnyArgs& a, const DevBuf& pk, hipStream_t s,
   return gemm_skinny(b, s);
 }
 
-// The argmax head of a grouped decode (> 32 rows) as RMSNorm + the tiled split-bf16 GEMM into a
-// logits buffer + a row argmax, instead of the skinny GEMV (which stages the rows once per 16
-// columns: 8,032 blocks re-reading 96 KB of rows for t5-base's 128-row head, 201 us).  Default
-// from d >= 768 (t5-base and up); MPR_TILED_HEAD=0 / 1 forces it off / on (read per call; a
-// captured decode graph keeps the head it was captured with).
+// The argmax head as RMSNorm + the tiled split-bf16 GEMM into a logits buffer + a row argmax,
+// instead of the skinny GEMV (which stages the rows once per 16 columns: 8,032 blocks re-reading
+// 96 KB of rows for t5-base's 128-row head, 201 us).  Default for d >= 768 (t5-base and up) at
+// every row count (fold_rows); MPR_TILED_HEAD=0 / 1 forces it off / on (read per call; a captured
+// decode graph keeps the head it was captured with).
 bool T5Model::tiled_head(int B) const {
   const char* e = getenv("MPR_TILED_HEAD");
   const bool on = e ? e[0] == '1' : d >= 768;
-  return on && B > 32 && !fold_rows(B);
+  return on && !fold_rows(B);
 }
 
 int T5Model::build_folded(hipStream_t s) {

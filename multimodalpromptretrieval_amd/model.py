@@ -539,9 +539,9 @@ class T5VisionModel(nn.Module):
         decode at the first chunk of MPR_EOS_STOP_CHUNK steps after which every row has emitted
         eos, as greedy search stops (architectures/T5VisionModel.py:200-205), polled without
         blocking the host; off, every call runs max_new_tokens steps.
-        Yields each batch's answers in order; every batch gets predict()'s answers up to fp32
-        near-ties (serving.ServingLoop: a grouped decode sums in another fp32-accurate order
-        than predict()'s 16-row folded chain).  ``_loop_out`` (a list) receives the ServingLoop."""
+        Yields each batch's answers in order; every batch gets exactly predict()'s answers (one
+        decode chain per model at every row count, whatever else shares the chip:
+        serving.ServingLoop).  ``_loop_out`` (a list) receives the ServingLoop."""
         from .serving import ServingLoop, ServingOptions
         opts = ServingOptions.resolve(decodes_in_flight, pair_decodes, lookahead, tower_slots,
                                       decode_group, tower_batches, eos_stop)

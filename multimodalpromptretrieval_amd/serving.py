@@ -19,12 +19,12 @@ overlapped across batches on their own streams:
   20-step headline);
 * answers are handed out in order as their calls complete (``_finish``).
 
-Every batch gets ``predict()``'s answers up to fp32 near-ties: a 16-row predict() decodes with
-the decoder layer's RMSNorms folded into its projections (csrc/t5.hip), a grouped decode (more
-than 16 rows) without, and t5-base's grouped argmax head runs on the tiled GEMM — other
-fp32-accurate summation orders, all pinned to the reference's goldens G3 / G7 / G8.  A grouped
-decode's rows do not depend on how many batches share it: every grouping of the same batches gives
-the same bits (tests/test_gpu_serving.py, tests/test_gpu_golden.py).
+Every batch gets exactly ``predict()``'s answers: a model decodes with one chain at every row
+count (t5-small: the decoder layer's RMSNorms folded into its projections; t5-base: the 8-launch
+chain with the tiled argmax head; csrc/t5.hip fold_rows), and rows are independent in every
+kernel of it, so a batch's tokens are the same bits alone and in any grouping
+(tests/test_gpu_serving.py, tests/test_gpu_determinism.py), pinned to the reference's goldens
+G3 / G7 / G8.
 """
 from __future__ import annotations
 

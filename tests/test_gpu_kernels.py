@@ -584,10 +584,13 @@ def grouped_40(t5_sd):
 @pytest.mark.parametrize("tiled", ["1", "0"])
 def test_t5_grouped_decode_head_vs_oracle(device, t5_sd, grouped_40, monkeypatch, tiled):
     """The argmax head of a decode over > 32 rows: RMSNorm + the tiled GEMM + a row argmax
-    (MPR_TILED_HEAD=1, the default from d >= 768) or the skinny GEMV (0).  Greedy ids equal the
-    oracle's per row up to (and including) its first step with a top-2 margin <= 1e-3."""
+    (MPR_TILED_HEAD=1, the default from d >= 768) or the skinny GEMV (0), on the 8-launch chain
+    (MPR_DECODE_FOLD=0: this t5-small model would otherwise take the folded chain, whose head is
+    the skinny GEMV).  Greedy ids equal the oracle's per row up to (and including) its first
+    step with a top-2 margin <= 1e-3."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     monkeypatch.setenv("MPR_TILED_HEAD", tiled)
+    monkeypatch.setenv("MPR_DECODE_FOLD", "0")
     m = DeviceT5(t5_sd, device)
     emb, fm, ref_toks, step_logits = grouped_40
     toks = m.generate_padded(emb, fm, 20).cpu().long()

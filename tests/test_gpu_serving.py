@@ -6,8 +6,9 @@ consumers that stop early, and beside predict().
   answers (architectures/T5VisionModel.py:196-216);
 * a generator dropped mid-way leaves no decode in flight: later predict() calls and a new loop
   run (their workspace slots are free);
-* a batch's greedy tokens are the same in a 128-row and a 256-row group, and agree with its
-  own 16-row decode up to fp32 near-ties, at full t5-small size.
+* a batch's greedy tokens are the same in a 128-row group, in a 256-row group and in its own
+  16-row decode, at full t5-small size (one decode chain per model at every row count:
+  t5.hip fold_rows).
 """
 import os
 import sys
@@ -73,24 +74,11 @@ def test_dropped_loop_frees_its_slots(device):
     assert list(model.predict_many(batches, decode_group=2)) == want
 
 
-def _near_tie_free(dev, emb, mask, toks, rel=1e-4):
-    """Per row, the number of leading decode steps whose greedy choice is not a near-tie: the
-    teacher-forced logits of the row's own tokens, top-2 gap > rel * max |logit|."""
-    dec_in = toks[:, :-1].long()
-    lg = dev.logits(emb, mask, dec_in).cpu().double()
-    top2 = lg.topk(2, dim=-1).values
-    ok = (top2[..., 0] - top2[..., 1]) > rel * lg.abs().amax(-1)
-    first_bad = torch.where(ok.all(1), torch.full((ok.shape[0],), ok.shape[1]),
-                            (~ok).float().argmax(1))
-    return first_bad
-
-
 @pytest.mark.slow
 def test_t5_small_grouped_rows_equal_alone(device):
-    """Full-size t5-small, eight 16-row batches: decoded as one 128-row group and as one 256-row
-    group they give bit-identical tokens (the grouped decode's GEMVs sum every row alike, in
-    32-row blocks); against each batch's own 16-row decode (the folded chain, another
-    fp32-accurate summation order) every row agrees up to its first near-tie."""
+    """Full-size t5-small, eight 16-row batches: decoded as one 128-row group, as one 256-row
+    group and each on its own they give bit-identical tokens (the same folded chain at every row
+    count; its GEMVs sum every row alike whatever the row blocking)."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     sd = syn.t5_state_dict(gi.G3["t5_seed"], syn.T5Config())
     dev = DeviceT5(sd, device)
@@ -108,10 +96,7 @@ def test_t5_small_grouped_rows_equal_alone(device):
         assert torch.equal(a, b) and torch.equal(a, c)
     for (e, m), gr in zip(ins, grouped):
         alone = dev.generate_padded(e, m, 20, slot=0).cpu()
-        safe = _near_tie_free(dev, e, m, alone)
-        for r in range(alone.shape[0]):
-            n = int(safe[r]) + 1  # column 0 is the start token
-            assert torch.equal(alone[r, :n], gr[r, :n]), (r, n)
+        assert torch.equal(alone, gr)
 
 
 @pytest.mark.parametrize("rows", [40, 130])
