@@ -61,6 +61,21 @@ __device__ __forceinline__ void pair(const AttnArgs& a, int b, int h, float* Ps,
     mraw[hf] = *mp;
     braw[hf] = *bp;
   }
+  // the P.V operands too, before any arithmetic: lane (dg, kq) reads dims 4 dg .. +3 of keys
+  // (hf * 4 + kq) * 16 .. +15, so every load of the pair is in flight at once (one memory round
+  // trip instead of two; the arithmetic is unchanged)
+  const int dg = lane & 15, kq = lane >> 4;
+  f32x4 vr[2][16];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf == 1 && !two) break;
+    const int jv0 = (hf * 4 + kq) * 16;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int jv = jv0 + u < lk_end ? jv0 + u : 0;
+      vr[hf][u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)jv * a.v_rs + 4 * dg);
+    }
+  }
   if (a.q_rms_part)
     qscale = a.scale * (1.0f / sqrtf(wsum(qpart) / (float)a.q_rms_n + a.q_rms_eps));
   float sc[2] = {-INFINITY, -INFINITY};
@@ -92,18 +107,6 @@ __device__ __forceinline__ void pair(const AttnArgs& a, int b, int h, float* Ps,
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // P.V: lane (dg, kq) sums dims 4 dg .. +3 over key group kq (and 4 + kq), 16 keys each, as the
   // block kernel's thread (dg, kg) does (o starts at 0 * alpha = 0)
-  const int dg = lane & 15, kq = lane >> 4;
-  f32x4 vr[2][16];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    if (hf == 1 && !two) break;
-    const int jv0 = (hf * 4 + kq) * 16;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int jv = jv0 + u < lk_end ? jv0 + u : 0;
-      vr[hf][u] = *reinterpret_cast<const f32x4*>(vb + (int64_t)jv * a.v_rs + 4 * dg);
-    }
-  }
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     if (hf == 1 && !two) break;

@@ -978,8 +978,8 @@ enum : int { SKF_RMS = 1, SKF_RES = 2, SKF_RELU = 4, SKF_AMAX = 8, SKF_RELU_IN =
 // dependent-MFMA latency.  MAXC = chunks of 16 columns staged per pass; LOOP = more than one
 // pass (K > 16 * 8 * MAXC).  (Issuing the next pass's loads before this pass's slab round trip,
 // two register sets at half the MAXC, measured no faster: 32-row FFN-out 10.32 vs 10.24 us.)
-template <int MAXC, int NT, int F, bool LOOP, int MR>
-__global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
+template <int MAXC, int NT, int F, bool LOOP, int MR, int SK_WAVES = 8>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(SkinnyArgs sa) {
   constexpr bool RMS = (F & SKF_RMS) != 0, RES = (F & SKF_RES) != 0,
                  RELU = (F & SKF_RELU) != 0, AMAX = (F & SKF_AMAX) != 0,
                  RELU_IN = (F & SKF_RELU_IN) != 0, RSCALE = (F & SKF_RSCALE) != 0,
@@ -1002,7 +1002,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   float(*ssq_s)[MROWS] = reinterpret_cast<float(*)[MROWS]>(smem + XS);
   const int tid = threadIdx.x, lane = tid & 63;
   if (sa.poison) {  // debug: a read of LDS this block never wrote yields NaN
-    for (int i = tid; i < (int)(sizeof(smem) / sizeof(float)); i += 512) smem[i] = __builtin_nanf("");
+    for (int i = tid; i < (int)(sizeof(smem) / sizeof(float)); i += 64 * SK_WAVES)
+      smem[i] = __builtin_nanf("");
     __syncthreads();
   }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
@@ -1036,7 +1037,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(SkinnyArgs sa) {
   }
   // RSCALE: the rows' partial sums of squares (<= 64 per row): wave w loads those of rows w,
   // w + 8, ... (lane = partial), issued with the first loads, summed after the main loop
-  constexpr int RPW = MROWS / SK_WAVES;  // rows per wave (2 or 4)
+  constexpr int RPW = MROWS / SK_WAVES;  // rows per wave (1, 2 or 4)
   float rsp[RSCALE ? RPW : 1];
   if constexpr (RSCALE) {
 #pragma unroll
@@ -1541,11 +1542,12 @@ int pack_rows16(const float* W, int64_t N, int64_t K, int64_t ldw, float* out, h
   return MPR_OK;
 }
 
-template <int MAXC, int NT, bool LOOP, int MR = 1>
+template <int MAXC, int NT, bool LOOP, int MR = 1, int W = 8>
 void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, unsigned gy = 1) {
 #define MPR_SK(f)                                                                          \
   case f:                                                                                  \
-    hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP, MR>), dim3(grid, gy), dim3(512), 0, s, sa); \
+    hipLaunchKernelGGL((gemm_skinny_kernel<MAXC, NT, f, LOOP, MR, W>), dim3(grid, gy),    \
+                       dim3(64 * W), 0, s, sa);                                            \
     break;
   if constexpr (NT > 1) {
     switch (F) { MPR_SK(SKF_AMAX) MPR_SK(SKF_AMAX | SKF_RMS) default: break; }
@@ -1595,6 +1597,9 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   MPR_REQUIRE(!(F & SKF_SSQ) || F == SKF_SSQ, "gemm_skinny: ssq only on a plain projection");
   const int per = (int)cdiv(cdiv(a.K, 16), SK_WAVES);  // 16-column chunks per wave
   const int64_t tiles = cdiv(a.N, 16);
+  // (16 waves splitting a long K — t5-small's K = 2048 FFN-out — chosen by K alone so every row
+  // count sums alike: 218.5 -> 215.8 us per 16-row step but 433.9 -> 437.1 per 128-row step,
+  // round 6, tools/decode_ab.py; not kept: the serving loop decodes 128-row groups.)
   if (debug_lds_poison() && !sa.poison) {
     SkinnyArgs p = sa;
     p.poison = 1;
@@ -1624,7 +1629,7 @@ int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
       // blocks of 64 (MR = 4, 2-chunk passes: 74 KB of slabs), halving the weight re-reads per
       // step: t5-base 256 rows 1621 -> 1430 us per step, 192 rows 1490 -> 1331; at 128 rows
       // (1055 -> 1200) and for t5-small (256 rows 514 -> 586) the 32-row blocks stay; 128-row
-      // blocks ran 2206 at 256, 48-row blocks 1712 vs 1479 (tools/decode_rows.py,
+      // blocks ran 2206 at 256, 48-row blocks 1712 vs 1479 (git show f10742c:tools/decode_rows.py,
       // profiles/r04_skinny_rows_ab.txt).  Rows
       // are independent and every chain keeps its chunk order: bit-identical.
       if (!amax && a.M > 128 && std::min(a.N, a.K) >= 768) {

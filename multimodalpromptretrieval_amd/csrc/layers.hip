@@ -945,9 +945,9 @@ int attention(const AttnArgs& a, hipStream_t s) {
     return attention(p, s);
   }
   if (a.Lq == 1) {
-    // Few pairs (one batch's decode): the block kernel (a wave-per-(b, h) form measured slower at
-    // 16 rows: 4.4 / 5.3 us self / cross against 3.8 / 4.1, a quarter of the loads in flight per
-    // pair).  Many pairs with few keys (grouped decodes): the wave form, bit-identical.
+    // Every form below sums in the block kernel's order: outputs bit-identical (tested).  Many
+    // pairs with few keys (grouped decodes): four pairs per block, a wave each (two per pair
+    // past 64 keys); few pairs: a block per pair (below); > 128 keys: the block kernel.
     const char* we = getenv("MPR_ATT_WAVE");  // read per call (a captured graph keeps its form)
     const bool wave_ok = !(we && we[0] == '0');
     const int lk_end = a.causal ? std::min(a.Lk, a.q_pos0 + 1) : a.Lk;
@@ -962,11 +962,14 @@ int attention(const AttnArgs& a, hipStream_t s) {
       MPR_LAUNCHED();
       return MPR_OK;
     }
-    // few pairs: MPR_ATT_SMALL=wave1 runs them one wave per block (A/B; read per call, a
-    // captured graph keeps its form), wave2 two waves per pair (65..128 keys)
+    // Few pairs (one batch's decode: 16 rows x 8 heads): one wave per block, a block per pair
+    // spread over as many CUs (16-row t5-small decode 227.9 -> 215.7 us per step against the
+    // 256-thread block kernel, same tokens: profiles/r06_decode_attn_ab.txt).  MPR_ATT_SMALL
+    // (read per call; a captured graph keeps its form): "block" = the block kernel, "wave2" =
+    // two waves per pair for 65..128 keys.
     const char* sm = getenv("MPR_ATT_SMALL");
-    if (sm && lk_end <= 128 && sm[0] == 'w') {
-      if (sm[4] == '2' && lk_end > 64)
+    if (wave_ok && lk_end <= 128 && !(sm && sm[0] == 'b')) {
+      if (sm && sm[0] == 'w' && sm[4] == '2' && lk_end > 64)
         hipLaunchKernelGGL(attention_decode_wave2_kernel,
                            dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(512), 0, s, a);
       else

@@ -379,7 +379,7 @@ class DeviceT5:
                  eos_token_id=1, pad_token_id=0, lens=None, while_running=None) -> torch.Tensor:
         """GenerationMixin.generate(do_sample=False) result (int64, host, trimmed).  Stops where
         greedy search stops: the decode runs in chunks of MPR_EOS_STOP_CHUNK steps (default 4:
-        no cost measurable against one graph, tools/eos_chunk_ab.py, where 2 cost ~0.07 ms;
+        no cost measurable against one graph, git show f10742c:tools/eos_chunk_ab.py, where 2 cost ~0.07 ms;
         0 = one graph of all steps) and no chunk is launched once every row has emitted eos
         (mpr_t5_generate_stop; the skipped columns are pad, as the full loop writes).
         ``while_running``: a host callable run once the encoder and the first decode chunks are

@@ -626,6 +626,23 @@ def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
     assert torch.equal(one_wave, want)
 
 
+@pytest.mark.parametrize("fold", ["1", "0"])
+def test_decode_attention_small_forms_match_block(device, t5_sd, monkeypatch, fold):
+    """A one-batch decode (16 rows: 128 batch x head pairs) runs its attention a block of one wave
+    per pair (attention_decode_wave1_kernel, default), two waves per pair past 64 keys
+    (MPR_ATT_SMALL=wave2) or the 256-thread block kernel (block): greedy tokens equal in all
+    three, on the folded and the 8-launch chain (73 source keys: the cross-attention takes both
+    halves)."""
+    from multimodalpromptretrieval_amd.t5 import DeviceT5
+    monkeypatch.setenv("MPR_DECODE_FOLD", fold)
+    emb, fm = _t5_batch(t5_sd, 16, 73)
+    got = {}
+    for form in ("block", "wave1", "wave2"):
+        monkeypatch.setenv("MPR_ATT_SMALL", form)
+        got[form] = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
+    assert torch.equal(got["wave1"], got["block"]) and torch.equal(got["wave2"], got["block"])
+
+
 def test_grouped_decode_row_blocks_match(device, monkeypatch):
     """A t5-base decode loop of more than 128 rows runs its GEMVs on 64-row blocks (MR = 4,
     2-chunk passes); the same rows decoded as loops of <= 128 rows (32-row blocks, 4-chunk
