@@ -148,3 +148,69 @@ def test_search_all_many_pipelined_on_rccl(device):
     finally:
         os.environ.pop("MPR_SHARDED_FORCE_COLLECTIVE", None)
         dist.destroy_process_group()
+
+
+def test_native_merge_reads_eight_prefilled_blocks(device):
+    """The packed layout a W = 8 exchange hands mpr_sharded_search_all's merge, on one GPU: an
+    index of 8 x 2500 rows cut into 8 shards (each a DeviceIndex with its global row offset);
+    shards 1-7 are searched and packed into blocks 1-7 of the [8 B, k, 2] receive buffer, and
+    shard 0's native call (world 1, rank 0, n_blocks = 8) writes block 0 and merges all eight.
+    The result must be the single index's: ids exact (a duplicate row across shards resolves to
+    the lower global id), distances bit-identical on the exact scan (b = 16) and within the cdist
+    bound on the coarse path (b = 96).  Run with and without the in-place RCCL all_gather (which
+    at world 1 must leave blocks 1-7 untouched)."""
+    from multimodalpromptretrieval_amd import synthetic as syn
+    from multimodalpromptretrieval_amd import _lib
+    from multimodalpromptretrieval_amd.distributed import ShardedIndex, shard_bounds
+    from multimodalpromptretrieval_amd.index import DeviceIndex
+    W, n, k = 8, 8 * 2500, 5
+    X = syn.index_rows(83, n, D)
+    X[5 * 2500 + 7] = X[11]  # shard 5 holds a copy of a shard-0 row
+    X[7 * 2500 + 1] = X[3 * 2500 + 9]
+    qs = {b: syn.index_rows(84 + b, b, D) for b in (16, 96)}
+    qs[16][0] = X[11]
+    qs[96][3] = X[3 * 2500 + 9]
+    full = DeviceIndex(X, device)
+    want = {b: tuple(t.cpu() for t in full.search(q.to(device), k)) for b, q in qs.items()}
+    del full
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0,
+                            world_size=1, device_id=device)
+    try:
+        shards = []
+        for r in range(W):
+            lo, hi = shard_bounds(n, W, r)
+            shards.append(ShardedIndex(X[lo:hi], device, rows_are_local=True, row_offset=lo))
+        s0 = shards[0]
+        assert s0._rccl_ok(k), "the native RCCL path (mpr_sharded_search_all) is not available"
+        for force in ("0", "1"):
+            if force == "1":
+                os.environ["MPR_SHARDED_FORCE_COLLECTIVE"] = "1"
+            for b, q in qs.items():
+                qd = q.to(device).contiguous()
+                recv = torch.full((W * b, k, 2), float("nan"), device=device, dtype=torch.float64)
+                for r in range(1, W):
+                    recv[r * b:(r + 1) * b] = shards[r]._pack(*shards[r]._local.search(qd, k))
+                foreign = recv[b:].clone()
+                od = torch.empty((b, k), device=device, dtype=torch.float32)
+                oi = torch.empty((b, k), device=device, dtype=torch.int64)
+                _lib.call("mpr_sharded_search_all", s0._local._h, _lib.c_void_p(s0._comm()), 1, 0,
+                          _lib.ptr(qd), b, k, _lib.ptr(recv), W, _lib.ptr(od), _lib.ptr(oi),
+                          _lib.stream_ptr(device))
+                torch.cuda.synchronize()
+                assert torch.equal(recv[b:], foreign), (force, b)  # blocks 1-7 untouched
+                assert not torch.isnan(recv[:b]).any(), (force, b)  # block 0 written
+                dw, iw = want[b]
+                assert torch.equal(oi.cpu(), iw), (force, b)
+                if b == 16:
+                    assert torch.equal(od.cpu(), dw), force
+                else:
+                    Xn = (X.double() ** 2).sum(1)[iw]
+                    scale = (q.double() ** 2).sum(1, keepdim=True) + Xn
+                    assert torch.all((od.cpu().double() ** 2 - dw.double() ** 2).abs()
+                                     <= 2e-6 * scale), force
+            assert int(want[16][1][0, 0]) == 11 and int(want[16][1][0, 1]) == 5 * 2500 + 7
+            assert int(want[96][1][3, 0]) == 3 * 2500 + 9
+            assert int(want[96][1][3, 1]) == 7 * 2500 + 1
+    finally:
+        os.environ.pop("MPR_SHARDED_FORCE_COLLECTIVE", None)
+        dist.destroy_process_group()
