@@ -591,8 +591,21 @@ int T5Model::decode_body(int B, int L, int max_new, int eos, int pad, hipStream_
 // the a half of [a | x], [x1 | u] (one GEMM over [a | x]), cross-attention (query scaled by
 // x1's RMS) into the c half of [c | x1 | u], [x2 | z] (one GEMM over [c | x1]), FFN-out (relu on
 // load, x2's RMS scale, + x2) into the x half of [a | x].
+// Timing bisection (tools/decode_ab.py): MPR_DEBUG_CHAIN_SKIP = a bit mask of the folded chain's
+// launch kinds a decode step leaves out (its tokens are then wrong): 1 q|k|v GEMVs, 2 self-
+// attentions, 4 o|cq GEMVs, 8 cross-attentions, 16 co|wi GEMVs, 32 FFN-out GEMVs, 64 the argmax
+// head, 128 the greedy step.
+static int chain_skip() {
+  static const int m = [] {
+    const char* e = getenv("MPR_DEBUG_CHAIN_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
 int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hipStream_t s,
                                 int t0, int t1) {
+  const int skip = chain_skip();
   const int T1 = max_new + 1, Tc = max_new > 0 ? max_new : 1;
   const int64_t cache_layer = (int64_t)B * Tc * 3 * inner;
   const float* maskp = ws->mask_in.as<float>();
@@ -624,15 +637,15 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       sq.g.A = xp; sq.g.lda = ldA;
       sq.g.C = cl + (int64_t)t * 3 * inner; sq.g.ldc = (int64_t)Tc * 3 * inner;
       sq.g.M = B; sq.g.N = 3 * inner; sq.g.K = d; sq.rms_w = ly.ln0.as<float>(); sq.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(sq, ly.pk_qkv, s));
+      if (!(skip & 1)) MPR_TRY(dec_gemm(sq, ly.pk_qkv, s));
       MPR_TRY(trace(TR_QKV, t, l, sq.g.C, B, 3 * inner, sq.g.ldc, s));
-      MPR_TRY(attention(at, s));
+      if (!(skip & 2)) MPR_TRY(attention(at, s));
       MPR_TRY(trace(TR_SELF_ATT, t, l, ax, B, inner, ldA, s));
       SkinnyArgs so;  // [x1 | u] = [a | x] W_ocq^T
       so.g.A = ax; so.g.lda = ldA; so.g.C = yq + inner; so.g.ldc = ldY;
       so.g.M = B; so.g.N = d + inner; so.g.K = inner + d;
       so.ssq_out = x1ss; so.ssq_cols = d;  // x1's per-tile sums of squares (its RMS)
-      MPR_TRY(dec_gemm(so, ly.pk_ocq, s));
+      if (!(skip & 4)) MPR_TRY(dec_gemm(so, ly.pk_ocq, s));
       MPR_TRY(trace(TR_OCQ, t, l, yq + inner, B, d + inner, ldY, s));
       MPR_TRY(trace(TR_X1SS, t, l, x1ss, B, d / 16, d / 16, s));
       AttnArgs ca;  // c = attention(u / rms_scale(x1), K_enc, V_enc)
@@ -643,13 +656,13 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       ca.B = B; ca.H = H; ca.Lq = 1; ca.Lk = L; ca.scale = 1.f;
       ca.key_mask = maskp; ca.mask_bs = L;
       ca.q_rms_part = x1ss; ca.q_rms_nparts = d / 16; ca.q_rms_n = d; ca.q_rms_eps = T5_EPS;
-      MPR_TRY(attention(ca, s));
+      if (!(skip & 8)) MPR_TRY(attention(ca, s));
       MPR_TRY(trace(TR_CROSS_ATT, t, l, yq, B, inner, ldY, s));
       SkinnyArgs cw;  // [x2 | z] = [c | x1] W_cowi^T
       cw.g.A = yq; cw.g.lda = ldY; cw.g.C = hz; cw.g.ldc = ldZ;
       cw.g.M = B; cw.g.N = d + dff; cw.g.K = inner + d;
       cw.ssq_out = x2ss; cw.ssq_cols = d;
-      MPR_TRY(dec_gemm(cw, ly.pk_cowi, s));
+      if (!(skip & 16)) MPR_TRY(dec_gemm(cw, ly.pk_cowi, s));
       MPR_TRY(trace(TR_COWI, t, l, hz, B, d + dff, ldZ, s));
       MPR_TRY(trace(TR_X2SS, t, l, x2ss, B, d / 16, d / 16, s));
       SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
@@ -657,7 +670,7 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
       fo.relu_in = true; fo.rs_part = x2ss; fo.rs_nparts = d / 16; fo.rs_n = d;
       fo.rms_eps = T5_EPS;
-      MPR_TRY(dec_gemm(fo, ly.pk_wo, s));
+      if (!(skip & 32)) MPR_TRY(dec_gemm(fo, ly.pk_wo, s));
       MPR_TRY(trace(TR_FO, t, l, xp, B, d, ldA, s));
     }
     SkinnyArgs hd;
@@ -665,13 +678,14 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
     hd.rms_w = dec_final.as<float>(); hd.rms_eps = T5_EPS; hd.a_scale = out_scale;
     hd.amax_val = ws->part_val.as<float>();
     hd.amax_idx = ws->part_idx.as<int32_t>();
-    int np = 0;
-    MPR_TRY(dec_gemm(hd, pk_lm_head, s, &np));
+    int np = (int)cdiv(V, 16);
+    if (!(skip & 64)) MPR_TRY(dec_gemm(hd, pk_lm_head, s, &np));
     MPR_TRY(trace(TR_HEAD_VAL, t, -1, ws->part_val.ptr, B, np, np, s));
     MPR_TRY(trace(TR_HEAD_IDX, t, -1, ws->part_idx.ptr, B, np, np, s));
-    MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks,
-                        T1, t + 1, eos, pad, shared.as<float>(), d,
-                        t + 1 < max_new ? xp : nullptr, s, ldA));
+    if (!(skip & 128))
+      MPR_TRY(greedy_step(ws->part_val.as<float>(), ws->part_idx.as<int32_t>(), np, B, unf, toks,
+                          T1, t + 1, eos, pad, shared.as<float>(), d,
+                          t + 1 < max_new ? xp : nullptr, s, ldA));
     MPR_TRY(trace(TR_TOKEN, t, -1, toks + t + 1, B, 1, T1, s));
     if (t + 1 < max_new) MPR_TRY(trace(TR_X_NEXT, t, -1, xp, B, d, ldA, s));
   }
