@@ -1036,6 +1036,11 @@ def main():
                          "a group of batches)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    # stdout carries exactly the one JSON line: everything else written to fd 1 (RCCL's version
+    # banner at communicator init, library prints) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1286,7 +1291,7 @@ def main():
             "cpu_baseline": cpu,
             "c5_scan": c5, "c4_projection_1_to_8": c4, "index_build": ib,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
