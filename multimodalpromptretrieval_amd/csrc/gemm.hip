@@ -16,6 +16,9 @@
 // LDS, and T5's RMSNorm of the activation rows is folded into the operand and the epilogue.
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <string>
 
 #include "kernels.h"
 #include "x3.h"
@@ -1478,6 +1481,24 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // tiles on the 128x128 blocks measured 5-15 % slower, profiles/r04_x3p_k32_ab.txt).  (The 64x64 tiles on the ViT fc2,
   // 113.0 us alone, fetched 314 MB per launch from beyond L2 against ~120 MB for 128x128 tiles:
   // r04_v2 PMC.)
+  if (getenv("MPR_GEMM_LOG")) {  // debug: each distinct launch shape once, to stderr
+    static std::mutex mu;
+    static std::set<std::string> seen;
+    std::string key = packed ? "x3p" : "x3";
+    for (int i = 0; i < fam.n; ++i)
+      key += " " + std::to_string(fam.g[i].M) + "x" + std::to_string(fam.g[i].N) + "x" +
+             std::to_string(fam.g[i].K) + (fam.g[i].batch > 1 ? "b" + std::to_string(fam.g[i].batch) : "");
+    std::lock_guard<std::mutex> lk(mu);
+    if (seen.insert(key).second)
+      fprintf(stderr, "[gemm] %s  blocks of 128x128: %lld\n", key.c_str(), (long long)b128);
+  }
+  // (128x256 blocks of 8 waves of 4x1 accumulators — W fragments loaded once per block, half
+  // the vector-memory bytes per MFMA of the 128x128 2x1 tile — ran the ViT qkv 1600x2304x768 x2
+  // in 65.4 against 74.0 us (tools/x3pbench.hip), but 186 VGPRs hold one block per CU and no
+  // serving-loop launch has 192-256 of them (the loop's qkv groups two ViT and two text problems:
+  // 276).  As a rule on 192-256 such blocks it took only predict()'s 800-row fc1 groups (192-200
+  // blocks), with no gain: 4057-4074 vs 4060-4092 QA pairs/s, sync 9.70-9.83 vs 9.65-9.76 ms,
+  // profiles/r06_gemm_tiles.txt.)
   if (fam.n && packed)
     return gemm_launch(fam, b128 > 160 && (max_n >= 2048 || max_k >= 2048) ? X3P_WIDE
                             : max_k >= 2048                                 ? X3P_SMALL3

@@ -9,10 +9,15 @@ stores are an uncalibrated width: see the note in the output).
 
 usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv>
                                    <out.json> [algorithmic_bytes_per_launch]
+       python tools/pmc_traffic.py --sum <dir>   (tools/gemm_pmc.sh's passes p1/ p2/ p3/: every
+       counter's mean per dispatch, the effective clock and the wait / issue shares of wave time)
 """
 import csv
+import glob
 import json
+import os
 import sys
+from collections import defaultdict
 
 
 def per_dispatch(path, counter, by_class=None):
@@ -41,7 +46,39 @@ def per_dispatch(path, counter, by_class=None):
     return [disp[k]["v"] for k in sel]
 
 
+def sum_passes(root):
+    per = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
+    dur = {}
+    for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            d = int(r["Dispatch_Id"])
+            per[r["Counter_Name"]][d] += float(r["Counter_Value"])
+            if "End_Timestamp" in r and r.get("Start_Timestamp"):
+                dur[(f, d)] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+    mean = {c: sum(v.values()) / max(1, len(v)) for c, v in per.items()}
+    for c in sorted(mean):
+        print(f"{c:32s} {mean[c]:16.1f}   ({len(per[c])} dispatches)")
+    if dur:
+        print(f"{'duration_us (profiled)':32s} {sum(dur.values()) / len(dur):16.2f}")
+    g = mean.get("GRBM_GUI_ACTIVE")
+    if g and dur:
+        us = sum(dur.values()) / len(dur)
+        print(f"effective clock GHz (GRBM_GUI_ACTIVE / 8 XCD / duration): {g / 8 / us * 1e-3:.3f}")
+    w, b = mean.get("SQ_WAVE_CYCLES"), mean.get("SQ_BUSY_CYCLES")
+    m = mean.get("SQ_VALU_MFMA_BUSY_CYCLES")
+    if m and b:
+        print(f"MFMA busy / (SQ_BUSY_CYCLES x 4 SIMD x 32 CU per SE...): raw ratio {m / b:.3f}")
+    if w:
+        for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                  "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_LDS"):
+            if c in mean:
+                print(f"{c} / SQ_WAVE_CYCLES = {mean[c] / w:.3f}")
+
+
+
 def main():
+    if sys.argv[1] == "--sum":
+        return sum_passes(sys.argv[2])
     fc, wc = {}, {}
     fetch = per_dispatch(sys.argv[1], "FETCH_SIZE", fc)
     write = per_dispatch(sys.argv[2], "WRITE_SIZE", wc)

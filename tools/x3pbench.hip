@@ -1,6 +1,7 @@
 // x3pbench.hip — the packed-W split-bf16 GEMM (gemm_x3p) against the LDS-staged one (gemm_x3) on
 // the tower shapes: device time per launch (graph of 100 launches) and bitwise equality of the
-// outputs (development aid).
+// outputs (development aid).  usage: x3pbench [shape substring] [variant substring] [launches]
+// (a filtered run of one shape / variant for PMC passes).
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/x3pbench.hip -o tools/x3pbench \
 //          -Lmultimodalpromptretrieval_amd -lmpr -Wl,-rpath,'$ORIGIN/../multimodalpromptretrieval_amd'
 #include <cstdio>
@@ -38,7 +39,10 @@ static double time_graph(hipStream_t s, const std::function<void()>& body, int n
   return ms * 1e3 / n;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const char* fshape = argc > 1 ? argv[1] : "";
+  const char* fvar = argc > 2 ? argv[2] : "";
+  const int nl = argc > 3 ? atoi(argv[3]) : 100;
   hipStream_t s;
   (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   const size_t bytes = 96 << 20;
@@ -99,9 +103,15 @@ int main() {
       {"x3p 64x64 1x1 D3", launch_gemm_x3p_group<64, 64, 1, 1, 3>, true},
       {"x3p 32x64 1x1 D2", launch_gemm_x3p_group<32, 64, 1, 1, 2>, true},
       {"x3p 64x32 1x1 D2", launch_gemm_x3p_group<64, 32, 1, 1, 2>, true},
+      {"x3p 128x128 4x1 D2 SB2 (4w)", launch_gemm_x3p_group<128, 128, 4, 1, 2, 16, 2>, true},
+      {"x3p 128x128 2x2 D2 SB2 (4w)", launch_gemm_x3p_group<128, 128, 2, 2, 2, 16, 2>, true},
+      {"x3p 128x256 2x2 D2 SB2 (8w)", launch_gemm_x3p_group<128, 256, 2, 2, 2, 16, 2>, true},
+      {"x3p 256x128 4x1 D2 SB2 (8w)", launch_gemm_x3p_group<256, 128, 4, 1, 2, 16, 2>, true},
+      {"x3p 128x256 4x1 D2 SB2 (8w)", launch_gemm_x3p_group<128, 256, 4, 1, 2, 16, 2>, true},
   };
 
   for (const Shape& sh : shapes) {
+    if (!strstr(sh.name, fshape)) continue;
     double gf = 2.0 * sh.grp * sh.M * sh.N * sh.K * 1e-9;
     printf("%s x%d (%.2f GFLOP)\n", sh.name, sh.grp, gf);
     const size_t off = 6 << 20;
@@ -111,6 +121,7 @@ int main() {
     std::vector<float> ref((size_t)sh.M * sh.N), got(ref.size());
     bool have_ref = false;
     for (const Var& v : vars) {
+      if (have_ref && !strstr(v.name, fvar)) continue;
       GemmGroup G;
       G.n = sh.grp;
       for (int i = 0; i < sh.grp; ++i) {
@@ -121,7 +132,7 @@ int main() {
         g.wp = v.packed ? (char*)P + i * (size_t)(24 << 20) : nullptr;
       }
       (void)hipMemset(C, 0, bytes);
-      const double us = time_graph(s, [&]() { v.fn(G, s); }, 100);
+      const double us = time_graph(s, [&]() { v.fn(G, s); }, nl);
       (void)hipStreamSynchronize(s);
       (void)hipMemcpy(got.data(), C, got.size() * 4, hipMemcpyDeviceToHost);
       const char* eq = "ref";
