@@ -2,7 +2,9 @@
 train leg (main.py:177-188 under serving.lookahead) with events around the T5 forward, the
 speculative backward (its side stream), predict()'s generate, the next batch's tower pass and
 the optimizer step; prints each phase's start / end relative to the step's start.
-usage: python tools/train_events.py [--eos-first]   (--eos-first: bench.eos_leg runs before)"""
+usage: python tools/train_events.py [--eos-first] [--alone]   (--eos-first: bench.eos_leg runs
+before; --alone: no predict() and no loader lookahead, so the T5 forward / backward / optimizer
+step run with nothing beside them)"""
 import os
 import sys
 import time
@@ -54,9 +56,13 @@ train.T5LossFn.forward = staticmethod(wrap("t5fwd", _fwd))
 opt.step = wrap("opt", opt.step)
 
 
+ALONE = "--alone" in sys.argv
+
+
 def step(b):
     loss = m(b)
-    m.predict(b)
+    if not ALONE:
+        m.predict(b)
     opt.zero_grad()
     loss.backward()
     opt.step()
@@ -66,7 +72,7 @@ def step(b):
 def run(n):
     src = (dict(b, image=b["image"].view_as(b["image"]))
            for b in (batches[i % len(batches)] for i in range(n)))
-    for b in lookahead(src, m):
+    for b in (src if ALONE else lookahead(src, m)):
         step(b)
 
 

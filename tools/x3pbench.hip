@@ -78,6 +78,15 @@ int main(int argc, char** argv) {
       {"odd 1000x1000x1000", 1000, 1000, 1000, 1},   {"odd 77x200x52", 77, 200, 52, 1},
       {"train dW ff 2048x512x1600", 2048, 512, 1600, 1}, {"train dW qkv 1536x512x1600", 1536, 512, 1600, 1},
       {"train qkv 1600x1536x512", 1600, 1536, 512, 1},
+      {"tr o 1440x512x512", 1440, 512, 512, 1},
+      {"tr wo 1440x512x2048", 1440, 512, 2048, 1},
+      {"tr qkv 1440x1536x512", 1440, 1536, 512, 1},
+      {"tr wi 1440x2048x512", 1440, 2048, 512, 1},
+      {"tr dckv 1440x512x6144", 1440, 512, 6144, 1},
+      {"tr dWckv 6144x512x1440", 6144, 512, 1440, 1},
+      {"tr dWwi 2048x512x1440", 2048, 512, 1440, 1},
+      {"tr dWo 512x512x1440", 512, 512, 1440, 1},
+      {"tr dxqkv 1440x512x1536", 1440, 512, 1536, 1},
   };
   using L = std::function<int(const GemmGroup&, hipStream_t)>;
   struct Var { const char* name; L fn; bool packed; };
@@ -87,6 +96,10 @@ int main(int argc, char** argv) {
       {"x3  64x64 k16", launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>, false},
       {"x3  128x128 2x1 k16 prio SB2", launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2, 2>, false},
       {"x3  64x64 k16 SB2", launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1, 0, 2>, false},
+      {"x3  32x64 k16", launch_gemm_x3_group<32, 64, 1, 1, 16, 2, 1>, false},
+      {"x3  64x32 k16", launch_gemm_x3_group<64, 32, 1, 1, 16, 2, 1>, false},
+      {"x3  32x32 k16", launch_gemm_x3_group<32, 32, 1, 1, 16, 2, 1>, false},
+      {"x3  32x64 k16 SB2", launch_gemm_x3_group<32, 64, 1, 1, 16, 2, 1, 0, 2>, false},
       {"x3p 128x128 4x1 D3", launch_gemm_x3p_group<128, 128, 4, 1, 3>, true},
       {"x3p 128x128 2x1 D2 (8w)", launch_gemm_x3p_group<128, 128, 2, 1, 2>, true},
       {"x3p 128x128 2x1 D3 (8w)", launch_gemm_x3p_group<128, 128, 2, 1, 3>, true},
