@@ -397,15 +397,6 @@ int mpr_t5_trainer_trim(mpr_model* trainer, int32_t keep_idle, void* stream);
 int mpr_gemm_f32_splitk(const float* A, int64_t lda, const float* W, int64_t ldw, float* C,
                         int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr,
                         int32_t act, int32_t splits, float* partial, void* stream);
-/* mpr_gemm_kmajor: C [M, N] = A W^T with either operand stored K-major (a_t: A[m, k] at
- * A + k lda + m; w_t: W[n, k] at W + k ldw + n), read in place by the split-bf16 tiles — every
- * result bit equal to transposing the operand first and calling mpr_gemm_f32 (the trainer's
- * dX = dY W and dW = dY^T X without transpose launches).  k_rows (0: K): the k rows a K-major
- * operand stores (rows past it read as zero: K padded to a multiple of 4 for a row-major
- * partner).  splits > 1: as mpr_gemm_f32_splitk (partial: splits x M x N floats). */
-int mpr_gemm_kmajor(const float* A, int64_t lda, int32_t a_t, const float* W, int64_t ldw,
-                    int32_t w_t, int32_t k_rows, float* C, int64_t ldc, int32_t M, int32_t N,
-                    int32_t K, int32_t splits, float* partial, void* stream);
 /* Fixed weights (the CLIP towers', the T5 encoder's and its cross-attention K/V projection) are
  * split once: mpr_pack_x3 writes W [N, K] (row stride ldw) as its three bf16 planes in the
  * matrix-core operand order (mpr_pack_x3_bytes bytes), and a GEMM handed that image loads its W

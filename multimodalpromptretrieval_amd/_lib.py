@@ -123,9 +123,6 @@ SIGNATURES = [
     ("mpr_gemm_f32_splitk", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                       c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
                                       c_int32, c_void_p, c_void_p]),
-    ("mpr_gemm_kmajor", c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_int32,
-                                  c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32, c_void_p,
-                                  c_void_p]),
     ("mpr_pack_x3_bytes", c_int32, [c_int64, c_int64, I64P]),
     ("mpr_pack_x3", c_int32, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
     ("mpr_gemm_f32_packed", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
@@ -320,10 +317,8 @@ def role_stream(device, role: str):
             call("mpr_stream_create", 0, mask, words, ctypes.byref(h))
         else:
             pe, pg = stream_priorities()
-            prio = pe if role.startswith(("encode", "train")) else pg
-            if role == "train:spec" and os.environ.get("MPR_SPEC_PRIO"):
-                prio = int(os.environ["MPR_SPEC_PRIO"])
-            call("mpr_stream_create", prio, None, 0, ctypes.byref(h))
+            call("mpr_stream_create", pe if role.startswith(("encode", "train")) else pg, None,
+                 0, ctypes.byref(h))
     st = torch.cuda.ExternalStream(h.value, device=dev)
     _role_streams[key] = st
     return st

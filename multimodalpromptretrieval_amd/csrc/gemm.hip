@@ -285,12 +285,7 @@ constexpr int x3_lds_floats() {
 // per model, copied into LDS without conversion: +8% on 64x128 tiles, -11% on 128x128 — the
 // planes' 32-byte row segments per k-tile coalesce worse than the 64-byte fp32 ones.)
 // SB = 2: four stages and a block barrier every second K tile, as gemm_x3p_tile's SB.
-// AT / WT: the operand is stored K-major (GemmArgs::a_t / w_t): each thread loads 4 x 4 blocks
-// (four k rows of four consecutive m / n, one 16-byte load each), transposes them in registers
-// and writes the same LDS images as the row-major loads: bit-identical results, no transpose
-// launch (the trainer's dX = dY W and dW = dY^T X).
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0, int SB = 1,
-          bool AT = false, bool WT = false>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0, int SB = 1>
 __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, float* smem_f) {
   static_assert(SB == 1 || (SB == 2 && D % 2 == 0), "SB = 2 needs an even D");
   constexpr int NSTG = 2 * SB, AHEAD = SB + 1;
@@ -316,60 +311,20 @@ __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, 
 
   f32x4 ra[D][LA], rb[D][LB];
   bool oka[D][LA], okb[D][LB];
-  // K-major operands: the tile's float4 cells are taken in 4 x 4 blocks (4 rows x 4 k), four
-  // consecutive threads per block, thread e loading k row 4q + e of the block as one float4
-  // along the rows (rows past the operand's end: scalar loads, clamped); the LDS write scatters
-  // its 4 values to the block's 4 rows (ds_write_b16 x 3 planes).  k past the stored rows reads
-  // the last one and is zeroed at the LDS write (kb: the slot's first k), so no loaded value is
-  // touched before its LDS write.
-  int kb[D];
-  const int kl = a.k_rows > 0 ? min(a.k_rows, K) : K;  // stored k rows of the K-major operands
-  auto tload = [&](const float* base, int64_t ld, int lim, int r0, int kk) -> f32x4 {
-    const float* p = base + (int64_t)min(kk, kl - 1) * ld;
-    if (r0 + 3 < lim) return *reinterpret_cast<const f32x4*>(p + r0);
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = p[min(r0 + e, lim - 1)];
-    return v;
-  };
   auto gload = [&](int j, int k0) {
-    kb[j] = k0;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = m0 + r;
-      if constexpr (AT) {
-        const int qb = idx >> 2, e = idx & 3;  // block (rows 4 (qb / KQ) .., k quad qb % KQ)
-        ra[j][i] = tload(a.A, a.lda, M, m0 + 4 * (qb / KQ), k0 + 4 * (qb % KQ) + e);
-      } else {
-        if constexpr (KT) oka[j][i] = c < K;
-        ra[j][i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
-                                                   min(c, K - 4));
-      }
+      if constexpr (KT) oka[j][i] = c < K;
+      ra[j][i] = *reinterpret_cast<const f32x4*>(a.A + (int64_t)min(row, M - 1) * a.lda +
+                                                 min(c, K - 4));
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT, r = idx / KQ, c = k0 + (idx % KQ) * 4, row = n0 + r;
-      if constexpr (WT) {
-        const int qb = idx >> 2, e = idx & 3;
-        rb[j][i] = tload(a.W, a.ldw, N, n0 + 4 * (qb / KQ), k0 + 4 * (qb % KQ) + e);
-      } else {
-        if constexpr (KT) okb[j][i] = c < K;
-        rb[j][i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
-                                                   min(c, K - 4));
-      }
-    }
-  };
-  // a K-major block's float4 (k row kc of the tile, rows r0 .. r0 + 3) into the LDS planes
-  auto tput = [&](__bf16* base, int r0, int kc, int j, f32x4 v) {
-    if (kb[j] + kc >= kl) v = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x4 h0, h1, h2;
-    split3(v, h0, h1, h2);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      __bf16* p = base + (r0 + e) * LDK + kc;
-      p[0] = h0[e];
-      p[PLANE] = h1[e];
-      p[2 * PLANE] = h2[e];
+      if constexpr (KT) okb[j][i] = c < K;
+      rb[j][i] = *reinterpret_cast<const f32x4*>(a.W + (int64_t)min(row, N - 1) * a.ldw +
+                                                 min(c, K - 4));
     }
   };
   auto put = [&](__bf16* base, int row, int kc, const f32x4& v) {
@@ -386,17 +341,13 @@ __device__ __forceinline__ void gemm_x3_tile(const GemmArgs& a, int bx, int by, 
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int idx = tid + i * NT;
-      if constexpr (AT) tput(base, 4 * ((idx >> 2) / KQ), 4 * ((idx >> 2) % KQ) + (idx & 3), j, ra[j][i]);
-      else if constexpr (KT) put(base, idx / KQ, (idx % KQ) * 4, oka[j][i] ? ra[j][i] : zero);
+      if constexpr (KT) put(base, idx / KQ, (idx % KQ) * 4, oka[j][i] ? ra[j][i] : zero);
       else put(base, idx / KQ, (idx % KQ) * 4, ra[j][i]);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int idx = tid + i * NT;
-      if constexpr (WT)
-        tput(base, BM + 4 * ((idx >> 2) / KQ), 4 * ((idx >> 2) % KQ) + (idx & 3), j, rb[j][i]);
-      else if constexpr (KT)
-        put(base, BM + idx / KQ, (idx % KQ) * 4, okb[j][i] ? rb[j][i] : zero);
+      if constexpr (KT) put(base, BM + idx / KQ, (idx % KQ) * 4, okb[j][i] ? rb[j][i] : zero);
       else put(base, BM + idx / KQ, (idx % KQ) * 4, rb[j][i]);
     }
   };
@@ -570,7 +521,6 @@ __device__ __forceinline__ GemmArgs select_problem(const GemmGroup& grp, int z) 
   a.act = MPR_SEL(act); a.c_rpb = MPR_SEL(c_rpb); a.c_bs = MPR_SEL(c_bs);
   a.batch = MPR_SEL(batch); a.a_bs = MPR_SEL(a_bs); a.w_bs = MPR_SEL(w_bs);
   a.cb_bs = MPR_SEL(cb_bs); a.wp = MPR_SEL(wp);
-  a.a_t = MPR_SEL(a_t); a.w_t = MPR_SEL(w_t); a.k_rows = MPR_SEL(k_rows);
 #undef MPR_SEL
   return a;
 }
@@ -612,8 +562,7 @@ int launch_gemm_group(const GemmGroup& g, hipStream_t s) {
 // by the largest problem instead (blockIdx.z per problem) leaves the small problems' slices
 // mostly empty, and the remap then gives whole XCDs nothing to do (the tower launches' text
 // problems: fc2 231 -> see DESIGN §3).
-template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0, int SB = 1,
-          bool AT = false, bool WT = false>
+template <int BM, int BN, int WM, int WN, int BK, int D, int KW, bool KT, int V = 0, int SB = 1>
 __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void gemm_x3_kernel(
     const GemmGroup grp) {
   __shared__ __attribute__((aligned(16))) float smem[x3_lds_floats<BM, BN, BK, SB>()];
@@ -670,7 +619,7 @@ __global__ __launch_bounds__(64 * (BM / (32 * WM)) * (BN / (32 * WN)) * KW) void
     bx = tt / rem;
     by = full + (tt - bx * rem);
   }
-  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT, V, SB, AT, WT>(a, bx, by, smem);
+  gemm_x3_tile<BM, BN, WM, WN, BK, D, KW, KT, V, SB>(a, bx, by, smem);
 }
 
 // KT when some K % BK != 0 or cdiv(K, BK) % D != 0
@@ -686,20 +635,13 @@ int launch_gemm_x3_group(const GemmGroup& g, hipStream_t s) {
     kt = kt || g.g[i].K % BK != 0 || cdiv(g.g[i].K, BK) % D != 0;
   }
   if (tiles == 0) return MPR_OK;
-  // operand layouts are uniform over a launch (gemm_group checks): K-major A and W (the
-  // trainer's dW = dY^T X), K-major W (dX = dY W), or row-major both; a K-major operand masks
-  // its own K tail (kt) per element
-  const int at = g.g[0].a_t, wt = g.g[0].w_t;
-  if (at || wt) kt = true;
-#define MPR_X3L(KTV, ATV, WTV)                                                                \
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, KTV, V, SB, ATV, WTV>),        \
-                     dim3((unsigned)tiles), dim3(NT), 0, s, g)
-  if (at && wt) MPR_X3L(true, true, true);
-  else if (wt) MPR_X3L(true, false, true);
-  else if (at) MPR_X3L(true, true, false);
-  else if (kt) MPR_X3L(true, false, false);
-  else MPR_X3L(false, false, false);
-#undef MPR_X3L
+  if (kt)
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, true, V, SB>),
+                       dim3((unsigned)tiles), dim3(NT), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, BK, D, KW, false, V, SB>),
+                       dim3((unsigned)tiles),
+                       dim3(NT), 0, s, g);
   MPR_LAUNCHED();
   return MPR_OK;
 }
@@ -1475,22 +1417,9 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
     const GemmArgs& a = g.g[i];
     MPR_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N,
                 a.K);
-    MPR_REQUIRE(a.a_t == g.g[0].a_t && a.w_t == g.g[0].w_t,
-                "gemm_group: operand layouts differ within one launch");
-    if (a.a_t || a.w_t) {
-      MPR_REQUIRE(!g_gemm_f32 && !a.wp && (a.a_t || (a.K % 4 == 0 && a.lda % 4 == 0 &&
-                                                      aligned16(a.A))) &&
-                      (a.w_t || (a.K % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.W))) &&
-                      (!a.a_t || a.lda >= a.M) && (!a.w_t || a.ldw >= a.N) &&
-                      a.k_rows >= 0 && a.k_rows <= a.K,
-                  "gemm: K-major operands need the split-bf16 LDS-staged kernel (no MPR_GEMM=f32, "
-                  "no packed W), ld >= the operand's rows, a row-major operand's K / ld multiples "
-                  "of 4 (M=%d N=%d K=%d)", a.M, a.N, a.K);
-    } else {
-      MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
-                      aligned16(a.W),
-                  "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
-    }
+    MPR_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && a.ldw % 4 == 0 && aligned16(a.A) &&
+                    aligned16(a.W),
+                "gemm: K/lda/ldw must be multiples of 4 and A/W 16-byte aligned (K=%d)", a.K);
     MPR_REQUIRE(a.batch >= 1 && (a.batch == 1 || (!a.R && !a.c_rpb && a.a_bs % 4 == 0 &&
                                                    a.w_bs % 4 == 0)),
                 "gemm: batch %d needs no residual / row batching and 16-byte batch strides",

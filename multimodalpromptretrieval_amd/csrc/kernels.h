@@ -36,17 +36,7 @@ struct GemmArgs {
   // Optional packed split image of W (pack_x3): the split-bf16 kernel then loads its W operand
   // fragments straight into registers instead of staging W through LDS (results identical).
   const void* wp = nullptr;
-  // K-major operands (split-bf16 LDS-staged kernel only): a_t — A[m, k] at A + k lda + m; w_t —
-  // W[n, k] at W + k ldw + n.  The tiles read them down the k rows and write the same LDS images
-  // as row-major operands, so every result bit equals a transpose + GEMM's.  k_rows (0: K): the
-  // k rows a K-major operand stores; rows past it read as zero (a K padded for the row-major one).
-  int a_t = 0, w_t = 0;
-  int k_rows = 0;
 };
-// gemm() with K split into `splits` chunks (partials [splits, M, N] in `partial`, summed in chunk
-// order by one reduce launch, then act and R): the trainer's few-tile long-K products
-// (train.hip; any operand layout).
-int gemm_splitk(const GemmArgs& a, int splits, float* partial, hipStream_t s);
 
 int gemm(const GemmArgs& a, hipStream_t s);
 

@@ -626,68 +626,6 @@ TrainAttn make_attn(const float* q, int64_t q_bs, int64_t q_rs, const float* k, 
 }
 
 }  // namespace
-
-// K chunks of `kc` (a multiple of every BK) side by side as one strided batch (the split-bf16
-// kernels sum every chunk in the same order alone or batched), or one problem per chunk
-// (MPR_GEMM=f32); then the partials' reduce in chunk order with act and R.  A K-major operand
-// steps its chunks down its k rows (k0 ld); its stored rows (k_rows) are cut per chunk.
-int gemm_splitk(const GemmArgs& a0, int splits, float* partial, hipStream_t s) {
-  const int M = a0.M, N = a0.N, K = a0.K;
-  MPR_REQUIRE(a0.act == ACT_NONE || a0.act == ACT_RELU, "gemm: act %d (none or relu)", a0.act);
-  MPR_REQUIRE(splits >= 1 && splits <= 64 && partial, "gemm_splitk: splits=%d", splits);
-  MPR_REQUIRE(M >= 0 && N >= 0 && K > 0, "gemm_splitk: bad shape M=%d N=%d K=%d", M, N, K);
-  MPR_REQUIRE(!a0.bias && !a0.c_rpb && a0.batch == 1 && !a0.wp, "gemm_splitk: plain problems");
-  if (M == 0 || N == 0) return MPR_OK;
-  const int kc = (int)cdiv(cdiv(K, splits), 32) * 32;
-  const int full = K / kc, rem = K - full * kc, used = full + (rem > 0);
-  const int64_t sa = a0.a_t ? a0.lda : 1, sw = a0.w_t ? a0.ldw : 1;  // k step of each operand
-  const int kr = a0.k_rows > 0 ? a0.k_rows : K;
-  GemmGroup g;
-  g.n = 0;
-  auto chunk = [&](int k0, int kk, int nb) -> int {
-    GemmArgs& a = g.g[g.n++];
-    a = GemmArgs();
-    a.A = a0.A + k0 * sa; a.lda = a0.lda; a.W = a0.W + k0 * sw; a.ldw = a0.ldw;
-    a.a_t = a0.a_t; a.w_t = a0.w_t;
-    if (a0.a_t || a0.w_t) {
-      MPR_REQUIRE(kr - k0 >= 1, "gemm_splitk: a chunk past the K-major operand's rows");
-      if (kr - k0 < kk) {
-        MPR_REQUIRE(nb == 1, "gemm_splitk: a short chunk inside the batch");
-        a.k_rows = kr - k0;
-      }
-    }
-    a.C = partial + (int64_t)(k0 / kc) * M * N; a.ldc = N;
-    a.M = M; a.N = N; a.K = kk;
-    a.batch = nb; a.a_bs = kc * sa; a.w_bs = kc * sw; a.cb_bs = (int64_t)M * N;
-    return MPR_OK;
-  };
-  // the chunks whose K-major rows are all stored go as one batch; a chunk cut by k_rows alone
-  const int whole = (a0.a_t || a0.w_t) ? std::min(full, (int)std::max<int64_t>(0, kr / kc)) : full;
-  if (gemm_uniform_order()) {
-    if (whole) MPR_TRY(chunk(0, kc, whole));
-    for (int c = whole; c < used; ++c) {
-      MPR_TRY(chunk(c * kc, std::min(kc, K - c * kc), 1));
-      if (g.n == GEMM_GROUP) {
-        MPR_TRY(gemm_group(g, s));
-        g.n = 0;
-      }
-    }
-    if (g.n) MPR_TRY(gemm_group(g, s));
-  } else {
-    for (int c = 0; c < used; ++c) {
-      MPR_TRY(chunk(c * kc, std::min(kc, K - c * kc), 1));
-      if (g.n == GEMM_GROUP || c == used - 1) {
-        MPR_TRY(gemm_group(g, s));
-        g.n = 0;
-      }
-    }
-  }
-  const int64_t n = (int64_t)M * N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, partial,
-                     used, M, N, a0.act, a0.R, a0.ldr, a0.C, a0.ldc);
-  MPR_LAUNCHED();
-  return MPR_OK;
-}
 }  // namespace mpr
 
 using namespace mpr;
@@ -770,22 +708,40 @@ int mpr_gemm_f32_splitk(const float* A, int64_t lda, const float* W, int64_t ldw
                         int64_t ldc, int32_t M, int32_t N, int32_t K, const float* R, int64_t ldr,
                         int32_t act, int32_t splits, float* partial, void* stream) {
   return guarded_call([&]() -> int {
-    GemmArgs g;
-    g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.C = C; g.ldc = ldc;
-    g.M = M; g.N = N; g.K = K; g.R = R; g.ldr = ldr; g.act = act;
-    return gemm_splitk(g, splits, partial, S(stream));
-  });
-}
-
-int mpr_gemm_kmajor(const float* A, int64_t lda, int32_t a_t, const float* W, int64_t ldw,
-                    int32_t w_t, int32_t k_rows, float* C, int64_t ldc, int32_t M, int32_t N,
-                    int32_t K, int32_t splits, float* partial, void* stream) {
-  return guarded_call([&]() -> int {
-    GemmArgs g;
-    g.A = A; g.lda = lda; g.a_t = a_t; g.W = W; g.ldw = ldw; g.w_t = w_t; g.k_rows = k_rows;
-    g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
-    if (splits > 1) return gemm_splitk(g, splits, partial, S(stream));
-    return gemm(g, S(stream));
+    MPR_REQUIRE(act == ACT_NONE || act == ACT_RELU, "gemm: act %d (none or relu)", act);
+    MPR_REQUIRE(splits >= 1 && splits <= 64 && partial, "gemm_splitk: splits=%d", splits);
+    MPR_REQUIRE(M >= 0 && N >= 0 && K > 0, "gemm_splitk: bad shape M=%d N=%d K=%d", M, N, K);
+    if (M == 0 || N == 0) return MPR_OK;
+    const int kc = (int)cdiv(cdiv(K, splits), 32) * 32;  // chunk: a multiple of every BK
+    const int full = K / kc, rem = K - full * kc, used = full + (rem > 0);
+    GemmGroup g;
+    g.n = 0;
+    auto chunk = [&](int k0, int kk, int nb) {
+      GemmArgs& a = g.g[g.n++];
+      a = GemmArgs();
+      a.A = A + k0; a.lda = lda; a.W = W + k0; a.ldw = ldw;
+      a.C = partial + (int64_t)(k0 / kc) * M * N; a.ldc = N;
+      a.M = M; a.N = N; a.K = kk;
+      a.batch = nb; a.a_bs = kc; a.w_bs = kc; a.cb_bs = (int64_t)M * N;
+    };
+    if (gemm_uniform_order()) {  // the full chunks as one strided batch, one launch
+      if (full) chunk(0, kc, full);
+      if (rem) chunk(full * kc, rem, 1);
+      MPR_TRY(gemm_group(g, S(stream)));
+    } else {
+      for (int c = 0; c < used; ++c) {
+        chunk(c * kc, std::min(kc, K - c * kc), 1);
+        if (g.n == GEMM_GROUP || c == used - 1) {
+          MPR_TRY(gemm_group(g, S(stream)));
+          g.n = 0;
+        }
+      }
+    }
+    const int64_t n = (int64_t)M * N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(stream),
+                       partial, used, M, N, act, R, ldr, C, ldc);
+    MPR_LAUNCHED();
+    return MPR_OK;
   });
 }
 

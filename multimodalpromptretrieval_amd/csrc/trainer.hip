@@ -186,33 +186,16 @@ struct T5Trainer : mpr_model {
     if (tiles >= 128 || K < 1024) return 1;
     return (int)std::max<int64_t>(1, std::min<int64_t>({16, cdiv(256, tiles), K / 256}));
   }
-  // C [M, N] = act(A [M, K] (row stride lda) W [N, K]^T (row stride ldw)) + R (row stride N);
-  // at / wt: that operand stored K-major (A[m, k] at A + k lda + m; W likewise), read in place by
-  // the split-bf16 tiles (GemmArgs::a_t / w_t; bit-identical to transposing it first); k_rows:
-  // the K-major operand's stored k rows when K is padded for the other
+  // C [M, N] = act(A [M, K] (row stride lda) W [N, K]^T (row stride ldw)) + R (row stride N)
   int gemm(Arena& ar, const float* A, int64_t lda, const float* W, int64_t ldw, float* C, int M,
-           int N, int K, const float* R = nullptr, int act = 0, int at = 0, int wt = 0,
-           int k_rows = 0) {
-    GemmArgs g;
-    g.A = A; g.lda = lda; g.W = W; g.ldw = ldw; g.C = C; g.ldc = N;
-    g.M = M; g.N = N; g.K = K; g.R = R; g.ldr = R ? N : 0; g.act = act;
-    g.a_t = at; g.w_t = wt; g.k_rows = k_rows;
+           int N, int K, const float* R = nullptr, int act = 0) {
     const int sp = splits(M, N, K);
     if (sp > 1) {
       float* part = ar.get((int64_t)sp * M * N);
       MPR_REQUIRE(part, "trainer: out of device memory");
-      return gemm_splitk(g, sp, part, s);
+      return mpr_gemm_f32_splitk(A, lda, W, ldw, C, N, M, N, K, R, R ? N : 0, act, sp, part, s);
     }
-    return mpr::gemm(g, s);
-  }
-  // the backward reads its K-major operands in place (no transpose launches) unless the tiles
-  // cannot (MPR_GEMM=f32) or MPR_TRAIN_KMAJOR=0 (A/B)
-  static bool kmajor() {
-    static const bool on = [] {
-      const char* e = getenv("MPR_TRAIN_KMAJOR");
-      return !(e && e[0] == '0');
-    }();
-    return on && gemm_uniform_order();
+    return mpr_gemm_f32(A, lda, W, ldw, C, N, M, N, K, R, R ? N : 0, act, s);
   }
   static int64_t r4(int64_t n) { return (n + 3) / 4 * 4; }
   // x [r, c] (row stride ld) -> [c, r4]
@@ -222,19 +205,13 @@ struct T5Trainer : mpr_model {
     return out;
   }
   // y = x W^T (x [M, K] row stride ldx, W [N, K]): dx (+)= dy W, dW = dy^T x (dy row stride ldy)
-  // (k_valid: dy's valid columns when N is padded to a multiple of 4 — the tied lm_head, V)
+  // (Measured and reverted, round 6: the split-bf16 tiles reading dy / x / W K-major in place —
+  // bit-identical, no transpose launches — as four scalar loads per float4 or as 4 x 4 blocks
+  // scattered into LDS: the GEMMs' own time rose 0.85-1.6 ms per step against ~0.3 ms of
+  // transposes saved; git show 49e0c84, profiles/r06_train_kmajor_ab.txt.)
   int linear_bwd(Arena& ar, const float* x, int64_t ldx, const float* W, int N, int K, int M,
                  const float* dy, int64_t ldy, float* dx, bool dx_acc, float* dW,
-                 const float* xt = nullptr, int n_valid = 0) {
-    if (kmajor()) {
-      // dW [N, K] = dy^T x: both operands K-major (rows of the product run over M)
-      if (dW) MPR_TRY(gemm(ar, dy, ldy, x, ldx, dW, n_valid ? n_valid : N, K, M, nullptr, 0, 1, 1));
-      // dx [M, K] = dy W: W K-major, its N rows (n_valid of them stored) along the product's k
-      if (dx)
-        MPR_TRY(gemm(ar, dy, ldy, W, K, dx, M, K, N, dx_acc ? dx : nullptr, 0, 0, 1,
-                     n_valid ? n_valid : 0));
-      return MPR_OK;
-    }
+                 const float* xt = nullptr) {
     if (dW) {
       const float* dyt = transpose(ar, dy, M, N, ldy);
       const float* xT = xt ? xt : transpose(ar, x, M, K, ldx);
@@ -477,10 +454,8 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
   const int64_t V4 = r4(V);
   auto want = [&](int i) { return grads[i] != nullptr; };
   // stacked-weight gradient: rows j * n .. of C [ids.size() * n, K] -> grads[ids[j]]
-  // (At / Wt: the transposed operands [., r4(Kc)], or with kt the K-major originals, row
-  // strides lda / ldw)
   auto stacked_dw = [&](const std::vector<int>& ids, int n, const float* At, const float* Wt,
-                        int K, int Kc, int kt = 0, int64_t lda = 0, int64_t ldw = 0) -> int {
+                        int K, int Kc) -> int {
     bool any = false, adjacent = true;
     for (size_t j = 0; j < ids.size(); ++j) {
       any = any || want(ids[j]);
@@ -488,11 +463,9 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
     }
     if (!any) return MPR_OK;
     const int M = (int)ids.size() * n;
-    const int64_t la = kt ? lda : r4(Kc), lw = kt ? ldw : r4(Kc);
-    const int kk = kt ? Kc : (int)r4(Kc);
-    if (adjacent) return gemm(ar, At, la, Wt, lw, grads[ids[0]], M, K, kk, nullptr, 0, kt, kt);
+    if (adjacent) return gemm(ar, At, r4(Kc), Wt, r4(Kc), grads[ids[0]], M, K, (int)r4(Kc));
     TR_GET(C, (int64_t)M * K);
-    MPR_TRY(gemm(ar, At, la, Wt, lw, C, M, K, kk, nullptr, 0, kt, kt));
+    MPR_TRY(gemm(ar, At, r4(Kc), Wt, r4(Kc), C, M, K, (int)r4(Kc)));
     std::vector<CopySeg> segs;
     for (size_t j = 0; j < ids.size(); ++j)
       if (want(ids[j])) segs.push_back({C + j * (int64_t)n * K, grads[ids[j]], (int64_t)n * K});
@@ -508,11 +481,6 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
     MPR_TRY(attn_bwd(ar, qkv, 3 * I, qkv + I, 3 * I, qkv + 2 * I, 3 * I, Pm, da, B, Lx, Lx, drel,
                      R, dr, st, dqkv, 3 * I, dqkv + I, 3 * I, dqkv + 2 * I, 3 * I));
     const bool wdw = want(ids[0]) || want(ids[1]) || want(ids[2]);
-    if (kmajor()) {  // dn = dqkv Wqkv (Wqkv K-major), dW = dqkv^T n1 (both K-major)
-      MPR_TRY(gemm(ar, dqkv, 3 * I, Wqkv, d, dn, M, d, 3 * I, nullptr, 0, 0, 1));
-      if (wdw) MPR_TRY(stacked_dw(ids, I, dqkv, n1, d, M, 1, 3 * I, d));
-      return MPR_OK;
-    }
     const float* WqkvT = transpose(ar, Wqkv, 3 * I, d, d);
     const float* dT = wdw ? transpose(ar, dqkv, M, 3 * I, 3 * I) : nullptr;
     const float* xT = wdw ? transpose(ar, n1, M, d, d) : nullptr;
@@ -530,10 +498,7 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
   // lm_head (tied): logits = hs shared^T; its weight gradient opens the tied gradient
   float* d_shared = grads[0];
   TR_GET(dhs, (int64_t)Md * d);
-  MPR_TRY(kmajor() ? linear_bwd(ar, tp.hs, d, shared(), (int)V4, d, Md, dlogits, V4, dhs, false,
-                                d_shared, nullptr, V)
-                   : linear_bwd(ar, tp.hs, d, shared(), V, d, Md, dlogits, V4, dhs, false,
-                                d_shared));
+  MPR_TRY(linear_bwd(ar, tp.hs, d, shared(), V, d, Md, dlogits, V4, dhs, false, d_shared));
   TR_GET(dg, (int64_t)Md * d);  // the decoder's gradient chain, updated in place layer by layer
   {
     const float* g = dmask(ar, dhs, (int64_t)Md * d, dr, site(1, 255, D_FINAL));
@@ -611,18 +576,12 @@ int T5Trainer::backward(Tape& tp, const float* dloss, float grad_scale, const in
       any = any || want(dp(l, 7)) || want(dp(l, 8));
     }
     d_enc = ar.get((int64_t)Me * d);
-    MPR_REQUIRE(d_enc, "trainer: out of device memory");
-    if (kmajor()) {  // d_enc = dckv Wckv (Wckv K-major), dW = dckv^T enc_out (both K-major)
-      MPR_TRY(gemm(ar, dckv, ckv_ld, tp.Wckv, d, d_enc, Me, d, (int)ckv_ld, nullptr, 0, 0, 1));
-      if (any) MPR_TRY(stacked_dw(ids, I, dckv, tp.enc_out, d, Me, 1, ckv_ld, d));
-    } else {
     const float* WckvT = transpose(ar, tp.Wckv, ckv_ld, d, d);
     const float* dT = any ? transpose(ar, dckv, Me, ckv_ld, ckv_ld) : nullptr;
     const float* xT = any ? transpose(ar, tp.enc_out, Me, d, d) : nullptr;
     MPR_REQUIRE(d_enc && WckvT && (!any || (dT && xT)), "trainer: out of device memory");
     MPR_TRY(gemm(ar, dckv, ckv_ld, WckvT, ckv_ld, d_enc, Me, d, (int)ckv_ld));
     if (any) MPR_TRY(stacked_dw(ids, I, dT, xT, d, Me));
-    }
   } else {
     d_enc = ar.get((int64_t)Me * d);
     MPR_REQUIRE(d_enc, "trainer: out of device memory");

@@ -99,63 +99,3 @@ def test_packed_weight_gemm_is_bit_identical(device, M, N, K, act, res):
               N, M, N, K, _lib.ptr(R), N if R is not None else 0, act, _lib.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(C, ref)
-
-
-def _kmajor(A_km, lda, at, W_km, ldw, wt, M, N, K, k_rows=0, splits=1):
-    C = torch.empty(M, N, device=A_km.device)
-    part = torch.empty(max(splits, 1) * M * N, device=A_km.device) if splits > 1 else None
-    _lib.call("mpr_gemm_kmajor", _lib.ptr(A_km), lda, at, _lib.ptr(W_km), ldw, wt, k_rows,
-              _lib.ptr(C), N, M, N, K, splits, _lib.ptr(part), _lib.stream_ptr())
-    torch.cuda.synchronize()
-    return C
-
-
-@pytest.mark.parametrize("M,N,K,at,wt,splits", [
-    (2048, 512, 1440, 1, 1, 1),    # the trainer's dW = dY^T X (FFN-in), 64x64 tiles
-    (1536, 512, 1424, 1, 1, 1),    # stacked q|k|v weight gradient
-    (6144, 512, 1440, 1, 1, 1),    # stacked cross k|v weight gradient (128x128 tiles)
-    (1440, 512, 6144, 0, 1, 1),    # dX = dY W over the cross k|v (long K)
-    (1440, 2048, 512, 0, 1, 1),    # dX of the FFN-out
-    (512, 512, 1440, 1, 1, 4),     # split-K, both K-major
-    (96, 160, 1000, 0, 1, 3),      # split-K, W K-major
-    (77, 200, 52, 1, 0, 1),        # ragged, A K-major
-    (77, 200, 53, 1, 1, 1),        # K-major both: K need not be a multiple of 4
-    (1000, 1000, 1000, 1, 1, 1),   # odd tile counts
-])
-def test_kmajor_operands_bit_identical(device, M, N, K, at, wt, splits):
-    """mpr_gemm_kmajor reads K-major operands in place (4 k-row loads per float4, transposed in
-    registers): the same LDS images, hence the same bits, as transposing them and calling the
-    row-major GEMM; leading dimensions past the rows are honoured."""
-    A, W = _operands(M, N, K, 11 * M + N + K)
-    Ad, Wd = A.to(device), W.to(device)
-    Kp = (K + 3) // 4 * 4
-    if Kp != K:  # the row-major reference needs K % 4 == 0: zero-pad both (exact zeros added)
-        Ad = torch.nn.functional.pad(Ad, (0, Kp - K))
-        Wd = torch.nn.functional.pad(Wd, (0, Kp - K))
-    ref = _gemm(Ad, Wd, splits=splits)
-    # K-major copies with a padded leading dimension (ld = rows + 8)
-    A_km = torch.zeros(K, M + 8, device=device)
-    A_km[:, :M] = A.to(device).t()
-    W_km = torch.zeros(K, N + 8, device=device)
-    W_km[:, :N] = W.to(device).t()
-    Aop, lda = (A_km, M + 8) if at else (Ad, Kp)
-    Wop, ldw = (W_km, N + 8) if wt else (Wd, Kp)
-    got = _kmajor(Aop, lda, at, Wop, ldw, wt, M, N, Kp if not (at and wt) else K, splits=splits)
-    assert torch.equal(got, ref), float((got - ref).abs().max())
-
-
-@pytest.mark.parametrize("splits", [1, 16])
-def test_kmajor_stored_rows_pad_zero(device, splits):
-    """The tied lm_head's input gradient: dX [32, 512] = dlogits [32, V4] (zero columns past V)
-    times the embedding [V, 512] read K-major with only V rows stored (k_rows = V): equal to the
-    row-major product with the embedding's transpose zero-padded to V4 columns."""
-    V, V4, d, Md = 32101, 32104, 512, 32
-    g = torch.Generator(device="cpu").manual_seed(3)
-    dl = torch.randn(Md, V4, generator=g)
-    dl[:, V:] = 0
-    emb = torch.randn(V, d, generator=g)
-    wt_pad = torch.zeros(d, V4)
-    wt_pad[:, :V] = emb.t()
-    ref = _gemm(dl.to(device), wt_pad.to(device), splits=splits)
-    got = _kmajor(dl.to(device), V4, 0, emb.to(device), d, 1, Md, d, V4, k_rows=V, splits=splits)
-    assert torch.equal(got, ref)
