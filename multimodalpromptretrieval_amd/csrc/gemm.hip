@@ -1367,7 +1367,7 @@ const bool g_x3_sb1 = [] {
 }();
 const bool g_x3p_sb1 = [] {
   const char* e = getenv("MPR_X3P_SB");
-  return e && e[0] == '1';
+  return !(e && e[0] == '2');
 }();
 
 int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
@@ -1398,7 +1398,12 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
       case X3_SMALL: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1>(g, s);
       case X3_WIDE_SB2: return launch_gemm_x3_group<128, 128, 2, 1, 16, 2, 1, 2, 2>(g, s);
       case X3_SMALL_SB2: return launch_gemm_x3_group<64, 64, 1, 1, 16, 2, 1, 0, 2>(g, s);
-      case X3P_WIDE:  // four A stages, a barrier every second K tile (MPR_X3P_SB=1: every tile)
+      // two A stages and a barrier every K tile (36.9 KB of LDS); MPR_X3P_SB=2: four stages, a
+      // barrier every second tile (73.7 KB).  Replayed alone the four-stage form is ~1 % faster
+      // (0.882 vs 0.874 of fp32 peak), but in the serving loop the two-stage blocks leave LDS for
+      // the decode chain's blocks beside them: 4,156-4,195 vs 4,066-4,153 QA pairs/s over 5 / 4
+      // alternating runs, in-loop GEMM frac 0.68 vs 0.66 (round 6, profiles/r06_loop_interference.txt)
+      case X3P_WIDE:
         return g_x3p_sb1 ? launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s)
                          : launch_gemm_x3p_group<128, 128, 2, 1, 2, 16, 2>(g, s);
       case X3P_SMALL: return launch_gemm_x3p_group<64, 64, 1, 1, 2>(g, s);
@@ -1586,6 +1591,9 @@ void launch_skinny(const SkinnyArgs& sa, int F, unsigned grid, hipStream_t s, un
 // (Measured and dropped: capping encoder GEMM blocks at 2-3 per CU by LDS padding and running
 // the K = 2048 GEMV in 43.5 KB passes, so a decode block always fits beside resident encoder
 // blocks, made the two-decodes-in-flight serving loop 1-6% slower.)
+// (Measured and dropped, round 6: the grouped-decode GEMVs in 2-chunk passes — 37 KB of LDS
+// slabs instead of 70 KB, so a decode block sits beside more tower blocks — 3,899-4,163 vs
+// 4,165-4,173 QA pairs/s, profiles/r06_loop_interference.txt.)
 int gemm_skinny(const SkinnyArgs& sa, hipStream_t s) {
   const GemmArgs& a = sa.g;
   MPR_REQUIRE(a.M >= 0 && a.M <= 256 && a.N >= 0 && a.K > 0, "gemm_skinny: bad shape M=%d", a.M);
