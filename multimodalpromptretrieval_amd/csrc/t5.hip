@@ -665,6 +665,11 @@ int T5Model::decode_body_folded(int B, int L, int max_new, int eos, int pad, hip
       if (!(skip & 16)) MPR_TRY(dec_gemm(cw, ly.pk_cowi, s));
       MPR_TRY(trace(TR_COWI, t, l, hz, B, d + dff, ldZ, s));
       MPR_TRY(trace(TR_X2SS, t, l, x2ss, B, d / 16, d / 16, s));
+      // (Measured and dropped, round 6: the FFN-out with K split over twice the blocks, its two
+      // partials summed into the residual stream by the next reader (the next layer's q|k|v, which
+      // stored x3, or the head) — tokens unchanged, 16-row step 207-215 vs 211-216 us, but the
+      // serving loop's 128-row step 487 vs 434 us: the readers' extra partial loads cost more
+      // than the split saves; profiles/r06_decode_chain_parts.txt.)
       SkinnyArgs fo;  // x3 = x2 + (relu(z) Wwo^T) / rms_scale(x2), into the x half of [a | x]
       fo.g.A = hz + d; fo.g.lda = ldZ; fo.g.R = hz; fo.g.ldr = ldZ;
       fo.g.C = xp; fo.g.ldc = ldA; fo.g.M = B; fo.g.N = d; fo.g.K = dff;
