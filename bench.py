@@ -42,6 +42,7 @@ sys.path.insert(0, ROOT)
 
 from multimodalpromptretrieval_amd import _lib  # noqa: E402
 from multimodalpromptretrieval_amd import synthetic as syn  # noqa: E402
+from multimodalpromptretrieval_amd import serving  # noqa: E402
 from multimodalpromptretrieval_amd.serving import lookahead, pipelined  # noqa: E402
 from multimodalpromptretrieval_amd.tokenization import SpmT5Tokenizer, clip_tokenize  # noqa: E402
 
@@ -1250,7 +1251,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "pipelining": f"serving loop (predict_many): next batch's towers + scan enqueued "
-                          f"ahead, {os.environ.get('MPR_DECODE_GROUP', '8')} batches per decode "
+                          f"ahead, {serving.ServingOptions.resolve().decode_group} batches per decode "
                           f"loop, {args.inflight} generate calls in flight; ramp-up and drain "
                           f"inside the timed steps; warmup: {args.warmup} steps per leg plus one "
                           f"untimed serving-loop pass of {args.steps} steps over the warmup "

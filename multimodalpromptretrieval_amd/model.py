@@ -522,7 +522,7 @@ class T5VisionModel(nn.Module):
                      eos_stop=None, _loop_out=None):
         """predict() over an iterable of batches as a serving pipeline.  A greedy decode is a
         chain of small latency-bound launches that leaves most of the chip idle, so
-        (1) ``decode_group`` (1-8, default MPR_DECODE_GROUP or 8; ``pair_decodes`` = False / True
+        (1) ``decode_group`` (1-16, default MPR_DECODE_GROUP or 12; ``pair_decodes`` = False / True
         is 1 / 2) consecutive batches share one decode loop: each is encoded as predict() would,
         then their rows step together, reading every decode weight once per step for all
         (mpr_t5_generate_batches);

@@ -35,7 +35,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from .t5 import length_pieces, pieces_per_call
+from .t5 import MAX_PIECES, length_pieces, pieces_per_call
 
 
 @dataclass(frozen=True)
@@ -63,7 +63,12 @@ class ServingOptions:
             elif env("MPR_PAIR_DECODE") == "0":
                 decode_group = 1
             else:
-                decode_group = int(env("MPR_DECODE_GROUP", "8"))
+                # 12 batches (192 rows) per decode loop: the per-row decode cost falls with the
+                # rows, so the loop's decodes take fewer CU slots from the tower GEMMs beside them
+                # (in-loop GEMM frac 0.69 -> 0.73); 16 leaves a long drain in a 20-step window.
+                # 20-step bench, alternating: 12 vs 8 won 5 of 5 pairs (+1.2 % mean), 16 lost 4 %
+                # (round 6, profiles/r06_loop_interference.txt)
+                decode_group = int(env("MPR_DECODE_GROUP", "12"))
         if lookahead is None:
             lookahead = env("MPR_LOOKAHEAD", "1") != "0"
         if tower_batches is None:
@@ -71,7 +76,7 @@ class ServingOptions:
         if tower_slots is None:
             tower_slots = int(env("MPR_TOWER_SLOTS", "1"))
         return ServingOptions(depth=max(1, min(int(decodes_in_flight), 4)),
-                              decode_group=max(1, min(int(decode_group), 8)),
+                              decode_group=max(1, min(int(decode_group), MAX_PIECES)),
                               lookahead=bool(lookahead),
                               tower_batches=max(1, min(int(tower_batches), 2)),
                               tower_slots=max(1, min(int(tower_slots),
