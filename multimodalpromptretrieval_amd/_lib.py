@@ -284,7 +284,11 @@ def separate_decode_stream(idx: int) -> bool:
     return bool(decode_cus(idx))
 
 
-PIPELINE_ROLES = ("encode:towers", "gen:0", "gen:1", "train:spec")
+# Created eagerly in this order (ensure_device).  The index build's second tower slot is made
+# second: created on first use it landed beside the first slot and the build ran at 8,530-9,040
+# rows/s against 10,470-11,300 with it here; training and serving unchanged (same-box A/Bs,
+# profiles/r06_stream_roles.txt).
+PIPELINE_ROLES = ("encode:towers", "encode:towers1", "train:spec", "gen:0", "gen:1")
 
 
 def role_stream(device, role: str):
@@ -342,7 +346,8 @@ def ensure_device(device) -> None:
         # loop's answers changed more often; the cause was packed-FP32 results corrupted beside
         # other kernels' MFMA waves, fixed by building without packed FP32 ops)
         if os.environ.get("MPR_EAGER_STREAMS", "1") == "1":
-            for role in PIPELINE_ROLES:
+            order = os.environ.get("MPR_EAGER_ORDER")  # A/B of the creation order
+            for role in (order.split(",") if order else PIPELINE_ROLES):
                 role_stream(torch.device("cuda", idx), role)
 
 
