@@ -11,6 +11,12 @@ usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter
                                    <out.json> [algorithmic_bytes_per_launch]
        python tools/pmc_traffic.py --sum <dir>   (tools/gemm_pmc.sh's passes p1/ p2/ p3/: every
        counter's mean per dispatch, the effective clock and the wait / issue shares of wave time)
+       python tools/pmc_traffic.py --model       (no GPU: the per-XCD L2 traffic model of the
+       packed 128x128 kernel's tile order over the serving loop's four grouped tower launches —
+       each XCD fetches every A row tile and packed W column tile its run of tiles touches once —
+       for the kernel's own band rule and for per-problem band heights; it has no L2 capacity
+       term: the bands it picks cut fc2's measured traffic 9 % but raised fc1's / qkv's 2-8 %,
+       profiles/r06_x3p_band_ab.txt)
 """
 import csv
 import glob
@@ -76,9 +82,71 @@ def sum_passes(root):
 
 
 
+def _cdiv(a, b):
+    return -(-a // b)
+
+
+def _tile(t, gy, gx, G):  # gemm_x3p_kernel's band order: (bx, by) of a problem's tile t
+    full, band = gy // G * G, G * gx
+    if t < (full // G) * band:
+        gb, tt = divmod(t, band)
+        bx = tt // G
+        return bx, gb * G + tt - bx * G
+    rem, tt = gy - full, t - (full // G) * band
+    return tt // rem, full + tt - (tt // rem) * rem
+
+
+def model_traffic(probs, bands=None, B=128):
+    """Bytes one launch's XCDs fetch beyond L2 (A row tiles fp32, packed W column tiles 6 B per
+    element, each once per XCD that touches it) + C written once; bands=None: the kernel's rule."""
+    total = sum(_cdiv(M, B) * _cdiv(N, B) for M, N, K in probs)
+    q, r = divmod(total, 8)
+    run = (total + 7) >> 3
+    g0 = int(run ** 0.5)
+    while (g0 + 1) ** 2 <= run:
+        g0 += 1
+    xcd = lambda t: t // (q + 1) if t < r * (q + 1) else r + (t - r * (q + 1)) // max(q, 1)
+    seen, off, byts = set(), 0, 0
+    for z, (M, N, K) in enumerate(probs):
+        gy, gx = _cdiv(M, B), _cdiv(N, B)
+        G = min(bands[z] if bands else g0, gy)
+        for t in range(gy * gx):
+            bx, by = _tile(t, gy, gx, G)
+            x = xcd(off + t)
+            for key, b in ((("A", x, z, by), min(B, M - by * B) * K * 4),
+                           (("W", x, z, bx), min(B, N - bx * B) * K * 6)):
+                if key not in seen:
+                    seen.add(key)
+                    byts += b
+        off += gy * gx
+    return byts + sum(M * N * 4 for M, N, K in probs)
+
+
+def model_main():
+    launches = {"qkv": [(1600, 2304, 768)] * 2 + [(400, 1536, 512), (384, 1536, 512)],
+                "out": [(1600, 768, 768)] * 2 + [(400, 512, 512), (384, 512, 512)],
+                "fc1": [(1600, 3072, 768)] * 2 + [(400, 2048, 512), (384, 2048, 512)],
+                "fc2": [(1600, 768, 3072)] * 2 + [(400, 512, 2048), (384, 512, 2048)]}
+    tot = [0, 0, 0]
+    for name, probs in launches.items():
+        alg = sum(M * K * 4 + N * K * 4 + M * N * 4 for M, N, K in probs)
+        bands = []
+        for z in range(len(probs)):  # each problem's band height alone (the others' costs fixed)
+            gy = _cdiv(probs[z][0], 128)
+            bands.append(min(range(1, gy + 1), key=lambda G: model_traffic(
+                probs, [*bands, G, *[1] * (len(probs) - z - 1)])))
+        own, tuned = model_traffic(probs), model_traffic(probs, bands)
+        tot[0] += alg; tot[1] += own; tot[2] += tuned
+        print(f"{name}: algorithmic {alg / 1e6:.1f} MB, kernel rule {own / 1e6:.1f} "
+              f"({own / alg:.2f}x), bands {bands} {tuned / 1e6:.1f} ({tuned / alg:.2f}x)")
+    print(f"all four: kernel rule {tot[1] / tot[0]:.2f}x, per-problem bands {tot[2] / tot[0]:.2f}x")
+
+
 def main():
     if sys.argv[1] == "--sum":
         return sum_passes(sys.argv[2])
+    if sys.argv[1] == "--model":
+        return model_main()
     fc, wc = {}, {}
     fetch = per_dispatch(sys.argv[1], "FETCH_SIZE", fc)
     write = per_dispatch(sys.argv[2], "WRITE_SIZE", wc)
