@@ -30,6 +30,10 @@ __device__ __forceinline__ float wmax(float v) {
 // of wave-private LDS.  Lane i scores keys i and 64 + i; softmax max / sum and the P.V partials
 // combine in attention_decode_kernel's order (its waves 2-3, and key groups past Lk, contribute
 // exact zeros).
+// TWO = false: the caller guarantees Lk <= 64 (after the causal clamp), so the second key half
+// is dead code and its K / V registers are never allocated (256 -> ~130 VGPRs, 1 -> 3 waves per
+// SIMD); every arithmetic expression is the one the runtime test would take: same bits.
+template <bool TWO = true>
 __device__ __forceinline__ void pair(const AttnArgs& a, int b, int h, float* Ps,
                                      float (*Os)[D]) {
   const int lane = threadIdx.x & 63;
@@ -40,7 +44,7 @@ __device__ __forceinline__ void pair(const AttnArgs& a, int b, int h, float* Ps,
   const float* vb = a.v + (int64_t)b * a.v_bs + h * D;
   int lk_end = a.Lk;
   if (a.causal) lk_end = min(lk_end, qpos + 1);
-  const bool two = lk_end > 64;  // wave-uniform
+  const bool two = TWO && lk_end > 64;  // wave-uniform
   float qscale = a.scale, qpart = 0.f;
   if (a.q_rms_part && lane < a.q_rms_nparts) qpart = a.q_rms_part[(int64_t)b * a.q_rms_nparts + lane];
   // scores of keys lane and 64 + lane (clamped rows / words as the block kernel's)

@@ -355,6 +355,7 @@ __global__ __launch_bounds__(256) void attention_decode_kernel(AttnArgs a) {
 // exact zeros), so outputs are bit-identical to attention_decode_kernel's.  The block kernel
 // issues 48 clamped 16-byte loads per thread for every key slot of its 256 whatever Lk: at 128
 // rows x 12 heads that load issue, not the bytes, was its 13.6 us.
+template <bool TWO>
 __global__ __launch_bounds__(256) void attention_decode_wave_kernel(AttnArgs a) {
   __shared__ float Ps[4][128];
   __shared__ __attribute__((aligned(16))) float Os[4][8][ATT_D];
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(256) void attention_decode_wave_kernel(AttnArgs a) 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pr = blockIdx.x * 4 + wave;
   if (pr >= a.B * a.H) return;  // wave-uniform; no block barrier below
-  dattn::pair(a, pr / a.H, pr % a.H, Ps[wave], Os[wave]);  // decode_attn.h
+  dattn::pair<TWO>(a, pr / a.H, pr % a.H, Ps[wave], Os[wave]);  // decode_attn.h
 }
 
 // The same pair per 64-thread block (one wave): the few-pair decodes (a 16-row batch: 128 pairs)
@@ -929,6 +930,16 @@ bool mfma_attention_disabled() {
   return off;
 }
 
+// MPR_ATT_KEYS64=0 (read per call, as MPR_ATT_WAVE): the grouped decodes' four-pair wave form
+// keeps the two-half code for <= 64 keys too (A/B of its TWO = false instantiation, 149 instead of
+// 256 VGPRs, 3 waves per SIMD instead of 1; same bits either way).  C5's 256-row t5-base generate
+// 44.6 -> 43.9 ms, C5 end to end 44.4-45.9 -> 43.7-43.8 ms per batch (round 6,
+// profiles/r06_attn_keys64_ab.txt).
+static bool small_keys_off() {
+  const char* e = getenv("MPR_ATT_KEYS64");
+  return e && e[0] == '0';
+}
+
 int attention(const AttnArgs& a, hipStream_t s) {
   MPR_REQUIRE(a.B >= 0 && a.H > 0 && a.Lq >= 0 && a.Lk > 0, "attention: bad shape");
   if (a.B == 0 || a.Lq == 0) return MPR_OK;
@@ -956,8 +967,11 @@ int attention(const AttnArgs& a, hipStream_t s) {
       if (lk_end > 64 && !(w2 && w2[0] == '0'))  // two 64-key halves: a wave each
         hipLaunchKernelGGL(attention_decode_wave2_kernel,
                            dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(512), 0, s, a);
+      else if (lk_end <= 64 && !small_keys_off())
+        hipLaunchKernelGGL(attention_decode_wave_kernel<false>,
+                           dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(256), 0, s, a);
       else
-        hipLaunchKernelGGL(attention_decode_wave_kernel,
+        hipLaunchKernelGGL(attention_decode_wave_kernel<true>,
                            dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(256), 0, s, a);
       MPR_LAUNCHED();
       return MPR_OK;
@@ -972,7 +986,8 @@ int attention(const AttnArgs& a, hipStream_t s) {
       if (sm && sm[0] == 'w' && sm[4] == '2' && lk_end > 64)
         hipLaunchKernelGGL(attention_decode_wave2_kernel,
                            dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(512), 0, s, a);
-      else
+      else  // (the single-half instantiation measured slower here, 16-row step 220-221 vs
+            // 214-215 us: one wave per CU gains nothing from its registers; round 6)
         hipLaunchKernelGGL(attention_decode_wave1_kernel, dim3((unsigned)((int64_t)a.B * a.H)),
                            dim3(64), 0, s, a);
       MPR_LAUNCHED();

@@ -605,14 +605,19 @@ def test_t5_grouped_decode_head_vs_oracle(device, t5_sd, grouped_40, monkeypatch
     assert compared > 200
 
 
-def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
+@pytest.mark.parametrize("text_only", [False, True])
+def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch, text_only):
     """Decodes over >= 64 rows (>= 512 batch x head pairs) run the decode attention one wave per
     pair (attention_decode_wave_kernel), whose outputs are bit-identical to the block kernel's
     (MPR_ATT_WAVE=0), and pairs with 65..128 keys (this cross-attention over 73 source rows) two
     waves per pair (attention_decode_wave2_kernel; MPR_ATT_WAVE2=0 keeps one): the greedy tokens
-    of 128 + 69 rows are equal in all three forms."""
+    of 128 + 69 rows are equal in all three forms.  At <= 64 keys (the self-attentions; the
+    cross-attention over the text-only prompts, <= 31 source rows) the one-wave form is the
+    single-half instantiation (MPR_ATT_KEYS64=0 keeps the two-half code): equal tokens too."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     A = _t5_batch(t5_sd, 16, 73)
+    if text_only:  # no 50 image-token prefix: the cross-attention takes <= 64 keys
+        A = (A[0][:, 50:].contiguous(), A[1][:, 50:].contiguous())
     emb = torch.cat([A[0]] * 12 + [A[0][:5]])
     emb = emb + 1e-3 * torch.randn(emb.shape, generator=torch.Generator().manual_seed(6))
     fm = torch.cat([A[1]] * 12 + [A[1][:5]])
@@ -624,23 +629,29 @@ def test_decode_attention_wave_form_matches_block(device, t5_sd, monkeypatch):
     monkeypatch.setenv("MPR_ATT_WAVE2", "0")
     one_wave = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
     assert torch.equal(one_wave, want)
+    monkeypatch.setenv("MPR_ATT_KEYS64", "0")
+    two_half = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
+    assert torch.equal(two_half, want)
 
 
-@pytest.mark.parametrize("fold", ["1", "0"])
-def test_decode_attention_small_forms_match_block(device, t5_sd, monkeypatch, fold):
+@pytest.mark.parametrize("fold,text_only", [("1", False), ("0", False), ("1", True)])
+def test_decode_attention_small_forms_match_block(device, t5_sd, monkeypatch, fold, text_only):
     """A one-batch decode (16 rows: 128 batch x head pairs) runs its attention a block of one wave
     per pair (attention_decode_wave1_kernel, default), two waves per pair past 64 keys
     (MPR_ATT_SMALL=wave2) or the 256-thread block kernel (block): greedy tokens equal in all
     three, on the folded and the 8-launch chain (73 source keys: the cross-attention takes both
-    halves)."""
+    halves; text-only prompts: one; MPR_ATT_KEYS64 does not change this form)."""
     from multimodalpromptretrieval_amd.t5 import DeviceT5
     monkeypatch.setenv("MPR_DECODE_FOLD", fold)
     emb, fm = _t5_batch(t5_sd, 16, 73)
+    if text_only:
+        emb, fm = emb[:, 50:].contiguous(), fm[:, 50:].contiguous()
     got = {}
-    for form in ("block", "wave1", "wave2"):
-        monkeypatch.setenv("MPR_ATT_SMALL", form)
+    for form in ("block", "wave1", "wave2", "keys64off"):
+        monkeypatch.setenv("MPR_ATT_SMALL", "wave1" if form == "keys64off" else form)
+        monkeypatch.setenv("MPR_ATT_KEYS64", "0" if form == "keys64off" else "1")
         got[form] = DeviceT5(t5_sd, device).generate_padded(emb, fm, 20).cpu()
-    assert torch.equal(got["wave1"], got["block"]) and torch.equal(got["wave2"], got["block"])
+    assert all(torch.equal(got[f], got["block"]) for f in ("wave1", "wave2", "keys64off"))
 
 
 def test_grouped_decode_row_blocks_match(device, monkeypatch):
