@@ -1370,6 +1370,11 @@ const bool g_x3p_sb1 = [] {
   return !(e && e[0] == '2');
 }();
 
+const bool g_x3p_k32 = [] {
+  const char* e = getenv("MPR_X3P_K32");
+  return e && e[0] == '1';
+}();
+
 int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
   double flops = 0, bytes = 0;
   for (int i = 0; i < g.n; ++i) {
@@ -1407,7 +1412,13 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
         return g_x3p_sb1 ? launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s)
                          : launch_gemm_x3p_group<128, 128, 2, 1, 2, 16, 2>(g, s);
       case X3P_SMALL: return launch_gemm_x3p_group<64, 64, 1, 1, 2>(g, s);
-      case X3P_SMALL3: return launch_gemm_x3p_group<64, 64, 1, 1, 2, 32>(g, s);
+      // K >= 2048 on 64x64 blocks: 16-deep K tiles in four A stages, a barrier every second
+      // tile (36.9 KB of LDS), not the 32-deep tiles of rounds 4-5: T5 wo 1536x512x2048 42.8 ->
+      // 33.8 us, ViT fc2 1600x768x3072 x2 137.6 -> 113.4, 800 rows 68.5 -> 68.3 (x3pbench, round
+      // 6, profiles/r06_x3p_small_ab.txt); same k order, bit-identical.  MPR_X3P_K32=1: 32-deep.
+      case X3P_SMALL3:
+        return g_x3p_k32 ? launch_gemm_x3p_group<64, 64, 1, 1, 2, 32>(g, s)
+                         : launch_gemm_x3p_group<64, 64, 1, 1, 2, 16, 2>(g, s);
       default: return launch_gemm_x3_group<64, 128, 1, 1, 32, 2, 1>(g, s);
     }
   });
@@ -1481,9 +1492,10 @@ int gemm_group(const GemmGroup& g, hipStream_t s) {
   // below): 128x128 blocks of 8 waves for launches of > 160 of them with a wide N or a long K
   // (ViT qkv 1600x2304x768 x2: 80.9 -> 73.5 us, fc1 110.7 -> 102.1, qkv at 800 rows 46.0 ->
   // 41.4, fc2 1600x768x3072 x2 127.7 -> 116.2), else 64x64 blocks of 4 waves (ViT out
-  // 1600x768x768 x2: 38.7 -> 33.6, T5 qkv 1536x1536x512 27.6 -> 24.3), 32-deep K tiles at
-  // K >= 2048 (T5 wo 1536x512x2048: 44.2 -> 36.4, ViT fc2 at 800 rows 76.5 -> 70.7; 32-deep
-  // tiles on the 128x128 blocks measured 5-15 % slower, profiles/r04_x3p_k32_ab.txt).  (The 64x64 tiles on the ViT fc2,
+  // 1600x768x768 x2: 38.7 -> 33.6, T5 qkv 1536x1536x512 27.6 -> 24.3), at K >= 2048 four A
+  // stages (round 6; rounds 4-5 took 32-deep K tiles there: T5 wo 1536x512x2048 44.2 -> 36.4,
+  // ViT fc2 at 800 rows 76.5 -> 70.7 against the two-stage 16-deep tile; 32-deep tiles on the
+  // 128x128 blocks measured 5-15 % slower, profiles/r04_x3p_k32_ab.txt).  (The 64x64 tiles on the ViT fc2,
   // 113.0 us alone, fetched 314 MB per launch from beyond L2 against ~120 MB for 128x128 tiles:
   // r04_v2 PMC.)
   if (getenv("MPR_GEMM_LOG")) {  // debug: each distinct launch shape once, to stderr

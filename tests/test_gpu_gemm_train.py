@@ -78,7 +78,8 @@ def _packed(W):
 
 @pytest.mark.parametrize("M,N,K,act,res", [
     (1600, 2304, 768, 0, False),    # ViT qkv, two batches (128x128 packed tiles)
-    (1600, 768, 3072, 0, True),     # ViT fc2 + residual (64x64, three W steps in flight)
+    (1600, 768, 3072, 0, True),     # ViT fc2 + residual (64x64, four A stages: K >= 2048)
+    (300, 512, 2052, 2, True),      # 64x64 four A stages with a K tail, odd K tiles
     (1536, 1536, 512, 0, False),    # T5 encoder qkv (64x64)
     (800, 3072, 768, 2, False),     # ViT fc1 shape, relu
     (77, 200, 52, 0, True),         # ragged: N and K tails, K % 16 != 0
