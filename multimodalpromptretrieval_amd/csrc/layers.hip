@@ -479,6 +479,10 @@ __global__ __launch_bounds__(512) void attention_decode_wave2_kernel(AttnArgs a)
 // The contraction order over the head dim inside a step is permuted identically for K and Q
 // (lane group g holds d = 16g .. 16g+15).  Softmax follows torch: p = exp(s - max) / sum, then
 // P @ V.
+// (Measured and dropped, round 6: an instantiation for <= 128 keys — staging registers and score
+// tiles sized for 128, 98 VGPRs and 4 waves per SIMD instead of 168 and 2 — ran the serving loop
+// 3,888-4,069 vs 3,891-4,033 QA pairs/s and the index build 10.4k vs 10.4-10.8k rows/s: the
+// towers' attentions, ~4 % of kernel time, are not occupancy-bound.)
 constexpr int ATT_MFMA_MAXK = 256;
 constexpr int ATT_MFMA_KT = ATT_MFMA_MAXK / 16;
 constexpr int ATT_MFMA_LD = 68;  // LDS row stride (floats)
