@@ -990,8 +990,9 @@ int attention(const AttnArgs& a, hipStream_t s) {
       if (sm && sm[0] == 'w' && sm[4] == '2' && lk_end > 64)
         hipLaunchKernelGGL(attention_decode_wave2_kernel,
                            dim3((unsigned)cdiv((int64_t)a.B * a.H, 4)), dim3(512), 0, s, a);
-      else  // (the single-half instantiation measured slower here, 16-row step 220-221 vs
-            // 214-215 us: one wave per CU gains nothing from its registers; round 6)
+      else  // (the single-half instantiation for the <= 64-key self-attentions measured no
+            // faster here: 16-row step 216.9-221.7 vs 218.7-220.2 us over 4 + 4 alternating
+            // tools/decode_ab.py runs — one wave per CU gains nothing from freed registers)
         hipLaunchKernelGGL(attention_decode_wave1_kernel, dim3((unsigned)((int64_t)a.B * a.H)),
                            dim3(64), 0, s, a);
       MPR_LAUNCHED();
