@@ -87,6 +87,11 @@ int main(int argc, char** argv) {
       {"tr dWwi 2048x512x1440", 2048, 512, 1440, 1},
       {"tr dWo 512x512x1440", 512, 512, 1440, 1},
       {"tr dxqkv 1440x512x1536", 1440, 512, 1536, 1},
+      {"loop t5 qkv 11776x1536x512", 11776, 1536, 512, 1},
+      {"loop t5 o 11776x512x512", 11776, 512, 512, 1},
+      {"loop t5 wi 11776x2048x512", 11776, 2048, 512, 1},
+      {"loop t5 wo 11776x512x2048", 11776, 512, 2048, 1},
+      {"c5 t5b qkv 10240x2304x768", 10240, 2304, 768, 1},
   };
   using L = std::function<int(const GemmGroup&, hipStream_t)>;
   struct Var { const char* name; L fn; bool packed; };
