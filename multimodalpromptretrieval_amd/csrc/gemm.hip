@@ -1375,6 +1375,11 @@ const bool g_x3p_k32 = [] {
   return e && e[0] == '1';
 }();
 
+const bool g_x3p_longk_sb = [] {
+  const char* e = getenv("MPR_X3P_LONGK_SB");
+  return !(e && e[0] == '0');
+}();
+
 int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
   double flops = 0, bytes = 0;
   for (int i = 0; i < g.n; ++i) {
@@ -1408,9 +1413,21 @@ int gemm_launch(const GemmGroup& g, int kind, hipStream_t s) {
       // (0.882 vs 0.874 of fp32 peak), but in the serving loop the two-stage blocks leave LDS for
       // the decode chain's blocks beside them: 4,156-4,195 vs 4,066-4,153 QA pairs/s over 5 / 4
       // alternating runs, in-loop GEMM frac 0.68 vs 0.66 (round 6, profiles/r06_loop_interference.txt)
-      case X3P_WIDE:
-        return g_x3p_sb1 ? launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s)
-                         : launch_gemm_x3p_group<128, 128, 2, 1, 2, 16, 2>(g, s);
+      // Long-K launches of one round of blocks (<= 256: the ViT fc2 groups, 184) take the four
+      // stages anyway: fc2 1600x768x3072 x2 107.7 -> 100.7 us (x3pbench, round 6); the K = 768
+      // qkv / fc1 and the 368-block grouped T5 FFN-out are faster on two stages
+      // (profiles/r06_x3p_small_ab.txt).  MPR_X3P_LONGK_SB=0: two stages there too.
+      case X3P_WIDE: {
+        int64_t b128 = 0;
+        int max_k = 0;
+        for (int i = 0; i < g.n; ++i) {
+          b128 += cdiv(g.g[i].M, 128) * cdiv(g.g[i].N, 128);
+          max_k = std::max(max_k, g.g[i].K);
+        }
+        const bool four = !g_x3p_sb1 || (g_x3p_longk_sb && max_k >= 2048 && b128 <= 256);
+        return four ? launch_gemm_x3p_group<128, 128, 2, 1, 2, 16, 2>(g, s)
+                    : launch_gemm_x3p_group<128, 128, 2, 1, 2>(g, s);
+      }
       case X3P_SMALL: return launch_gemm_x3p_group<64, 64, 1, 1, 2>(g, s);
       // K >= 2048 on 64x64 blocks: 16-deep K tiles in four A stages, a barrier every second
       // tile (36.9 KB of LDS), not the 32-deep tiles of rounds 4-5: T5 wo 1536x512x2048 42.8 ->
